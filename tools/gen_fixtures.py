@@ -1,0 +1,592 @@
+#!/usr/bin/env python3
+"""Golden-vector generator for the 6 nimmt! hot path.
+
+Runs ONLY in the build container (never on the GPU box): it imports the
+reference implementation from /root/reference (read-only) and records its
+outputs as small JSON / NPZ fixtures under tests/golden/.  The fixtures are
+data (inputs + expected outputs); no reference source is copied.
+
+The reference imports three third-party modules that are absent from this
+image (gym, numba, multi_elo).  None of them takes part in the arithmetic
+being pinned (env.py only subclasses gym.Env and builds Discrete/Box space
+descriptors, numba only decorates the out-of-scope PER buffer, multi_elo is
+only called by Tournament._compute_elos, which is not exercised here), so the
+generator puts attribute-holder stand-ins for them on sys.path in a
+temporary directory before importing the reference.
+
+Usage:  PYTHONDONTWRITEBYTECODE=1 python tools/gen_fixtures.py [--out tests/golden]
+
+Fixture families (SURVEY.md §4 "What the build must add"):
+  F0 mt19937.json        numpy legacy MT19937 seeding / shuffle / choice vectors
+  F1 notebook_games.json five rendered games from experiments/simple_tournament.ipynb
+  F2 random_games.npz    seeded GameSession(DrunkHamster x N) games, N = 1..10
+     random_sessions.json multi-episode sessions (auto-reset stream continuation)
+  F3 edge_cases.json     crafted + random reset_to positions, one step each
+  F4 mcs_games.json      seeded GameSession(MCSAgent, DrunkHamster...) games
+  F5 puct_math.json      PUCTAgent._compute_pucts / _normalize_q vectors
+  F6 normalization.json  SechsNimmtStateNormalization vectors
+  F7 positions.json      Tournament._compute_relative/absolute_positions vectors
+  F8 puct_policy.npz     PUCTAgent policy-net weights + _compute_policy outputs
+"""
+import argparse
+import json
+import os
+import re
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+REF = "/root/reference"
+
+_STUBS = {
+    "gym/__init__.py": "class Env:\n    def __init__(self):\n        pass\nfrom . import spaces\n",
+    "gym/spaces.py": (
+        "class Discrete:\n    def __init__(self, n):\n        self.n = n\n"
+        "class Box:\n    def __init__(self, low, high, shape, dtype=None):\n"
+        "        self.low, self.high, self.shape, self.dtype = low, high, shape, dtype\n"
+    ),
+    "numba/__init__.py": (
+        "def jit(*a, **k):\n    if a and callable(a[0]):\n        return a[0]\n    return lambda f: f\n"
+    ),
+    "multi_elo/__init__.py": (
+        "class EloPlayer:\n    def __init__(self, place, elo):\n        self.place, self.elo = place, elo\n"
+        "def calc_elo(players, k):\n    raise NotImplementedError('multi_elo is not installed')\n"
+    ),
+}
+
+
+def import_reference():
+    d = tempfile.mkdtemp(prefix="sechs_stubs_")
+    for rel, text in _STUBS.items():
+        p = os.path.join(d, rel)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        with open(p, "w") as f:
+            f.write(text)
+    sys.path.insert(0, d)
+    sys.path.insert(0, REF)
+    sys.dont_write_bytecode = True
+    import logging
+
+    logging.disable(logging.CRITICAL)
+    import rl_6_nimmt  # noqa: F401
+
+    return rl_6_nimmt
+
+
+# ----------------------------------------------------------------------------
+# helpers
+# ----------------------------------------------------------------------------
+def board_of(env):
+    return [[int(c) for c in row] for row in env._board]
+
+
+def hands_of(env):
+    return [[int(c) for c in h] for h in env._hands]
+
+
+def obs_of(states):
+    return [[int(v) for v in s] for s in states]
+
+
+# ----------------------------------------------------------------------------
+# F0: numpy legacy MT19937
+# ----------------------------------------------------------------------------
+def gen_mt(out):
+    seeds = [0, 1, 2, 5, 42, 1234, 65535, 2**31 - 1, 2**32 - 1]
+    rec = {"seeds": [], "shuffles": [], "choices": []}
+    for s in seeds:
+        np.random.seed(s)
+        st = np.random.get_state()
+        key = [int(x) for x in st[1]]
+        rec["seeds"].append({"seed": s, "key_head": key[:8], "key_tail": key[-8:], "pos": int(st[2])})
+        np.random.seed(s)
+        raw = [int(x) for x in np.random.randint(0, 2**32, size=700, dtype=np.uint64)]
+        rec["seeds"][-1]["raw_u32"] = raw  # legacy full-range draws == raw genrand_int32 outputs? verified below
+    for s in list(range(40)) + [65535, 99991]:
+        np.random.seed(s)
+        deck = np.arange(104, dtype=np.int32)
+        np.random.shuffle(deck)
+        deck2 = np.arange(57, dtype=np.int32)
+        np.random.shuffle(deck2)
+        rec["shuffles"].append({"seed": s, "deck104_then_deck57": [int(x) for x in deck] + [int(x) for x in deck2]})
+    for s in range(20):
+        np.random.seed(s)
+        seq = []
+        for n in [10, 9, 8, 7, 6, 5, 4, 3, 2, 1, 17, 33, 64, 65, 100]:
+            arr = np.arange(n, dtype=np.int32) * 3 + 1
+            seq.append([n, int(np.random.choice(arr, size=1)[0])])
+        rec["choices"].append({"seed": s, "n_and_pick": seq})
+    with open(os.path.join(out, "mt19937.json"), "w") as f:
+        json.dump(rec, f)
+
+
+# ----------------------------------------------------------------------------
+# F1: notebook traces
+# ----------------------------------------------------------------------------
+_CARD = re.compile(r"\s*(\d+)([ .:+#])")
+
+
+def _parse_cards(text):
+    cards = []
+    for tok in re.findall(r"(\d+)[ .:+#]?", text):
+        cards.append(int(tok) - 1)
+    return cards
+
+
+def parse_notebook_games(ref):
+    from rl_6_nimmt.env import SechsNimmtEnv
+
+    nb = json.load(open(os.path.join(REF, "experiments/simple_tournament.ipynb")))
+    games = []
+    for cell in nb["cells"]:
+        if cell.get("cell_type") != "code":
+            continue
+        text = "".join(
+            "".join(o.get("text", "")) for o in cell.get("outputs", []) if o.get("output_type") == "stream"
+        )
+        if "Dealing cards" not in text:
+            continue
+        for chunk in text.split("Dealing cards")[1:]:
+            lines = chunk.split("\n")
+            board, hands, names = [], [], []
+            i = 0
+            while "Board:" not in lines[i]:
+                i += 1
+            i += 1
+            while "Players:" not in lines[i]:
+                row = lines[i].split("_")[0].split("*")[0]
+                board.append(_parse_cards(row))
+                i += 1
+            i += 1
+            while lines[i].startswith("  ") and "(player" in lines[i]:
+                name = lines[i].split("(player")[0].strip()
+                names.append(name)
+                hand_txt = lines[i].split("cards", 1)[1]
+                hands.append(_parse_cards(hand_txt))
+                i += 1
+            plays = []
+            for ln in lines[i:]:
+                m = re.search(r"\(player (\d+)\) plays card (\d+)", ln)
+                if m:
+                    plays.append((int(m.group(1)) - 1, int(m.group(2)) - 1))
+                if "The game is over" in ln:
+                    break
+            final = None
+            # final scores from the last rendered "Players:" block
+            score_re = re.compile(r"\(player (\d+)\):\s+(-?\d+) Hornochsen")
+            last = {}
+            for ln in lines:
+                m = score_re.search(ln)
+                if m:
+                    last[int(m.group(1)) - 1] = int(m.group(2))
+                if "The game is over" in ln:
+                    break
+            final = [last[p] for p in range(len(names))]
+            n = len(names)
+            # plays are logged in ascending card order per step; regroup by step
+            steps = []
+            for k in range(0, len(plays), n):
+                acts = [None] * n
+                for p, c in plays[k : k + n]:
+                    acts[p] = c
+                steps.append(acts)
+            games.append({"names": names, "board": board, "hands": hands, "actions": steps, "final_penalties": final})
+    # replay through the reference env to record per-step expected outputs
+    for g in games:
+        env = SechsNimmtEnv(len(g["names"]), verbose=False)
+        states, legal = env.reset_to([list(r) for r in g["board"]], [list(h) for h in g["hands"]])
+        g["obs0"] = obs_of(states)
+        recs = []
+        scores = np.zeros(len(g["names"]), dtype=np.int64)
+        for acts in g["actions"]:
+            (states, legal), rew, done, _ = env.step(list(acts))
+            scores += rew
+            recs.append({"rewards": [int(r) for r in rew], "done": bool(done), "board": board_of(env), "obs": obs_of(states)})
+        g["steps"] = recs
+        g["final_scores"] = [int(x) for x in scores]
+        assert [int(x) for x in env._scores] == g["final_penalties"], (env._scores, g["final_penalties"])
+    return games
+
+
+def gen_notebook(ref, out):
+    games = parse_notebook_games(ref)
+    assert len(games) == 5, len(games)
+    with open(os.path.join(out, "notebook_games.json"), "w") as f:
+        json.dump({"source": "experiments/simple_tournament.ipynb rendered DEBUG logs", "games": games}, f)
+
+
+# ----------------------------------------------------------------------------
+# F2: seeded random games
+# ----------------------------------------------------------------------------
+def play_recorded(env, agents):
+    """Mirror of GameSession.play_game's RNG-consuming call order (play.py:23-75)."""
+    states, legal = env.reset()
+    deal = (board_of(env), hands_of(env))
+    obs = [obs_of(states)]
+    acts, rews, dones = [], [], []
+    done = False
+    while not done:
+        a = []
+        for agent, s, l in zip(agents, states, legal):
+            action, _ = agent(s, legal_actions=l)
+            a.append(int(action))
+        (states, legal), r, done, _ = env.step(a)
+        acts.append(a)
+        rews.append([int(x) for x in r])
+        dones.append(bool(done))
+        obs.append(obs_of(states))
+    return deal, acts, rews, dones, obs
+
+
+def gen_random_games(ref, out):
+    from rl_6_nimmt.env import SechsNimmtEnv
+    from rl_6_nimmt.play import GameSession
+    from rl_6_nimmt.agents import DrunkHamster
+
+    arrays = {}
+    meta = []
+    configs = []
+    for n in range(1, 11):
+        configs.append((n, 104, True, 60 if n == 4 else 12))
+    configs += [(2, 24, True, 8), (3, 40, True, 8), (4, 80, True, 6), (4, 104, False, 8), (2, 104, False, 4)]
+    for ci, (n, c, summ, nseeds) in enumerate(configs):
+        L = 10 + 1 + (12 if summ else 0) + 24
+        decks_board, hands_all, acts_all, rews_all, obs_all, res_all = [], [], [], [], [], []
+        for s in range(nseeds):
+            np.random.seed(s)
+            env = SechsNimmtEnv(n, num_cards=c, include_summaries=summ, verbose=False)
+            agents = [DrunkHamster() for _ in range(n)]
+            deal, acts, rews, dones, obs = play_recorded(env, agents)
+            assert dones == [False] * 9 + [True]
+            res = np.sum(np.array(rews), axis=0)
+            if summ and c == 104:
+                # cross-check against the real GameSession harness (play.py)
+                np.random.seed(s)
+                sess = GameSession(*[DrunkHamster() for _ in range(n)])
+                sess.play_game()
+                assert [int(x) for x in sess.results[0]] == [int(x) for x in res]
+            decks_board.append([r[0] for r in deal[0]])
+            hands_all.append(deal[1])
+            acts_all.append(acts)
+            rews_all.append(rews)
+            obs_all.append(obs)
+            res_all.append([int(x) for x in res])
+        key = f"c{ci}"
+        arrays[key + "_board0"] = np.array(decks_board, dtype=np.int16)  # [S,4]
+        arrays[key + "_hands0"] = np.array(hands_all, dtype=np.int16)  # [S,N,10]
+        arrays[key + "_actions"] = np.array(acts_all, dtype=np.int16)  # [S,10,N]
+        arrays[key + "_rewards"] = np.array(rews_all, dtype=np.int16)  # [S,10,N]
+        arrays[key + "_obs"] = np.array(obs_all, dtype=np.int8)  # [S,11,N,L]
+        arrays[key + "_results"] = np.array(res_all, dtype=np.int16)  # [S,N]
+        meta.append({"key": key, "num_players": n, "num_cards": c, "include_summaries": summ, "seeds": nseeds, "obs_len": L})
+    np.savez_compressed(os.path.join(out, "random_games.npz"), **arrays)
+    with open(os.path.join(out, "random_games_meta.json"), "w") as f:
+        json.dump(
+            {
+                "protocol": "np.random.seed(s); env=SechsNimmtEnv(N, num_cards=C, include_summaries=S); "
+                "GameSession(DrunkHamster()*N).play_game() call order; obs[0] = reset obs, obs[t+1] = obs after step t",
+                "configs": meta,
+            },
+            f,
+        )
+
+    # multi-episode sessions: the deal of game e+1 continues the RNG stream after game e
+    sessions = []
+    for n, seeds, eps in [(4, list(range(12)) + [65535], 8), (2, list(range(4)), 5), (3, [7, 8], 5), (10, [3], 4)]:
+        for s in seeds:
+            np.random.seed(s)
+            sess = GameSession(*[DrunkHamster() for _ in range(n)])
+            for _ in range(eps):
+                sess.play_game()
+            sessions.append({"num_players": n, "seed": s, "results": [[int(x) for x in r] for r in sess.results]})
+    # long sessions for a few bench lanes (bench: game g seeded g, 100 episodes back to back)
+    for s in [0, 1, 2, 4097, 65535]:
+        np.random.seed(s)
+        sess = GameSession(*[DrunkHamster() for _ in range(4)])
+        for _ in range(100):
+            sess.play_game()
+        tot = np.sum(np.array(sess.results), axis=0)
+        sessions.append(
+            {
+                "num_players": 4,
+                "seed": s,
+                "episodes": 100,
+                "results_last": [int(x) for x in sess.results[-1]],
+                "results_sum": [int(x) for x in tot],
+            }
+        )
+    with open(os.path.join(out, "random_sessions.json"), "w") as f:
+        json.dump({"protocol": "np.random.seed(s); sess=GameSession(DrunkHamster()*N); sess.play_game() x episodes", "sessions": sessions}, f)
+
+
+# ----------------------------------------------------------------------------
+# F3: edge cases through reset_to
+# ----------------------------------------------------------------------------
+def _one_step_case(SechsNimmtEnv, InvalidMoveException, board, hands, actions, label, summ=True):
+    n = len(hands)
+    env = SechsNimmtEnv(n, include_summaries=summ, verbose=False)
+    states0, legal0 = env.reset_to([list(r) for r in board], [list(h) for h in hands])
+    case = {"label": label, "board": board, "hands": hands, "actions": actions, "include_summaries": summ, "obs0": obs_of(states0)}
+    try:
+        (states, legal), rew, done, _ = env.step(list(actions))
+        case["expect"] = {
+            "rewards": [int(x) for x in rew],
+            "done": bool(done),
+            "board": board_of(env),
+            "hands": hands_of(env),
+            "scores": [int(x) for x in env._scores],
+            "obs": obs_of(states),
+            "legal": [[int(c) for c in l] for l in legal],
+        }
+    except InvalidMoveException as e:
+        case["error"] = {"type": "InvalidMoveException", "message": str(e)}
+    except AssertionError:
+        case["error"] = {"type": "AssertionError", "message": ""}
+    return case
+
+
+def gen_edge_cases(ref, out):
+    from rl_6_nimmt.env import SechsNimmtEnv, InvalidMoveException
+
+    cases = []
+    add = lambda *a, **k: cases.append(_one_step_case(SechsNimmtEnv, InvalidMoveException, *a, **k))
+    # crafted
+    add([[10], [20], [30], [40]], [[5], [6]], [5, 6], "double undercut, equal row values -> lowest row index first")
+    add([[10, 11], [20], [30, 31], [40]], [[5, 50], [6, 51]], [5, 6], "undercut picks min heads row (row 1)")
+    add([[10, 11, 12, 13, 14], [20], [30], [40]], [[15, 0], [16, 1]], [15, 16], "6th card take then append to new row")
+    add([[10, 11, 12, 13, 14], [20, 21, 22, 23, 24], [30], [40]], [[15, 0], [25, 1], [26, 2]], [15, 25, 26], "two takes in one step")
+    add([[50, 51, 52, 53], [60], [70], [80]], [[54, 1], [55, 2]], [54, 55], "card 55 (idx 54, 7 heads) completes row then 6th takes it")
+    add([[50, 51, 52, 53], [60], [70], [80]], [[54, 1], [56, 2], [57, 3]], [54, 56, 57], "6th card on a row a lower card extended this step")
+    add([[54], [10], [21], [98]], [[0], [1], [2], [3]], [0, 1, 2, 3], "four undercuts in one step")
+    add([[54, 64, 74, 84, 94], [10, 20, 30, 40, 43], [9], [8]], [[95, 0], [44, 1], [3, 2], [2, 5]], [95, 44, 3, 2], "big penalties")
+    add([[10], [20], [30], [40]], [[5, 6], [7, 8]], [6, 9], "invalid move by player 2")
+    add([[10], [20], [30], [40]], [[5, 6], [7, 8]], [99, 7], "invalid move by player 1")
+    add([[10], [20], [30], [40]], [[5, 6], [7, 8]], [5], "wrong number of actions")
+    add([[10], [20], [30], [40]], [[5], [7]], [5, 7], "last card -> done", summ=False)
+    # N = 10 with the whole deck in play
+    rng = np.random.RandomState(1234)
+    deck = list(rng.permutation(104))
+    hands = [sorted(int(c) for c in deck[10 * p : 10 * p + 10]) for p in range(10)]
+    board = [[int(deck[103 - r])] for r in range(4)]
+    add(board, hands, [h[rng.randint(len(h))] for h in hands], "N=10 full deck first step")
+    # random positions: rows of 1..5 cards, hands of n cards
+    rng = np.random.RandomState(20251015)
+    for k in range(320):
+        n_players = int(rng.choice([2, 3, 4, 4, 4, 5, 6, 8, 10]))
+        n = int(rng.randint(1, 11))
+        lens = [int(rng.randint(1, 6)) for _ in range(4)]
+        need = sum(lens) + n_players * n
+        if need > 104:
+            continue
+        perm = [int(c) for c in rng.permutation(104)[:need]]
+        board = []
+        pos = 0
+        for L in lens:
+            board.append(sorted(perm[pos : pos + L]) if rng.rand() < 0.8 else perm[pos : pos + L])
+            pos += L
+        hands = []
+        for p in range(n_players):
+            hands.append(sorted(perm[pos : pos + n]))
+            pos += n
+        actions = [h[int(rng.randint(len(h)))] for h in hands]
+        if rng.rand() < 0.03:
+            actions[int(rng.randint(n_players))] = int(rng.randint(0, 104))
+        add(board, hands, actions, f"random #{k}", summ=bool(rng.rand() < 0.9))
+    with open(os.path.join(out, "edge_cases.json"), "w") as f:
+        json.dump({"protocol": "env=SechsNimmtEnv(N, include_summaries=S); env.reset_to(board, hands); env.step(actions)", "cases": cases}, f)
+
+
+# ----------------------------------------------------------------------------
+# F4: seeded MCS games
+# ----------------------------------------------------------------------------
+def gen_mcs(ref, out):
+    from rl_6_nimmt.env import SechsNimmtEnv
+    from rl_6_nimmt.agents import DrunkHamster, MCSAgent
+    from rl_6_nimmt.play import GameSession
+
+    games = []
+    specs = []
+    specs += [("MRRR", 4, 100, 10, s) for s in range(6)]
+    specs += [("MR", 2, 100, 10, s) for s in range(3)]
+    specs += [("MMRR", 4, 40, 4, s) for s in range(3)]
+    specs += [("RMR", 3, 30, 10, s) for s in range(3)]
+    specs += [("MRRR", 4, 200, 10, s) for s in range(2)]
+    t0 = time.time()
+    for seats, n, mc_max, mc_per_card, s in specs:
+        agents = [MCSAgent(mc_max=mc_max, mc_per_card=mc_per_card) if ch == "M" else DrunkHamster() for ch in seats]
+        np.random.seed(s)
+        env = SechsNimmtEnv(n, verbose=False)
+        try:
+            deal, acts, rews, dones, obs = play_recorded_tensor(env, agents)
+            rec = {"seats": seats, "mc_max": mc_max, "mc_per_card": mc_per_card, "seed": s, "board0": deal[0], "hands0": deal[1], "actions": acts, "rewards": rews}
+        except IndexError:
+            rec = {"seats": seats, "mc_max": mc_max, "mc_per_card": mc_per_card, "seed": s, "error": "IndexError (mcts.py:170 debug f-string, quirk Q6)"}
+        # cross-check with the real harness
+        if "error" not in rec:
+            agents = [MCSAgent(mc_max=mc_max, mc_per_card=mc_per_card) if ch == "M" else DrunkHamster() for ch in seats]
+            np.random.seed(s)
+            sess = GameSession(*agents)
+            sess.play_game()
+            assert [int(x) for x in sess.results[0]] == [int(x) for x in np.sum(np.array(rec["rewards"]), axis=0)]
+            rec["results"] = [int(x) for x in sess.results[0]]
+        games.append(rec)
+        print(f"  mcs {seats} mc_max={mc_max} seed={s}: {time.time() - t0:.1f}s", flush=True)
+    with open(os.path.join(out, "mcs_games.json"), "w") as f:
+        json.dump({"protocol": "np.random.seed(s); GameSession(*agents).play_game(); M=MCSAgent(mc_max, mc_per_card), R=DrunkHamster", "games": games}, f)
+
+
+def play_recorded_tensor(env, agents):
+    """Same as play_recorded but hands agents float tensors like GameSession._tensorize (play.py:77-78)."""
+    import torch
+
+    states, legal = env.reset()
+    deal = (board_of(env), hands_of(env))
+    tens = lambda st: [torch.tensor(x).to(torch.device("cpu"), torch.float) for x in st]
+    states = tens(states)
+    acts, rews, dones = [], [], []
+    done = False
+    while not done:
+        a = []
+        for agent, s, l in zip(agents, states, legal):
+            action, _ = agent(s, legal_actions=l)
+            a.append(int(action))
+        (states, legal), r, done, _ = env.step(a)
+        states = tens(states)
+        acts.append(a)
+        rews.append([int(x) for x in r])
+        dones.append(bool(done))
+    return deal, acts, rews, dones, None
+
+
+# ----------------------------------------------------------------------------
+# F5/F6/F8: PUCT math, normalisation, policy
+# ----------------------------------------------------------------------------
+def gen_puct(ref, out):
+    import torch
+    from rl_6_nimmt.agents import PUCTAgent
+    from rl_6_nimmt.utils.preprocessing import SechsNimmtStateNormalization
+
+    torch.manual_seed(0)
+    agent = PUCTAgent()
+    rng = np.random.RandomState(7)
+    cases = []
+    for k in range(300):
+        n = int(rng.randint(2, 11))
+        legal = sorted(int(c) for c in rng.permutation(104)[:n])
+        total = int(rng.choice([0, 3, 9, 10, 11, 40, 200]))
+        outcomes = {a: [] for a in legal}
+        mode = k % 5
+        for _ in range(total):
+            a = legal[int(rng.randint(n))]
+            if mode == 0:
+                outcomes[a].append(-7.0)  # max == min  -> NaN q (quirk Q7)
+            else:
+                outcomes[a].append(float(-rng.randint(0, 40)))
+        p = rng.rand(n).astype(np.float32) + 1e-3
+        p = p / p.sum()
+        probs = torch.tensor(p)
+        with np.errstate(all="ignore"):
+            pucts = agent._compute_pucts(legal, outcomes, probs)
+            nq = agent._normalize_q(outcomes)
+        best, choice = -float("inf"), 0
+        for i, v in enumerate(pucts):
+            if v > best:
+                best, choice = v, i
+        cases.append(
+            {
+                "legal": legal,
+                "outcomes": [outcomes[a] for a in legal],
+                "probs": [float(x) for x in p],
+                "pucts": [None if np.isnan(x) else float(x) for x in pucts],
+                "normalize_q": [float(x) for x in nq],
+                "choice": choice,
+            }
+        )
+    with open(os.path.join(out, "puct_math.json"), "w") as f:
+        json.dump({"c_puct": 2.0, "cases": cases}, f)
+
+    # F6 normalisation
+    norm = SechsNimmtStateNormalization(action=True)
+    norm0 = SechsNimmtStateNormalization(action=False)
+    x = np.concatenate(
+        [rng.randint(-1, 104, size=(64, 1 + 10)), rng.randint(1, 11, size=(64, 1)), rng.randint(-1, 104, size=(64, 36))], axis=1
+    ).astype(np.float32)
+    y = norm(torch.tensor(x)).numpy()
+    y0 = norm0(torch.tensor(x[:, 1:])).numpy()
+    with open(os.path.join(out, "normalization.json"), "w") as f:
+        json.dump({"x_with_action": x.tolist(), "y_with_action": y.tolist(), "y_without_action": y0.tolist()}, f)
+
+    # F8 policy forward with fixed weights
+    from rl_6_nimmt.env import SechsNimmtEnv
+
+    arrays = {k: v.detach().numpy().astype(np.float32) for k, v in agent.actor.state_dict().items()}
+    names = sorted(arrays)
+    env = SechsNimmtEnv(4, verbose=False)
+    np.random.seed(3)
+    states, legal = env.reset()
+    xs, ps = [], []
+    for p in range(4):
+        st = torch.tensor(states[p]).to(torch.float)
+        with torch.no_grad():
+            pr = agent._compute_policy(legal[p], st).numpy()
+        xs.append(np.array(states[p], dtype=np.int16))
+        ps.append(pr.astype(np.float32))
+    arrays["states"] = np.stack(xs)
+    arrays["legal"] = np.array(legal, dtype=np.int16)
+    arrays["probs"] = np.stack(ps)
+    np.savez_compressed(os.path.join(out, "puct_policy.npz"), **arrays)
+    with open(os.path.join(out, "puct_policy_meta.json"), "w") as f:
+        json.dump({"weights": names, "init": "torch.manual_seed(0); PUCTAgent()"}, f)
+
+
+# ----------------------------------------------------------------------------
+# F7: tournament positions
+# ----------------------------------------------------------------------------
+def gen_positions(ref, out):
+    from rl_6_nimmt.tournament import Tournament
+
+    rng = np.random.RandomState(11)
+    cases = []
+    for k in range(200):
+        n = int(rng.randint(2, 7))
+        scores = -rng.randint(0, 8 if k % 3 == 0 else 40, size=n)
+        scores = scores.astype(np.int32)
+        rel = Tournament._compute_relative_positions(scores)
+        ab = Tournament._compute_absolute_positions(scores)
+        cases.append({"scores": [int(s) for s in scores], "relative": [float(v) for v in rel], "absolute": [float(v) for v in ab], "winner_index": int(np.argmax(scores))})
+    with open(os.path.join(out, "positions.json"), "w") as f:
+        json.dump({"cases": cases}, f)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests", "golden"))
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    out = os.path.abspath(args.out)
+    os.makedirs(out, exist_ok=True)
+    ref = import_reference()
+    steps = [
+        ("mt", gen_mt),
+        ("notebook", gen_notebook),
+        ("random", gen_random_games),
+        ("edge", gen_edge_cases),
+        ("puct", gen_puct),
+        ("positions", gen_positions),
+        ("mcs", gen_mcs),
+    ]
+    for name, fn in steps:
+        if args.only and name not in args.only.split(","):
+            continue
+        t = time.time()
+        if fn is gen_mt:
+            fn(out)
+        else:
+            fn(ref, out)
+        print(f"{name}: {time.time() - t:.1f}s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
