@@ -1,0 +1,266 @@
+"""GPU parity: libsechs.so kernels vs the CPU oracle and the reference's golden vectors.
+
+Bit-exact for everything (integer/index work): rewards, done flags,
+actions, observations, hands, board, scores, RNG streams.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RNG = {"numpy": O.RNG_NUMPY_MT, "philox": O.RNG_PHILOX}
+
+
+def venv(*a, **k):
+    from rl_6_nimmt.vec_env import VecSechsNimmtEnv
+
+    return VecSechsNimmtEnv(*a, **k)
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("rng", ["numpy", "philox"])
+@pytest.mark.parametrize("N,C,summ", [(4, 104, True), (2, 104, True), (3, 40, True), (10, 104, True), (1, 104, True),
+                                      (5, 104, False), (7, 80, True)])
+def test_rollout_matches_oracle(rng, N, C, summ):
+    B, T = 1000, 23  # ragged B (not a multiple of 256), episodes cross launch boundaries
+    seed = 12345
+    env = venv(B, N, C, seed=seed, rng=rng, include_summaries=summ)
+    env.reset()
+    ref = O.VecOracle(B, N, C, rng_mode=RNG[rng], seed=seed)
+    ref.reset()
+    L = O.obs_len(summ)
+    for chunk in (T, 1, 16):
+        out = env.rollout(chunk, want_actions=True, want_obs=True)
+        rr, rd, ra, ro = ref.rollout(chunk, include_summaries=summ, want_obs=True)
+        torch.cuda.synchronize()
+        assert np.array_equal(out["actions"].cpu().numpy(), ra)
+        assert np.array_equal(out["rewards"].cpu().numpy(), rr)
+        assert np.array_equal(out["done"].cpu().numpy(), rd)
+        o = out["obs"].cpu().numpy()
+        assert np.array_equal(o[..., :L], ro)
+        assert not o[..., L:].any()
+    assert np.array_equal(env.hands().cpu().numpy(), _pad_hands(ref.hands(), N))
+    assert np.array_equal(env.scores().cpu().numpy(), ref.scores())
+    s, e = env.results()
+    assert np.array_equal(s.cpu().numpy(), ref.sum_results())
+    assert np.array_equal(e.cpu().numpy(), ref.episodes())
+    for dt in (torch.int8, torch.int16, torch.int64, torch.float32):
+        assert np.array_equal(env.obs(dt).cpu().numpy(), ref.obs(summ).astype(np.int64).astype(dt_np(dt)))
+
+
+def dt_np(dt):
+    return {torch.int8: np.int8, torch.int16: np.int16, torch.int64: np.int64, torch.float32: np.float32}[dt]
+
+
+def _pad_hands(hands, N):
+    out = np.full((len(hands), N, 10), -1, dtype=np.int8)
+    for g, hs in enumerate(hands):
+        for p, h in enumerate(hs):
+            out[g, p, : len(h)] = h
+    return out
+
+
+@pytest.mark.parametrize("rng", ["numpy", "philox"])
+def test_full_size_episode_matches_oracle(rng):
+    """BASELINE config 2 size: 65 536 x 4-player games, one full episode, bit-exact."""
+    B, N = 65536, 4
+    env = venv(B, N, seed=0, rng=rng)
+    env.reset()
+    out = env.rollout(10, want_actions=True)
+    ref = O.VecOracle(B, N, rng_mode=RNG[rng], seed=0)
+    ref.reset()
+    rr, rd, ra, _ = ref.rollout(10, nthreads=8)
+    torch.cuda.synchronize()
+    assert np.array_equal(out["actions"].cpu().numpy(), ra)
+    assert np.array_equal(out["rewards"].cpu().numpy(), rr)
+    assert np.array_equal(out["done"].cpu().numpy(), rd)
+    # size-independent properties: every game ends after exactly 10 steps, the
+    # 104-card deck holds 171 heads, so no episode can cost more than that
+    d = out["done"].cpu().numpy()
+    assert d[9].all() and not d[:9].any()
+    tot = -out["rewards"].cpu().numpy().sum(axis=(0, 2))
+    assert tot.min() >= 0 and tot.max() <= 171
+
+
+def test_bench_lanes_replay_reference_sessions():
+    """game g seeded g, 100 episodes back to back == reference GameSession(DrunkHamster x4)."""
+    d = load("random_sessions.json")
+    recs = [r for r in d["sessions"] if r.get("episodes") == 100]
+    B = 65536
+    env = venv(B, 4, seed=0, rng="numpy")
+    env.reset()
+    last = None
+    for ep in range(100):
+        out = env.rollout(10)
+        last = out["rewards"]
+    s, e = env.results()
+    s, e = s.cpu().numpy(), e.cpu().numpy()
+    last = last.sum(dim=0).cpu().numpy()
+    for r in recs:
+        g = r["seed"]
+        assert e[g] == 100
+        assert s[g].tolist() == r["results_sum"]
+        assert last[g].tolist() == r["results_last"]
+
+
+def test_multi_episode_sessions_all_sizes():
+    d = load("random_sessions.json")
+    for r in d["sessions"]:
+        if "results" not in r:
+            continue
+        n, eps = r["num_players"], len(r["results"])
+        env = venv(1, n, seed=r["seed"], rng="numpy")
+        env.reset()
+        out = env.rollout(10 * eps)
+        per_ep = out["rewards"][:, 0, :].reshape(eps, 10, n).sum(dim=1).cpu().numpy()
+        assert per_ep.tolist() == r["results"]
+
+
+def test_random_games_golden_obs():
+    meta = load("random_games_meta.json")
+    z = np.load(os.path.join(GOLDEN, "random_games.npz"))
+    for cfg in meta["configs"]:
+        k, n, c, summ, S = cfg["key"], cfg["num_players"], cfg["num_cards"], cfg["include_summaries"], cfg["seeds"]
+        L = cfg["obs_len"]
+        # game g of a handle with seed 0 is np.random.seed(g)
+        env = venv(S, n, c, seed=0, rng="numpy", include_summaries=summ)
+        env.reset()
+        out = env.rollout(10, want_actions=True, want_obs=True)
+        assert np.array_equal(out["actions"].cpu().numpy().transpose(1, 0, 2), z[k + "_actions"])
+        assert np.array_equal(out["rewards"].cpu().numpy().transpose(1, 0, 2), z[k + "_rewards"])
+        assert np.array_equal(out["obs"].cpu().numpy()[..., :L].transpose(1, 0, 2, 3), z[k + "_obs"][:, :10])
+
+
+def test_reset_to_edge_cases_golden():
+    d = load("edge_cases.json")
+    by_n = {}
+    for case in d["cases"]:
+        if case.get("error", {}).get("type") == "AssertionError":
+            continue
+        by_n.setdefault((len(case["hands"]), case["include_summaries"]), []).append(case)
+    for (n, summ), cases in by_n.items():
+        B = len(cases)
+        board = np.full((B, 4, 6), -1, dtype=np.int8)
+        hands = np.full((B, n, 10), -1, dtype=np.int8)
+        acts = np.zeros((B, n), dtype=np.int32)
+        for g, c in enumerate(cases):
+            for r, row in enumerate(c["board"]):
+                board[g, r, : len(row)] = row
+            for p, h in enumerate(c["hands"]):
+                hands[g, p, : len(h)] = h
+            acts[g] = c["actions"]
+        env = venv(B, n, seed=0, rng="philox", include_summaries=summ)
+        env.reset_to(board, hands)
+        L = O.obs_len(summ)
+        obs0 = env.obs(torch.int64).cpu().numpy()
+        rew, done, inv = env.step(torch.from_numpy(acts))
+        obs1 = env.obs(torch.int64).cpu().numpy()
+        b1, h1, s1 = env.board().cpu().numpy(), env.hands().cpu().numpy(), env.scores().cpu().numpy()
+        rew, done, inv = rew.cpu().numpy(), done.cpu().numpy(), inv.cpu().numpy()
+        for g, c in enumerate(cases):
+            # hands are card sets on the device: reset_to with an unsorted hand
+            # list yields the sorted legal list (the reference's own callers
+            # always pass sorted hands, env.py:108 and mcts.py:118-125)
+            canon = lambda o: [sorted(x for x in row[:10] if x >= 0) + [-1] * sum(1 for x in row[:10] if x < 0) + row[10:] for row in o]
+            assert obs0[g, :, :L].tolist() == canon(c["obs0"]), c["label"]
+            if "error" in c:
+                assert inv[g] >= 0, c["label"]
+                assert c["error"]["message"].startswith(f"Player {inv[g] + 1} tried")
+                continue
+            e = c["expect"]
+            assert inv[g] == -1, c["label"]
+            assert rew[g].tolist() == e["rewards"], c["label"]
+            assert bool(done[g]) == e["done"]
+            assert [[x for x in row if x >= 0] for row in b1[g].tolist()] == e["board"], c["label"]
+            assert [[x for x in h if x >= 0] for h in h1[g].tolist()] == [sorted(h) for h in e["hands"]]
+            assert s1[g].tolist() == e["scores"]
+            assert obs1[g, :, :L].tolist() == canon(e["obs"]), c["label"]
+
+
+def test_notebook_games_through_step_api():
+    d = load("notebook_games.json")
+    games = d["games"]
+    B = len(games)
+    board = np.full((B, 4, 6), -1, dtype=np.int8)
+    hands = np.full((B, 2, 10), -1, dtype=np.int8)
+    for g, G in enumerate(games):
+        for r, row in enumerate(G["board"]):
+            board[g, r, : len(row)] = row
+        for p, h in enumerate(G["hands"]):
+            hands[g, p, : len(h)] = h
+    env = venv(B, 2, seed=0, rng="philox")
+    env.reset_to(board, hands)
+    for t in range(10):
+        acts = torch.tensor([G["actions"][t] for G in games], dtype=torch.int32)
+        rew, done, inv = env.step(acts)
+        obs = env.obs(torch.int64).cpu().numpy()
+        for g, G in enumerate(games):
+            assert inv[g].item() == -1
+            assert rew[g].tolist() == G["steps"][t]["rewards"]
+            assert obs[g].tolist() == G["steps"][t]["obs"]
+            assert bool(done[g]) == G["steps"][t]["done"]
+    assert (-env.scores().cpu().numpy()).tolist() == [G["final_scores"] for G in games]
+
+
+@pytest.mark.parametrize("rng", ["numpy", "philox"])
+def test_step_api_external_actions_vs_oracle(rng):
+    B, N = 3000, 4
+    env = venv(B, N, seed=77, rng=rng)
+    env.reset()
+    ref = O.VecOracle(B, N, rng_mode=RNG[rng], seed=77)
+    ref.reset()
+    gen = np.random.RandomState(5)
+    for t in range(25):
+        h = env.hands().cpu().numpy()
+        n = (h[:, 0] >= 0).sum(axis=1)
+        pick = (gen.rand(B, N) * n[:, None]).astype(np.int64)
+        acts = np.take_along_axis(h, pick[..., None], axis=2)[..., 0].astype(np.int32)
+        bad = gen.rand(B) < 0.02  # sprinkle illegal moves
+        acts[bad, 1] = 103 - acts[bad, 1]
+        rew, done, inv = env.step(torch.from_numpy(acts), auto_reset=True)
+        r_rew, r_done, r_inv = ref.step(acts, auto_reset=True)
+        assert np.array_equal(inv.cpu().numpy(), r_inv)
+        assert np.array_equal(rew.cpu().numpy(), r_rew)
+        assert np.array_equal(done.cpu().numpy().astype(np.uint8), r_done)
+        assert np.array_equal(env.obs().cpu().numpy(), ref.obs())
+
+
+def test_numpy_rng_bridge_roundtrip():
+    env = venv(2, 4, seed=0, rng="numpy")
+    env.reset()
+    env.rollout(7)
+    key, pos = env.get_mt_state(1)
+    rs = np.random.RandomState(1)
+    gs = O.VecOracle(2, 4, rng_mode=O.RNG_NUMPY_MT, seed=0)
+    gs.reset()
+    gs.rollout(7)
+    # the exported state must continue the stream exactly like numpy
+    rs.set_state(("MT19937", key, pos, 0, 0.0))
+    nxt = rs.randint(0, 2**32, size=1000, dtype=np.uint64)
+    r = gs.v.contents.rngs[1]
+    ora = O.Rng.__new__(O.Rng)
+    ora.s = r
+    assert [int(x) for x in nxt] == [ora.next() for _ in range(1000)]
+    # import a numpy state and draw on the device
+    rs = np.random.RandomState(99)
+    rs.randint(0, 10, size=37)
+    st = rs.get_state()
+    env.set_mt_state(st[1], st[2], game=0)
+    env.reset()
+    deck = np.arange(104)
+    rs.shuffle(deck)
+    b = env.board().cpu().numpy()[0]
+    assert [int(x) for x in b[:, 0]] == [int(deck[103 - r]) for r in range(4)]
+    k2, p2 = env.get_mt_state(0)
+    assert np.array_equal(k2, rs.get_state()[1]) and p2 == rs.get_state()[2]
