@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""Benchmark: env-steps/s at 65 536 concurrent 4-player games per MI355X.
+
+Driver contract: `python bench.py --gpus N --steps K --warmup W` (N>1 under
+torch.distributed.run, one rank per GPU).  Prints ONE JSON line on rank 0.
+
+Workload (BASELINE.json configs[1]): per GPU,
+B = 65 536 independent 4-player games of DrunkHamster self-play in
+numpy-compat RNG mode (game g replays np.random.seed(g) +
+GameSession(DrunkHamster() x 4) of the reference, episode after episode).
+One bench step = one launch of the fused rollout kernel that advances every
+game by one full episode (10 env-steps: policy draw, simultaneous-play
+resolution, scoring, per-seat int8 observation, auto-reset deal) and writes
+the whole trajectory (obs, actions, rewards, done) to HBM.  Inputs are
+resident on the device before timing starts.
+
+Multi-GPU: game shards are independent (rank r owns global games
+[r*B, (r+1)*B), streams keyed by the global id), so there is no collective
+on the data path; one RCCL all_reduce of the per-rank score sums after the
+timed loop is the "tournament score gather" (SURVEY.md §8(e)).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "rl-6-nimmt_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+N_PLAYERS = 4
+STEPS_PER_LAUNCH = 10
+# algorithmic bytes per env-step at N players = 33N + 57
+# (state round trip: hands 10N, board 24, lens 4, scores 4N, actions N read;
+# hands, board, lens, scores, rewards 4N, done 1 written) + 47N for the int8
+# observation the step emits.
+ALGO_BYTES_PER_STEP = (33 * N_PLAYERS + 57) + 47 * N_PLAYERS  # 377 B at N = 4
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100, help="timed launches (episodes)")
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--games", type=int, default=65536, help="games per GPU")
+    ap.add_argument("--rng", default="numpy", choices=["numpy", "philox"])
+    ap.add_argument("--no-obs", action="store_true", help="do not emit observations (not the headline)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--extras", action="store_true", help="also time the philox mode and the per-step API")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def time_rollouts(env, out, steps, warmup, world):
+    """Warm up, then time exactly `steps` launches between barrier+sync on
+    both sides.  Returns (wall seconds, mean per-launch kernel ms measured
+    with HIP events on the launch stream)."""
+    for _ in range(warmup):
+        env.rollout(STEPS_PER_LAUNCH, out=out)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record()
+        env.rollout(STEPS_PER_LAUNCH, out=out)
+        ev[i][1].record()
+    torch.cuda.synchronize()
+    barrier(world)
+    t1 = time.perf_counter()
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    return t1 - t0, kern_ms
+
+
+def make_out(env, games, with_obs):
+    T, B, N = STEPS_PER_LAUNCH, games, N_PLAYERS
+    dev = env.device
+    out = {
+        "rewards": torch.empty((T, B, N), dtype=torch.int32, device=dev),
+        "done": torch.empty((T, B), dtype=torch.uint8, device=dev),
+        "actions": torch.empty((T, B, N), dtype=torch.uint8, device=dev),
+    }
+    if with_obs:
+        out["obs"] = torch.empty((T, B, N, 48), dtype=torch.int8, device=dev)
+    return out
+
+
+def cpu_baseline(budget_s, rng):
+    """The oracle's C restatement of env.py + DrunkHamster (oracle/, kind
+    "port"), single thread, on a bounded sample of the same workload."""
+    from oracle import oracle as O
+
+    mode = O.RNG_NUMPY_MT if rng == "numpy" else O.RNG_PHILOX
+    # calibrate on a small batch, then size the sample to ~budget_s seconds
+    B = 2048
+    v = O.VecOracle(B, N_PLAYERS, rng_mode=mode, seed=0)
+    v.reset()
+    t = time.perf_counter()
+    v.rollout(STEPS_PER_LAUNCH, want_obs=True, want_actions=True, nthreads=1)
+    dt = time.perf_counter() - t
+    per_game_ep = dt / B
+    games = int(max(256, min(65536, budget_s / max(per_game_ep, 1e-9) / 2)))
+    episodes = max(1, int(budget_s / (per_game_ep * games)))
+    v = O.VecOracle(games, N_PLAYERS, rng_mode=mode, seed=0)
+    v.reset()
+    t = time.perf_counter()
+    for _ in range(episodes):
+        v.rollout(STEPS_PER_LAUNCH, want_obs=True, want_actions=True, nthreads=1)
+    dt = time.perf_counter() - t
+    steps = games * episodes * STEPS_PER_LAUNCH
+    return {
+        "value": steps / dt,
+        "unit": "env-steps/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{games} games x {episodes} episodes x 10 env-steps ({steps} env-steps, {dt:.1f} s) of the same "
+                  f"workload (DrunkHamster self-play, {rng} RNG, int8 obs + actions + rewards written) on the "
+                  f"oracle's single-threaded C restatement of env.py",
+    }
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    from rl_6_nimmt.vec_env import VecSechsNimmtEnv
+
+    B = args.games
+    env = VecSechsNimmtEnv(B, N_PLAYERS, seed=0, game_offset=rank * B, rng=args.rng)
+    env.reset()
+    out = make_out(env, B, not args.no_obs)
+    wall, kern_ms = time_rollouts(env, out, args.steps, args.warmup, world)
+
+    # tournament score gather over RCCL (outside the timed region)
+    sums, eps = env.results()
+    tot = sums.to(torch.float64).sum(dim=0)
+    if world > 1:
+        import torch.distributed as dist
+
+        walls = torch.tensor([wall], dtype=torch.float64, device=env.device)
+        dist.all_reduce(walls, op=dist.ReduceOp.MAX)
+        wall = float(walls.item())
+        kms = torch.tensor([kern_ms], dtype=torch.float64, device=env.device)
+        dist.all_reduce(kms, op=dist.ReduceOp.MAX)
+        kern_ms = float(kms.item())
+        dist.all_reduce(tot)
+
+    total_steps = world * B * STEPS_PER_LAUNCH * args.steps
+    value = total_steps / wall
+    launch_steps = B * STEPS_PER_LAUNCH
+    achieved = launch_steps * ALGO_BYTES_PER_STEP / (kern_ms * 1e-3) / 1e9
+    result = {
+        "metric": "env-steps/sec at 65536 concurrent 4-player games, 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded deals: game g = np.random.seed(g) stream)",
+        "config": {
+            "workload": "config2: 65536 x 4-player DrunkHamster self-play per GPU, one episode (10 env-steps) per "
+                        "launch, numpy-MT RNG, int8 obs + actions + rewards + done emitted",
+            "games_per_gpu": B,
+            "players": N_PLAYERS,
+            "env_steps_per_launch": launch_steps,
+            "rng": args.rng,
+            "obs": not args.no_obs,
+            "parallelism": f"dp{world} (independent game shards, no data-path collective)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "kernel": "k_play<4, RNG_NUMPY_MT>",
+            "kernel_ms": kern_ms,
+            "algo_bytes_per_env_step": ALGO_BYTES_PER_STEP,
+        },
+        "episodes_checksum": {"episodes": int(eps.sum().item()) * world, "mean_score_per_seat": (tot / (eps.sum().item() * world)).tolist()},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.rng)
+    if args.extras and world == 1:
+        env2 = VecSechsNimmtEnv(B, N_PLAYERS, seed=0, rng="philox")
+        env2.reset()
+        w2, k2 = time_rollouts(env2, out, args.steps, args.warmup, world)
+        result["extra_philox"] = {"value": B * STEPS_PER_LAUNCH * args.steps / w2, "kernel_ms": k2}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
