@@ -1,21 +1,26 @@
 // sechs_device.h -- per-lane 6 nimmt! game engine for gfx950 (CDNA4).
 //
-// One lane = one game.  Everything a step touches lives in VGPRs:
-//   * a hand is a 128-bit card set (4 x u32), so the reference's sorted
-//     `legal_actions` list (env.py:209) is the set bits in ascending order,
-//     `card in hand` (env.py:117) is a bit test and `hands[p].remove(card)`
-//     (env.py:131) is a bit clear;
-//   * a row is two u32: `lo` = cards 0..3 (bytes), `hi` = card 4 | len << 8 |
-//     heads << 16 | end << 24, where heads = bull heads of the whole row
-//     (env.py:214-218 with include_last=True) and end = the last card
-//     (env.py:140).  Bytes past `len` are kept zero.
-// Rules restated from env.py:120-172.  The
-// kernels never call the oracle; they are checked against it in tests/.
+// One lane = one game; everything a step touches lives in VGPRs:
+//   * a hand is the reference's sorted `legal_actions` list (env.py:209)
+//     as 12 bytes {u64 lo = cards 0..7, u32 hi = cards 8..11}, ascending,
+//     padded with 0xFF.  DrunkHamster's `legal[k]` (agents/random.py:9) is
+//     a byte extract, `hands[p].remove(card)` (env.py:131) a byte delete,
+//     and the observation's hand field (env.py:210) is the bytes as stored.
+//   * the board is two 4-vectors: lo[r] = cards 0..3 of row r (bytes),
+//     hi[r] = card4 | len << 8 | heads << 16 | end << 24, heads = bull heads
+//     of the whole row (env.py:214-218, include_last=True), end = last card
+//     (env.py:140).  Bytes past `len` are zero.
+// Rules restated from env.py:120-172.  Small arrays
+// that are indexed with run-time values are vector types on purpose: LLVM
+// keeps those in registers, whereas plain arrays indexed that way end up in
+// scratch memory.  The kernels never call the oracle; tests/ compare them.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace sechs {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kRows = 4;
 constexpr int kThreshold = 6;
@@ -41,154 +46,177 @@ __device__ __forceinline__ uint32_t heads_of(uint32_t c) {
 }
 
 // --------------------------------------------------------------------------
-// 128-bit card sets
+// 128-bit card sets (deal construction, card memory)
+// --------------------------------------------------------------------------
+__device__ __forceinline__ u32x4 set_bit(u32x4 s, uint32_t c) {
+    const uint32_t bit = 1u << (c & 31u), q = c >> 5;
+    s.x |= (q == 0u) ? bit : 0u;
+    s.y |= (q == 1u) ? bit : 0u;
+    s.z |= (q == 2u) ? bit : 0u;
+    s.w |= (q == 3u) ? bit : 0u;
+    return s;
+}
+
+__device__ __forceinline__ bool has_bit(u32x4 s, uint32_t c) {
+    const uint32_t q = c >> 5, sh = c & 31u;
+    const uint32_t w = (q == 0u) ? s.x : (q == 1u) ? s.y : (q == 2u) ? s.z : s.w;
+    return (w >> sh) & 1u;
+}
+
+__device__ __forceinline__ uint32_t set_count(u32x4 s) { return __popc(s.x) + __popc(s.y) + __popc(s.z) + __popc(s.w); }
+
+// --------------------------------------------------------------------------
+// sorted hands as byte lists
 // --------------------------------------------------------------------------
 struct Hand {
-    uint32_t w[4];
+    uint64_t lo;  // cards 0..7
+    uint32_t hi;  // cards 8..9, bytes 10..11 = 0xFF
 };
 
-__device__ __forceinline__ void hand_clear(Hand& h) { h.w[0] = h.w[1] = h.w[2] = h.w[3] = 0u; }
+// legal_actions[k]
+__device__ __forceinline__ uint32_t hand_get(const Hand& h, uint32_t k) {
+    const uint32_t a = (uint32_t)(h.lo >> ((8u * k) & 63u));
+    const uint32_t b = h.hi >> ((8u * (k - 8u)) & 31u);
+    return (k < 8u ? a : b) & 0xFFu;
+}
 
-__device__ __forceinline__ void hand_add(Hand& h, uint32_t c) {
-    uint32_t bit = 1u << (c & 31u), q = c >> 5;
+// hands[p].remove(legal_actions[k])
+__device__ __forceinline__ void hand_del(Hand& h, uint32_t k) {
+    const uint64_t m = (k < 8u) ? ((1ull << (8u * k)) - 1ull) : ~0ull;
+    const uint64_t lo_del = (h.lo & m) | ((h.lo >> 8) & ~m) | ((uint64_t)(h.hi & 0xFFu) << 56);
+    const uint32_t m2 = (k < 8u) ? 0u : ((k >= 12u) ? ~0u : ((1u << (8u * (k - 8u))) - 1u));
+    const uint32_t hi_del = (h.hi & m2) | ((h.hi >> 8) & ~m2) | 0xFF000000u;
+    h.lo = (k < 8u) ? lo_del : h.lo;
+    h.hi = hi_del;
+}
+
+// index of card c in the hand, or -1 (SWAR zero-byte search; the lowest
+// flagged byte of the classic test is exact)
+__device__ __forceinline__ int hand_find(const Hand& h, uint32_t c) {
+    if (c > 0xFEu) return -1;
+    const uint64_t x = h.lo ^ (0x0101010101010101ull * (uint64_t)c);
+    const uint64_t z = (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;
+    const uint32_t y = h.hi ^ (0x01010101u * c);
+    const uint32_t zy = (y - 0x01010101u) & ~y & 0x80808080u;
+    if (z) return (int)(__builtin_ctzll(z) >> 3);
+    if (zy) return 8 + (int)(__builtin_ctz(zy) >> 3);
+    return -1;
+}
+
+// number of cards (first 0xFF byte)
+__device__ __forceinline__ uint32_t hand_len(const Hand& h) {
+    const uint64_t x = ~h.lo;  // 0xFF bytes -> zero bytes
+    const uint64_t z = (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;
+    const uint32_t y = ~h.hi;
+    const uint32_t zy = (y - 0x01010101u) & ~y & 0x80808080u;
+    return z ? (uint32_t)(__builtin_ctzll(z) >> 3) : 8u + (uint32_t)(__builtin_ctz(zy | 0x80000000u) >> 3);
+}
+
+// sorted byte list from a card set of at most 10 cards
+__device__ __forceinline__ Hand hand_from_set(u32x4 s) {
+    Hand h;
+    h.lo = ~0ull;
+    h.hi = ~0u;
+    uint32_t w0 = s.x, w1 = s.y, w2 = s.z, w3 = s.w;
 #pragma unroll
-    for (int i = 0; i < 4; i++) h.w[i] |= (q == (uint32_t)i) ? bit : 0u;
-}
-
-__device__ __forceinline__ void hand_remove(Hand& h, uint32_t c) {
-    uint32_t bit = 1u << (c & 31u), q = c >> 5;
-#pragma unroll
-    for (int i = 0; i < 4; i++) h.w[i] &= (q == (uint32_t)i) ? ~bit : 0xFFFFFFFFu;
-}
-
-__device__ __forceinline__ bool hand_has(const Hand& h, uint32_t c) {
-    uint32_t q = c >> 5;
-    uint32_t w = h.w[0];
-    w = (q == 1u) ? h.w[1] : w;
-    w = (q == 2u) ? h.w[2] : w;
-    w = (q == 3u) ? h.w[3] : w;
-    return (c < 128u) && ((w >> (c & 31u)) & 1u);
-}
-
-__device__ __forceinline__ uint32_t hand_count(const Hand& h) {
-    return __popc(h.w[0]) + __popc(h.w[1]) + __popc(h.w[2]) + __popc(h.w[3]);
-}
-
-// position of the k-th (0-based) set bit of a 32-bit word (must exist)
-__device__ __forceinline__ uint32_t select32(uint32_t w, uint32_t k) {
-    uint32_t pos = 0, c;
-    c = __popc(w & 0xFFFFu);
-    if (k >= c) { k -= c; pos += 16; w >>= 16; }
-    c = __popc(w & 0xFFu);
-    if (k >= c) { k -= c; pos += 8; w >>= 8; }
-    c = __popc(w & 0xFu);
-    if (k >= c) { k -= c; pos += 4; w >>= 4; }
-    c = __popc(w & 0x3u);
-    if (k >= c) { k -= c; pos += 2; w >>= 2; }
-    c = w & 1u;
-    if (k >= c) pos += 1;
-    return pos;
-}
-
-// k-th smallest card of the hand == legal_actions[k]
-__device__ __forceinline__ uint32_t hand_select(const Hand& h, uint32_t k) {
-    uint32_t c0 = __popc(h.w[0]), c1 = __popc(h.w[1]), c2 = __popc(h.w[2]);
-    uint32_t w = h.w[0], base = 0;
-    if (k >= c0) { k -= c0; w = h.w[1]; base = 32;
-        if (k >= c1) { k -= c1; w = h.w[2]; base = 64;
-            if (k >= c2) { k -= c2; w = h.w[3]; base = 96; } } }
-    return base + select32(w, k);
-}
-
-// smallest card, and remove it (hand must be non-empty)
-__device__ __forceinline__ uint32_t hand_pop_min(Hand& h) {
-    uint32_t c;
-    if (h.w[0]) { c = __builtin_ctz(h.w[0]); h.w[0] &= h.w[0] - 1u; }
-    else if (h.w[1]) { c = 32 + __builtin_ctz(h.w[1]); h.w[1] &= h.w[1] - 1u; }
-    else if (h.w[2]) { c = 64 + __builtin_ctz(h.w[2]); h.w[2] &= h.w[2] - 1u; }
-    else { c = 96 + __builtin_ctz(h.w[3]); h.w[3] &= h.w[3] - 1u; }
-    return c;
+    for (int k = 0; k < kHand; k++) {
+        uint32_t c;
+        if (w0) { c = __builtin_ctz(w0); w0 &= w0 - 1u; }
+        else if (w1) { c = 32u + __builtin_ctz(w1); w1 &= w1 - 1u; }
+        else if (w2) { c = 64u + __builtin_ctz(w2); w2 &= w2 - 1u; }
+        else if (w3) { c = 96u + __builtin_ctz(w3); w3 &= w3 - 1u; }
+        else c = 0xFFu;
+        if (k < 8) h.lo = (h.lo & ~(0xFFull << (8 * k))) | ((uint64_t)c << (8 * k));
+        else h.hi = (h.hi & ~(0xFFu << (8 * (k - 8)))) | (c << (8 * (k - 8)));
+    }
+    return h;
 }
 
 // --------------------------------------------------------------------------
 // board rows
 // --------------------------------------------------------------------------
 struct Board {
-    uint32_t lo[kRows];  // cards 0..3 of each row
-    uint32_t hi[kRows];  // card4 | len << 8 | heads << 16 | end << 24
+    u32x4 lo;  // cards 0..3 of each row
+    u32x4 hi;  // card4 | len << 8 | heads << 16 | end << 24
 };
 
-__device__ __forceinline__ uint32_t row_len(const Board& b, int r) { return (b.hi[r] >> 8) & 0xFFu; }
-__device__ __forceinline__ uint32_t row_heads(const Board& b, int r) { return (b.hi[r] >> 16) & 0xFFu; }
-__device__ __forceinline__ uint32_t row_end(const Board& b, int r) { return b.hi[r] >> 24; }
+__device__ __forceinline__ uint32_t meta_row(uint32_t c) { return (1u << 8) | (heads_of(c) << 16) | (c << 24); }
+__device__ __forceinline__ uint32_t len_of(uint32_t hi) { return (hi >> 8) & 0xFFu; }
+__device__ __forceinline__ uint32_t heads_in(uint32_t hi) { return (hi >> 16) & 0xFFu; }
+__device__ __forceinline__ uint32_t end_of(uint32_t hi) { return hi >> 24; }
 
-__device__ __forceinline__ void row_start(Board& b, int r, uint32_t c) {
-    b.lo[r] = c;
-    b.hi[r] = (1u << 8) | (heads_of(c) << 16) | (c << 24);
+// card i (0..4) of a row given its two words
+__device__ __forceinline__ uint32_t card_at(uint32_t lo, uint32_t hi, int i) {
+    return i < 4 ? (lo >> (8 * i)) & 0xFFu : hi & 0xFFu;
 }
 
-// card of row r at position i (i < len)
-__device__ __forceinline__ uint32_t row_card(const Board& b, int r, int i) {
-    return i < 4 ? (b.lo[r] >> (8 * i)) & 0xFFu : b.hi[r] & 0xFFu;
+// place card c on the board (env.py:127-134 for one card); returns the
+// bull heads its player takes
+__device__ __forceinline__ uint32_t place_card(Board& b, uint32_t c) {
+    const uint32_t h[4] = {b.hi.x, b.hi.y, b.hi.z, b.hi.w};
+    // _find_row: the row whose last card is the largest one below c
+    int best = -1;
+    uint32_t best_end = 0u;
+#pragma unroll
+    for (int r = 0; r < kRows; r++) {
+        const uint32_t e = end_of(h[r]);
+        const bool ok = (e < c) && (best < 0 || e > best_end);
+        best = ok ? r : best;
+        best_end = ok ? e : best_end;
+    }
+    // undercut: _pick_row_to_replace = np.argmin(row values), first minimum
+    int minr = 0;
+    uint32_t minh = heads_in(h[0]);
+#pragma unroll
+    for (int r = 1; r < kRows; r++) {
+        const uint32_t v = heads_in(h[r]);
+        const bool lt = v < minh;
+        minr = lt ? r : minr;
+        minh = lt ? v : minh;
+    }
+    const bool under = best < 0;
+    const int tr = under ? minr : best;
+    const uint32_t hc = heads_of(c);
+    const uint32_t lo_t = (tr == 0) ? b.lo.x : (tr == 1) ? b.lo.y : (tr == 2) ? b.lo.z : b.lo.w;
+    const uint32_t hi_t = (tr == 0) ? h[0] : (tr == 1) ? h[1] : (tr == 2) ? h[2] : h[3];
+    const uint32_t len = len_of(hi_t);
+    const bool take = under || len == (uint32_t)(kThreshold - 1);  // 6th card, env.py:133
+    const uint32_t penalty = take ? heads_in(hi_t) : 0u;           // _score_row: the whole old row
+    const uint32_t lo_new = take ? c : (lo_t | (len < 4u ? (c << (8u * len)) : 0u));
+    const uint32_t hi_new = take ? ((1u << 8) | (hc << 16) | (c << 24))
+                                 : ((len == 4u ? c : (hi_t & 0xFFu)) | ((len + 1u) << 8) |
+                                    ((heads_in(hi_t) + hc) << 16) | (c << 24));
+    b.lo.x = (tr == 0) ? lo_new : b.lo.x;
+    b.lo.y = (tr == 1) ? lo_new : b.lo.y;
+    b.lo.z = (tr == 2) ? lo_new : b.lo.z;
+    b.lo.w = (tr == 3) ? lo_new : b.lo.w;
+    b.hi.x = (tr == 0) ? hi_new : b.hi.x;
+    b.hi.y = (tr == 1) ? hi_new : b.hi.y;
+    b.hi.z = (tr == 2) ? hi_new : b.hi.z;
+    b.hi.w = (tr == 3) ? hi_new : b.hi.w;
+    return penalty;
 }
 
-// --------------------------------------------------------------------------
-// simultaneous play resolution, env.py:120-172.  card[p] must be legal.
-// pen[p] receives the bull heads seat p takes (reward = -pen).
-// --------------------------------------------------------------------------
+// simultaneous play, env.py:120-136: cards in ascending order, each placed
+// in turn.  card[p] must be legal.  pen[p] = bull heads seat p takes.
 template <int N>
 __device__ __forceinline__ void resolve(Board& b, const uint32_t (&card)[N], uint32_t (&pen)[N]) {
-    // (card, player) ascending by card (env.py:124-125); cards are distinct
     uint32_t key[N];
 #pragma unroll
-    for (int p = 0; p < N; p++) { key[p] = (card[p] << 4) | (uint32_t)p; pen[p] = 0u; }
+    for (int p = 0; p < N; p++) key[p] = (card[p] << 4) | (uint32_t)p;
 #pragma unroll
     for (int i = 0; i < N; i++)
 #pragma unroll
         for (int j = 0; j + 1 < N - i; j++) {
-            uint32_t lo = min(key[j], key[j + 1]), hi = max(key[j], key[j + 1]);
+            const uint32_t lo = min(key[j], key[j + 1]), hi = max(key[j], key[j + 1]);
             key[j] = lo, key[j + 1] = hi;
         }
 #pragma unroll
+    for (int p = 0; p < N; p++) pen[p] = 0u;
+#pragma unroll
     for (int k = 0; k < N; k++) {
-        const uint32_t c = key[k] >> 4, p = key[k] & 15u;
-        // _find_row: the row whose last card is the largest one below c
-        int best = -1;
-        uint32_t best_end = 0u;
-#pragma unroll
-        for (int r = 0; r < kRows; r++) {
-            uint32_t e = row_end(b, r);
-            bool ok = (e < c) && (best < 0 || e > best_end);
-            best = ok ? r : best;
-            best_end = ok ? e : best_end;
-        }
-        // undercut: _pick_row_to_replace = argmin row value, first minimum
-        int minr = 0;
-        uint32_t minh = row_heads(b, 0);
-#pragma unroll
-        for (int r = 1; r < kRows; r++) {
-            uint32_t h = row_heads(b, r);
-            bool lt = h < minh;
-            minr = lt ? r : minr;
-            minh = lt ? h : minh;
-        }
-        const bool under = best < 0;
-        const int tr = under ? minr : best;
-        const uint32_t hc = heads_of(c);
-        uint32_t penalty = 0u;
-#pragma unroll
-        for (int r = 0; r < kRows; r++) {
-            if (r == tr) {
-                const uint32_t len = row_len(b, r);
-                const bool take = under || len == (uint32_t)(kThreshold - 1);
-                penalty = take ? row_heads(b, r) : 0u;  // _score_row: whole old row
-                uint32_t lo_app = b.lo[r] | (len < 4u ? (c << (8u * len)) : 0u);
-                uint32_t hi_app = (len == 4u ? c : (b.hi[r] & 0xFFu)) | ((len + 1u) << 8) |
-                                  ((row_heads(b, r) + hc) << 16) | (c << 24);
-                b.lo[r] = take ? c : lo_app;
-                b.hi[r] = take ? ((1u << 8) | (hc << 16) | (c << 24)) : hi_app;
-            }
-        }
+        const uint32_t penalty = place_card(b, key[k] >> 4);
+        const uint32_t p = key[k] & 15u;
 #pragma unroll
         for (int q = 0; q < N; q++) pen[q] += (p == (uint32_t)q) ? penalty : 0u;
     }
@@ -198,6 +226,93 @@ __device__ __forceinline__ void resolve(Board& b, const uint32_t (&card)[N], uin
 // Random word sources.  Both feed numpy's legacy masked-rejection
 // random_interval; only the 32-bit word stream differs.
 // --------------------------------------------------------------------------
+// --------------------------------------------------------------------------
+// Word buffer.  Every random_interval on this path has max <= 127 (cards
+// and hand indices) and numpy masks the whole 32-bit word, so only the low
+// byte of each word decides anything: the buffer keeps the low bytes of the
+// next `cnt` (<= 32) words of the game's stream, byte 0 = next word.
+// --------------------------------------------------------------------------
+struct ByteBuf {
+    uint64_t b0, b1, b2, b3;
+    uint32_t cnt;
+
+    __device__ __forceinline__ void clear() { b0 = b1 = b2 = b3 = 0ull, cnt = 0u; }
+
+    // append k (1..8) bytes, requires cnt + k <= 32
+    __device__ __forceinline__ void append(uint64_t bytes, uint32_t k) {
+        bytes &= (k >= 8u) ? ~0ull : ((1ull << (8u * k)) - 1ull);
+        const uint32_t bit = 8u * cnt, q = bit >> 6, off = bit & 63u;
+        const uint64_t lo = bytes << off;
+        const uint64_t hi = off ? (bytes >> (64u - off)) : 0ull;
+        b0 |= (q == 0u) ? lo : 0ull;
+        b1 |= (q == 1u) ? lo : (q == 0u) ? hi : 0ull;
+        b2 |= (q == 2u) ? lo : (q == 1u) ? hi : 0ull;
+        b3 |= (q == 3u) ? lo : (q == 2u) ? hi : 0ull;
+        cnt += k;
+    }
+    // drop the next k (0..8) bytes
+    __device__ __forceinline__ void drop(uint32_t k) {
+        const uint32_t s = 8u * k;
+        if (s >= 64u) {
+            b0 = b1, b1 = b2, b2 = b3, b3 = 0ull;
+        } else if (s) {
+            b0 = (b0 >> s) | (b1 << (64u - s));
+            b1 = (b1 >> s) | (b2 << (64u - s));
+            b2 = (b2 >> s) | (b3 << (64u - s));
+            b3 = b3 >> s;
+        }
+        cnt -= k;
+    }
+};
+
+// numpy legacy random_interval(max), 1 <= max <= 127, on the buffered low
+// bytes: the first of the next (up to) 8 words whose masked value is <= max
+// is found with one SWAR compare, so a wave almost never loops.
+// G::gen(buf) appends the next words of the stream (returns false if it
+// cannot right now, see MtGen).
+__device__ __forceinline__ uint64_t swar_le_mask(uint64_t x, uint32_t max) {
+    // bit 7 of byte k set iff byte k of x (<= 127) is <= max (<= 127): no
+    // byte borrows because (max | 0x80) - x_k lies in [1, 255]
+    return ((0x0101010101010101ull * (uint64_t)(max | 0x80u)) - x) & 0x8080808080808080ull;
+}
+
+template <class G>
+__device__ __forceinline__ uint32_t rng_interval(G& gen, ByteBuf& buf, uint32_t max) {
+    if (max == 0u) return 0u;
+    // wave-uniform top-up: all lanes with room refill together
+    if (__any(buf.cnt < 8u)) gen.topup(buf);
+    const uint32_t mask = 0xFFFFFFFFu >> __builtin_clz(max);
+    const uint64_t mbytes = 0x0101010101010101ull * (uint64_t)mask;
+    while (true) {
+        if (buf.cnt == 0u) gen.force(buf);
+        const uint32_t valid = min(buf.cnt, 8u);
+        const uint64_t vmask = (valid >= 8u) ? ~0ull : ((1ull << (8u * valid)) - 1ull);
+        const uint64_t x = buf.b0 & mbytes;
+        const uint64_t t = swar_le_mask(x, max) & vmask;
+        if (t) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(t) >> 3;
+            const uint32_t v = (uint32_t)(x >> (8u * k)) & 0xFFu;
+            buf.drop(k + 1u);
+            return v;
+        }
+        buf.drop(valid);
+    }
+}
+
+// ---- numpy legacy MT19937, twisted lazily 8 words at a time ---------------
+// State code (mt_pos[g]): bits 0..10 pos, 16..21 cnt, bit 31 direct.
+//  lazy (bit 31 = 0): words [0,pos) of the game's 624 hold this round's
+//    values, [pos,624) the previous round's (numpy's in-place twist order,
+//    done 8 words at a time as draws need them).
+//  direct (bit 31 = 1): the array is one whole twisted round as
+//    np.random.get_state() returns it; pos = next word to hand out.
+//  cnt = words just before pos that were generated but not consumed (the
+//    buffer).  A round boundary is only crossed with an empty buffer, so
+//    [pos-cnt, pos) never straddles rounds and the state always converts
+//    back to numpy's (key, pos) form.
+// np.random.seed(s) == init_genrand(s) with code 0.
+constexpr uint32_t kMtDirect = 0x80000000u;
+
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     y ^= y >> 11;
     y ^= (y << 7) & 0x9d2c5680u;
@@ -206,78 +321,139 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     return y;
 }
 
-// numpy legacy MT19937 with the twist done lazily, one word per draw, in
-// place.  pos < 624: "lazy" -- words [0,pos) already hold this round's
-// values, [pos,624) the previous round's; pos >= 624: "direct" -- the
-// array is a fully twisted round (as np.random.get_state() returns it) and
-// pos-624 is the next word to hand out.
-struct MtRng {
-    uint32_t* st;  // this game's 624 words
-    uint32_t pos;
-    __device__ __forceinline__ uint32_t next() {
-        uint32_t v;
-        if (pos >= (uint32_t)kMtN) {
-            v = st[pos - kMtN];
-            pos = (pos + 1u == 2u * kMtN) ? 0u : pos + 1u;
-        } else {
-            const uint32_t i = pos;
-            const uint32_t i1 = (i == kMtN - 1) ? 0u : i + 1u;
-            const uint32_t im = (i < (uint32_t)(kMtN - kMtM)) ? i + kMtM : i - (kMtN - kMtM);
-            const uint32_t a = st[i], b = st[i1], c = st[im];
-            const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
-            v = c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-            st[i] = v;
-            pos = i1;
-        }
-        return mt_temper(v);
+__device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c) {
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
+struct MtGen {
+    uint32_t* st;
+    uint32_t pos, direct;
+
+    __device__ __forceinline__ void load(uint32_t* state, uint32_t code, ByteBuf& buf) {
+        st = state;
+        pos = code & 0x7FFu;
+        direct = code >> 31;
+        const uint32_t cnt = (code >> 16) & 0x3Fu;
+        buf.clear();
+        for (uint32_t k = 0; k < cnt; k++) buf.append(mt_temper(st[pos - cnt + k]) & 0xFFu, 1u);
     }
+    __device__ __forceinline__ uint32_t save(const ByteBuf& buf) const {
+        return pos | (buf.cnt << 16) | (direct << 31);
+    }
+    // one batch of words; false if the round boundary needs an empty buffer
+    __device__ __forceinline__ bool gen(ByteBuf& buf) {
+        if (direct) {
+            if (pos < (uint32_t)kMtN) {
+                const uint32_t k = min(8u, (uint32_t)kMtN - pos);
+                uint64_t bytes = 0ull;
+                for (uint32_t i = 0; i < k; i++) bytes |= (uint64_t)(mt_temper(st[pos + i]) & 0xFFu) << (8u * i);
+                buf.append(bytes, k);
+                pos += k;
+                return true;
+            }
+            if (buf.cnt) return false;
+            direct = 0u;  // round used up: twist lazily from here on
+            pos = 0u;
+        }
+        if (pos == (uint32_t)kMtN) {
+            if (buf.cnt) return false;
+            pos = 0u;
+        }
+        const uint32_t i = pos;  // multiple of 8
+        const u32x4 a0 = *(const u32x4*)(st + i);
+        const u32x4 a1 = *(const u32x4*)(st + i + 4);
+        const uint32_t a8 = st[(i + 8u == (uint32_t)kMtN) ? 0u : i + 8u];
+        uint32_t c[8];
+        if (i + 8u <= (uint32_t)(kMtN - kMtM) || i >= (uint32_t)(kMtN - kMtM)) {
+            // mt[j+397] (j < 227) or this round's mt[j-227]: one run of 8
+            // words starting at an index = 5 mod 8; read it as 3 aligned x4
+            const uint32_t base = (i < (uint32_t)(kMtN - kMtM)) ? i + kMtM - 1u : i - (uint32_t)(kMtN - kMtM) - 1u;
+            const u32x4 r0 = *(const u32x4*)(st + base);
+            const u32x4 r1 = *(const u32x4*)(st + base + 4);
+            const u32x4 r2 = *(const u32x4*)(st + base + 8);
+            c[0] = r0.y, c[1] = r0.z, c[2] = r0.w, c[3] = r1.x, c[4] = r1.y, c[5] = r1.z, c[6] = r1.w, c[7] = r2.x;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t j = i + (uint32_t)k;
+                c[k] = st[(j < (uint32_t)(kMtN - kMtM)) ? j + kMtM : j - (uint32_t)(kMtN - kMtM)];
+            }
+        }
+        u32x4 n0, n1;
+        n0.x = mt_mix(a0.x, a0.y, c[0]);
+        n0.y = mt_mix(a0.y, a0.z, c[1]);
+        n0.z = mt_mix(a0.z, a0.w, c[2]);
+        n0.w = mt_mix(a0.w, a1.x, c[3]);
+        n1.x = mt_mix(a1.x, a1.y, c[4]);
+        n1.y = mt_mix(a1.y, a1.z, c[5]);
+        n1.z = mt_mix(a1.z, a1.w, c[6]);
+        n1.w = mt_mix(a1.w, a8, c[7]);
+        *(u32x4*)(st + i) = n0;
+        *(u32x4*)(st + i + 4) = n1;
+        const uint64_t lo = (uint64_t)((mt_temper(n0.x) & 0xFFu) | ((mt_temper(n0.y) & 0xFFu) << 8) |
+                                       ((mt_temper(n0.z) & 0xFFu) << 16) | (mt_temper(n0.w) << 24));
+        const uint64_t hi = (uint64_t)((mt_temper(n1.x) & 0xFFu) | ((mt_temper(n1.y) & 0xFFu) << 8) |
+                                       ((mt_temper(n1.z) & 0xFFu) << 16) | (mt_temper(n1.w) << 24));
+        buf.append(lo | (hi << 32), 8u);
+        pos = i + 8u;
+        return true;
+    }
+    __device__ __forceinline__ void topup(ByteBuf& buf) {
+        if (buf.cnt <= 24u) gen(buf);
+    }
+    __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf); }  // cnt == 0: always succeeds
 };
 
-__device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
-                                              uint32_t k1, uint32_t (&o)[4]) {
+// ---- Philox4x32-10 counter-based stream -----------------------------------
+// word w of game s = philox({w/4 lo, w/4 hi, s lo, s hi}, seed)[w % 4]
+__device__ __forceinline__ u32x4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                               uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; r++) {
-        uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-        uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
-        uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
         c0 = n0, c1 = lo1, c2 = n2, c3 = lo0;
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
     }
-    o[0] = c0, o[1] = c1, o[2] = c2, o[3] = c3;
+    u32x4 o;
+    o.x = c0, o.y = c1, o.z = c2, o.w = c3;
+    return o;
 }
 
-// counter-based stream: word w of game s = philox({w/4, s}, seed)[w % 4]
-struct PhiloxRng {
+struct PhiloxGen {
     uint32_t k0, k1, s0, s1;
-    uint64_t ctr;
-    uint32_t buf[4];
-    __device__ __forceinline__ void refill() {
-        uint64_t blk = ctr >> 2;
-        philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), s0, s1, k0, k1, buf);
-    }
-    __device__ __forceinline__ uint32_t next() {
-        uint32_t j = (uint32_t)ctr & 3u;
-        if (j == 0u) refill();
-        uint32_t v = buf[0];
-        v = (j == 1u) ? buf[1] : v;
-        v = (j == 2u) ? buf[2] : v;
-        v = (j == 3u) ? buf[3] : v;
-        ctr++;
-        return v;
-    }
-};
+    uint64_t next_blk;  // next block to generate (words 4*next_blk ..)
 
-// numpy legacy random_interval(max)
-template <class R>
-__device__ __forceinline__ uint32_t rng_interval(R& r, uint32_t max) {
-    if (max == 0u) return 0u;
-    const uint32_t mask = 0xFFFFFFFFu >> __builtin_clz(max);
-    uint32_t v;
-    do {
-        v = r.next() & mask;
-    } while (v > max);
-    return v;
-}
+    __device__ __forceinline__ uint64_t block_bytes(uint64_t blk) const {
+        const u32x4 o = philox4x32_10((uint32_t)blk, (uint32_t)(blk >> 32), s0, s1, k0, k1);
+        return (uint64_t)((o.x & 0xFFu) | ((o.y & 0xFFu) << 8) | ((o.z & 0xFFu) << 16) | (o.w << 24));
+    }
+    __device__ __forceinline__ void load(uint32_t seed_lo, uint32_t seed_hi, uint64_t gid, uint64_t consumed,
+                                         ByteBuf& buf) {
+        k0 = seed_lo, k1 = seed_hi;
+        s0 = (uint32_t)gid, s1 = (uint32_t)(gid >> 32);
+        buf.clear();
+        next_blk = consumed >> 2;
+        const uint32_t j = (uint32_t)consumed & 3u;
+        if (j) {  // resume inside a block
+            buf.append(block_bytes(next_blk), 4u);
+            next_blk++;
+            buf.drop(j);
+        }
+    }
+    __device__ __forceinline__ uint64_t consumed(const ByteBuf& buf) const { return 4ull * next_blk - buf.cnt; }
+    __device__ __forceinline__ void gen8(ByteBuf& buf) {
+        const uint64_t a = block_bytes(next_blk), b = block_bytes(next_blk + 1);
+        buf.append(a | (b << 32), 8u);
+        next_blk += 2;
+    }
+    __device__ __forceinline__ void topup(ByteBuf& buf) {
+        if (buf.cnt <= 24u) gen8(buf);
+    }
+    __device__ __forceinline__ void force(ByteBuf& buf) { gen8(buf); }
+};
 
 }  // namespace sechs

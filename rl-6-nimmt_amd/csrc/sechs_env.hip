@@ -1,20 +1,20 @@
 // sechs_env.hip -- vectorised SechsNimmtEnv for gfx950 + the C ABI (include/sechs.h).
 //
-// Device state is struct-of-arrays over games (lane g reads element g of
-// every array, so each load/store instruction of a wave is one contiguous
-// 256-B segment):
-//   hand   [N][4][B] u32   128-bit card set per seat
+// Device state is struct-of-arrays over games, so lane g of a wave reads
+// element g of every array and each load/store instruction of a wave is one
+// contiguous 256-B segment:
+//   hand   [N][3][B] u32   sorted hand bytes: lo.lo32, lo.hi32, hi (sechs_device.h)
 //   row_lo [4][B]    u32   cards 0..3 of each row
 //   row_hi [4][B]    u32   card4 | len<<8 | heads<<16 | end<<24
 //   score  [N][B]    i32   penalties this episode (env.py:32)
 //   sum_res[N][B]    i32   sum of finished episodes' results (-penalty)
 //   episodes [B]     i32
-//   mt [B][624] u32 + mt_pos [B]   (numpy-compat mode; per-game AoS so a
-//                                   lane's lazy twist walks its own lines)
-//   ctr [B] u64                    (philox mode: words consumed)
-// A launch loads a game into VGPRs, plays `steps` env-steps and stores it
-// back; the only per-step HBM traffic is the caller's outputs and, in
-// numpy-compat mode, the MT19937 words.
+//   mt [B][624] u32 + mt_pos [B]   numpy-compat mode: per-game MT19937 (AoS,
+//                                  so a lane's lazy twist walks its own lines)
+//   ctr [B] u64                    philox mode: words consumed
+// A launch loads each game into VGPRs, plays `steps` env-steps and stores it
+// back; per step the only HBM traffic is the caller's outputs and, in
+// numpy-compat mode, the MT19937 words (8 per refill, 16-B accesses).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -51,38 +51,30 @@ struct sn_env {
 };
 
 constexpr int kBlock = 256;
-constexpr int kDeckStride = 108;  // 27 dwords: odd stride -> conflict-free LDS lanes
+constexpr int kDeckStride = 108;  // 27 dwords: odd dword stride -> conflict-free LDS lanes
 
 // ---------------------------------------------------------------- rng glue
 template <int MODE>
 struct RngOf;
 template <>
 struct RngOf<RNG_NUMPY_MT> {
-    using T = MtRng;
-    static __device__ __forceinline__ T load(const DevState& s, int64_t g) {
-        T r;
-        r.st = s.mt + g * kMtN;
-        r.pos = s.mt_pos[g];
-        return r;
+    using T = MtGen;
+    static __device__ __forceinline__ void load(const DevState& s, int64_t g, T& r, ByteBuf& buf) {
+        r.load(s.mt + g * kMtN, s.mt_pos[g], buf);
     }
-    static __device__ __forceinline__ void store(const DevState& s, int64_t g, const T& r) { s.mt_pos[g] = r.pos; }
+    static __device__ __forceinline__ void store(const DevState& s, int64_t g, const T& r, const ByteBuf& buf) {
+        s.mt_pos[g] = r.save(buf);
+    }
 };
 template <>
 struct RngOf<RNG_PHILOX> {
-    using T = PhiloxRng;
-    static __device__ __forceinline__ T load(const DevState& s, int64_t g) {
-        T r;
-        r.k0 = (uint32_t)s.seed;
-        r.k1 = (uint32_t)(s.seed >> 32);
-        uint64_t gid = s.game_offset + (uint64_t)g;
-        r.s0 = (uint32_t)gid;
-        r.s1 = (uint32_t)(gid >> 32);
-        r.ctr = s.ctr[g];
-        if (r.ctr & 3u) r.refill();
-        else r.buf[0] = r.buf[1] = r.buf[2] = r.buf[3] = 0u;
-        return r;
+    using T = PhiloxGen;
+    static __device__ __forceinline__ void load(const DevState& s, int64_t g, T& r, ByteBuf& buf) {
+        r.load((uint32_t)s.seed, (uint32_t)(s.seed >> 32), s.game_offset + (uint64_t)g, s.ctr[g], buf);
     }
-    static __device__ __forceinline__ void store(const DevState& s, int64_t g, const T& r) { s.ctr[g] = r.ctr; }
+    static __device__ __forceinline__ void store(const DevState& s, int64_t g, const T& r, const ByteBuf& buf) {
+        s.ctr[g] = r.consumed(buf);
+    }
 };
 
 // ---------------------------------------------------------------- game in VGPRs
@@ -91,22 +83,36 @@ struct Game {
     Hand hand[N];
     Board b;
     int32_t score[N];
+    uint32_t n;  // cards per hand (all seats hold the same count)
 };
+
+__device__ __forceinline__ Hand load_hand(const DevState& s, int p, int64_t g) {
+    const int64_t B = s.B;
+    Hand h;
+    const uint32_t w0 = s.hand[(int64_t)(p * 3 + 0) * B + g];
+    const uint32_t w1 = s.hand[(int64_t)(p * 3 + 1) * B + g];
+    h.lo = (uint64_t)w0 | ((uint64_t)w1 << 32);
+    h.hi = s.hand[(int64_t)(p * 3 + 2) * B + g];
+    return h;
+}
+
+__device__ __forceinline__ Board load_board(const DevState& s, int64_t g) {
+    const int64_t B = s.B;
+    Board b;
+    b.lo.x = s.row_lo[0 * B + g], b.lo.y = s.row_lo[1 * B + g], b.lo.z = s.row_lo[2 * B + g], b.lo.w = s.row_lo[3 * B + g];
+    b.hi.x = s.row_hi[0 * B + g], b.hi.y = s.row_hi[1 * B + g], b.hi.z = s.row_hi[2 * B + g], b.hi.w = s.row_hi[3 * B + g];
+    return b;
+}
 
 template <int N>
 __device__ __forceinline__ void load_game(const DevState& s, int64_t g, Game<N>& G) {
-    const int64_t B = s.B;
 #pragma unroll
     for (int p = 0; p < N; p++) {
-#pragma unroll
-        for (int w = 0; w < 4; w++) G.hand[p].w[w] = s.hand[(int64_t)(p * 4 + w) * B + g];
-        G.score[p] = s.score[(int64_t)p * B + g];
+        G.hand[p] = load_hand(s, p, g);
+        G.score[p] = s.score[(int64_t)p * s.B + g];
     }
-#pragma unroll
-    for (int r = 0; r < kRows; r++) {
-        G.b.lo[r] = s.row_lo[(int64_t)r * B + g];
-        G.b.hi[r] = s.row_hi[(int64_t)r * B + g];
-    }
+    G.b = load_board(s, g);
+    G.n = hand_len(G.hand[0]);
 }
 
 template <int N>
@@ -114,103 +120,98 @@ __device__ __forceinline__ void store_game(const DevState& s, int64_t g, const G
     const int64_t B = s.B;
 #pragma unroll
     for (int p = 0; p < N; p++) {
-#pragma unroll
-        for (int w = 0; w < 4; w++) s.hand[(int64_t)(p * 4 + w) * B + g] = G.hand[p].w[w];
+        s.hand[(int64_t)(p * 3 + 0) * B + g] = (uint32_t)G.hand[p].lo;
+        s.hand[(int64_t)(p * 3 + 1) * B + g] = (uint32_t)(G.hand[p].lo >> 32);
+        s.hand[(int64_t)(p * 3 + 2) * B + g] = G.hand[p].hi;
         s.score[(int64_t)p * B + g] = G.score[p];
     }
-#pragma unroll
-    for (int r = 0; r < kRows; r++) {
-        s.row_lo[(int64_t)r * B + g] = G.b.lo[r];
-        s.row_hi[(int64_t)r * B + g] = G.b.hi[r];
-    }
+    s.row_lo[0 * B + g] = G.b.lo.x, s.row_lo[1 * B + g] = G.b.lo.y, s.row_lo[2 * B + g] = G.b.lo.z, s.row_lo[3 * B + g] = G.b.lo.w;
+    s.row_hi[0 * B + g] = G.b.hi.x, s.row_hi[1 * B + g] = G.b.hi.y, s.row_hi[2 * B + g] = G.b.hi.z, s.row_hi[3 * B + g] = G.b.hi.w;
 }
 
-// env.py:99-112 _deal after np.random.shuffle(arange(C)) (legacy
-// Fisher-Yates from the end, j = random_interval(i)).  The deck lives in
-// this lane's LDS slot; hands come from deck[0..10N), rows from deck[C-1-r].
+// env.py:99-112 _deal from a dealt deck: hand p = sorted(deck[10p:10p+10]),
+// row r = [deck[C-1-r]]
+template <int N, class D>
+__device__ __forceinline__ void deal_from(const D& deck, int C, Game<N>& G) {
+#pragma unroll
+    for (int p = 0; p < N; p++) {
+        u32x4 set = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int k = 0; k < kHand; k++) set = set_bit(set, deck(kHand * p + k));
+        G.hand[p] = hand_from_set(set);
+        G.score[p] = 0;
+    }
+    const uint32_t r0 = deck(C - 1), r1 = deck(C - 2), r2 = deck(C - 3), r3 = deck(C - 4);
+    G.b.lo.x = r0, G.b.lo.y = r1, G.b.lo.z = r2, G.b.lo.w = r3;
+    G.b.hi.x = meta_row(r0), G.b.hi.y = meta_row(r1), G.b.hi.z = meta_row(r2), G.b.hi.w = meta_row(r3);
+    G.n = kHand;
+}
+
+// np.random.shuffle(arange(C)) (legacy Fisher-Yates from the end,
+// j = random_interval(i)) in this lane's LDS slot, then deal.
 template <int N, class R>
-__device__ __forceinline__ void deal_shuffle(R& rng, uint8_t* deck, int C, Game<N>& G) {
+__device__ __forceinline__ void deal_shuffle(R& rng, ByteBuf& buf, uint8_t* deck, int C, Game<N>& G) {
     for (int i = 0; i < C; i += 4) *(uint32_t*)(deck + i) = (uint32_t)i * 0x01010101u + 0x03020100u;
     for (int i = C - 1; i >= 1; --i) {
-        uint32_t j = rng_interval(rng, (uint32_t)i);
-        uint8_t di = deck[i], dj = deck[j];
+        const uint32_t j = rng_interval(rng, buf, (uint32_t)i);
+        const uint8_t di = deck[i], dj = deck[j];
         deck[i] = dj;
         deck[j] = di;
     }
-#pragma unroll
-    for (int p = 0; p < N; p++) {
-        hand_clear(G.hand[p]);
-#pragma unroll
-        for (int k = 0; k < kHand; k++) hand_add(G.hand[p], deck[kHand * p + k]);
-        G.score[p] = 0;
-    }
-#pragma unroll
-    for (int r = 0; r < kRows; r++) row_start(G.b, r, deck[C - 1 - r]);
-}
-
-template <int N>
-__device__ __forceinline__ void deal_given(const uint8_t* deck, int C, Game<N>& G) {
-#pragma unroll
-    for (int p = 0; p < N; p++) {
-        hand_clear(G.hand[p]);
-#pragma unroll
-        for (int k = 0; k < kHand; k++) hand_add(G.hand[p], deck[kHand * p + k]);
-        G.score[p] = 0;
-    }
-#pragma unroll
-    for (int r = 0; r < kRows; r++) row_start(G.b, r, deck[C - 1 - r]);
+    deal_from<N>([&](int i) -> uint32_t { return deck[i]; }, C, G);
 }
 
 // ---------------------------------------------------------------- observation
-// env.py:188-212 for one seat, as 12 little-endian u32 words (48 bytes,
-// bytes >= L zero): [hand asc, -1 pad to 10][N][lens][ends][heads][4x6 board]
+// env.py:188-212.  A seat's 48-byte row = [hand asc, -1 pad to 10][N]
+// [lens][ends][heads][4x6 board, -1 pad][0 pad]; bytes 0..9 are the seat's
+// hand bytes, bytes 10..47 are the same for every seat (game words).
 template <bool SUMM>
-__device__ __forceinline__ void obs_words(Hand h, int N, const Board& b, uint32_t (&w)[12]) {
+__device__ __forceinline__ void game_words(int N, const Board& b, uint32_t& w2hi, uint32_t (&w)[9]) {
+    uint32_t bytes[48];
 #pragma unroll
-    for (int i = 0; i < 12; i++) w[i] = 0u;
-    uint32_t n = hand_count(h);
-#pragma unroll
-    for (int k = 0; k < kHand; k++) {
-        uint32_t c = ((uint32_t)k < n) ? hand_pop_min(h) : 0xFFu;
-        w[k >> 2] |= (c & 0xFFu) << (8 * (k & 3));
-    }
+    for (int i = 0; i < 48; i++) bytes[i] = 0u;
+    const uint32_t lo[4] = {b.lo.x, b.lo.y, b.lo.z, b.lo.w};
+    const uint32_t hi[4] = {b.hi.x, b.hi.y, b.hi.z, b.hi.w};
     int pos = 10;
-    w[pos >> 2] |= ((uint32_t)N & 0xFFu) << (8 * (pos & 3));
-    pos++;
+    bytes[pos++] = (uint32_t)N & 0xFFu;
     if (SUMM) {
 #pragma unroll
-        for (int r = 0; r < kRows; r++, pos++) w[pos >> 2] |= row_len(b, r) << (8 * (pos & 3));
+        for (int r = 0; r < kRows; r++) bytes[pos++] = len_of(hi[r]);
 #pragma unroll
-        for (int r = 0; r < kRows; r++, pos++) w[pos >> 2] |= row_end(b, r) << (8 * (pos & 3));
+        for (int r = 0; r < kRows; r++) bytes[pos++] = end_of(hi[r]);
 #pragma unroll
-        for (int r = 0; r < kRows; r++, pos++) w[pos >> 2] |= row_heads(b, r) << (8 * (pos & 3));
+        for (int r = 0; r < kRows; r++) bytes[pos++] = heads_in(hi[r]);
     }
 #pragma unroll
     for (int r = 0; r < kRows; r++) {
-        const uint32_t len = row_len(b, r);
+        const uint32_t len = len_of(hi[r]);
 #pragma unroll
-        for (int i = 0; i < kThreshold; i++, pos++) {
-            uint32_t c = ((uint32_t)i < len) ? row_card(b, r, i) : 0xFFu;
-            w[pos >> 2] |= c << (8 * (pos & 3));
-        }
+        for (int i = 0; i < kThreshold; i++, pos++)
+            bytes[pos] = (i < 5 && (uint32_t)i < len) ? card_at(lo[r], hi[r], i < 5 ? i : 0) : 0xFFu;
     }
+    w2hi = (bytes[10] << 16) | (bytes[11] << 24);
+#pragma unroll
+    for (int k = 0; k < 9; k++)
+        w[k] = bytes[12 + 4 * k] | (bytes[13 + 4 * k] << 8) | (bytes[14 + 4 * k] << 16) | (bytes[15 + 4 * k] << 24);
 }
 
-// store one seat's obs row of `stride` bytes (stride % 4 == 0, >= L; bytes
-// past the 48 packed ones are zero).  16-B stores when the row allows it.
-__device__ __forceinline__ void store_obs_row(int8_t* dst, const uint32_t (&w)[12], int stride) {
+// one seat's obs row of `stride` bytes (stride % 4 == 0, >= L)
+__device__ __forceinline__ void store_obs_row(int8_t* dst, const Hand& h, uint32_t w2hi, const uint32_t (&gw)[9],
+                                              int stride) {
+    const uint32_t w0 = (uint32_t)h.lo, w1 = (uint32_t)(h.lo >> 32), w2 = (h.hi & 0xFFFFu) | w2hi;
     if ((stride & 15) == 0 && (((uintptr_t)dst) & 15) == 0) {  // stride >= 48 here
-        uint4* d = (uint4*)dst;
-        d[0] = make_uint4(w[0], w[1], w[2], w[3]);
-        d[1] = make_uint4(w[4], w[5], w[6], w[7]);
-        d[2] = make_uint4(w[8], w[9], w[10], w[11]);
-        for (int i = 3; i < (stride >> 4); i++) d[i] = make_uint4(0u, 0u, 0u, 0u);
+        u32x4* d = (u32x4*)dst;
+        d[0] = u32x4{w0, w1, w2, gw[0]};
+        d[1] = u32x4{gw[1], gw[2], gw[3], gw[4]};
+        d[2] = u32x4{gw[5], gw[6], gw[7], gw[8]};
+        for (int i = 3; i < (stride >> 4); i++) d[i] = u32x4{0u, 0u, 0u, 0u};
     } else {
         uint32_t* d = (uint32_t*)dst;
         const int nw = stride >> 2;
+        const uint32_t all[12] = {w0, w1, w2, gw[0], gw[1], gw[2], gw[3], gw[4], gw[5], gw[6], gw[7], gw[8]};
 #pragma unroll
         for (int i = 0; i < 12; i++)
-            if (i < nw) d[i] = w[i];
+            if (i < nw) d[i] = all[i];
         for (int i = 12; i < nw; i++) d[i] = 0u;
     }
 }
@@ -222,7 +223,7 @@ __global__ void k_seed(DevState s) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= s.B) return;
     if (s.rng_mode == RNG_NUMPY_MT) {
-        // np.random.seed(seed + gid): init_genrand, numpy pos = 624 (== lazy 0)
+        // np.random.seed(seed + gid): init_genrand; numpy pos 624 == lazy code 0
         uint32_t* st = s.mt + g * kMtN;
         uint32_t v = (uint32_t)(s.seed + s.game_offset + (uint64_t)g);
         st[0] = v;
@@ -245,11 +246,14 @@ __global__ __launch_bounds__(kBlock) void k_reset(DevState s, const uint8_t* dec
     if (g >= s.B) return;
     Game<N> G;
     if (decks) {
-        deal_given<N>(decks + g * s.C, s.C, G);
+        const uint8_t* d = decks + g * s.C;
+        deal_from<N>([&](int i) -> uint32_t { return d[i]; }, s.C, G);
     } else {
-        auto rng = RngOf<MODE>::load(s, g);
-        deal_shuffle<N>(rng, lds_deck + threadIdx.x * kDeckStride, s.C, G);
-        RngOf<MODE>::store(s, g, rng);
+        typename RngOf<MODE>::T rng;
+        ByteBuf buf;
+        RngOf<MODE>::load(s, g, rng, buf);
+        deal_shuffle<N>(rng, buf, lds_deck + threadIdx.x * kDeckStride, s.C, G);
+        RngOf<MODE>::store(s, g, rng, buf);
     }
     store_game<N>(s, g, G);
 }
@@ -261,28 +265,32 @@ __global__ __launch_bounds__(kBlock) void k_reset_to(DevState s, const int8_t* b
     Game<N> G;
 #pragma unroll
     for (int p = 0; p < N; p++) {
-        hand_clear(G.hand[p]);
+        u32x4 set = {0u, 0u, 0u, 0u};
         for (int k = 0; k < kHand; k++) {
-            int c = hands[(g * N + p) * kHand + k];
-            if (c >= 0) hand_add(G.hand[p], (uint32_t)c);
+            const int c = hands[(g * N + p) * kHand + k];
+            if (c >= 0) set = set_bit(set, (uint32_t)c);
         }
+        G.hand[p] = hand_from_set(set);
         G.score[p] = 0;
     }
+    uint32_t lo[4], hi[4];
 #pragma unroll
     for (int r = 0; r < kRows; r++) {
-        uint32_t lo = 0, hi = 0, len = 0, heads = 0, end = 0;
+        uint32_t l = 0, card4 = 0, len = 0, heads = 0, end = 0;
         for (int i = 0; i < kThreshold; i++) {
-            int c = board[(g * kRows + r) * kThreshold + i];
+            const int c = board[(g * kRows + r) * kThreshold + i];
             if (c < 0) continue;
-            if (len < 4) lo |= (uint32_t)c << (8 * len);
-            else hi = (uint32_t)c;
+            if (len < 4) l |= (uint32_t)c << (8 * len);
+            else card4 = (uint32_t)c;
             heads += heads_of((uint32_t)c);
             end = (uint32_t)c;
             len++;
         }
-        G.b.lo[r] = lo;
-        G.b.hi[r] = (hi & 0xFFu) | (len << 8) | (heads << 16) | (end << 24);
+        lo[r] = l;
+        hi[r] = (card4 & 0xFFu) | (len << 8) | (heads << 16) | (end << 24);
     }
+    G.b.lo = u32x4{lo[0], lo[1], lo[2], lo[3]};
+    G.b.hi = u32x4{hi[0], hi[1], hi[2], hi[3]};
     store_game<N>(s, g, G);
 }
 
@@ -304,67 +312,90 @@ __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
     const int64_t B = s.B;
     Game<N> G;
     load_game<N>(s, g, G);
-    auto rng = RngOf<MODE>::load(s, g);
+    typename RngOf<MODE>::T rng;
+    ByteBuf buf;
+    RngOf<MODE>::load(s, g, rng, buf);
     const bool summ = !(a.flags & SN_NO_SUMMARIES);
+    int32_t* rew = a.rewards ? a.rewards + g * N : nullptr;
+    uint8_t* act = a.actions_out ? a.actions_out + g * N : nullptr;
+    uint8_t* dn = a.done ? a.done + g : nullptr;
+    int8_t* ob = a.obs ? a.obs + g * N * a.obs_stride : nullptr;
     for (int t = 0; t < a.steps; t++) {
-        const uint32_t n = hand_count(G.hand[0]);
-        if (a.obs) {
-            int8_t* base = a.obs + ((int64_t)t * B + g) * N * a.obs_stride;
+        if (ob) {
+            uint32_t w2hi, gw[9];
+            if (summ) game_words<true>(N, G.b, w2hi, gw);
+            else game_words<false>(N, G.b, w2hi, gw);
 #pragma unroll
-            for (int p = 0; p < N; p++) {
-                uint32_t w[12];
-                if (summ) obs_words<true>(G.hand[p], N, G.b, w);
-                else obs_words<false>(G.hand[p], N, G.b, w);
-                store_obs_row(base + p * a.obs_stride, w, a.obs_stride);
-            }
+            for (int p = 0; p < N; p++) store_obs_row(ob + p * a.obs_stride, G.hand[p], w2hi, gw, a.obs_stride);
+            ob += B * N * a.obs_stride;
         }
-        uint32_t card[N], pen[N];
+        uint32_t card[N], pen[N], idx[N];
         int bad = -1;
-        if (n == 0u) {
+        if (G.n == 0u) {
             bad = 0;  // finished game stepped without auto-reset: nothing to play
         } else if (a.actions) {
 #pragma unroll
             for (int p = N - 1; p >= 0; p--) {
-                int32_t c = a.actions[g * N + p];
+                const int32_t c = a.actions[g * N + p];
+                const int k = (c >= 0 && c < s.C) ? hand_find(G.hand[p], (uint32_t)c) : -1;
                 card[p] = (uint32_t)c;
-                bool ok = c >= 0 && c < s.C && hand_has(G.hand[p], (uint32_t)c);
-                bad = ok ? bad : p;
+                idx[p] = (uint32_t)k;
+                bad = (k >= 0) ? bad : p;
             }
         } else {
-            // DrunkHamster for every seat, in seat order (play.py:38-41)
+            // DrunkHamster for every seat in seat order (play.py:38-41):
+            // legal[random_interval(n-1)], agents/random.py:9
 #pragma unroll
-            for (int p = 0; p < N; p++) card[p] = hand_select(G.hand[p], rng_interval(rng, n - 1u));
+            for (int p = 0; p < N; p++) {
+                idx[p] = rng_interval(rng, buf, G.n - 1u);
+                card[p] = hand_get(G.hand[p], idx[p]);
+            }
         }
         if (a.invalid) a.invalid[g] = bad;
         if (bad >= 0) {
-            if (a.rewards)
+            if (rew) {
 #pragma unroll
-                for (int p = 0; p < N; p++) a.rewards[((int64_t)t * B + g) * N + p] = 0;
-            if (a.done) a.done[(int64_t)t * B + g] = (n == 0u) ? 1 : 0;
+                for (int p = 0; p < N; p++) rew[p] = 0;
+                rew += B * N;
+            }
+            if (act) act += B * N;
+            if (dn) {
+                *dn = (G.n == 0u) ? 1 : 0;
+                dn += B;
+            }
             continue;
         }
 #pragma unroll
-        for (int p = 0; p < N; p++) hand_remove(G.hand[p], card[p]);
+        for (int p = 0; p < N; p++) hand_del(G.hand[p], idx[p]);
         resolve<N>(G.b, card, pen);
 #pragma unroll
         for (int p = 0; p < N; p++) G.score[p] += (int32_t)pen[p];
-        const bool done = (n == 1u);
-        if (a.rewards)
+        G.n -= 1u;
+        const bool done = (G.n == 0u);  // env.py:246-249
+        if (rew) {
 #pragma unroll
-            for (int p = 0; p < N; p++) a.rewards[((int64_t)t * B + g) * N + p] = -(int32_t)pen[p];
-        if (a.actions_out)
+            for (int p = 0; p < N; p++) rew[p] = -(int32_t)pen[p];
+            rew += B * N;
+        }
+        if (act) {
 #pragma unroll
-            for (int p = 0; p < N; p++) a.actions_out[((int64_t)t * B + g) * N + p] = (uint8_t)card[p];
-        if (a.done) a.done[(int64_t)t * B + g] = done ? 1 : 0;
+            for (int p = 0; p < N; p++) act[p] = (uint8_t)card[p];
+            act += B * N;
+        }
+        if (dn) {
+            *dn = done ? 1 : 0;
+            dn += B;
+        }
         if (done && (a.flags & SN_AUTO_RESET)) {
+            // GameSession.results.append(scores) then the next play_game()
 #pragma unroll
             for (int p = 0; p < N; p++) s.sum_res[(int64_t)p * B + g] -= G.score[p];
             s.episodes[g] += 1;
-            deal_shuffle<N>(rng, lds_deck + threadIdx.x * kDeckStride, s.C, G);
+            deal_shuffle<N>(rng, buf, lds_deck + threadIdx.x * kDeckStride, s.C, G);
         }
     }
     store_game<N>(s, g, G);
-    RngOf<MODE>::store(s, g, rng);
+    RngOf<MODE>::store(s, g, rng, buf);
 }
 
 // obs in any dtype, one thread per (game, seat)
@@ -374,18 +405,13 @@ __global__ void k_obs(DevState s, T* out, int stride, int summ) {
     if (i >= s.B * s.N) return;
     const int64_t g = i / s.N;
     const int p = (int)(i - g * s.N);
-    Hand h;
-#pragma unroll
-    for (int w = 0; w < 4; w++) h.w[w] = s.hand[(int64_t)(p * 4 + w) * s.B + g];
-    Board b;
-#pragma unroll
-    for (int r = 0; r < kRows; r++) {
-        b.lo[r] = s.row_lo[(int64_t)r * s.B + g];
-        b.hi[r] = s.row_hi[(int64_t)r * s.B + g];
-    }
-    uint32_t w[12];
-    if (summ) obs_words<true>(h, s.N, b, w);
-    else obs_words<false>(h, s.N, b, w);
+    const Hand h = load_hand(s, p, g);
+    const Board b = load_board(s, g);
+    uint32_t w2hi, gw[9];
+    if (summ) game_words<true>(s.N, b, w2hi, gw);
+    else game_words<false>(s.N, b, w2hi, gw);
+    const uint32_t all[12] = {(uint32_t)h.lo, (uint32_t)(h.lo >> 32), (h.hi & 0xFFFFu) | w2hi,
+                              gw[0], gw[1], gw[2], gw[3], gw[4], gw[5], gw[6], gw[7], gw[8]};
     T* dst = out + i * stride;
     const int L = summ ? 47 : 35;
 #pragma unroll
@@ -393,7 +419,7 @@ __global__ void k_obs(DevState s, T* out, int stride, int summ) {
 #pragma unroll
         for (int bi = 0; bi < 4; bi++) {
             const int k = 4 * wi + bi;
-            if (k < stride) dst[k] = (k < L) ? (T)(int8_t)((w[wi] >> (8 * bi)) & 0xFFu) : (T)0;
+            if (k < stride) dst[k] = (k < L) ? (T)(int8_t)((all[wi] >> (8 * bi)) & 0xFFu) : (T)0;
         }
     for (int k = 48; k < stride; k++) dst[k] = (T)0;
 }
@@ -403,26 +429,23 @@ __global__ void k_hands(DevState s, int8_t* out) {
     if (i >= s.B * s.N) return;
     const int64_t g = i / s.N;
     const int p = (int)(i - g * s.N);
-    Hand h;
+    const Hand h = load_hand(s, p, g);
 #pragma unroll
-    for (int w = 0; w < 4; w++) h.w[w] = s.hand[(int64_t)(p * 4 + w) * s.B + g];
-    uint32_t n = hand_count(h);
-    for (int k = 0; k < kHand; k++) out[i * kHand + k] = ((uint32_t)k < n) ? (int8_t)hand_pop_min(h) : (int8_t)-1;
+    for (int k = 0; k < kHand; k++) out[i * kHand + k] = (int8_t)hand_get(h, (uint32_t)k);
 }
 
 __global__ void k_board(DevState s, int8_t* out) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= s.B) return;
-    Board b;
-#pragma unroll
-    for (int r = 0; r < kRows; r++) {
-        b.lo[r] = s.row_lo[(int64_t)r * s.B + g];
-        b.hi[r] = s.row_hi[(int64_t)r * s.B + g];
-    }
+    const Board b = load_board(s, g);
+    const uint32_t lo[4] = {b.lo.x, b.lo.y, b.lo.z, b.lo.w};
+    const uint32_t hi[4] = {b.hi.x, b.hi.y, b.hi.z, b.hi.w};
 #pragma unroll
     for (int r = 0; r < kRows; r++)
+#pragma unroll
         for (int i = 0; i < kThreshold; i++)
-            out[(g * kRows + r) * kThreshold + i] = ((uint32_t)i < row_len(b, r)) ? (int8_t)row_card(b, r, i) : (int8_t)-1;
+            out[(g * kRows + r) * kThreshold + i] =
+                (i < 5 && (uint32_t)i < len_of(hi[r])) ? (int8_t)card_at(lo[r], hi[r], i < 5 ? i : 0) : (int8_t)-1;
 }
 
 __global__ void k_scores(DevState s, int32_t* scores, int32_t* sum_res, int32_t* episodes) {
@@ -502,7 +525,7 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
         void** p;
         size_t bytes;
     } allocs[] = {
-        {(void**)&s.hand, sizeof(uint32_t) * N * 4 * B},   {(void**)&s.row_lo, sizeof(uint32_t) * kRows * B},
+        {(void**)&s.hand, sizeof(uint32_t) * N * 3 * B},   {(void**)&s.row_lo, sizeof(uint32_t) * kRows * B},
         {(void**)&s.row_hi, sizeof(uint32_t) * kRows * B}, {(void**)&s.score, sizeof(int32_t) * N * B},
         {(void**)&s.sum_res, sizeof(int32_t) * N * B},     {(void**)&s.episodes, sizeof(int32_t) * B},
         {(void**)&s.mt_pos, sizeof(uint32_t) * B},         {(void**)&s.ctr, sizeof(uint64_t) * B},
@@ -685,13 +708,15 @@ sn_status sn_mt_get(sn_env* e, int64_t game, uint32_t* key, int32_t* pos) {
     uint32_t code = 0;
     HIP_TRY(hipMemcpy(key, e->s.mt + game * kMtN, sizeof(uint32_t) * kMtN, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(&code, e->s.mt_pos + game, sizeof(uint32_t), hipMemcpyDeviceToHost));
-    if (code >= (uint32_t)kMtN) {
-        *pos = (int32_t)(code - kMtN);
-    } else if (code == 0) {
-        *pos = kMtN;
+    // decode (sechs_device.h MtRng): words [pos-cnt, pos) generated, unconsumed
+    const int p = (int)(code & 0x7FFu), cnt = (int)((code >> 16) & 0x3Fu);
+    if (code & kMtDirect) {
+        *pos = (int32_t)(p - cnt);
+    } else if (p == 0) {
+        *pos = kMtN;  // previous round complete, next draw twists
     } else {
-        mt_finish_round(key, (int)code);
-        *pos = (int32_t)code;
+        mt_finish_round(key, p);  // twist the rest of this round in place
+        *pos = (int32_t)(p - cnt);
     }
     return SN_OK;
 }
@@ -703,7 +728,7 @@ sn_status sn_mt_set(sn_env* e, int64_t game, const uint32_t* key, int32_t pos) {
     if (pos < 0 || pos > kMtN) return fail(SN_EINVAL, "pos must be in 0..624");
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipDeviceSynchronize());
-    uint32_t code = (pos == kMtN) ? 0u : (uint32_t)(kMtN + pos);
+    uint32_t code = (pos == kMtN) ? 0u : (kMtDirect | (uint32_t)pos);
     HIP_TRY(hipMemcpy(e->s.mt + game * kMtN, key, sizeof(uint32_t) * kMtN, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(e->s.mt_pos + game, &code, sizeof(uint32_t), hipMemcpyHostToDevice));
     return SN_OK;
