@@ -127,6 +127,50 @@ sn_status sn_mt_set(sn_env* env, int64_t game, const uint32_t* key_host, int32_t
 /* philox word counter of game g [sync] */
 sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
 
+/* ---- Monte-Carlo search, MCSAgent (agents/mcts.py:17-188) ------------- */
+
+/* Card memory of every seat (mcts.py:62-73), updated in place from the
+   current position: at a hand of 10 it restarts as range(mcs_num_cards),
+   then the own hand and every card on the board are removed.
+   avail: [4][B*N] uint32 card sets (word-major, decision d = g*N + p). */
+sn_status sn_mcs_memorize(sn_env* env, uint32_t* avail, int mcs_num_cards, void* stream);
+
+/* Stratified Monte-Carlo search for every (game, seat) at once (BASELINE
+   config 3): `rollouts` playouts per legal first move, opponents dealt from
+   the seat's memory, every later move uniform (mcts.py:108-154).
+   sums [B*N][10] int32 = summed return of the seat per first move (slots
+   >= the hand size are 0).  Random words: Philox keyed (seed ^
+   decision_step, game id, seat, move, playout).  rollouts: 64, 128, 192 or
+   a multiple of 256. */
+sn_status sn_mcs_rollouts(sn_env* env, const uint32_t* avail, int rollouts, uint64_t seed, uint32_t decision_step,
+                          int32_t* sums, void* stream);
+
+/* _choose_action_from_outcomes (mcts.py:156-165) with equal playout counts:
+   actions [B][N] int32 = legal[argmax sums] (ties -> lowest card), legal[0]
+   for a one-card hand, -1 for an empty hand. */
+sn_status sn_mcs_choose(sn_env* env, const int32_t* sums, int32_t* actions, void* stream);
+
+/* Reference-exact replay (numpy-MT env only): every game of the handle plays
+   one whole GameSession game (reset + 10 steps) with seat p an
+   MCSAgent(mc_per_card, mc_max) if bit p of mcs_seats is set, else a
+   DrunkHamster, consuming the game's MT19937 stream in the reference's
+   exact order.  actions / rewards [10][B][N] int32; status [B] = 1 where the
+   reference would have raised IndexError (quirk Q6, a move without playouts). */
+sn_status sn_mcs_play_exact(sn_env* env, uint32_t mcs_seats, int mc_per_card, int mc_max, int32_t* actions,
+                            int32_t* rewards, int32_t* status, void* stream);
+
+/* Reference-exact MCSAgent._mcts for D independent decisions (one lane
+   each), for the drop-in agent.  Device buffers: board [D][4][6] int8 (-1
+   pad), hand [D][10] int8 (the legal actions, -1 pad), avail [D][4] uint32
+   card memory, mt_keys [D][624] + mt_pos [D]: numpy-form MT19937 states
+   (np.random.get_state()[1:3]) advanced in place.  actions [D] int32: the
+   chosen card, or -(card)-2 when quirk Q6 applies; sums / counts [D][10]
+   (optional) = per-move playout sums and counts. */
+sn_status sn_mcs_decide_exact(int device, int64_t num_decisions, int num_players, const int8_t* board,
+                              const int8_t* hand, const uint32_t* avail, int mc_per_card, int mc_max,
+                              uint32_t* mt_keys, int32_t* mt_pos, int32_t* actions, int32_t* sums, int32_t* counts,
+                              void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -274,3 +274,21 @@ def mcs_game(seats, mc_per_card, mc_max, seed):
     r = np.zeros((10, n), dtype=np.int32)
     rc = lib().or_mcs_game(seats.encode(), n, mc_per_card, mc_max, seed & 0xFFFFFFFF, _p(a), _p(r))
     return rc, a, r
+
+
+def mcs_memorize(avail, game, seat, mcs_cards=104):
+    a = np.zeros(MAX_CARDS, dtype=np.int32)
+    a[: len(avail)] = avail
+    lib().or_mcs_memorize.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(_Game), ctypes.c_int, ctypes.c_int]
+    n = lib().or_mcs_memorize(_p(a), len(avail), ctypes.byref(game.g), seat, mcs_cards)
+    return [int(x) for x in a[:n]]
+
+
+def mcs_stratified(game, seat, avail, rollouts, seed, step, gid):
+    a = np.ascontiguousarray(avail, dtype=np.int32)
+    s = np.zeros(HAND, dtype=np.int32)
+    L = lib()
+    L.or_mcs_stratified.argtypes = [ctypes.POINTER(_Game), ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p]
+    L.or_mcs_stratified(ctypes.byref(game.g), seat, _p(a), len(a), rollouts, seed, step, gid, _p(s))
+    return s

@@ -503,3 +503,72 @@ int or_mcs_game(const char* seats, int num_players, int mc_per_card, int mc_max,
     }
     return 0;
 }
+
+/* ===================================================================== */
+/* MCS, stratified mode: restatement of the batched engine's sampling      */
+/* (mcts.py:108-154 with a fixed first move and philox words)              */
+/* ===================================================================== */
+int or_mcs_memorize(int* avail, int n_avail, const or_game* g, int seat, int mcs_cards) {
+    or_mcs m;
+    if (g->hand_len[seat] == OR_HAND) { /* _initialize_game */
+        n_avail = mcs_cards;
+        for (int i = 0; i < mcs_cards; i++) avail[i] = i;
+    }
+    m.n_avail = n_avail;
+    for (int i = 0; i < n_avail; i++) m.avail[i] = avail[i];
+    for (int i = 0; i < g->hand_len[seat]; i++) avail_remove(&m, g->hands[seat][i]);
+    for (int r = 0; r < OR_ROWS; r++)
+        for (int i = 0; i < g->row_len[r]; i++) avail_remove(&m, g->rows[r][i]);
+    for (int i = 0; i < m.n_avail; i++) avail[i] = m.avail[i];
+    return m.n_avail;
+}
+
+void or_mcs_stratified(const or_game* root, int seat, const int* avail, int n_avail, int rollouts, uint64_t seed,
+                       uint32_t step, uint64_t gid, int32_t* sums) {
+    const int N = root->num_players, n = root->hand_len[seat];
+    for (int a = 0; a < OR_HAND; a++) sums[a] = 0;
+    if (n <= 1) return;
+    const uint64_t key = ((seed & 0xFFFFFFFF00000000ull) | (uint32_t)((uint32_t)seed ^ step));
+    for (int a = 0; a < n; a++) {
+        for (int r = 0; r < rollouts; r++) {
+            or_rng rng;
+            or_rng_init_philox(&rng, key,
+                               ((uint64_t)(uint32_t)gid << 32) | ((uint64_t)seat << 24) | ((uint64_t)a << 16) | (uint64_t)r);
+            /* rollout seat 0 = the decider, then the other seats in order */
+            or_game g;
+            memset(&g, 0, sizeof(g));
+            g.num_players = N;
+            g.num_cards = root->num_cards;
+            for (int rr = 0; rr < OR_ROWS; rr++) {
+                g.row_len[rr] = root->row_len[rr];
+                for (int i = 0; i < root->row_len[rr]; i++) g.rows[rr][i] = root->rows[rr][i];
+            }
+            g.hand_len[0] = n;
+            for (int i = 0; i < n; i++) g.hands[0][i] = root->hands[seat][i];
+            int pool[OR_MAX_CARDS], left = n_avail;
+            for (int i = 0; i < n_avail; i++) pool[i] = avail[i];
+            for (int q = 1; q < N; q++) {
+                g.hand_len[q] = 0;
+                for (int i = 0; i < n && left > 0; i++) {
+                    int k = (int)or_rng_interval(&rng, (uint32_t)(left - 1));
+                    g.hands[q][g.hand_len[q]++] = pool[k];
+                    for (int j = k; j + 1 < left; j++) pool[j] = pool[j + 1];
+                    left--;
+                }
+                sort_int(g.hands[q], g.hand_len[q]);
+            }
+            int32_t outcome = 0;
+            for (int t = 0; t < n; t++) {
+                int acts[OR_MAX_PLAYERS];
+                int32_t rw[OR_MAX_PLAYERS];
+                for (int q = 0; q < N; q++) {
+                    int idx = (q == 0 && t == 0) ? a : (int)or_rng_interval(&rng, (uint32_t)(g.hand_len[q] - 1));
+                    acts[q] = g.hands[q][idx];
+                }
+                or_step(&g, acts, rw);
+                outcome += rw[0];
+            }
+            sums[a] += outcome;
+        }
+    }
+}

@@ -1,0 +1,241 @@
+// sechs_state.h -- device-side game state shared by the env and MCS kernels.
+//
+// Device state is struct-of-arrays over games, so lane g of a wave reads
+// element g of every array and each load/store instruction of a wave is one
+// contiguous 256-B segment:
+//   hand   [N][3][B] u32   sorted hand bytes: lo.lo32, lo.hi32, hi (sechs_device.h)
+//   row_lo [4][B]    u32   cards 0..3 of each row
+//   row_hi [4][B]    u32   card4 | len<<8 | heads<<16 | end<<24
+//   score  [N][B]    i32   penalties this episode (env.py:32)
+//   sum_res[N][B]    i32   sum of finished episodes' results (-penalty)
+//   episodes [B]     i32
+//   mt [B][624] u32 + mt_pos [B]   numpy-compat mode: per-game MT19937 (AoS,
+//                                  so a lane's lazy twist walks its own lines)
+//   ctr [B] u64                    philox mode: words consumed
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "../../include/sechs.h"
+#include "sechs_device.h"
+
+namespace sechs {
+
+// ============================================================================
+// device state
+// ============================================================================
+struct DevState {
+    int64_t B;
+    int N, C, rng_mode, pad_;
+    uint64_t seed, game_offset;
+    uint32_t* hand;
+    uint32_t* row_lo;
+    uint32_t* row_hi;
+    int32_t* score;
+    int32_t* sum_res;
+    int32_t* episodes;
+    uint32_t* mt;
+    uint32_t* mt_pos;
+    uint64_t* ctr;
+};
+
+constexpr int kBlock = 256;
+constexpr int kDeckStride = 108;  // 27 dwords: odd dword stride -> conflict-free LDS lanes
+
+// ---------------------------------------------------------------- rng glue
+template <int MODE>
+struct RngOf;
+template <>
+struct RngOf<RNG_NUMPY_MT> {
+    using T = MtGen;
+    static __device__ __forceinline__ void load(const DevState& s, int64_t g, T& r, ByteBuf& buf) {
+        r.load(s.mt + g * kMtN, s.mt_pos[g], buf);
+    }
+    static __device__ __forceinline__ void store(const DevState& s, int64_t g, const T& r, const ByteBuf& buf) {
+        s.mt_pos[g] = r.save(buf);
+    }
+};
+template <>
+struct RngOf<RNG_PHILOX> {
+    using T = PhiloxGen;
+    static __device__ __forceinline__ void load(const DevState& s, int64_t g, T& r, ByteBuf& buf) {
+        r.load((uint32_t)s.seed, (uint32_t)(s.seed >> 32), s.game_offset + (uint64_t)g, s.ctr[g], buf);
+    }
+    static __device__ __forceinline__ void store(const DevState& s, int64_t g, const T& r, const ByteBuf& buf) {
+        s.ctr[g] = r.consumed(buf);
+    }
+};
+
+// ---------------------------------------------------------------- game in VGPRs
+template <int N>
+struct Game {
+    Hand hand[N];
+    Board b;
+    int32_t score[N];
+    uint32_t n;  // cards per hand (all seats hold the same count)
+};
+
+__device__ __forceinline__ Hand load_hand(const DevState& s, int p, int64_t g) {
+    const int64_t B = s.B;
+    Hand h;
+    const uint32_t w0 = s.hand[(int64_t)(p * 3 + 0) * B + g];
+    const uint32_t w1 = s.hand[(int64_t)(p * 3 + 1) * B + g];
+    h.lo = (uint64_t)w0 | ((uint64_t)w1 << 32);
+    h.hi = s.hand[(int64_t)(p * 3 + 2) * B + g];
+    return h;
+}
+
+__device__ __forceinline__ Board load_board(const DevState& s, int64_t g) {
+    const int64_t B = s.B;
+    Board b;
+    b.lo.x = s.row_lo[0 * B + g], b.lo.y = s.row_lo[1 * B + g], b.lo.z = s.row_lo[2 * B + g], b.lo.w = s.row_lo[3 * B + g];
+    b.hi.x = s.row_hi[0 * B + g], b.hi.y = s.row_hi[1 * B + g], b.hi.z = s.row_hi[2 * B + g], b.hi.w = s.row_hi[3 * B + g];
+    return b;
+}
+
+template <int N>
+__device__ __forceinline__ void load_game(const DevState& s, int64_t g, Game<N>& G) {
+#pragma unroll
+    for (int p = 0; p < N; p++) {
+        G.hand[p] = load_hand(s, p, g);
+        G.score[p] = s.score[(int64_t)p * s.B + g];
+    }
+    G.b = load_board(s, g);
+    G.n = hand_len(G.hand[0]);
+}
+
+template <int N>
+__device__ __forceinline__ void store_game(const DevState& s, int64_t g, const Game<N>& G) {
+    const int64_t B = s.B;
+#pragma unroll
+    for (int p = 0; p < N; p++) {
+        s.hand[(int64_t)(p * 3 + 0) * B + g] = (uint32_t)G.hand[p].lo;
+        s.hand[(int64_t)(p * 3 + 1) * B + g] = (uint32_t)(G.hand[p].lo >> 32);
+        s.hand[(int64_t)(p * 3 + 2) * B + g] = G.hand[p].hi;
+        s.score[(int64_t)p * B + g] = G.score[p];
+    }
+    s.row_lo[0 * B + g] = G.b.lo.x, s.row_lo[1 * B + g] = G.b.lo.y, s.row_lo[2 * B + g] = G.b.lo.z, s.row_lo[3 * B + g] = G.b.lo.w;
+    s.row_hi[0 * B + g] = G.b.hi.x, s.row_hi[1 * B + g] = G.b.hi.y, s.row_hi[2 * B + g] = G.b.hi.z, s.row_hi[3 * B + g] = G.b.hi.w;
+}
+
+// env.py:99-112 _deal from a dealt deck: hand p = sorted(deck[10p:10p+10]),
+// row r = [deck[C-1-r]]
+template <int N, class D>
+__device__ __forceinline__ void deal_from(const D& deck, int C, Game<N>& G) {
+#pragma unroll
+    for (int p = 0; p < N; p++) {
+        u32x4 set = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int k = 0; k < kHand; k++) set = set_bit(set, deck(kHand * p + k));
+        G.hand[p] = hand_from_set(set);
+        G.score[p] = 0;
+    }
+    const uint32_t r0 = deck(C - 1), r1 = deck(C - 2), r2 = deck(C - 3), r3 = deck(C - 4);
+    G.b.lo.x = r0, G.b.lo.y = r1, G.b.lo.z = r2, G.b.lo.w = r3;
+    G.b.hi.x = meta_row(r0), G.b.hi.y = meta_row(r1), G.b.hi.z = meta_row(r2), G.b.hi.w = meta_row(r3);
+    G.n = kHand;
+}
+
+// np.random.shuffle(arange(C)) (legacy Fisher-Yates from the end,
+// j = random_interval(i)) in this lane's LDS slot, then deal.
+template <int N, class R>
+__device__ __forceinline__ void deal_shuffle(R& rng, ByteBuf& buf, uint8_t* deck, int C, Game<N>& G) {
+    for (int i = 0; i < C; i += 4) *(uint32_t*)(deck + i) = (uint32_t)i * 0x01010101u + 0x03020100u;
+    for (int i = C - 1; i >= 1; --i) {
+        const uint32_t j = rng_interval(rng, buf, (uint32_t)i);
+        const uint8_t di = deck[i], dj = deck[j];
+        deck[i] = dj;
+        deck[j] = di;
+    }
+    deal_from<N>([&](int i) -> uint32_t { return deck[i]; }, C, G);
+}
+
+// ---------------------------------------------------------------- observation
+// env.py:188-212.  A seat's 48-byte row = [hand asc, -1 pad to 10][N]
+// [lens][ends][heads][4x6 board, -1 pad][0 pad]; bytes 0..9 are the seat's
+// hand bytes, bytes 10..47 are the same for every seat (game words).
+template <bool SUMM>
+__device__ __forceinline__ void game_words(int N, const Board& b, uint32_t& w2hi, uint32_t (&w)[9]) {
+    uint32_t bytes[48];
+#pragma unroll
+    for (int i = 0; i < 48; i++) bytes[i] = 0u;
+    const uint32_t lo[4] = {b.lo.x, b.lo.y, b.lo.z, b.lo.w};
+    const uint32_t hi[4] = {b.hi.x, b.hi.y, b.hi.z, b.hi.w};
+    int pos = 10;
+    bytes[pos++] = (uint32_t)N & 0xFFu;
+    if (SUMM) {
+#pragma unroll
+        for (int r = 0; r < kRows; r++) bytes[pos++] = len_of(hi[r]);
+#pragma unroll
+        for (int r = 0; r < kRows; r++) bytes[pos++] = end_of(hi[r]);
+#pragma unroll
+        for (int r = 0; r < kRows; r++) bytes[pos++] = heads_in(hi[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < kRows; r++) {
+        const uint32_t len = len_of(hi[r]);
+#pragma unroll
+        for (int i = 0; i < kThreshold; i++, pos++)
+            bytes[pos] = (i < 5 && (uint32_t)i < len) ? card_at(lo[r], hi[r], i < 5 ? i : 0) : 0xFFu;
+    }
+    w2hi = (bytes[10] << 16) | (bytes[11] << 24);
+#pragma unroll
+    for (int k = 0; k < 9; k++)
+        w[k] = bytes[12 + 4 * k] | (bytes[13 + 4 * k] << 8) | (bytes[14 + 4 * k] << 16) | (bytes[15 + 4 * k] << 24);
+}
+
+// one seat's obs row of `stride` bytes (stride % 4 == 0, >= L)
+__device__ __forceinline__ void store_obs_row(int8_t* dst, const Hand& h, uint32_t w2hi, const uint32_t (&gw)[9],
+                                              int stride) {
+    const uint32_t w0 = (uint32_t)h.lo, w1 = (uint32_t)(h.lo >> 32), w2 = (h.hi & 0xFFFFu) | w2hi;
+    if ((stride & 15) == 0 && (((uintptr_t)dst) & 15) == 0) {  // stride >= 48 here
+        u32x4* d = (u32x4*)dst;
+        d[0] = u32x4{w0, w1, w2, gw[0]};
+        d[1] = u32x4{gw[1], gw[2], gw[3], gw[4]};
+        d[2] = u32x4{gw[5], gw[6], gw[7], gw[8]};
+        for (int i = 3; i < (stride >> 4); i++) d[i] = u32x4{0u, 0u, 0u, 0u};
+    } else {
+        uint32_t* d = (uint32_t*)dst;
+        const int nw = stride >> 2;
+        const uint32_t all[12] = {w0, w1, w2, gw[0], gw[1], gw[2], gw[3], gw[4], gw[5], gw[6], gw[7], gw[8]};
+#pragma unroll
+        for (int i = 0; i < 12; i++)
+            if (i < nw) d[i] = all[i];
+        for (int i = 12; i < nw; i++) d[i] = 0u;
+    }
+}
+
+
+// ---------------------------------------------------------------- host helpers
+sn_status set_error(sn_status st, const std::string& msg);
+inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+#define HIP_TRY(expr)                                                                                    \
+    do {                                                                                                 \
+        hipError_t e_ = (expr);                                                                          \
+        if (e_ != hipSuccess) return ::sechs::set_error(SN_EHIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+// instantiate BODY with constexpr int NN = N_ for N in 1..10
+#define SN_DISPATCH_N(N_, BODY)                                                          \
+    switch (N_) {                                                                        \
+        case 1: { constexpr int NN = 1; BODY; } break;                                   \
+        case 2: { constexpr int NN = 2; BODY; } break;                                   \
+        case 3: { constexpr int NN = 3; BODY; } break;                                   \
+        case 4: { constexpr int NN = 4; BODY; } break;                                   \
+        case 5: { constexpr int NN = 5; BODY; } break;                                   \
+        case 6: { constexpr int NN = 6; BODY; } break;                                   \
+        case 7: { constexpr int NN = 7; BODY; } break;                                   \
+        case 8: { constexpr int NN = 8; BODY; } break;                                   \
+        case 9: { constexpr int NN = 9; BODY; } break;                                   \
+        case 10: { constexpr int NN = 10; BODY; } break;                                 \
+        default: return ::sechs::set_error(SN_EINVAL, "num_players out of range");      \
+    }
+
+}  // namespace sechs
+
+struct sn_env {
+    int device;
+    sechs::DevState s;
+};

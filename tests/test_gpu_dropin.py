@@ -1,0 +1,91 @@
+"""The reference's own API on the MI355X engine: seeded scripts written for
+the reference (np.random.seed + GameSession(...)) give the reference's results."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def test_game_session_random_games_all_sizes():
+    from rl_6_nimmt import GameSession
+    from rl_6_nimmt.agents import DrunkHamster
+
+    meta = load("random_games_meta.json")
+    z = np.load(os.path.join(GOLDEN, "random_games.npz"))
+    for cfg in meta["configs"]:
+        if cfg["num_cards"] != 104 or not cfg["include_summaries"]:
+            continue
+        n = cfg["num_players"]
+        for s in range(min(cfg["seeds"], 6)):
+            np.random.seed(s)
+            sess = GameSession(*[DrunkHamster() for _ in range(n)])
+            sess.play_game()
+            assert sess.results[0].tolist() == z[cfg["key"] + "_results"][s].tolist(), (n, s)
+
+
+def test_game_session_multi_episode_stream():
+    from rl_6_nimmt import GameSession
+    from rl_6_nimmt.agents import DrunkHamster
+
+    for r in load("random_sessions.json")["sessions"]:
+        if "results" not in r or r["num_players"] > 4:
+            continue
+        np.random.seed(r["seed"])
+        sess = GameSession(*[DrunkHamster() for _ in range(r["num_players"])])
+        for _ in range(len(r["results"])):
+            sess.play_game()
+        assert [x.tolist() for x in sess.results] == r["results"]
+
+
+def test_env_dropin_trace_and_errors():
+    from rl_6_nimmt import InvalidMoveException, SechsNimmtEnv
+
+    meta = load("random_games_meta.json")
+    z = np.load(os.path.join(GOLDEN, "random_games.npz"))
+    cfg = [c for c in meta["configs"] if c["num_players"] == 3 and c["num_cards"] == 104][0]
+    k = cfg["key"]
+    np.random.seed(2)
+    env = SechsNimmtEnv(3, verbose=False)
+    states, legal = env.reset()
+    assert all(s.dtype == np.int64 and s.shape == (47,) for s in states)
+    assert np.array_equal(np.stack(states), z[k + "_obs"][2, 0])
+    assert env.action_space.n == 104 and env.observation_space.shape == (47,)
+    for t in range(10):
+        acts = z[k + "_actions"][2, t].tolist()
+        (states, legal), rew, done, info = env.step(acts)
+        assert rew.dtype == np.int32 and rew.tolist() == z[k + "_rewards"][2, t].tolist()
+        assert np.array_equal(np.stack(states), z[k + "_obs"][2, t + 1])
+        assert done == (t == 9) and info == {}
+    # errors: wrong arity and illegal cards keep the reference's types and messages
+    env.reset_to([[10], [20], [30], [40]], [[5, 6], [7, 8], [50, 51]])
+    with pytest.raises(AssertionError):
+        env.step([5, 7])
+    with pytest.raises(InvalidMoveException, match=r"Player 2 tried to play card 10, but their hand is \[7, 8\]"):
+        env.step([5, 9, 50])
+    (states, legal), rew, done, _ = env.step([5, 7, 51])  # state untouched by the failed step
+    assert legal == [[6], [8], [50]]
+
+
+def test_notebook_games_through_dropin_env():
+    from rl_6_nimmt import SechsNimmtEnv
+
+    for G in load("notebook_games.json")["games"]:
+        env = SechsNimmtEnv(2, player_names=G["names"])
+        states, legal = env.reset_to([list(r) for r in G["board"]], [list(h) for h in G["hands"]])
+        assert [s.tolist() for s in states] == G["obs0"]
+        for acts, rec in zip(G["actions"], G["steps"]):
+            (states, legal), rew, done, _ = env.step(acts)
+            assert rew.tolist() == rec["rewards"] and env._board == rec["board"] and done == rec["done"]
+        env.render()
+        assert (-env._scores).tolist() == G["final_scores"]
