@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--extras", action="store_true", help="also time the philox mode and the per-step API")
+    ap.add_argument("--no-mcs", action="store_true", help="skip the config-3 MCS leg")
+    ap.add_argument("--mcs-games", type=int, default=8192)
+    ap.add_argument("--mcs-rollouts", type=int, default=256)
     return ap.parse_args()
 
 
@@ -146,6 +149,41 @@ def cpu_baseline(budget_s, rng):
     }
 
 
+def bench_mcs(games, rollouts, episodes=1):
+    """BASELINE config 3: every seat of `games` 4-player games is an MCS
+    agent with `rollouts` playouts per legal move (stratified), one whole
+    game (10 decisions per seat, 9 of them searched) per episode.  Unit:
+    playout env-steps (one playout game advancing one turn)."""
+    from rl_6_nimmt.mcs import BatchedMCS, rollout_env_steps_per_seat_game
+    from rl_6_nimmt.vec_env import VecSechsNimmtEnv
+
+    env = VecSechsNimmtEnv(games, N_PLAYERS, seed=1, rng="philox")
+    mcs = BatchedMCS(env, rollouts=rollouts, seed=2)
+    mcs.play_episode()  # warm-up
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    total = None
+    for _ in range(episodes):
+        total = mcs.play_episode()
+    ev1.record()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    steps = rollout_env_steps_per_seat_game(rollouts) * N_PLAYERS * games * episodes
+    decisions = 9 * N_PLAYERS * games * episodes
+    return {
+        "workload": f"config3: {games} x 4-player games, all seats MCS, {rollouts} playouts per legal move, "
+                    f"{episodes} game(s); philox RNG",
+        "value": steps / wall,
+        "unit": "playout env-steps/s",
+        "decisions_per_s": decisions / wall,
+        "wall_s": wall,
+        "gpu_ms": ev0.elapsed_time(ev1),
+        "mean_score_per_seat": (total.double().mean(dim=0)).tolist(),
+    }
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
@@ -213,6 +251,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.rng)
+    if world == 1 and not args.no_mcs:
+        result["extra_config3_mcs"] = bench_mcs(args.mcs_games, args.mcs_rollouts)
     if args.extras and world == 1:
         env2 = VecSechsNimmtEnv(B, N_PLAYERS, seed=0, rng="philox")
         env2.reset()
