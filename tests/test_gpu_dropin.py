@@ -89,3 +89,24 @@ def test_notebook_games_through_dropin_env():
             assert rew.tolist() == rec["rewards"] and env._board == rec["board"] and done == rec["done"]
         env.render()
         assert (-env._scores).tolist() == G["final_scores"]
+
+
+def test_tournament_dropin_plays_games():
+    from rl_6_nimmt import Tournament
+    from rl_6_nimmt.agents import DrunkHamster, MCSAgent
+
+    np.random.seed(11)
+    t = Tournament(min_players=2, max_players=4)
+    t.add_player("Random1", DrunkHamster())
+    t.add_player("Random2", DrunkHamster())
+    t.add_player("MCS", MCSAgent(mc_max=20, mc_per_card=2))
+    t.add_player("Random3", DrunkHamster())
+    for _ in range(6):
+        t.play_game()
+    assert t.total_games == 6
+    assert sum(t.played_games.values()) >= 12
+    for name in t.agents:
+        assert all(s <= 0 for s in t.tournament_scores[name])
+        assert all(0.0 <= p <= 1.0 for p in t.tournament_positions[name])
+        assert len(t.elos[name]) == 1 + t.played_games[name]
+    assert "Tournament after 6 games:" in str(t)

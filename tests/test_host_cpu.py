@@ -1,0 +1,106 @@
+"""Host-side logic that needs no GPU: tournament scoring (golden F7), the
+multiplayer Elo stand-in, evolve bookkeeping, the agent registry."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def test_positions_match_reference():
+    from rl_6_nimmt.tournament import Tournament
+
+    for c in load("positions.json")["cases"]:
+        s = np.array(c["scores"], dtype=np.int32)
+        assert Tournament._compute_relative_positions(s).tolist() == c["relative"]
+        assert Tournament._compute_absolute_positions(s).tolist() == c["absolute"]
+        assert int(np.argmax(s)) == c["winner_index"]
+
+
+def test_elo_properties():
+    """parity unpinned (multi_elo absent): conservation and ordering properties"""
+    from rl_6_nimmt.elo import EloPlayer, calc_elo
+
+    rng = np.random.RandomState(0)
+    for _ in range(50):
+        n = rng.randint(2, 6)
+        elos = rng.uniform(1400, 1800, n)
+        places = rng.permutation(n) + 1.0
+        new = calc_elo([EloPlayer(p, e) for p, e in zip(places, elos)], 32)
+        assert abs(sum(new) - sum(elos)) < 1e-9  # zero-sum
+        # equal ratings: the winner gains, the loser loses
+    new = calc_elo([EloPlayer(1, 1600), EloPlayer(2, 1600)], 32)
+    assert new == [1616.0, 1584.0]
+    new = calc_elo([EloPlayer(1.5, 1600), EloPlayer(1.5, 1600)], 32)
+    assert new == [1600.0, 1600.0]
+
+
+class _Dummy:
+    def __init__(self):
+        self.w = 1
+
+
+def test_tournament_bookkeeping_and_evolve():
+    import torch
+
+    from rl_6_nimmt.tournament import Tournament
+
+    class A(torch.nn.Module):
+        pass
+
+    t = Tournament(min_players=2, max_players=3)
+    for name in ["a", "b", "c", "d"]:
+        t.add_player(name, A())
+    assert len(t) == 4
+    t.score_game(["a", "b", "c"], np.array([-3, -10, -3], dtype=np.int32))
+    assert t.tournament_wins["a"] == [1.0] and t.tournament_wins["c"] == [0.0]
+    assert t.tournament_positions["a"][0] == pytest.approx(0.75)
+    assert t.played_games["b"] == 1 and t.total_games == 1
+    assert t.elos["b"][-1] < 1600 < t.elos["a"][-1]
+    table = str(t)
+    assert "Tournament after 1 games:" in table and " Agent                | Games |" in table
+    t.evolve(copies=(2,), max_players=None, max_per_descendant=2, metric="elo")
+    names = t.active_agents()
+    assert "a_0" in names and "a_1" in names and "a" not in t.agents  # best agent cloned twice
+    assert t.agents["a_0"].__name__ == "a_0"
+
+
+def test_registry_and_spaces():
+    from rl_6_nimmt.agents import AGENTS, DrunkHamster, MCSAgent
+    from rl_6_nimmt.agents.base import Agent
+
+    assert AGENTS["random"] is DrunkHamster and AGENTS["mcts"] is MCSAgent
+    a = MCSAgent(mc_max=50)
+    assert isinstance(a, Agent) and a.num_actions == 104 and a.state_length == 47
+    np.random.seed(3)
+    legal = [4, 17, 88]
+    picks = [int(DrunkHamster()(None, legal)[0]) for _ in range(20)]
+    np.random.seed(3)
+    ref = [int(np.random.choice(np.array(legal, dtype=np.int32), size=1)[0]) for _ in range(20)]
+    assert picks == ref
+
+
+def test_mcs_agent_memory_bookkeeping():
+    """card memory semantics of mcts.py:62-89 (host side of the drop-in agent)"""
+    import torch
+
+    from rl_6_nimmt.agents import MCSAgent
+
+    a = MCSAgent()
+    state = torch.tensor([1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 4, 1, 1, 1, 1, 50, 60, 70, 80, 3, 1, 1, 1]
+                         + [50, -1, -1, -1, -1, -1, 60, -1, -1, -1, -1, -1, 70, -1, -1, -1, -1, -1, 80, -1, -1, -1, -1, -1],
+                         dtype=torch.float)
+    legal = list(range(1, 11))
+    a._initialize_game(state)
+    a._memorize_cards(state, legal)
+    assert a.num_players == 4
+    assert len(a.available_cards) == 104 - 10 - 4
+    assert 50 not in a.available_cards and 0 in a.available_cards
+    assert a._compute_n_mc(10) == 100 and a._compute_n_mc(3) == 60 and a._compute_n_mc(2) == 20

@@ -1,11 +1,18 @@
+#!/bin/bash
+# PMC passes for the headline kernel (separate passes per the gfx950 slot
+# limits: FETCH_SIZE and WRITE_SIZE cannot share one).  Run on the GPU box:
+#   gpurun -- bash tools/pmc_config2.sh <tag>
+set -e
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-mkdir -p $R/gpurun_out/pmc
-rocprofv3 -L > $R/gpurun_out/pmc/counters_list.txt 2>&1 || true
+TAG=${1:-cur}
+OUT=$R/gpurun_out/pmc_$TAG
+mkdir -p $OUT
 for mode in numpy philox; do
-  timeout -k 10 180 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS --kernel-include-regex k_play --output-format csv -d $R/gpurun_out/pmc/sq_$mode -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --rng $mode > $R/gpurun_out/pmc/sq_$mode.log 2>&1 || exit 1
-  timeout -k 10 180 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_play --output-format csv -d $R/gpurun_out/pmc/fetch_$mode -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --rng $mode > $R/gpurun_out/pmc/fetch_$mode.log 2>&1 || exit 1
-  timeout -k 10 180 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_play --output-format csv -d $R/gpurun_out/pmc/write_$mode -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --rng $mode > $R/gpurun_out/pmc/write_$mode.log 2>&1 || exit 1
-  timeout -k 10 180 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT --kernel-include-regex k_play --output-format csv -d $R/gpurun_out/pmc/sq2_$mode -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --rng $mode > $R/gpurun_out/pmc/sq2_$mode.log 2>&1 || echo "sq2 failed $mode"
+  timeout -k 10 180 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_play --output-format csv -d $OUT/fetch_$mode -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-mcs --rng $mode > $OUT/fetch_$mode.log 2>&1
+  timeout -k 10 180 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_play --output-format csv -d $OUT/write_$mode -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-mcs --rng $mode > $OUT/write_$mode.log 2>&1
+  timeout -k 10 180 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS --kernel-include-regex k_play --output-format csv -d $OUT/sq_$mode -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-mcs --rng $mode > $OUT/sq_$mode.log 2>&1
+  python3 tools/pmc_traffic.py $OUT/fetch_$mode/run_counter_collection.csv $OUT/write_$mode/run_counter_collection.csv "k_play<4" $OUT/traffic_$mode.json "config2 $mode, 65536 games x 10 env-steps per launch"
 done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- python3 bench.py --no-cpu > $OUT/stats.log 2>&1
 echo done
