@@ -329,6 +329,28 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c) {
 struct MtGen {
     uint32_t* st;
     uint32_t pos, direct;
+    // Inputs of the next lazy refill, loaded one refill ahead: chunk
+    // c = (pos == 624 ? 0 : pos) needs mt[c..c+8), mt[c+8] and the run
+    // mt[j+397] (j < 227) / mt[j-227] (j >= 227), j = c..c+7 -- words the
+    // current refill does not write -- so their latency hides behind the
+    // draws in between.  (At a round's end the next round's chunk 0 is
+    // prefetched: its inputs are final by then.)
+    u32x4 pa0, pa1, pr0, pr1, pr2;
+    uint32_t pa8;
+
+    __device__ __forceinline__ void prefetch(uint32_t c) {
+        pa0 = *(const u32x4*)(st + c);
+        pa1 = *(const u32x4*)(st + c + 4);
+        pa8 = st[(c + 8u == (uint32_t)kMtN) ? 0u : c + 8u];
+        // the run starts at s = 1 (mod 4); read it as three aligned x4 from
+        // s-1, s+3, s+7 (mod 624: the chunk at 224 wraps 621..623 -> 0..4)
+        const uint32_t s = (c < (uint32_t)(kMtN - kMtM)) ? c + kMtM : c - (uint32_t)(kMtN - kMtM);
+        const uint32_t b1 = (s + 3u >= (uint32_t)kMtN) ? s + 3u - kMtN : s + 3u;
+        const uint32_t b2 = (s + 7u >= (uint32_t)kMtN) ? s + 7u - kMtN : s + 7u;
+        pr0 = *(const u32x4*)(st + s - 1u);
+        pr1 = *(const u32x4*)(st + b1);
+        pr2 = *(const u32x4*)(st + b2);
+    }
 
     __device__ __forceinline__ void load(uint32_t* state, uint32_t code, ByteBuf& buf) {
         st = state;
@@ -337,73 +359,70 @@ struct MtGen {
         const uint32_t cnt = (code >> 16) & 0x3Fu;
         buf.clear();
         for (uint32_t k = 0; k < cnt; k++) buf.append(mt_temper(st[pos - cnt + k]) & 0xFFu, 1u);
+        prefetch((direct || pos == (uint32_t)kMtN) ? 0u : pos);
     }
     __device__ __forceinline__ uint32_t save(const ByteBuf& buf) const {
         return pos | (buf.cnt << 16) | (direct << 31);
     }
     // one batch of words; false if the round boundary needs an empty buffer
-    __device__ __forceinline__ bool gen(ByteBuf& buf) {
-        if (direct) {
-            if (pos < (uint32_t)kMtN) {
-                const uint32_t k = min(8u, (uint32_t)kMtN - pos);
-                uint64_t bytes = 0ull;
-                for (uint32_t i = 0; i < k; i++) bytes |= (uint64_t)(mt_temper(st[pos + i]) & 0xFFu) << (8u * i);
-                buf.append(bytes, k);
-                pos += k;
-                return true;
-            }
-            if (buf.cnt) return false;
-            direct = 0u;  // round used up: twist lazily from here on
-            pos = 0u;
-        }
-        if (pos == (uint32_t)kMtN) {
-            if (buf.cnt) return false;
-            pos = 0u;
-        }
-        const uint32_t i = pos;  // multiple of 8
-        const u32x4 a0 = *(const u32x4*)(st + i);
-        const u32x4 a1 = *(const u32x4*)(st + i + 4);
-        const uint32_t a8 = st[(i + 8u == (uint32_t)kMtN) ? 0u : i + 8u];
-        uint32_t c[8];
-        if (i + 8u <= (uint32_t)(kMtN - kMtM) || i >= (uint32_t)(kMtN - kMtM)) {
-            // mt[j+397] (j < 227) or this round's mt[j-227]: one run of 8
-            // words starting at an index = 5 mod 8; read it as 3 aligned x4
-            const uint32_t base = (i < (uint32_t)(kMtN - kMtM)) ? i + kMtM - 1u : i - (uint32_t)(kMtN - kMtM) - 1u;
-            const u32x4 r0 = *(const u32x4*)(st + base);
-            const u32x4 r1 = *(const u32x4*)(st + base + 4);
-            const u32x4 r2 = *(const u32x4*)(st + base + 8);
-            c[0] = r0.y, c[1] = r0.z, c[2] = r0.w, c[3] = r1.x, c[4] = r1.y, c[5] = r1.z, c[6] = r1.w, c[7] = r2.x;
-        } else {
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const uint32_t j = i + (uint32_t)k;
-                c[k] = st[(j < (uint32_t)(kMtN - kMtM)) ? j + kMtM : j - (uint32_t)(kMtN - kMtM)];
-            }
-        }
-        u32x4 n0, n1;
-        n0.x = mt_mix(a0.x, a0.y, c[0]);
-        n0.y = mt_mix(a0.y, a0.z, c[1]);
-        n0.z = mt_mix(a0.z, a0.w, c[2]);
-        n0.w = mt_mix(a0.w, a1.x, c[3]);
-        n1.x = mt_mix(a1.x, a1.y, c[4]);
-        n1.y = mt_mix(a1.y, a1.z, c[5]);
-        n1.z = mt_mix(a1.z, a1.w, c[6]);
-        n1.w = mt_mix(a1.w, a8, c[7]);
-        *(u32x4*)(st + i) = n0;
-        *(u32x4*)(st + i + 4) = n1;
-        const uint64_t lo = (uint64_t)((mt_temper(n0.x) & 0xFFu) | ((mt_temper(n0.y) & 0xFFu) << 8) |
-                                       ((mt_temper(n0.z) & 0xFFu) << 16) | (mt_temper(n0.w) << 24));
-        const uint64_t hi = (uint64_t)((mt_temper(n1.x) & 0xFFu) | ((mt_temper(n1.y) & 0xFFu) << 8) |
-                                       ((mt_temper(n1.z) & 0xFFu) << 16) | (mt_temper(n1.w) << 24));
-        buf.append(lo | (hi << 32), 8u);
-        pos = i + 8u;
-        return true;
-    }
+    __device__ __forceinline__ bool gen(ByteBuf& buf);
     __device__ __forceinline__ void topup(ByteBuf& buf) {
         if (buf.cnt <= 24u) gen(buf);
     }
     __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf); }  // cnt == 0: always succeeds
 };
+
+// Direct mode (only after importing a numpy state mid-round): hand out the
+// remaining words of the imported round; scalar arguments only, out of line.
+struct MtSlow {
+    uint64_t bytes;
+    uint32_t k, pos, direct;
+};
+
+static __device__ __noinline__ MtSlow mt_direct(const uint32_t* st, uint32_t pos, uint32_t bufcnt) {
+    MtSlow o{0ull, 0u, pos, 1u};
+    if (pos < (uint32_t)kMtN) {
+        const uint32_t k = min(8u, (uint32_t)kMtN - pos);
+        for (uint32_t i = 0; i < k; i++) o.bytes |= (uint64_t)(mt_temper(st[pos + i]) & 0xFFu) << (8u * i);
+        o.k = k, o.pos = pos + k;
+    } else if (bufcnt == 0u) {
+        o.direct = 0u, o.pos = (uint32_t)kMtN;  // round used up: lazy twist from chunk 0 on
+    }
+    return o;
+}
+
+__device__ __forceinline__ bool MtGen::gen(ByteBuf& buf) {
+    if (direct) {
+        const MtSlow o = mt_direct(st, pos, buf.cnt);
+        pos = o.pos, direct = o.direct;
+        if (o.k) buf.append(o.bytes, o.k);
+        return o.k != 0u;
+    }
+    uint32_t i = pos;
+    if (i == (uint32_t)kMtN) {
+        if (buf.cnt) return false;  // cross a round boundary only with an empty buffer
+        i = 0u;
+    }
+    u32x4 n0, n1;
+    n0.x = mt_mix(pa0.x, pa0.y, pr0.y);
+    n0.y = mt_mix(pa0.y, pa0.z, pr0.z);
+    n0.z = mt_mix(pa0.z, pa0.w, pr0.w);
+    n0.w = mt_mix(pa0.w, pa1.x, pr1.x);
+    n1.x = mt_mix(pa1.x, pa1.y, pr1.y);
+    n1.y = mt_mix(pa1.y, pa1.z, pr1.z);
+    n1.z = mt_mix(pa1.z, pa1.w, pr1.w);
+    n1.w = mt_mix(pa1.w, pa8, pr2.x);
+    *(u32x4*)(st + i) = n0;
+    *(u32x4*)(st + i + 4) = n1;
+    const uint64_t lo = (uint64_t)((mt_temper(n0.x) & 0xFFu) | ((mt_temper(n0.y) & 0xFFu) << 8) |
+                                   ((mt_temper(n0.z) & 0xFFu) << 16) | (mt_temper(n0.w) << 24));
+    const uint64_t hi = (uint64_t)((mt_temper(n1.x) & 0xFFu) | ((mt_temper(n1.y) & 0xFFu) << 8) |
+                                   ((mt_temper(n1.z) & 0xFFu) << 16) | (mt_temper(n1.w) << 24));
+    buf.append(lo | (hi << 32), 8u);
+    pos = i + 8u;
+    prefetch(pos == (uint32_t)kMtN ? 0u : pos);
+    return true;
+}
 
 // ---- Philox4x32-10 counter-based stream -----------------------------------
 // word w of game s = philox({w/4 lo, w/4 hi, s lo, s hi}, seed)[w % 4]
