@@ -171,6 +171,51 @@ sn_status sn_mcs_decide_exact(int device, int64_t num_decisions, int num_players
                               uint32_t* mt_keys, int32_t* mt_pos, int32_t* actions, int32_t* sums, int32_t* counts,
                               void* stream);
 
+/* ---- "Alpha0.5" PUCT search, PUCTAgent / PolicyMCSAgent (mcts.py:191-323) ----
+   The rollouts of one decision are a dependent chain (each root choice reads
+   the outcomes so far), so a batch advances rollout `rollout` of every
+   decision by one step per call; the policy MLP runs between the calls in
+   PyTorch-ROCm.  Per decision d (game g = d / M, seat = the (d % M)-th set
+   bit of seats_mask, M = popcount):
+     sn_puct_root_rows  rows [D*n][48] (bf16 or f32): [legal[k], obs] normalised
+                        as SechsNimmtStateNormalization (preprocessing.py:12-57)
+     sn_puct_init       root_probs = softmax(root logits [D*n] f32); clears stats
+     for rollout r:  sn_puct_deal (opponents from the memory, mcts.py:116-127)
+       for t < n:    sn_puct_rows (rows [D*N*(n-t)][48] of every rollout seat),
+                     MLP -> logits [D*N*(n-t)] f32, sn_puct_step (PUCT at the
+                     root / policy samples elsewhere, env step, backup at the end)
+     sn_puct_choose     actions [B][N] int32 of the deciding seats = best mean
+   Buffers (device, caller-owned): rollouts [D][48] i32, stats [D][24] i32,
+   hist [D][172] i32, root_probs [D][10] f32. */
+typedef struct {
+    uint32_t seats_mask;   /* deciding seats (bit p = seat p) */
+    int n;                 /* hand size at the root (all games in lockstep) */
+    int puct_root;         /* 1: PUCTAgent (PUCT at the root), 0: PolicyMCSAgent (sampled root) */
+    double c_puct;         /* mcts.py:267, default 2.0 */
+    uint64_t seed;
+    uint32_t step;         /* decision counter, mixed into the Philox key */
+    uint32_t rollout;      /* rollout index r */
+    const uint32_t* avail; /* [4][B*N] card memory from sn_mcs_memorize */
+    int32_t* rollouts;
+    int32_t* stats;
+    int32_t* hist;
+    float* root_probs;
+} sn_puct;
+
+sn_status sn_puct_root_rows(sn_env* env, const sn_puct* q, void* rows, int bf16, void* stream);
+sn_status sn_puct_init(sn_env* env, const sn_puct* q, const float* root_logits, void* stream);
+sn_status sn_puct_deal(sn_env* env, const sn_puct* q, void* stream);
+sn_status sn_puct_rows(sn_env* env, const sn_puct* q, int n_cur, void* rows, int bf16, void* stream);
+sn_status sn_puct_step(sn_env* env, const sn_puct* q, const float* logits, int t, int n_cur, void* stream);
+/* best_index [D] (optional): index of the chosen card in the root legal list */
+sn_status sn_puct_choose(sn_env* env, const sn_puct* q, int32_t* actions, int32_t* best_index, void* stream);
+/* _compute_pucts + argmax (mcts.py:282-315) for D given states: n [D],
+   stats [D][24] (sums[10], counts[10], total, min, max), hist [D][172]
+   outcome counts (value v at bin v+171), probs [D][10] f32 -> pucts [D][10]
+   f64, choice [D] (formula test hook). */
+sn_status sn_puct_score(int64_t num, const int32_t* n, const int32_t* stats, const int32_t* hist, const float* probs,
+                        double c_puct, double* pucts, int32_t* choice, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

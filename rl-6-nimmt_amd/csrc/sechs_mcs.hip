@@ -17,87 +17,6 @@
 
 using namespace sechs;
 
-// ---------------------------------------------------------------- card-set helpers
-__device__ __forceinline__ uint32_t select32(uint32_t w, uint32_t k) {
-    uint32_t pos = 0, c;
-    c = __popc(w & 0xFFFFu);
-    if (k >= c) { k -= c; pos += 16; w >>= 16; }
-    c = __popc(w & 0xFFu);
-    if (k >= c) { k -= c; pos += 8; w >>= 8; }
-    c = __popc(w & 0xFu);
-    if (k >= c) { k -= c; pos += 4; w >>= 4; }
-    c = __popc(w & 0x3u);
-    if (k >= c) { k -= c; pos += 2; w >>= 2; }
-    c = w & 1u;
-    if (k >= c) pos += 1;
-    return pos;
-}
-
-// k-th smallest card of a set (must exist)
-__device__ __forceinline__ uint32_t set_select(u32x4 s, uint32_t k) {
-    const uint32_t c0 = __popc(s.x), c1 = __popc(s.y), c2 = __popc(s.z);
-    uint32_t w = s.x, base = 0u;
-    if (k >= c0) {
-        k -= c0, w = s.y, base = 32u;
-        if (k >= c1) {
-            k -= c1, w = s.z, base = 64u;
-            if (k >= c2) k -= c2, w = s.w, base = 96u;
-        }
-    }
-    return base + select32(w, k);
-}
-
-__device__ __forceinline__ u32x4 clear_bit(u32x4 s, uint32_t c) {
-    const uint32_t bit = ~(1u << (c & 31u)), q = c >> 5;
-    s.x &= (q == 0u) ? bit : ~0u;
-    s.y &= (q == 1u) ? bit : ~0u;
-    s.z &= (q == 2u) ? bit : ~0u;
-    s.w &= (q == 3u) ? bit : ~0u;
-    return s;
-}
-
-__device__ __forceinline__ u32x4 full_set(uint32_t cards) {
-    u32x4 s;
-    s.x = cards >= 32u ? ~0u : ((1u << cards) - 1u);
-    s.y = cards >= 64u ? ~0u : cards <= 32u ? 0u : ((1u << (cards - 32u)) - 1u);
-    s.z = cards >= 96u ? ~0u : cards <= 64u ? 0u : ((1u << (cards - 64u)) - 1u);
-    s.w = cards >= 128u ? ~0u : cards <= 96u ? 0u : ((1u << (cards - 96u)) - 1u);
-    return s;
-}
-
-__device__ __forceinline__ u32x4 hand_set(const Hand& h) {
-    u32x4 s = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int k = 0; k < kHand; k++) {
-        const uint32_t c = hand_get(h, (uint32_t)k);
-        if (c != 0xFFu) s = set_bit(s, c);
-    }
-    return s;
-}
-
-__device__ __forceinline__ u32x4 board_set(const Board& b) {
-    const uint32_t lo[4] = {b.lo.x, b.lo.y, b.lo.z, b.lo.w};
-    const uint32_t hi[4] = {b.hi.x, b.hi.y, b.hi.z, b.hi.w};
-    u32x4 s = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int r = 0; r < kRows; r++)
-#pragma unroll
-        for (int i = 0; i < 5; i++)
-            if ((uint32_t)i < len_of(hi[r])) s = set_bit(s, card_at(lo[r], hi[r], i));
-    return s;
-}
-
-__device__ __forceinline__ u32x4 andnot(u32x4 a, u32x4 b) { return u32x4{a.x & ~b.x, a.y & ~b.y, a.z & ~b.z, a.w & ~b.w}; }
-
-// agents/mcts.py:62-73: at the first decision of a game (n == handsize) the
-// memory is range(num_cards); every decision removes the own hand and every
-// card visible on the board (cards placed and taken within one step are
-// never seen -- quirk Q5, reproduced).
-__device__ __forceinline__ u32x4 memorize(u32x4 mem, uint32_t n, uint32_t mcs_cards, const Hand& h, const Board& b) {
-    if (n == (uint32_t)kHand) mem = full_set(mcs_cards);
-    return andnot(andnot(mem, hand_set(h)), board_set(b));
-}
-
 // ============================================================================
 // stratified engine
 // ============================================================================

@@ -1,0 +1,454 @@
+// sechs_puct.hip -- "Alpha0.5" PUCT search (PUCTAgent / PolicyMCSAgent,
+// agents/mcts.py:191-323) for many decisions at once on gfx950.
+//
+// The reference's rollouts of one decision form a dependent chain (each
+// root choice reads the outcomes so far, mcts.py:276-302), so the batch
+// runs over decisions: every launch advances rollout r of all D decisions
+// by one step.  Per rollout step the host enqueues
+//   k_puct_rows  -> candidate rows [D*N*n_cur][48], normalised exactly as
+//                   SechsNimmtStateNormalization (utils/preprocessing.py:12-57)
+//   policy MLP   -> logits (PyTorch-ROCm, bf16 or fp32: the north star's
+//                   "policy/value net forward via PyTorch-ROCm")
+//   k_puct_step  -> per seat: softmax; PUCT selection at the root (seat 0,
+//                   first step: mcts.py:282-302) or a policy sample (:209-217);
+//                   env step; at the last step the backup (mcts.py:100).
+// Random words: Philox keyed (seed ^ step, game id / seat / rollout / phase).
+// The root policy is evaluated once per decision (k_puct_root_rows): the
+// reference re-evaluates it every rollout, with the same weights and the
+// same input, so the probabilities are the same.
+#include <hip/hip_bf16.h>
+
+#include "sechs_state.h"
+
+using namespace sechs;
+
+constexpr int kRoWords = 48;     // rollout state words per decision
+constexpr int kStatWords = 24;   // sums[10] counts[10] total min max
+constexpr int kHistBins = 172;   // outcomes of seat 0: -171..0
+constexpr int kRowLen = 48;      // 1 (action) + 47 (observation)
+
+struct PuctArgs {
+    int64_t D;                // decisions = B * popcount(seats_mask)
+    uint32_t seats_mask, M;   // deciding seats, M = popcount
+    int n;                    // root hand size (all decisions in lockstep)
+    int flags;                // 1: PUCT at the root (PUCTAgent), 0: sample it (PolicyMCSAgent)
+    double c_puct;
+    uint32_t seed_lo, seed_hi, step, rollout;
+    const uint32_t* avail;    // [4][B*N] card memory (sn_mcs_memorize)
+    int32_t* ro;              // [D][48] rollout games
+    int32_t* stats;           // [D][24]
+    int32_t* hist;            // [D][172]
+    float* root_probs;        // [D][10]
+};
+
+__device__ __forceinline__ void dec_to_gp(const PuctArgs& a, int64_t d, int64_t& g, int& p) {
+    g = d / a.M;
+    uint32_t k = (uint32_t)(d - g * a.M), m = a.seats_mask;
+    for (uint32_t i = 0; i < k; i++) m &= m - 1u;  // drop the k lowest deciding seats
+    p = __builtin_ctz(m);
+}
+
+// utils/preprocessing.py:55-57 in float32, same operation order as torch
+__device__ __forceinline__ float nrm(float x, float lo, float hi) {
+    float t = x - lo;
+    t = 2.0f * t;
+    t = t / (hi - lo);
+    return -1.0f + t;
+}
+
+template <typename T>
+__device__ __forceinline__ T to_out(float v);
+template <>
+__device__ __forceinline__ float to_out<float>(float v) { return v; }
+template <>
+__device__ __forceinline__ __hip_bfloat16 to_out<__hip_bfloat16>(float v) { return __float2bfloat16(v); }
+
+// one candidate row: [card, observation of a seat holding `h` on board `b`]
+template <typename T>
+__device__ __forceinline__ void write_row(T* dst, uint32_t card, const Hand& h, int N, const Board& b) {
+    dst[0] = to_out<T>(nrm((float)card, 0.f, 103.f));
+#pragma unroll
+    for (int k = 0; k < kHand; k++) {
+        const uint32_t c = hand_get(h, (uint32_t)k);
+        dst[1 + k] = to_out<T>(nrm(c == 0xFFu ? -1.f : (float)c, 0.f, 103.f));
+    }
+    dst[11] = to_out<T>(nrm((float)N, 0.f, 6.f));
+    const uint32_t lo[4] = {b.lo.x, b.lo.y, b.lo.z, b.lo.w};
+    const uint32_t hi[4] = {b.hi.x, b.hi.y, b.hi.z, b.hi.w};
+#pragma unroll
+    for (int r = 0; r < kRows; r++) {
+        dst[12 + r] = to_out<T>(nrm((float)len_of(hi[r]), 1.f, 5.f));
+        dst[16 + r] = to_out<T>(nrm((float)end_of(hi[r]), 0.f, 103.f));
+        dst[20 + r] = to_out<T>(nrm((float)heads_in(hi[r]), 1.f, 10.f));
+#pragma unroll
+        for (int i = 0; i < kThreshold; i++) {
+            const float v = (i < 5 && (uint32_t)i < len_of(hi[r])) ? (float)card_at(lo[r], hi[r], i < 5 ? i : 0) : -1.f;
+            dst[24 + r * kThreshold + i] = to_out<T>(nrm(v, 0.f, 103.f));
+        }
+    }
+}
+
+__device__ __forceinline__ Hand ro_hand(const int32_t* ro, int q) {
+    Hand h;
+    h.lo = (uint32_t)ro[8 + 3 * q] | ((uint64_t)(uint32_t)ro[9 + 3 * q] << 32);
+    h.hi = (uint32_t)ro[10 + 3 * q];
+    return h;
+}
+__device__ __forceinline__ Board ro_board(const int32_t* ro) {
+    Board b;
+    b.lo = u32x4{(uint32_t)ro[0], (uint32_t)ro[1], (uint32_t)ro[2], (uint32_t)ro[3]};
+    b.hi = u32x4{(uint32_t)ro[4], (uint32_t)ro[5], (uint32_t)ro[6], (uint32_t)ro[7]};
+    return b;
+}
+
+// ---------------------------------------------------------------- root
+template <typename T>
+__global__ void k_puct_root_rows(DevState s, PuctArgs a, T* rows) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.D * a.n) return;
+    const int64_t d = i / a.n;
+    const uint32_t k = (uint32_t)(i - d * a.n);
+    int64_t g;
+    int p;
+    dec_to_gp(a, d, g, p);
+    const Hand h = load_hand(s, p, g);
+    write_row<T>(rows + i * kRowLen, hand_get(h, k), h, s.N, load_board(s, g));
+}
+
+// softmax(dim=0) of the root logits (mcts.py:227) and empty statistics
+__global__ void k_puct_init(PuctArgs a, const float* logits) {
+    const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= a.D) return;
+    const float* x = logits + d * a.n;
+    float m = x[0];
+    for (int k = 1; k < a.n; k++) m = fmaxf(m, x[k]);
+    float e[kHand], sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < kHand; k++) {
+        e[k] = (k < a.n) ? __expf(x[k < a.n ? k : 0] - m) : 0.f;
+        sum += e[k];
+    }
+#pragma unroll
+    for (int k = 0; k < kHand; k++) a.root_probs[d * kHand + k] = (k < a.n) ? e[k] / sum : 0.f;
+    for (int w = 0; w < kStatWords; w++) a.stats[d * kStatWords + w] = 0;
+    a.stats[d * kStatWords + 21] = 1;     // min (set by the first backup)
+    a.stats[d * kStatWords + 22] = -1000;  // max
+    for (int b = 0; b < kHistBins; b++) a.hist[d * kHistBins + b] = 0;
+}
+
+// ---------------------------------------------------------------- rollouts
+// _draw_env + _deal_hands (mcts.py:108-127): the decider is seat 0 of the
+// rollout game, opponents are dealt from its memory
+template <int N>
+__global__ void k_puct_deal(DevState s, PuctArgs a) {
+    const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= a.D) return;
+    int64_t g;
+    int p;
+    dec_to_gp(a, d, g, p);
+    const int64_t DN = s.B * N, dn = g * N + p;
+    u32x4 av = {a.avail[dn], a.avail[DN + dn], a.avail[2 * DN + dn], a.avail[3 * DN + dn]};
+    const uint64_t gid = s.game_offset + (uint64_t)g;
+    PhiloxGen gen;
+    ByteBuf buf;
+    gen.load(a.seed_lo ^ a.step, a.seed_hi, ((uint64_t)(uint32_t)gid << 32) | ((uint64_t)p << 28) | ((uint64_t)a.rollout << 8),
+             0ull, buf);
+    int32_t* ro = a.ro + d * kRoWords;
+    const Board b = load_board(s, g);
+    const Hand me = load_hand(s, p, g);
+    const uint32_t n = (uint32_t)a.n;
+    ro[0] = b.lo.x, ro[1] = b.lo.y, ro[2] = b.lo.z, ro[3] = b.lo.w;
+    ro[4] = b.hi.x, ro[5] = b.hi.y, ro[6] = b.hi.z, ro[7] = b.hi.w;
+    ro[8] = (int32_t)(uint32_t)me.lo, ro[9] = (int32_t)(uint32_t)(me.lo >> 32), ro[10] = (int32_t)me.hi;
+    uint32_t left = set_count(av);
+#pragma unroll
+    for (int q = 1; q < N; q++) {
+        u32x4 set = {0u, 0u, 0u, 0u};
+        for (uint32_t i = 0; i < n && left > 0u; i++) {
+            const uint32_t k = rng_interval(gen, buf, left - 1u);
+            const uint32_t c = set_select(av, k);
+            av = clear_bit(av, c);
+            set = set_bit(set, c);
+            left--;
+        }
+        const Hand h = hand_from_set(set);
+        ro[8 + 3 * q] = (int32_t)(uint32_t)h.lo, ro[9 + 3 * q] = (int32_t)(uint32_t)(h.lo >> 32), ro[10 + 3 * q] = (int32_t)h.hi;
+    }
+    ro[40] = 0;   // outcome
+    ro[41] = -1;  // first move (index into the root's legal list)
+}
+
+// candidate rows of every seat of every rollout game: row (d, q, k)
+template <typename T>
+__global__ void k_puct_rows(PuctArgs a, int N, int n_cur, T* rows) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per_d = (int64_t)N * n_cur;
+    if (i >= a.D * per_d) return;
+    const int64_t d = i / per_d;
+    const int rem = (int)(i - d * per_d);
+    const int q = rem / n_cur, k = rem - q * n_cur;
+    const int32_t* ro = a.ro + d * kRoWords;
+    const Hand h = ro_hand(ro, q);
+    write_row<T>(rows + i * kRowLen, hand_get(h, (uint32_t)k), h, N, ro_board(ro));
+}
+
+// np.median of all outcomes so far, from the histogram (kth smallest)
+__device__ double hist_median(const int32_t* hist, int32_t total) {
+    const int32_t k0 = (total - 1) / 2, k1 = total / 2;
+    int32_t acc = 0, v0 = 0, v1 = 0;
+    bool got0 = false;
+    for (int b = 0; b < kHistBins; b++) {
+        const int32_t c = hist[b];
+        if (!got0 && acc + c > k0) v0 = b - 171, got0 = true;
+        if (acc + c > k1) {
+            v1 = b - 171;
+            break;
+        }
+        acc += c;
+    }
+    return 0.5 * ((double)v0 + (double)v1);
+}
+
+// PUCTAgent._compute_pucts + argmax (mcts.py:282-315) with numpy's float
+// types: c_puct * probs is float32 (a Python float times a float32 array);
+// (n_total + 1e-9) ** 0.5 is a numpy float64 scalar, which promotes the
+// product to float64 (numpy >= 2 promotion, the version the golden vectors
+// were recorded with); q and the division by (1 + n) are float64
+__device__ int puct_choose(const int32_t* st, const int32_t* hist, const float* probs, int n, double c_puct,
+                           double* pucts_out) {
+    const int32_t total = st[20];
+    int32_t n_total = 0;
+    for (int k = 0; k < n; k++) n_total += st[10 + k];
+    double mx, mn, med;
+    if (total < 10) {
+        mx = 0.0, mn = -10.0, med = -5.0;  // _normalize_q fallback (quirk Q8)
+    } else {
+        mx = (double)st[22], mn = (double)st[21], med = hist_median(hist, total);
+    }
+    const double sq = sqrt((double)n_total + 1e-9);
+    double best = -__builtin_inf();
+    int choice = 0;
+    for (int k = 0; k < n; k++) {
+        const int32_t cnt = st[10 + k];
+        double q = cnt ? (double)st[k] / (double)cnt : med;
+        q = (q - mn) / (mx - mn);         // max == min: NaN for every move (quirk Q7)
+        q = (q < 0.0) ? 0.0 : (q > 1.0) ? 1.0 : q;  // np.clip keeps NaN
+        const double t = (double)((float)c_puct * probs[k]) * sq;
+        const double v = q + t / (1.0 + (double)cnt);
+        if (pucts_out) pucts_out[k] = v;
+        if (v > best) best = v, choice = k;  // strict '>': NaN never wins, index 0 stays
+    }
+    return choice;
+}
+
+// Categorical(probs).sample() with u from Philox: the first k whose
+// running sum of the float32 softmax exceeds u
+__device__ __forceinline__ int sample_softmax(const float* x, int n, float u) {
+    float m = x[0];
+    for (int k = 1; k < n; k++) m = fmaxf(m, x[k]);
+    float sum = 0.f;
+    for (int k = 0; k < n; k++) sum += __expf(x[k] - m);
+    const float target = u * sum;
+    float acc = 0.f;
+    for (int k = 0; k < n - 1; k++) {
+        acc += __expf(x[k] - m);
+        if (acc > target) return k;
+    }
+    return n - 1;
+}
+
+template <int N>
+__global__ void k_puct_step(DevState s, PuctArgs a, const float* logits, int t, int n_cur) {
+    const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= a.D) return;
+    int64_t g;
+    int p;
+    dec_to_gp(a, d, g, p);
+    int32_t* ro = a.ro + d * kRoWords;
+    Game<N> G;
+#pragma unroll
+    for (int q = 0; q < N; q++) G.hand[q] = ro_hand(ro, q);
+    G.b = ro_board(ro);
+    const uint64_t gid = s.game_offset + (uint64_t)g;
+    const uint64_t stream = ((uint64_t)(uint32_t)gid << 32) | ((uint64_t)p << 28) | ((uint64_t)a.rollout << 8) | (uint64_t)(1 + t);
+    uint32_t card[N], pen[N];
+    int first = ro[41];
+#pragma unroll
+    for (int q = 0; q < N; q++) {
+        int idx;
+        const float* x = logits + (d * N + q) * n_cur;
+        if (t == 0 && q == 0 && (a.flags & 1)) {
+            idx = puct_choose(a.stats + d * kStatWords, a.hist + d * kHistBins, a.root_probs + d * kHand, n_cur,
+                              a.c_puct, nullptr);
+        } else {
+            idx = sample_softmax(x, n_cur, philox_uniform(a.seed_lo ^ a.step, a.seed_hi, stream, (uint32_t)q));
+        }
+        if (t == 0 && q == 0) first = idx;
+        card[q] = hand_get(G.hand[q], (uint32_t)idx);
+        hand_del(G.hand[q], (uint32_t)idx);
+    }
+    resolve<N>(G.b, card, pen);
+    const int32_t outcome = ro[40] - (int32_t)pen[0];
+    if (n_cur == 1) {
+        // backup: outcomes[first].append(outcome) (mcts.py:100)
+        int32_t* st = a.stats + d * kStatWords;
+        st[first] += outcome;
+        st[10 + first] += 1;
+        st[20] += 1;
+        st[21] = (st[20] == 1) ? outcome : min(st[21], outcome);
+        st[22] = (st[20] == 1) ? outcome : max(st[22], outcome);
+        a.hist[d * kHistBins + (outcome + 171)] += 1;
+    } else {
+        ro[0] = G.b.lo.x, ro[1] = G.b.lo.y, ro[2] = G.b.lo.z, ro[3] = G.b.lo.w;
+        ro[4] = G.b.hi.x, ro[5] = G.b.hi.y, ro[6] = G.b.hi.z, ro[7] = G.b.hi.w;
+#pragma unroll
+        for (int q = 0; q < N; q++) {
+            ro[8 + 3 * q] = (int32_t)(uint32_t)G.hand[q].lo;
+            ro[9 + 3 * q] = (int32_t)(uint32_t)(G.hand[q].lo >> 32);
+            ro[10 + 3 * q] = (int32_t)G.hand[q].hi;
+        }
+        ro[40] = outcome;
+        ro[41] = first;
+    }
+}
+
+// _choose_action_from_outcomes (mcts.py:156-165, temperature None): best mean
+// over moves with playouts, strict '>'; one-card hands play it directly
+__global__ void k_puct_choose(DevState s, PuctArgs a, int32_t* actions, int32_t* best_index) {
+    const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= a.D) return;
+    int64_t g;
+    int p;
+    dec_to_gp(a, d, g, p);
+    const Hand h = load_hand(s, p, g);
+    int best = 0;
+    if (a.n > 1) {
+        const int32_t* st = a.stats + d * kStatWords;
+        double bm = -__builtin_inf();
+        for (int k = 0; k < a.n; k++) {
+            if (st[10 + k] == 0) continue;
+            const double m = (double)st[k] / (double)st[10 + k];
+            if (m > bm) bm = m, best = k;
+        }
+    }
+    actions[g * s.N + p] = (int32_t)hand_get(h, (uint32_t)best);
+    if (best_index) best_index[d] = best;
+}
+
+// test hook for the formula fixtures (F5): stats/hist/probs given per decision
+__global__ void k_puct_score(int64_t D, int n_max, const int32_t* n, const int32_t* stats, const int32_t* hist,
+                             const float* probs, double c_puct, double* pucts, int32_t* choice) {
+    const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= D) return;
+    choice[d] = puct_choose(stats + d * kStatWords, hist + d * kHistBins, probs + d * kHand, n[d], c_puct,
+                            pucts + d * kHand);
+    (void)n_max;
+}
+
+// ============================================================================
+// C ABI
+// ============================================================================
+static sn_status puct_args(sn_env* e, const sn_puct* q, PuctArgs& a) {
+    if (!e || !q) return set_error(SN_EINVAL, "NULL argument");
+    const uint32_t mask = q->seats_mask & ((1u << e->s.N) - 1u);
+    if (!mask) return set_error(SN_EINVAL, "seats_mask selects no seat");
+    if (q->n < 1 || q->n > kHand) return set_error(SN_EINVAL, "hand size out of range");
+    a.M = (uint32_t)__builtin_popcount(mask);
+    a.seats_mask = mask;
+    a.D = e->s.B * a.M;
+    a.n = q->n;
+    a.flags = q->puct_root ? 1 : 0;
+    a.c_puct = q->c_puct;
+    a.seed_lo = (uint32_t)q->seed, a.seed_hi = (uint32_t)(q->seed >> 32), a.step = q->step;
+    a.rollout = q->rollout;
+    a.avail = q->avail;
+    a.ro = q->rollouts;
+    a.stats = q->stats;
+    a.hist = q->hist;
+    a.root_probs = q->root_probs;
+    return SN_OK;
+}
+
+extern "C" {
+
+sn_status sn_puct_root_rows(sn_env* e, const sn_puct* q, void* rows, int bf16, void* stream) {
+    PuctArgs a{};
+    sn_status st = puct_args(e, q, a);
+    if (st != SN_OK) return st;
+    hipStream_t s = (hipStream_t)stream;
+    if (bf16)
+        hipLaunchKernelGGL(k_puct_root_rows<__hip_bfloat16>, dim3(grid_for(a.D * a.n)), dim3(kBlock), 0, s, e->s, a,
+                           (__hip_bfloat16*)rows);
+    else
+        hipLaunchKernelGGL(k_puct_root_rows<float>, dim3(grid_for(a.D * a.n)), dim3(kBlock), 0, s, e->s, a, (float*)rows);
+    HIP_TRY(hipGetLastError());
+    return SN_OK;
+}
+
+sn_status sn_puct_init(sn_env* e, const sn_puct* q, const float* root_logits, void* stream) {
+    PuctArgs a{};
+    sn_status st = puct_args(e, q, a);
+    if (st != SN_OK) return st;
+    hipLaunchKernelGGL(k_puct_init, dim3(grid_for(a.D)), dim3(kBlock), 0, (hipStream_t)stream, a, root_logits);
+    HIP_TRY(hipGetLastError());
+    return SN_OK;
+}
+
+sn_status sn_puct_deal(sn_env* e, const sn_puct* q, void* stream) {
+    PuctArgs a{};
+    sn_status st = puct_args(e, q, a);
+    if (st != SN_OK) return st;
+    hipStream_t s = (hipStream_t)stream;
+    SN_DISPATCH_N(e->s.N, hipLaunchKernelGGL((k_puct_deal<NN>), dim3(grid_for(a.D)), dim3(kBlock), 0, s, e->s, a));
+    HIP_TRY(hipGetLastError());
+    return SN_OK;
+}
+
+sn_status sn_puct_rows(sn_env* e, const sn_puct* q, int n_cur, void* rows, int bf16, void* stream) {
+    PuctArgs a{};
+    sn_status st = puct_args(e, q, a);
+    if (st != SN_OK) return st;
+    if (n_cur < 1 || n_cur > a.n) return set_error(SN_EINVAL, "n_cur out of range");
+    const int64_t total = a.D * e->s.N * n_cur;
+    hipStream_t s = (hipStream_t)stream;
+    if (bf16)
+        hipLaunchKernelGGL(k_puct_rows<__hip_bfloat16>, dim3(grid_for(total)), dim3(kBlock), 0, s, a, e->s.N, n_cur,
+                           (__hip_bfloat16*)rows);
+    else
+        hipLaunchKernelGGL(k_puct_rows<float>, dim3(grid_for(total)), dim3(kBlock), 0, s, a, e->s.N, n_cur, (float*)rows);
+    HIP_TRY(hipGetLastError());
+    return SN_OK;
+}
+
+sn_status sn_puct_step(sn_env* e, const sn_puct* q, const float* logits, int t, int n_cur, void* stream) {
+    PuctArgs a{};
+    sn_status st = puct_args(e, q, a);
+    if (st != SN_OK) return st;
+    if (n_cur < 1 || n_cur > a.n || t < 0 || t + n_cur != a.n) return set_error(SN_EINVAL, "t / n_cur inconsistent");
+    hipStream_t s = (hipStream_t)stream;
+    SN_DISPATCH_N(e->s.N, hipLaunchKernelGGL((k_puct_step<NN>), dim3(grid_for(a.D)), dim3(kBlock), 0, s, e->s, a, logits,
+                                             t, n_cur));
+    HIP_TRY(hipGetLastError());
+    return SN_OK;
+}
+
+sn_status sn_puct_choose(sn_env* e, const sn_puct* q, int32_t* actions, int32_t* best_index, void* stream) {
+    PuctArgs a{};
+    sn_status st = puct_args(e, q, a);
+    if (st != SN_OK) return st;
+    hipLaunchKernelGGL(k_puct_choose, dim3(grid_for(a.D)), dim3(kBlock), 0, (hipStream_t)stream, e->s, a, actions,
+                       best_index);
+    HIP_TRY(hipGetLastError());
+    return SN_OK;
+}
+
+sn_status sn_puct_score(int64_t D, const int32_t* n, const int32_t* stats, const int32_t* hist, const float* probs,
+                        double c_puct, double* pucts, int32_t* choice, void* stream) {
+    if (D <= 0 || !n || !stats || !hist || !probs || !pucts || !choice) return set_error(SN_EINVAL, "bad argument");
+    hipLaunchKernelGGL(k_puct_score, dim3(grid_for(D)), dim3(kBlock), 0, (hipStream_t)stream, D, kHand, n, stats, hist,
+                       probs, c_puct, pucts, choice);
+    HIP_TRY(hipGetLastError());
+    return SN_OK;
+}
+
+}  // extern "C"

@@ -21,6 +21,25 @@ SN_RNG_PHILOX, SN_RNG_NUMPY_MT = 0, 1
 SN_I8, SN_I16, SN_I32, SN_I64, SN_F32 = 1, 2, 3, 4, 5
 SN_AUTO_RESET, SN_NO_SUMMARIES = 1, 2
 
+class SnPuct(ctypes.Structure):
+    """sn_puct (include/sechs.h)"""
+
+    _fields_ = [
+        ("seats_mask", ctypes.c_uint32),
+        ("n", ctypes.c_int),
+        ("puct_root", ctypes.c_int),
+        ("c_puct", ctypes.c_double),
+        ("seed", ctypes.c_uint64),
+        ("step", ctypes.c_uint32),
+        ("rollout", ctypes.c_uint32),
+        ("avail", ctypes.c_void_p),
+        ("rollouts", ctypes.c_void_p),
+        ("stats", ctypes.c_void_p),
+        ("hist", ctypes.c_void_p),
+        ("root_probs", ctypes.c_void_p),
+    ]
+
+
 # every symbol include/sechs.h declares, with its ctypes signature
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -50,6 +69,13 @@ SIGNATURES = {
     "sn_mcs_choose": ([_P, _P, _P, _P], _I),
     "sn_mcs_play_exact": ([_P, ctypes.c_uint32, _I, _I, _P, _P, _P, _P], _I),
     "sn_mcs_decide_exact": ([_I, _I64, _I, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P], _I),
+    "sn_puct_root_rows": ([_P, _P, _P, _I, _P], _I),
+    "sn_puct_init": ([_P, _P, _P, _P], _I),
+    "sn_puct_deal": ([_P, _P, _P], _I),
+    "sn_puct_rows": ([_P, _P, _I, _P, _I, _P], _I),
+    "sn_puct_step": ([_P, _P, _P, _I, _I, _P], _I),
+    "sn_puct_choose": ([_P, _P, _P, _P, _P], _I),
+    "sn_puct_score": ([_I64, _P, _P, _P, _P, ctypes.c_double, _P, _P, _P], _I),
 }
 
 

@@ -1,13 +1,13 @@
 """Agents on the hot path (reference registry: rl_6_nimmt/agents/__init__.py:33-53).
 
-Kept: Agent, DrunkHamster ("random"), MCSAgent ("mcts").  The model-free
-learners (DQN / ACER / REINFORCE), the human UI and the PUCT variants are
-outside this build's scope; their registry keys map to
-`None` so scripts fail with a clear message instead of a missing key.
+Kept: Agent, DrunkHamster ("random"), MCSAgent ("mcts"), PolicyMCSAgent
+("pmcs"), PUCTAgent ("puct").  The model-free
+learners (DQN / ACER / REINFORCE), the human UI and PUCTCustomedAgent are
+outside this build's scope and absent from AGENTS.
 """
 from .base import Agent
 from .random import DrunkHamster
-from .mcts import BaseMCAgent, MCSAgent
+from .mcts import BaseMCAgent, MCSAgent, PolicyMCSAgent, PUCTAgent
 
 HUMAN = "human"
 RANDOM_AGENT = "random"
@@ -18,4 +18,6 @@ PUCT = "puct"
 AGENTS = {
     RANDOM_AGENT: DrunkHamster,
     MCS: MCSAgent,
+    PMCS: PolicyMCSAgent,
+    PUCT: PUCTAgent,
 }

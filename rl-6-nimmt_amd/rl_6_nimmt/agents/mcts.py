@@ -113,3 +113,139 @@ class MCSAgent(BaseMCAgent):
             logger.warning("MCS: a legal move got no playout (the reference raises IndexError here, quirk Q6)")
         self.last_search = {"sums": d_sums.cpu().numpy()[0], "counts": d_cnts.cpu().numpy()[0]}
         return act, {"log_prob": torch.tensor(0.0).to(self.device, self.dtype)}
+
+
+# ---------------------------------------------------------------------------
+# policy-guided search ("Alpha0.5"): mcts.py:191-323
+# ---------------------------------------------------------------------------
+from torch import nn  # noqa: E402
+
+from ..utils.nets import MultiHeadedMLP  # noqa: E402
+from ..utils.preprocessing import SechsNimmtStateNormalization  # noqa: E402
+
+
+class PolicyMCSAgent(BaseMCAgent):
+    """Monte-Carlo search whose playouts sample every move from a learnable
+    policy (mcts.py:191-261).  The search runs on the GPU (sechs_puct.hip:
+    candidate rows -> policy MLP via PyTorch-ROCm -> select/step kernels);
+    its random numbers are Philox, not numpy/torch's global generators, so
+    runs are statistically -- not bitwise -- equivalent to the reference."""
+
+    _puct_root = False
+
+    def __init__(self, hidden_sizes=(100, 100), activation=nn.ReLU(), r_factor=0.1, **kwargs):
+        super().__init__(**kwargs)
+        self.r_factor = r_factor
+        self.preprocessor = SechsNimmtStateNormalization(action=True)
+        self.actor = MultiHeadedMLP(self.state_length + 1, hidden_sizes=hidden_sizes, head_sizes=(1,),
+                                    activation=activation, head_activations=(None,))
+        self.softmax = nn.Softmax(dim=0)
+        self.search_seed = int(torch.randint(0, 2**62, (1,)).item())
+        self._engine = None
+        self._decisions = 0
+
+    # policy as in mcts.py:219-228 (host torch; also gives the training log-prob)
+    def _compute_policy(self, legal_actions, state):
+        state = torch.as_tensor(state).to(self.device, self.dtype).reshape(-1)
+        cards = torch.tensor(legal_actions, device=self.device).to(self.dtype)[:, None]
+        batch = torch.cat((cards, state[None, :].expand(len(legal_actions), -1)), dim=1)
+        (logits,) = self.actor(self.preprocessor(batch))
+        return self.softmax(logits).flatten()
+
+    def _search_engine(self):
+        from ..puct import BatchedPUCT
+        from ..vec_env import VecSechsNimmtEnv
+
+        if self._engine is None or self._engine.env.num_players != self.num_players:
+            env = VecSechsNimmtEnv(1, self.num_players, seed=0, rng="philox")
+            self._engine = BatchedPUCT(env, self.actor, mc_per_card=self.mc_per_card, mc_max=self.mc_max,
+                                       c_puct=getattr(self, "c_puct", 2.0), seed=self.search_seed, seats_mask=1,
+                                       puct_root=self._puct_root, net_dtype=torch.float32)
+        eng = self._engine
+        eng.mc_per_card, eng.mc_max = self.mc_per_card, self.mc_max
+        eng.c_puct = float(getattr(self, "c_puct", 2.0))
+        return eng
+
+    def _mcts(self, legal_actions, state):
+        nat.require_gpu()
+        eng = self._search_engine()
+        n = len(legal_actions)
+        legal = sorted(int(c) for c in legal_actions)
+        board = self._board_from_state(state, flatten=False)
+        # the other seats' hands are never read by the search (their cards are
+        # dealt from the memory); reset_to only needs n distinct cards each
+        used = set(legal) | {c for row in board for c in row}
+        spare = [c for c in self.available_cards if c not in used] + [c for c in range(104) if c not in used]
+        spare = list(dict.fromkeys(spare))
+        hands = [legal] + [sorted(spare[i * n:(i + 1) * n]) for i in range(self.num_players - 1)]
+        b = np.full((1, ROWS, THRESHOLD), -1, dtype=np.int8)
+        for r, row in enumerate(board):
+            b[0, r, : len(row)] = row
+        h = np.full((1, self.num_players, HAND), -1, dtype=np.int8)
+        for p, hand in enumerate(hands):
+            h[0, p, : len(hand)] = hand
+        eng.env.reset_to(torch.from_numpy(b), torch.from_numpy(h))
+        words = np.zeros(4, dtype=np.uint64)
+        for c in self.available_cards:
+            words[c >> 5] |= np.uint64(1) << np.uint64(c & 31)
+        eng.avail.zero_()
+        eng.avail[:, 0] = torch.from_numpy(words.astype(np.uint32).view(np.int32)).to(eng.avail.device)
+        eng.step_id = self._decisions
+        self._decisions += 1
+        eng.decide(n, memorize=False)
+        best = int(eng.best_index[0].item())
+        probs = self._compute_policy(legal, state)
+        return legal[best], {"log_prob": torch.log(probs[best])}
+
+    # learning (mcts.py:230-261)
+    def learn(self, state, reward, action, done, next_state, next_reward, episode_end, num_episode, legal_actions,
+              *args, **kwargs):
+        self.history.store(log_prob=kwargs["log_prob"], reward=reward * self.r_factor)
+        if not episode_end or not self.training:
+            return 0.0
+        loss = self._train()
+        self.history.clear()
+        return loss
+
+    def _train(self):
+        log_probs = torch.stack(self.history.rollout()["log_prob"], dim=0)
+        loss = -torch.sum(log_probs)
+        self._gradient_step(loss)
+        return loss.item()
+
+    def _gradient_step(self, loss):
+        self.optimizer.zero_grad()
+        loss.backward()
+        self.optimizer.step()
+
+
+class PUCTAgent(PolicyMCSAgent):
+    """PolicyMCSAgent whose root move is chosen by PUCT (mcts.py:264-323)."""
+
+    _puct_root = True
+
+    def __init__(self, c_puct=2.0, temperature=None, **kwargs):
+        super().__init__(**kwargs)
+        self.c_puct = c_puct
+        self.temperature = temperature
+
+    def _mcts(self, legal_actions, state):
+        if self.temperature is not None and self.temperature > 1.0e-12:
+            raise NotImplementedError  # mcts.py:318-323 (quirk Q9)
+        return super()._mcts(legal_actions, state)
+
+    # host forms of the root formulas (mcts.py:295-315), kept for the API
+    def _compute_pucts(self, legal_actions, outcomes, probs):
+        n = np.array([len(outcomes[a]) for a in legal_actions])
+        hi, lo, mid = self._normalize_q(outcomes)
+        q = np.array([np.mean(outcomes[a]) if outcomes[a] else mid for a in legal_actions])
+        with np.errstate(invalid="ignore", divide="ignore"):
+            q = np.clip((q - lo) / (hi - lo), 0.0, 1.0)
+        p = probs.detach().cpu().numpy() if hasattr(probs, "detach") else np.asarray(probs, dtype=np.float32)
+        return q + self.c_puct * p * (n.sum() + 1.0e-9) ** 0.5 / (1.0 + n)
+
+    def _normalize_q(self, outcomes):
+        every = [o for lst in outcomes.values() for o in lst]
+        if len(every) < 10:
+            return 0.0, -10.0, -5.0  # quirk Q8: the "mean" is a median, with this fallback
+        return np.max(every), np.min(every), np.median(every)

@@ -1,0 +1,167 @@
+"""Batched "Alpha0.5" PUCT search on one MI355X (BASELINE config 4).
+
+Reference: PUCTAgent / PolicyMCSAgent (agents/mcts.py:191-323).  A decision
+runs n_mc = min(mc_max, mc_per_card * n!) rollouts; at each rollout's first
+step the deciding seat picks its move by PUCT over the statistics so far,
+every other move is sampled from the policy net, and the return is backed
+up to the root move; finally the move with the best mean return is played.
+
+Here all decisions of a batch (every deciding seat of every game) advance
+together: for each rollout r and rollout step t, the HIP kernels emit the
+normalised candidate rows of every seat, the policy MLP (PyTorch-ROCm,
+bf16 by default) turns them into logits, and sn_puct_step selects / samples,
+plays the step and, at the end, backs up.  Rollouts of one decision stay a
+sequential chain, exactly as in the reference.
+"""
+import math
+
+import torch
+from torch import nn
+
+from . import _native as nat
+from .utils.nets import MultiHeadedMLP
+
+ROW = 48
+
+
+def make_actor(hidden_sizes=(100, 100), activation=None):
+    """the reference's policy net: MultiHeadedMLP(48, (100, 100), (1,), ReLU, (None,))"""
+    return MultiHeadedMLP(ROW, hidden_sizes=hidden_sizes, head_sizes=(1,), activation=activation or nn.ReLU(),
+                          head_activations=(None,))
+
+
+class BatchedPUCT:
+    def __init__(self, env, actor, mc_per_card=10, mc_max=100, c_puct=2.0, seed=0, seats_mask=None, puct_root=True,
+                 net_dtype=torch.bfloat16, mcs_num_cards=104):
+        self.env, self.actor = env, actor
+        self.mc_per_card, self.mc_max, self.c_puct = mc_per_card, mc_max, float(c_puct)
+        self.seed = int(seed)
+        self.puct_root = bool(puct_root)
+        self.net_dtype = net_dtype
+        self.mcs_num_cards = mcs_num_cards
+        B, N, dev = env.num_games, env.num_players, env.device
+        self.seats_mask = ((1 << N) - 1) if seats_mask is None else int(seats_mask)
+        self.M = bin(self.seats_mask & ((1 << N) - 1)).count("1")
+        self.D = B * self.M
+        D = self.D
+        self.avail = torch.zeros((4, B * N), dtype=torch.int32, device=dev)
+        self.ro = torch.zeros((D, 48), dtype=torch.int32, device=dev)
+        self.stats = torch.zeros((D, 24), dtype=torch.int32, device=dev)
+        self.hist = torch.zeros((D, 172), dtype=torch.int32, device=dev)
+        self.root_probs = torch.zeros((D, 10), dtype=torch.float32, device=dev)
+        self.best_index = torch.zeros((D,), dtype=torch.int32, device=dev)
+        self.actions = torch.zeros((B, N), dtype=torch.int32, device=dev)
+        self.step_id = 0
+        self.decisions = []  # (root rows, best index) per decision batch, for learn()
+        self._net = None
+        self._net_version = None
+        self.rows_evaluated = 0
+
+    # ------------------------------------------------------------ policy net on the device
+    def sync_net(self):
+        """(re)build the device copy of the actor in net_dtype"""
+        version = tuple(p._version for p in self.actor.parameters())
+        if self._net is None or version != self._net_version:
+            import copy
+
+            net = copy.deepcopy(self.actor).to(self.env.device, self.net_dtype)
+            net.eval()
+            self._net, self._net_version = net, version
+        return self._net
+
+    def _logits(self, rows):
+        with torch.no_grad():
+            (out,) = self._net(rows)
+        self.rows_evaluated += rows.shape[0]
+        return out.reshape(-1).float().contiguous()
+
+    def n_mc(self, n):
+        return min(self.mc_max, self.mc_per_card * math.factorial(n))
+
+    def _params(self, n, rollout=0):
+        q = nat.SnPuct()
+        q.seats_mask, q.n, q.puct_root, q.c_puct = self.seats_mask, n, int(self.puct_root), self.c_puct
+        q.seed, q.step, q.rollout = self.seed & (2**64 - 1), self.step_id & 0xFFFFFFFF, rollout
+        q.avail, q.rollouts, q.stats = self.avail.data_ptr(), self.ro.data_ptr(), self.stats.data_ptr()
+        q.hist, q.root_probs = self.hist.data_ptr(), self.root_probs.data_ptr()
+        return q
+
+    # ------------------------------------------------------------ one decision per deciding seat
+    def memorize(self):
+        nat.check(nat.lib().sn_mcs_memorize(self.env._h, nat.ptr(self.avail), self.mcs_num_cards, self.env._stream()),
+                  "sn_mcs_memorize")
+
+    def decide(self, n, memorize=True, record=False):
+        """Search every deciding seat at hand size n; returns actions [B, N]
+        (int32, deciding seats filled in)."""
+        L, h, st = nat.lib(), self.env._h, self.env._stream()
+        if memorize:
+            self.memorize()
+        bf16 = int(self.net_dtype == torch.bfloat16)
+        q = self._params(n)
+        if n > 1:
+            self.sync_net()
+            rows = torch.empty((self.D * n, ROW), dtype=self.net_dtype, device=self.env.device)
+            nat.check(L.sn_puct_root_rows(h, ctypes_ref(q), nat.ptr(rows), bf16, st), "sn_puct_root_rows")
+            nat.check(L.sn_puct_init(h, ctypes_ref(q), nat.ptr(self._logits(rows)), st), "sn_puct_init")
+            N = self.env.num_players
+            bufs = {m: torch.empty((self.D * N * m, ROW), dtype=self.net_dtype, device=self.env.device)
+                    for m in range(1, n + 1)}
+            for r in range(self.n_mc(n)):
+                q.rollout = r
+                nat.check(L.sn_puct_deal(h, ctypes_ref(q), st), "sn_puct_deal")
+                for t in range(n):
+                    m = n - t
+                    nat.check(L.sn_puct_rows(h, ctypes_ref(q), m, nat.ptr(bufs[m]), bf16, st), "sn_puct_rows")
+                    nat.check(L.sn_puct_step(h, ctypes_ref(q), nat.ptr(self._logits(bufs[m])), t, m, st), "sn_puct_step")
+        nat.check(L.sn_puct_choose(h, ctypes_ref(q), nat.ptr(self.actions), nat.ptr(self.best_index), st),
+                  "sn_puct_choose")
+        if record and n > 1:
+            self.decisions.append((rows.float(), n, self.best_index.clone()))
+        self.step_id += 1
+        return self.actions
+
+    def play_episode(self, others=None, record=False):
+        """One whole game of every env game; deciding seats search, the other
+        seats (if any) play DrunkHamster moves in-kernel.  Returns the summed
+        rewards [B, N] int32."""
+        env = self.env
+        env.reset()
+        total = torch.zeros((env.num_games, env.num_players), dtype=torch.int32, device=env.device)
+        for t in range(10):
+            acts = self.decide(10 - t, record=record)
+            if self.M < env.num_players:
+                rnd = self._random_moves()
+                keep = torch.tensor([(self.seats_mask >> p) & 1 for p in range(env.num_players)], device=env.device,
+                                    dtype=torch.bool)
+                acts = torch.where(keep[None, :], acts, rnd)
+            rew, done, inv = env.step(acts)
+            total += rew
+        return total
+
+    def _random_moves(self):
+        """uniform legal moves for the non-deciding seats (host-side torch RNG)"""
+        hands = self.env.hands().long()
+        n = (hands >= 0).sum(dim=2)
+        k = (torch.rand(hands.shape[:2], device=hands.device) * n).long().clamp(max=9)
+        return hands.gather(2, k[..., None])[..., 0].to(torch.int32)
+
+    # ------------------------------------------------------------ training (mcts.py:230-261)
+    def policy_loss(self):
+        """-sum over recorded decisions of log pi(chosen root move) under the
+        current weights (the reference stores log(probs[best]) from the
+        rollout that first chose it -- same weights during an episode, so the
+        same value)."""
+        dev_actor = self.actor.to(self.env.device)
+        loss = torch.zeros((), device=self.env.device)
+        for rows, n, best in self.decisions:
+            (logits,) = dev_actor(rows)
+            logp = torch.log_softmax(logits.reshape(-1, n), dim=1)
+            loss = loss - logp.gather(1, best.long()[:, None]).sum()
+        return loss
+
+
+def ctypes_ref(q):
+    import ctypes
+
+    return ctypes.byref(q)

@@ -104,3 +104,60 @@ def test_mcs_agent_memory_bookkeeping():
     assert len(a.available_cards) == 104 - 10 - 4
     assert 50 not in a.available_cards and 0 in a.available_cards
     assert a._compute_n_mc(10) == 100 and a._compute_n_mc(3) == 60 and a._compute_n_mc(2) == 20
+
+
+def test_normalization_golden():
+    import torch
+
+    from rl_6_nimmt.utils.preprocessing import SechsNimmtStateNormalization
+
+    d = load("normalization.json")
+    x = torch.tensor(d["x_with_action"], dtype=torch.float32)
+    assert torch.equal(SechsNimmtStateNormalization(action=True)(x), torch.tensor(d["y_with_action"]))
+    assert torch.equal(SechsNimmtStateNormalization(action=False)(x[:, 1:]), torch.tensor(d["y_without_action"]))
+
+
+def test_policy_golden_with_reference_weights():
+    """PUCTAgent._compute_policy with the reference's own initial weights
+    (torch.manual_seed(0); PUCTAgent()) reproduces its probabilities"""
+    import torch
+
+    from rl_6_nimmt.agents import PUCTAgent
+
+    z = np.load(os.path.join(GOLDEN, "puct_policy.npz"))
+    a = PUCTAgent()
+    sd = {k: torch.from_numpy(z[k]) for k in a.actor.state_dict()}
+    a.actor.load_state_dict(sd)
+    for p in range(4):
+        legal = [int(c) for c in z["legal"][p] if c >= 0]
+        with torch.no_grad():
+            probs = a._compute_policy(legal, torch.tensor(z["states"][p]).float()).numpy()
+        assert np.allclose(probs, z["probs"][p][: len(legal)], rtol=0, atol=1e-7)
+
+
+def test_reference_init_matches():
+    """same module layout and init order as the reference: torch.manual_seed(0); PUCTAgent() gives its weights"""
+    import torch
+
+    from rl_6_nimmt.agents import PUCTAgent
+
+    z = np.load(os.path.join(GOLDEN, "puct_policy.npz"))
+    torch.manual_seed(0)
+    a = PUCTAgent()
+    for k, v in a.actor.state_dict().items():
+        assert np.array_equal(v.numpy(), z[k]), k
+
+
+def test_puct_formulas_golden():
+    from rl_6_nimmt.agents import PUCTAgent
+
+    a = PUCTAgent()
+    d = load("puct_math.json")
+    for c in d["cases"]:
+        legal = c["legal"]
+        outcomes = {x: list(o) for x, o in zip(legal, c["outcomes"])}
+        probs = np.array(c["probs"], dtype=np.float32)
+        pucts = a._compute_pucts(legal, outcomes, probs)
+        ref = [np.nan if v is None else v for v in c["pucts"]]
+        assert np.array_equal(np.asarray(pucts), np.asarray(ref), equal_nan=True)
+        assert [float(v) for v in a._normalize_q(outcomes)] == c["normalize_q"]
