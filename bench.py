@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--no-mcs", action="store_true", help="skip the config-3 MCS leg")
     ap.add_argument("--mcs-games", type=int, default=8192)
     ap.add_argument("--mcs-rollouts", type=int, default=256)
+    ap.add_argument("--no-puct", action="store_true", help="skip the config-4 PUCT leg")
+    ap.add_argument("--puct-games", type=int, default=8192)
     return ap.parse_args()
 
 
@@ -184,6 +186,41 @@ def bench_mcs(games, rollouts, episodes=1):
     }
 
 
+def bench_puct(games, mc_max=100, mc_per_card=10):
+    """BASELINE config 4: Alpha0.5 (PUCT) self-play, every seat of `games`
+    4-player games searches with the reference's defaults (mc_max=100,
+    mc_per_card=10, c_puct=2); the policy MLP runs in bf16 through
+    PyTorch-ROCm.  One whole game per measurement.  Units: playout env-steps
+    (one rollout game advancing one turn) and policy rows (one candidate
+    move scored, 2*(48*100+100*100+100) = 29 800 FLOP)."""
+    from rl_6_nimmt.puct import BatchedPUCT, make_actor
+    from rl_6_nimmt.vec_env import VecSechsNimmtEnv
+
+    env = VecSechsNimmtEnv(games, N_PLAYERS, seed=3, rng="philox")
+    torch.manual_seed(0)
+    eng = BatchedPUCT(env, make_actor(), mc_per_card=mc_per_card, mc_max=mc_max, seed=4, net_dtype=torch.bfloat16)
+    env.reset()
+    eng.decide(2)  # warm-up (kernels, GEMM heuristics)
+    torch.cuda.synchronize()
+    eng.rows_evaluated = 0
+    t0 = time.perf_counter()
+    total = eng.play_episode()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    steps = sum(eng.n_mc(n) * n for n in range(2, 11)) * N_PLAYERS * games
+    return {
+        "workload": f"config4: {games} x 4-player games, all seats PUCT (mc_max={mc_max}, mc_per_card={mc_per_card}, "
+                    f"c_puct=2), bf16 policy MLP 48-100-100-1 via PyTorch-ROCm, 1 game",
+        "value": steps / wall,
+        "unit": "playout env-steps/s",
+        "decisions_per_s": 9 * N_PLAYERS * games / wall,
+        "policy_rows_per_s": eng.rows_evaluated / wall,
+        "policy_tflops": eng.rows_evaluated * 29800 / wall / 1e12,
+        "wall_s": wall,
+        "mean_score_per_seat": total.double().mean(dim=0).tolist(),
+    }
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
@@ -253,6 +290,8 @@ def main():
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.rng)
     if world == 1 and not args.no_mcs:
         result["extra_config3_mcs"] = bench_mcs(args.mcs_games, args.mcs_rollouts)
+    if world == 1 and not args.no_puct:
+        result["extra_config4_puct"] = bench_puct(args.puct_games)
     if args.extras and world == 1:
         env2 = VecSechsNimmtEnv(B, N_PLAYERS, seed=0, rng="philox")
         env2.reset()
