@@ -144,6 +144,9 @@ sn_status sn_mcs_memorize(sn_env* env, uint32_t* avail, int mcs_num_cards, void*
    a multiple of 256. */
 sn_status sn_mcs_rollouts(sn_env* env, const uint32_t* avail, int rollouts, uint64_t seed, uint32_t decision_step,
                           int32_t* sums, void* stream);
+/* same, also writing every playout's return: playouts [B*N][10][rollouts] int32 (may be NULL) */
+sn_status sn_mcs_rollouts_ex(sn_env* env, const uint32_t* avail, int rollouts, uint64_t seed, uint32_t decision_step,
+                             int32_t* sums, int32_t* playouts, void* stream);
 
 /* _choose_action_from_outcomes (mcts.py:156-165) with equal playout counts:
    actions [B][N] int32 = legal[argmax sums] (ties -> lowest card), legal[0]

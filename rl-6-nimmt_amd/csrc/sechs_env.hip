@@ -94,7 +94,7 @@ __global__ __launch_bounds__(kBlock) void k_reset_to(DevState s, const int8_t* b
 }
 
 struct PlayArgs {
-    int steps, flags, obs_stride, pad_;
+    int steps, flags, obs_stride, wave_lds;  // wave_lds: bytes of LDS per wave (dynamic)
     const int32_t* actions;  // [B][N] (steps == 1) or NULL = DrunkHamster
     int32_t* rewards;        // [steps][B][N]
     uint8_t* done;           // [steps][B]
@@ -103,12 +103,23 @@ struct PlayArgs {
     int32_t* invalid;        // [B]
 };
 
+// Each wave owns a private LDS region: the lanes' deal decks, and -- when
+// the observation rows are 48 bytes -- a staging area where the wave's 64
+// rows are assembled so that they leave as 1-KB contiguous stores instead
+// of 64 scattered 16-B pieces per instruction.  (Both uses never overlap in
+// time within a step: observations first, the deal at the very end.)
 template <int N, int MODE>
 __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
-    __shared__ uint8_t lds_deck[kBlock * kDeckStride];
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= s.B) return;
     const int64_t B = s.B;
+    const int lane = threadIdx.x & 63;
+    uint8_t* wave_lds = lds_dyn + (threadIdx.x >> 6) * a.wave_lds;
+    uint8_t* my_deck = wave_lds + lane * kDeckStride;
+    const bool staged = a.obs && a.obs_stride == 48;
+    const int64_t g0 = g - lane;                       // first game of this wave
+    const int wave_games = (int)min((int64_t)64, B - g0);  // = active lanes (lanes past B left)
     Game<N> G;
     load_game<N>(s, g, G);
     typename RngOf<MODE>::T rng;
@@ -124,8 +135,25 @@ __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
             uint32_t w2hi, gw[9];
             if (summ) game_words<true>(N, G.b, w2hi, gw);
             else game_words<false>(N, G.b, w2hi, gw);
+            if (staged) {
+                u32x4* row = (u32x4*)(wave_lds + lane * N * 48);
 #pragma unroll
-            for (int p = 0; p < N; p++) store_obs_row(ob + p * a.obs_stride, G.hand[p], w2hi, gw, a.obs_stride);
+                for (int p = 0; p < N; p++) {
+                    const Hand& h = G.hand[p];
+                    row[3 * p + 0] = u32x4{(uint32_t)h.lo, (uint32_t)(h.lo >> 32), (h.hi & 0xFFFFu) | w2hi, gw[0]};
+                    row[3 * p + 1] = u32x4{gw[1], gw[2], gw[3], gw[4]};
+                    row[3 * p + 2] = u32x4{gw[5], gw[6], gw[7], gw[8]};
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                const u32x4* src = (const u32x4*)wave_lds;
+                u32x4* dst = (u32x4*)(a.obs + ((int64_t)t * B + g0) * N * 48);
+                const int pieces = wave_games * N * 3;
+                for (int i = lane; i < pieces; i += wave_games) dst[i] = src[i];
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            } else {
+#pragma unroll
+                for (int p = 0; p < N; p++) store_obs_row(ob + p * a.obs_stride, G.hand[p], w2hi, gw, a.obs_stride);
+            }
             ob += B * N * a.obs_stride;
         }
         uint32_t card[N], pen[N], idx[N];
@@ -190,7 +218,7 @@ __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
 #pragma unroll
             for (int p = 0; p < N; p++) s.sum_res[(int64_t)p * B + g] -= G.score[p];
             s.episodes[g] += 1;
-            deal_shuffle<N>(rng, buf, lds_deck + threadIdx.x * kDeckStride, s.C, G);
+            deal_shuffle<N>(rng, buf, my_deck, s.C, G);
         }
     }
     store_game<N>(s, g, G);
@@ -370,12 +398,25 @@ sn_status sn_reset_to(sn_env* e, const int8_t* board, const int8_t* hands, void*
     return SN_OK;
 }
 
-static sn_status launch_play(sn_env* e, const PlayArgs& a, hipStream_t st) {
+static sn_status launch_play(sn_env* e, PlayArgs a, hipStream_t st) {
     const DevState& s = e->s;
+    int wave = 64 * kDeckStride;
+    if (a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15) == 0) wave = max(wave, 64 * s.N * 48);
+    a.wave_lds = wave;
+    const size_t shmem = (size_t)wave * (kBlock / 64);
+    if (a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15)) return fail(SN_EINVAL, "obs with stride 48 must be 16-byte aligned");
     if (s.rng_mode == SN_RNG_NUMPY_MT) {
-        SN_DISPATCH_N(s.N, hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_MT>), dim3(grid_for(s.B)), dim3(kBlock), 0, st, s, a));
+        SN_DISPATCH_N(s.N, {
+            HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_MT>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
+            hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_MT>), dim3(grid_for(s.B)), dim3(kBlock), shmem, st, s, a);
+        });
     } else {
-        SN_DISPATCH_N(s.N, hipLaunchKernelGGL((k_play<NN, RNG_PHILOX>), dim3(grid_for(s.B)), dim3(kBlock), 0, st, s, a));
+        SN_DISPATCH_N(s.N, {
+            HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_PHILOX>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)shmem));
+            hipLaunchKernelGGL((k_play<NN, RNG_PHILOX>), dim3(grid_for(s.B)), dim3(kBlock), shmem, st, s, a);
+        });
     }
     HIP_TRY(hipGetLastError());
     return SN_OK;

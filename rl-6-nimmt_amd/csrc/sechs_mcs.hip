@@ -36,7 +36,8 @@ __global__ void k_mcs_memorize(DevState s, uint32_t* avail, int mcs_cards) {
 struct McsArgs {
     const uint32_t* avail;  // [4][B*N]
     int32_t* sums;          // [B*N][10]
-    uint32_t seed_lo, seed_hi, step, pad_;
+    int32_t* playouts;      // optional [B*N][10][R]: every playout's return
+    uint32_t seed_lo, seed_hi, step, rollouts;
 };
 
 // one playout (mcts.py:108-154) from decision (g, p) with first move legal[a]
@@ -98,6 +99,7 @@ __global__ __launch_bounds__(kBlock) void k_mcs_rollouts(DevState s, McsArgs a) 
     const uint64_t stream = ((uint64_t)(uint32_t)gid << 32) | ((uint64_t)p << 24) | ((uint64_t)act << 16) | r;
     gen.load(a.seed_lo ^ a.step, a.seed_hi, stream, 0ull, buf);
     int32_t v = playout<N>(gen, buf, root, me, n, av, act);
+    if (a.playouts) a.playouts[(dec * kHand + act) * a.rollouts + r] = v;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     if ((threadIdx.x & 63u) == 0u) part[threadIdx.x >> 6] = v;
@@ -373,8 +375,8 @@ sn_status sn_mcs_memorize(sn_env* e, uint32_t* avail, int mcs_num_cards, void* s
     return SN_OK;
 }
 
-sn_status sn_mcs_rollouts(sn_env* e, const uint32_t* avail, int rollouts, uint64_t seed, uint32_t decision_step,
-                          int32_t* sums, void* stream) {
+sn_status sn_mcs_rollouts_ex(sn_env* e, const uint32_t* avail, int rollouts, uint64_t seed, uint32_t decision_step,
+                             int32_t* sums, int32_t* playouts, void* stream) {
     if (!e || !avail || !sums) return set_error(SN_EINVAL, "NULL argument");
     if (rollouts < 64 || rollouts > 65536 || (rollouts & 63) || (rollouts > kBlock && rollouts % kBlock))
         return set_error(SN_EINVAL, "rollouts must be 64, 128, 192 or a multiple of 256 (<= 65536)");
@@ -383,6 +385,8 @@ sn_status sn_mcs_rollouts(sn_env* e, const uint32_t* avail, int rollouts, uint64
     McsArgs a{};
     a.avail = avail;
     a.sums = sums;
+    a.playouts = playouts;
+    a.rollouts = (uint32_t)rollouts;
     a.seed_lo = (uint32_t)seed, a.seed_hi = (uint32_t)(seed >> 32), a.step = decision_step;
     const unsigned block = rollouts < kBlock ? (unsigned)rollouts : (unsigned)kBlock;
     const dim3 grid((unsigned)(s.B * s.N), kHand, (unsigned)rollouts / block);
@@ -391,6 +395,11 @@ sn_status sn_mcs_rollouts(sn_env* e, const uint32_t* avail, int rollouts, uint64
     SN_DISPATCH_N(s.N, hipLaunchKernelGGL((k_mcs_rollouts<NN>), grid, dim3(block), 0, st, s, a));
     HIP_TRY(hipGetLastError());
     return SN_OK;
+}
+
+sn_status sn_mcs_rollouts(sn_env* e, const uint32_t* avail, int rollouts, uint64_t seed, uint32_t decision_step,
+                          int32_t* sums, void* stream) {
+    return sn_mcs_rollouts_ex(e, avail, rollouts, seed, decision_step, sums, nullptr, stream);
 }
 
 sn_status sn_mcs_choose(sn_env* e, const int32_t* sums, int32_t* actions, void* stream) {

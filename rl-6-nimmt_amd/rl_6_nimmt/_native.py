@@ -66,6 +66,7 @@ SIGNATURES = {
     "sn_philox_counter": ([_P, _I64, _P], _I),
     "sn_mcs_memorize": ([_P, _P, _I, _P], _I),
     "sn_mcs_rollouts": ([_P, _P, _I, _U64, ctypes.c_uint32, _P, _P], _I),
+    "sn_mcs_rollouts_ex": ([_P, _P, _I, _U64, ctypes.c_uint32, _P, _P, _P], _I),
     "sn_mcs_choose": ([_P, _P, _P, _P], _I),
     "sn_mcs_play_exact": ([_P, ctypes.c_uint32, _I, _I, _P, _P, _P, _P], _I),
     "sn_mcs_decide_exact": ([_I, _I64, _I, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P], _I),
