@@ -390,10 +390,19 @@ __device__ __forceinline__ uint32_t rng_interval(G& gen, ByteBuf& buf, uint32_t 
 //  direct (bit 31 = 1): the array is one whole twisted round as
 //    np.random.get_state() returns it; pos = next word to hand out.
 //  cnt = words just before pos that were generated but not consumed (the
-//    buffer).  A round boundary is only crossed with an empty buffer, so
-//    [pos-cnt, pos) never straddles rounds and the state always converts
-//    back to numpy's (key, pos) form.
+//    buffer).  The saved state never straddles a round, so it always
+//    converts back to numpy's (key, pos) form.
 // np.random.seed(s) == init_genrand(s) with code 0.
+//
+// Round boundary.  A lane that reaches word 624 with words of the old round
+// still buffered twists the new round's chunk 0 into registers but holds the
+// store back ("straddle"): mt[0..8) keeps the old round's values until the
+// old words are consumed (then the chunk is committed).  A launch that ends
+// mid-straddle drops the held-back chunk -- it is a pure function of the old
+// round and is twisted again, identically, by the next launch.  (The first
+// version stopped refilling instead, so every lane of a wave drained its
+// buffer and refilled alone: one divergent pass per lane, +55 % VALU in the
+// episodes that crossed a round.)
 constexpr uint32_t kMtDirect = 0x80000000u;
 
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
@@ -409,51 +418,32 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c) {
     return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
 }
 
-struct MtGen {
-    uint32_t* st;
-    uint32_t pos, direct;
-    // Inputs of the next lazy refill, loaded one refill ahead: chunk
-    // c = (pos == 624 ? 0 : pos) needs mt[c..c+8), mt[c+8] and the run
-    // mt[j+397] (j < 227) / mt[j-227] (j >= 227), j = c..c+7 -- words the
-    // current refill does not write -- so their latency hides behind the
-    // draws in between.  (At a round's end the next round's chunk 0 is
-    // prefetched: its inputs are final by then.)
-    u32x4 pa0, pa1, pr0, pr1, pr2;
-    uint32_t pa8;
-
-    __device__ __forceinline__ void prefetch(uint32_t c) {
-        pa0 = *(const u32x4*)(st + c);
-        pa1 = *(const u32x4*)(st + c + 4);
-        pa8 = st[(c + 8u == (uint32_t)kMtN) ? 0u : c + 8u];
-        // the run starts at s = 1 (mod 4); read it as three aligned x4 from
-        // s-1, s+3, s+7 (mod 624: the chunk at 224 wraps 621..623 -> 0..4)
-        const uint32_t s = (c < (uint32_t)(kMtN - kMtM)) ? c + kMtM : c - (uint32_t)(kMtN - kMtM);
-        const uint32_t b1 = (s + 3u >= (uint32_t)kMtN) ? s + 3u - kMtN : s + 3u;
-        const uint32_t b2 = (s + 7u >= (uint32_t)kMtN) ? s + 7u - kMtN : s + 7u;
-        pr0 = *(const u32x4*)(st + s - 1u);
-        pr1 = *(const u32x4*)(st + b1);
-        pr2 = *(const u32x4*)(st + b2);
-    }
-
-    __device__ __forceinline__ void load(uint32_t* state, uint32_t code, ByteBuf& buf) {
-        st = state;
-        pos = code & 0x7FFu;
-        direct = code >> 31;
-        const uint32_t cnt = (code >> 16) & 0x3Fu;
-        buf.clear();
-        for (uint32_t k = 0; k < cnt; k++) buf.append(mt_temper(st[pos - cnt + k]) & 0xFFu, 1u);
-        prefetch((direct || pos == (uint32_t)kMtN) ? 0u : pos);
-    }
-    __device__ __forceinline__ uint32_t save(const ByteBuf& buf) const {
-        return pos | (buf.cnt << 16) | (direct << 31);
-    }
-    // one batch of words; false if the round boundary needs an empty buffer
-    __device__ __forceinline__ bool gen(ByteBuf& buf);
-    __device__ __forceinline__ void topup(ByteBuf& buf) {
-        if (buf.cnt <= 24u) gen(buf);
-    }
-    __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf); }  // cnt == 0: always succeeds
+// Inputs of one lazy refill of chunk c (8 words): mt[c..c+8), mt[c+8] and
+// the run mt[j+397] (j < 227) / mt[j-227] (j >= 227), j = c..c+7.  None of
+// them is written by the refills of the next 224 words, so they can be
+// loaded refills ahead and their latency hides behind the draws in between.
+struct MtPre {
+    u32x4 a0, a1, r0, r1, r2;
+    uint32_t a8;
 };
+
+__device__ __forceinline__ uint32_t mt_next_chunk(uint32_t c) { return (c + 8u == (uint32_t)kMtN) ? 0u : c + 8u; }
+
+__device__ __forceinline__ MtPre mt_prefetch(const uint32_t* st, uint32_t c) {
+    MtPre p;
+    p.a0 = *(const u32x4*)(st + c);
+    p.a1 = *(const u32x4*)(st + c + 4);
+    p.a8 = st[(c + 8u == (uint32_t)kMtN) ? 0u : c + 8u];
+    // the run starts at s = 1 (mod 4); read it as three aligned x4 from
+    // s-1, s+3, s+7 (mod 624: the chunk at 224 wraps 621..623 -> 0..4)
+    const uint32_t s = (c < (uint32_t)(kMtN - kMtM)) ? c + kMtM : c - (uint32_t)(kMtN - kMtM);
+    const uint32_t b1 = (s + 3u >= (uint32_t)kMtN) ? s + 3u - kMtN : s + 3u;
+    const uint32_t b2 = (s + 7u >= (uint32_t)kMtN) ? s + 7u - kMtN : s + 7u;
+    p.r0 = *(const u32x4*)(st + s - 1u);
+    p.r1 = *(const u32x4*)(st + b1);
+    p.r2 = *(const u32x4*)(st + b2);
+    return p;
+}
 
 // Direct mode (only after importing a numpy state mid-round): hand out the
 // remaining words of the imported round; scalar arguments only, out of line.
@@ -462,50 +452,115 @@ struct MtSlow {
     uint32_t k, pos, direct;
 };
 
-static __device__ __noinline__ MtSlow mt_direct(const uint32_t* st, uint32_t pos, uint32_t bufcnt) {
+static __device__ __noinline__ MtSlow mt_direct(const uint32_t* st, uint32_t pos) {
     MtSlow o{0ull, 0u, pos, 1u};
     if (pos < (uint32_t)kMtN) {
         const uint32_t k = min(8u, (uint32_t)kMtN - pos);
         for (uint32_t i = 0; i < k; i++) o.bytes |= (uint64_t)(mt_temper(st[pos + i]) & 0xFFu) << (8u * i);
         o.k = k, o.pos = pos + k;
-    } else if (bufcnt == 0u) {
-        o.direct = 0u, o.pos = (uint32_t)kMtN;  // round used up: lazy twist from chunk 0 on
+    } else {
+        // imported round used up: a whole twisted round == lazy code pos 624
+        o.direct = 0u, o.pos = (uint32_t)kMtN;
     }
     return o;
 }
 
-__device__ __forceinline__ bool MtGen::gen(ByteBuf& buf) {
+// D = refills whose inputs are in flight (1 keeps the register footprint of
+// the latency-tolerant search kernels small; the env kernel, alone on its
+// SIMD, takes 2).
+template <int D>
+struct MtGenT {
+    uint32_t* st;
+    uint32_t pos, direct, straddle;
+    u32x4 pn0, pn1;  // held-back chunk 0 of the next round (straddle)
+    MtPre pf[D];     // pf[k] = inputs of the (k+1)-th next lazy refill
+
+    __device__ __forceinline__ void load(uint32_t* state, uint32_t code, ByteBuf& buf) {
+        st = state;
+        pos = code & 0x7FFu;
+        direct = code >> 31;
+        straddle = 0u;
+        const uint32_t cnt = (code >> 16) & 0x3Fu;
+        buf.clear();
+        for (uint32_t k = 0; k < cnt; k++) buf.append(mt_temper(st[pos - cnt + k]) & 0xFFu, 1u);
+        uint32_t c = (direct || pos == (uint32_t)kMtN) ? 0u : pos;
+#pragma unroll
+        for (int k = 0; k < D; k++) {
+            pf[k] = mt_prefetch(st, c);
+            c = mt_next_chunk(c);
+        }
+    }
+    // state code for mt_pos[]; commits or drops a held-back chunk
+    __device__ __forceinline__ uint32_t save(const ByteBuf& buf) {
+        if (straddle) {
+            if (buf.cnt > 8u) return (uint32_t)kMtN | ((buf.cnt - 8u) << 16);  // old words left: drop the chunk
+            *(u32x4*)(st) = pn0;
+            *(u32x4*)(st + 4) = pn1;
+            return 8u | (buf.cnt << 16);
+        }
+        return pos | (buf.cnt << 16) | (direct << 31);
+    }
+    // one batch of words; false if it cannot run now (direct mode at the end
+    // of a round's words, or a straddle whose old words are still buffered)
+    __device__ __forceinline__ bool gen(ByteBuf& buf);
+    __device__ __forceinline__ void topup(ByteBuf& buf) {
+        if (buf.cnt <= 24u) gen(buf);
+    }
+    __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf); }  // cnt == 0: always succeeds
+};
+
+template <int D>
+__device__ __forceinline__ bool MtGenT<D>::gen(ByteBuf& buf) {
     if (direct) {
-        const MtSlow o = mt_direct(st, pos, buf.cnt);
+        const MtSlow o = mt_direct(st, pos);
         pos = o.pos, direct = o.direct;
-        if (o.k) buf.append(o.bytes, o.k);
-        return o.k != 0u;
+        if (o.k) {
+            buf.append(o.bytes, o.k);
+            return true;
+        }
+        // fall through: the lazy twist of the next round (pos == 624)
     }
-    uint32_t i = pos;
-    if (i == (uint32_t)kMtN) {
-        if (buf.cnt) return false;  // cross a round boundary only with an empty buffer
-        i = 0u;
+    if (straddle) {
+        if (buf.cnt > 8u) return false;
+        *(u32x4*)(st) = pn0;  // old round consumed: commit chunk 0
+        *(u32x4*)(st + 4) = pn1;
+        straddle = 0u;
     }
+    const bool wrap = (pos == (uint32_t)kMtN);
+    const uint32_t i = wrap ? 0u : pos;
+    const MtPre& p = pf[0];
     u32x4 n0, n1;
-    n0.x = mt_mix(pa0.x, pa0.y, pr0.y);
-    n0.y = mt_mix(pa0.y, pa0.z, pr0.z);
-    n0.z = mt_mix(pa0.z, pa0.w, pr0.w);
-    n0.w = mt_mix(pa0.w, pa1.x, pr1.x);
-    n1.x = mt_mix(pa1.x, pa1.y, pr1.y);
-    n1.y = mt_mix(pa1.y, pa1.z, pr1.z);
-    n1.z = mt_mix(pa1.z, pa1.w, pr1.w);
-    n1.w = mt_mix(pa1.w, pa8, pr2.x);
-    *(u32x4*)(st + i) = n0;
-    *(u32x4*)(st + i + 4) = n1;
+    n0.x = mt_mix(p.a0.x, p.a0.y, p.r0.y);
+    n0.y = mt_mix(p.a0.y, p.a0.z, p.r0.z);
+    n0.z = mt_mix(p.a0.z, p.a0.w, p.r0.w);
+    n0.w = mt_mix(p.a0.w, p.a1.x, p.r1.x);
+    n1.x = mt_mix(p.a1.x, p.a1.y, p.r1.y);
+    n1.y = mt_mix(p.a1.y, p.a1.z, p.r1.z);
+    n1.z = mt_mix(p.a1.z, p.a1.w, p.r1.w);
+    n1.w = mt_mix(p.a1.w, p.a8, p.r2.x);
+    if (wrap && buf.cnt) {
+        pn0 = n0, pn1 = n1, straddle = 1u;
+    } else {
+        *(u32x4*)(st + i) = n0;
+        *(u32x4*)(st + i + 4) = n1;
+    }
     const uint64_t lo = (uint64_t)((mt_temper(n0.x) & 0xFFu) | ((mt_temper(n0.y) & 0xFFu) << 8) |
                                    ((mt_temper(n0.z) & 0xFFu) << 16) | (mt_temper(n0.w) << 24));
     const uint64_t hi = (uint64_t)((mt_temper(n1.x) & 0xFFu) | ((mt_temper(n1.y) & 0xFFu) << 8) |
                                    ((mt_temper(n1.z) & 0xFFu) << 16) | (mt_temper(n1.w) << 24));
     buf.append(lo | (hi << 32), 8u);
     pos = i + 8u;
-    prefetch(pos == (uint32_t)kMtN ? 0u : pos);
+    uint32_t c = mt_next_chunk(i);
+#pragma unroll
+    for (int k = 0; k + 1 < D; k++) {
+        pf[k] = pf[k + 1];
+        c = mt_next_chunk(c);
+    }
+    pf[D - 1] = mt_prefetch(st, c);
     return true;
 }
+
+using MtGen = MtGenT<1>;
 
 // ---- Philox4x32-10 counter-based stream -----------------------------------
 // word w of game s = philox({w/4 lo, w/4 hi, s lo, s hi}, seed)[w % 4]

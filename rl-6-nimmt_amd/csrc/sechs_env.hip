@@ -93,8 +93,13 @@ __global__ __launch_bounds__(kBlock) void k_reset_to(DevState s, const int8_t* b
     store_game<N>(s, g, G);
 }
 
+// MT19937 refills whose inputs are in flight in k_play (one wave per SIMD
+// at B = 65 536: nothing else hides the latency)
+constexpr int kPlayPrefetch = 2;
+
 struct PlayArgs {
     int steps, flags, obs_stride, wave_lds;  // wave_lds: bytes of LDS per wave (dynamic)
+    int vec_out;             // rewards 16-B and actions 4-B aligned: one store per lane each (N == 4)
     const int32_t* actions;  // [B][N] (steps == 1) or NULL = DrunkHamster
     int32_t* rewards;        // [steps][B][N]
     uint8_t* done;           // [steps][B]
@@ -122,9 +127,17 @@ __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
     const int wave_games = (int)min((int64_t)64, B - g0);  // = active lanes (lanes past B left)
     Game<N> G;
     load_game<N>(s, g, G);
-    typename RngOf<MODE>::T rng;
+    typename RngOf<MODE, kPlayPrefetch>::T rng;
     ByteBuf buf;
-    RngOf<MODE>::load(s, g, rng, buf);
+    RngOf<MODE, kPlayPrefetch>::load(s, g, rng, buf);
+    // episode results stay in registers for the launch (one load, one store)
+    const bool auto_reset = (a.flags & SN_AUTO_RESET) != 0;
+    int32_t sum_res[N], episodes = 0;
+    if (auto_reset) {
+#pragma unroll
+        for (int p = 0; p < N; p++) sum_res[p] = s.sum_res[(int64_t)p * B + g];
+        episodes = s.episodes[g];
+    }
     const bool summ = !(a.flags & SN_NO_SUMMARIES);
     int32_t* rew = a.rewards ? a.rewards + g * N : nullptr;
     uint8_t* act = a.actions_out ? a.actions_out + g * N : nullptr;
@@ -200,29 +213,42 @@ __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
         G.n -= 1u;
         const bool done = (G.n == 0u);  // env.py:246-249
         if (rew) {
+            if (N == 4 && a.vec_out) {  // one 16-B store per lane: 1 KB contiguous per wave
+                *(u32x4*)rew = u32x4{-pen[0], -pen[1 % N], -pen[2 % N], -pen[3 % N]};
+            } else {
 #pragma unroll
-            for (int p = 0; p < N; p++) rew[p] = -(int32_t)pen[p];
+                for (int p = 0; p < N; p++) rew[p] = -(int32_t)pen[p];
+            }
             rew += B * N;
         }
         if (act) {
+            if (N == 4 && a.vec_out) {
+                *(uint32_t*)act = card[0] | (card[1 % N] << 8) | (card[2 % N] << 16) | (card[3 % N] << 24);
+            } else {
 #pragma unroll
-            for (int p = 0; p < N; p++) act[p] = (uint8_t)card[p];
+                for (int p = 0; p < N; p++) act[p] = (uint8_t)card[p];
+            }
             act += B * N;
         }
         if (dn) {
             *dn = done ? 1 : 0;
             dn += B;
         }
-        if (done && (a.flags & SN_AUTO_RESET)) {
+        if (done && auto_reset) {
             // GameSession.results.append(scores) then the next play_game()
 #pragma unroll
-            for (int p = 0; p < N; p++) s.sum_res[(int64_t)p * B + g] -= G.score[p];
-            s.episodes[g] += 1;
+            for (int p = 0; p < N; p++) sum_res[p] -= G.score[p];
+            episodes += 1;
             deal_shuffle<N>(rng, buf, my_deck, s.C, G);
         }
     }
     store_game<N>(s, g, G);
-    RngOf<MODE>::store(s, g, rng, buf);
+    RngOf<MODE, kPlayPrefetch>::store(s, g, rng, buf);
+    if (auto_reset) {
+#pragma unroll
+        for (int p = 0; p < N; p++) s.sum_res[(int64_t)p * B + g] = sum_res[p];
+        s.episodes[g] = episodes;
+    }
 }
 
 // obs in any dtype, one thread per (game, seat)
@@ -403,6 +429,7 @@ static sn_status launch_play(sn_env* e, PlayArgs a, hipStream_t st) {
     int wave = 64 * kDeckStride;
     if (a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15) == 0) wave = max(wave, 64 * s.N * 48);
     a.wave_lds = wave;
+    a.vec_out = ((((uintptr_t)a.rewards) & 15) == 0) && ((((uintptr_t)a.actions_out) & 3) == 0);
     const size_t shmem = (size_t)wave * (kBlock / 64);
     if (a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15)) return fail(SN_EINVAL, "obs with stride 48 must be 16-byte aligned");
     if (s.rng_mode == SN_RNG_NUMPY_MT) {

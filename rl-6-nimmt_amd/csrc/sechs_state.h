@@ -44,20 +44,21 @@ constexpr int kBlock = 256;
 constexpr int kDeckStride = 108;  // 27 dwords: odd dword stride -> conflict-free LDS lanes
 
 // ---------------------------------------------------------------- rng glue
-template <int MODE>
+// PF = MT19937 refills prefetched ahead (MtGenT); Philox ignores it.
+template <int MODE, int PF = 1>
 struct RngOf;
-template <>
-struct RngOf<RNG_NUMPY_MT> {
-    using T = MtGen;
+template <int PF>
+struct RngOf<RNG_NUMPY_MT, PF> {
+    using T = MtGenT<PF>;
     static __device__ __forceinline__ void load(const DevState& s, int64_t g, T& r, ByteBuf& buf) {
         r.load(s.mt + g * kMtN, s.mt_pos[g], buf);
     }
-    static __device__ __forceinline__ void store(const DevState& s, int64_t g, const T& r, const ByteBuf& buf) {
+    static __device__ __forceinline__ void store(const DevState& s, int64_t g, T& r, const ByteBuf& buf) {
         s.mt_pos[g] = r.save(buf);
     }
 };
-template <>
-struct RngOf<RNG_PHILOX> {
+template <int PF>
+struct RngOf<RNG_PHILOX, PF> {
     using T = PhiloxGen;
     static __device__ __forceinline__ void load(const DevState& s, int64_t g, T& r, ByteBuf& buf) {
         r.load((uint32_t)s.seed, (uint32_t)(s.seed >> 32), s.game_offset + (uint64_t)g, s.ctr[g], buf);

@@ -264,3 +264,47 @@ def test_numpy_rng_bridge_roundtrip():
     assert [int(x) for x in b[:, 0]] == [int(deck[103 - r]) for r in range(4)]
     k2, p2 = env.get_mt_state(0)
     assert np.array_equal(k2, rs.get_state()[1]) and p2 == rs.get_state()[2]
+
+
+def _np_form(key, pos):
+    """(key, pos) with a pending twist applied, so equal streams compare equal."""
+    key = np.array(key, dtype=np.uint32)
+    if pos < 624:
+        return key, pos
+    rs = np.random.RandomState()
+    rs.set_state(("MT19937", key, 624, 0, 0.0))
+    rs.randint(0, 2**32, size=1, dtype=np.uint64)  # forces the twist, consumes word 0
+    k2, p2 = rs.get_state()[1:3]
+    return np.array(k2, dtype=np.uint32), p2 - 1
+
+
+def test_mt_state_across_round_boundaries_every_step():
+    """Single-step launches: after every env-step the exported MT19937 state
+    of every game equals the oracle's numpy state, across several 624-word
+    rounds (launches end mid-straddle for some games), and after importing a
+    mid-round numpy state that runs out during the next episodes."""
+    B, N, seed = 64, 4, 7
+    env = venv(B, N, seed=seed, rng="numpy")
+    env.reset()
+    ref = O.VecOracle(B, N, rng_mode=O.RNG_NUMPY_MT, seed=seed)
+    ref.reset()
+    rngs = ref.v.contents.rngs
+    for t in range(90):
+        if t == 45:  # import a state 20 words before the end of its round into games 0..7
+            rs = np.random.RandomState(1234 + t)
+            rs.randint(0, 2**32, size=604, dtype=np.uint64)
+            key, pos = rs.get_state()[1:3]
+            for g in range(8):
+                env.set_mt_state(key, pos, game=g)
+                for i in range(624):
+                    rngs[g].mt[i] = int(key[i])
+                rngs[g].pos = int(pos)
+        out = env.rollout(1, want_actions=True)
+        rr, rd, ra, _ = ref.rollout(1)
+        torch.cuda.synchronize()
+        assert np.array_equal(out["actions"].cpu().numpy(), ra), t
+        assert np.array_equal(out["rewards"].cpu().numpy(), rr), t
+        for g in range(B):
+            k, p = _np_form(*env.get_mt_state(g))
+            rk, rp = _np_form(np.frombuffer(bytes(rngs[g].mt), dtype=np.uint32), rngs[g].pos)
+            assert p == rp and np.array_equal(k, rk), (t, g)
