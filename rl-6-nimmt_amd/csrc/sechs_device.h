@@ -382,28 +382,60 @@ __device__ __forceinline__ uint32_t rng_interval(G& gen, ByteBuf& buf, uint32_t 
     }
 }
 
+// K draws with the same max (DrunkHamster for every seat of one step,
+// agents/random.py:9 called in seat order, play.py:38-41): the accepted
+// bytes of one 8-word window are the next draws in order, so the common
+// case takes all K from one SWAR compare; draws the window could not
+// supply fall back to rng_interval.
+template <int K, class G>
+__device__ __forceinline__ void rng_draws(G& gen, ByteBuf& buf, uint32_t max, uint32_t (&out)[K]) {
+    if (max == 0u) {
+#pragma unroll
+        for (int k = 0; k < K; k++) out[k] = 0u;
+        return;
+    }
+    if (__any(buf.cnt < 8u)) gen.topup(buf);
+    if (buf.cnt == 0u) gen.force(buf);
+    const uint32_t mask = 0xFFFFFFFFu >> __builtin_clz(max);
+    const uint32_t valid = min(buf.cnt, 8u);
+    const uint64_t vmask = (valid >= 8u) ? ~0ull : ((1ull << (8u * valid)) - 1ull);
+    const uint64_t x = buf.b0 & (0x0101010101010101ull * (uint64_t)mask);
+    uint64_t t = swar_le_mask(x, max) & vmask;
+    uint32_t got = 0u, last = 0u;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const bool has = t != 0ull;
+        const uint32_t pos = (uint32_t)__builtin_ctzll(t | (1ull << 63));  // bit index (8*byte + 7)
+        out[k] = (uint32_t)(x >> (pos & 56u)) & 0xFFu;
+        t &= t - 1ull;
+        last = has ? pos : last;
+        got += has ? 1u : 0u;
+    }
+    // consumed: through the K-th accepted word, or the whole window
+    buf.drop(got == (uint32_t)K ? (last >> 3) + 1u : valid);
+#pragma unroll
+    for (int k = 0; k < K; k++)
+        if ((uint32_t)k >= got) out[k] = rng_interval(gen, buf, max);
+}
+
 // ---- numpy legacy MT19937, twisted lazily 8 words at a time ---------------
-// State code (mt_pos[g]): bits 0..10 pos, 16..21 cnt, bit 31 direct.
-//  lazy (bit 31 = 0): words [0,pos) of the game's 624 hold this round's
-//    values, [pos,624) the previous round's (numpy's in-place twist order,
-//    done 8 words at a time as draws need them).
-//  direct (bit 31 = 1): the array is one whole twisted round as
-//    np.random.get_state() returns it; pos = next word to hand out.
-//  cnt = words just before pos that were generated but not consumed (the
-//    buffer).  The saved state never straddles a round, so it always
-//    converts back to numpy's (key, pos) form.
-// np.random.seed(s) == init_genrand(s) with code 0.
+// State code (mt_pos[g]): bits 0..10 pos, bits 16..25 cnt.
+//  Words [0,pos) of the game's 624 hold this round's values, [pos,624) the
+//  previous round's (numpy's in-place twist order, done 8 words at a time
+//  as draws need them; pos = 624: the round is complete).
+//  cnt = words just before pos that were twisted but not consumed yet: the
+//  stream continues with st[pos-cnt .. pos), then twists on.  The saved
+//  state never straddles a round, so it always converts back to numpy's
+//  (key, pos) form: np.random.seed(s) == init_genrand(s) with code 0, and an
+//  imported numpy (key, p) is code 624 | (624 - p) << 16.
 //
 // Round boundary.  A lane that reaches word 624 with words of the old round
 // still buffered twists the new round's chunk 0 into registers but holds the
 // store back ("straddle"): mt[0..8) keeps the old round's values until the
 // old words are consumed (then the chunk is committed).  A launch that ends
 // mid-straddle drops the held-back chunk -- it is a pure function of the old
-// round and is twisted again, identically, by the next launch.  (The first
-// version stopped refilling instead, so every lane of a wave drained its
-// buffer and refilled alone: one divergent pass per lane, +55 % VALU in the
-// episodes that crossed a round.)
-constexpr uint32_t kMtDirect = 0x80000000u;
+// round and is twisted again, identically, by the next launch.
+constexpr uint32_t kMtCntMask = 0x3FFu;
 
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     y ^= y >> 11;
@@ -420,11 +452,12 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c) {
 
 // Inputs of one lazy refill of chunk c (8 words): mt[c..c+8), mt[c+8] and
 // the run mt[j+397] (j < 227) / mt[j-227] (j >= 227), j = c..c+7.  None of
-// them is written by the refills of the next 224 words, so they can be
-// loaded refills ahead and their latency hides behind the draws in between.
+// them is written by the refills of the next 224 words.  Every loaded word
+// is used: a dead lane of a vector load lets the register allocator reuse
+// its register at once, which forces an s_waitcnt on the whole load.
 struct MtPre {
-    u32x4 a0, a1, r0, r1, r2;
-    uint32_t a8;
+    u32x4 a0, a1, r1;
+    uint32_t a8, r00, r01, r02, r03;
 };
 
 __device__ __forceinline__ uint32_t mt_next_chunk(uint32_t c) { return (c + 8u == (uint32_t)kMtN) ? 0u : c + 8u; }
@@ -434,133 +467,151 @@ __device__ __forceinline__ MtPre mt_prefetch(const uint32_t* st, uint32_t c) {
     p.a0 = *(const u32x4*)(st + c);
     p.a1 = *(const u32x4*)(st + c + 4);
     p.a8 = st[(c + 8u == (uint32_t)kMtN) ? 0u : c + 8u];
-    // the run starts at s = 1 (mod 4); read it as three aligned x4 from
-    // s-1, s+3, s+7 (mod 624: the chunk at 224 wraps 621..623 -> 0..4)
+    // the run starts at s = 1 (mod 4): s..s+2 (never past 623), s+3 (mod
+    // 624, aligned), s+4..s+7 (mod 624: the chunk at 224 wraps to 1..4)
     const uint32_t s = (c < (uint32_t)(kMtN - kMtM)) ? c + kMtM : c - (uint32_t)(kMtN - kMtM);
-    const uint32_t b1 = (s + 3u >= (uint32_t)kMtN) ? s + 3u - kMtN : s + 3u;
-    const uint32_t b2 = (s + 7u >= (uint32_t)kMtN) ? s + 7u - kMtN : s + 7u;
-    p.r0 = *(const u32x4*)(st + s - 1u);
-    p.r1 = *(const u32x4*)(st + b1);
-    p.r2 = *(const u32x4*)(st + b2);
+    const uint32_t s3 = (s + 3u >= (uint32_t)kMtN) ? s + 3u - kMtN : s + 3u;
+    const uint32_t s4 = (s + 4u >= (uint32_t)kMtN) ? s + 4u - kMtN : s + 4u;
+    p.r00 = st[s];
+    p.r01 = st[s + 1u];
+    p.r02 = st[s + 2u];
+    p.r03 = st[s3];
+    p.r1 = u32x4{st[s4], st[s4 + 1u], st[s4 + 2u], st[s4 + 3u]};
     return p;
 }
 
-// Direct mode (only after importing a numpy state mid-round): hand out the
-// remaining words of the imported round; scalar arguments only, out of line.
-struct MtSlow {
-    uint64_t bytes;
-    uint32_t k, pos, direct;
-};
-
-static __device__ __noinline__ MtSlow mt_direct(const uint32_t* st, uint32_t pos) {
-    MtSlow o{0ull, 0u, pos, 1u};
-    if (pos < (uint32_t)kMtN) {
-        const uint32_t k = min(8u, (uint32_t)kMtN - pos);
-        for (uint32_t i = 0; i < k; i++) o.bytes |= (uint64_t)(mt_temper(st[pos + i]) & 0xFFu) << (8u * i);
-        o.k = k, o.pos = pos + k;
-    } else {
-        // imported round used up: a whole twisted round == lazy code pos 624
-        o.direct = 0u, o.pos = (uint32_t)kMtN;
-    }
-    return o;
+// the 8 new words of a chunk from its inputs
+__device__ __forceinline__ void mt_twist8(const MtPre& p, u32x4& n0, u32x4& n1) {
+    n0.x = mt_mix(p.a0.x, p.a0.y, p.r00);
+    n0.y = mt_mix(p.a0.y, p.a0.z, p.r01);
+    n0.z = mt_mix(p.a0.z, p.a0.w, p.r02);
+    n0.w = mt_mix(p.a0.w, p.a1.x, p.r03);
+    n1.x = mt_mix(p.a1.x, p.a1.y, p.r1.x);
+    n1.y = mt_mix(p.a1.y, p.a1.z, p.r1.y);
+    n1.z = mt_mix(p.a1.z, p.a1.w, p.r1.z);
+    n1.w = mt_mix(p.a1.w, p.a8, p.r1.w);
 }
 
-// D = refills whose inputs are in flight (1 keeps the register footprint of
-// the latency-tolerant search kernels small; the env kernel, alone on its
-// SIMD, takes 2).
+// low bytes of the 8 tempered words
+__device__ __forceinline__ uint64_t mt_bytes8(const u32x4& n0, const u32x4& n1) {
+    const uint64_t lo = (uint64_t)((mt_temper(n0.x) & 0xFFu) | ((mt_temper(n0.y) & 0xFFu) << 8) |
+                                   ((mt_temper(n0.z) & 0xFFu) << 16) | (mt_temper(n0.w) << 24));
+    const uint64_t hi = (uint64_t)((mt_temper(n1.x) & 0xFFu) | ((mt_temper(n1.y) & 0xFFu) << 8) |
+                                   ((mt_temper(n1.z) & 0xFFu) << 16) | (mt_temper(n1.w) << 24));
+    return lo | (hi << 32);
+}
+
+// Replay of k (1..8) words that are already twisted (the unconsumed words of
+// the previous launch, or an imported numpy round); scalar, out of line.
+static __device__ __noinline__ uint64_t mt_replay(const uint32_t* st, uint32_t from, uint32_t k) {
+    uint64_t b = 0ull;
+    for (uint32_t i = 0; i < k; i++) b |= (uint64_t)(mt_temper(st[from + i]) & 0xFFu) << (8u * i);
+    return b;
+}
+
+// D = chunks (8 words) twisted per refill, 1 or 2.  A refill's loads are
+// issued right after the previous refill, so D = 2 doubles the draws that
+// hide their latency.  Two-chunk refills start at a multiple of 16 words
+// (624 = 39 * 16, so they never cross a round); a state left at 8 mod 16 by
+// a one-chunk user of the same stream realigns with one single chunk.
 template <int D>
 struct MtGenT {
     uint32_t* st;
-    uint32_t pos, direct, straddle;
-    u32x4 pn0, pn1;  // held-back chunk 0 of the next round (straddle)
-    MtPre pf[D];     // pf[k] = inputs of the (k+1)-th next lazy refill
+    uint32_t pos, rem, straddle;
+    u32x4 pn[2 * D];  // held-back first words of the next round (straddle)
+    MtPre pf[D];      // inputs of the next refill's chunks
 
+    __device__ __forceinline__ void prefetch_next() {
+        const uint32_t c = (pos == (uint32_t)kMtN) ? 0u : pos;
+        pf[0] = mt_prefetch(st, c);
+        if (D == 2) pf[D - 1] = mt_prefetch(st, mt_next_chunk(c));
+    }
+    __device__ __forceinline__ void commit() {
+#pragma unroll
+        for (int k = 0; k < 2 * D; k++) *(u32x4*)(st + 4 * k) = pn[k];
+        straddle = 0u;
+    }
     __device__ __forceinline__ void load(uint32_t* state, uint32_t code, ByteBuf& buf) {
         st = state;
         pos = code & 0x7FFu;
-        direct = code >> 31;
+        rem = (code >> 16) & kMtCntMask;
         straddle = 0u;
-        const uint32_t cnt = (code >> 16) & 0x3Fu;
         buf.clear();
-        for (uint32_t k = 0; k < cnt; k++) buf.append(mt_temper(st[pos - cnt + k]) & 0xFFu, 1u);
-        uint32_t c = (direct || pos == (uint32_t)kMtN) ? 0u : pos;
-#pragma unroll
-        for (int k = 0; k < D; k++) {
-            pf[k] = mt_prefetch(st, c);
-            c = mt_next_chunk(c);
-        }
+        prefetch_next();
     }
     // state code for mt_pos[]; commits or drops a held-back chunk
     __device__ __forceinline__ uint32_t save(const ByteBuf& buf) {
         if (straddle) {
-            if (buf.cnt > 8u) return (uint32_t)kMtN | ((buf.cnt - 8u) << 16);  // old words left: drop the chunk
-            *(u32x4*)(st) = pn0;
-            *(u32x4*)(st + 4) = pn1;
-            return 8u | (buf.cnt << 16);
+            if (buf.cnt > 8u * D) return (uint32_t)kMtN | ((buf.cnt - 8u * D) << 16);  // old words left: drop
+            commit();
+            return 8u * D | (buf.cnt << 16);
         }
-        return pos | (buf.cnt << 16) | (direct << 31);
+        return pos | ((rem + buf.cnt) << 16);
     }
-    // one batch of words; false if it cannot run now (direct mode at the end
-    // of a round's words, or a straddle whose old words are still buffered)
+    // one batch of words; false if it cannot run now (a straddle whose old
+    // words are still buffered)
     __device__ __forceinline__ bool gen(ByteBuf& buf);
     __device__ __forceinline__ void topup(ByteBuf& buf) {
-        if (buf.cnt <= 24u) gen(buf);
+        if (buf.cnt <= 32u - 8u * D) gen(buf);
     }
     __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf); }  // cnt == 0: always succeeds
 };
 
 template <int D>
 __device__ __forceinline__ bool MtGenT<D>::gen(ByteBuf& buf) {
-    if (direct) {
-        const MtSlow o = mt_direct(st, pos);
-        pos = o.pos, direct = o.direct;
-        if (o.k) {
-            buf.append(o.bytes, o.k);
-            return true;
-        }
-        // fall through: the lazy twist of the next round (pos == 624)
+    if (rem) {
+        const uint32_t k = min(8u, rem);
+        buf.append(mt_replay(st, pos - rem, k), k);
+        rem -= k;
+        return true;
     }
     if (straddle) {
-        if (buf.cnt > 8u) return false;
-        *(u32x4*)(st) = pn0;  // old round consumed: commit chunk 0
-        *(u32x4*)(st + 4) = pn1;
-        straddle = 0u;
+        if (buf.cnt > 8u * D) return false;
+        commit();  // old round consumed
     }
     const bool wrap = (pos == (uint32_t)kMtN);
     const uint32_t i = wrap ? 0u : pos;
-    const MtPre& p = pf[0];
-    u32x4 n0, n1;
-    n0.x = mt_mix(p.a0.x, p.a0.y, p.r0.y);
-    n0.y = mt_mix(p.a0.y, p.a0.z, p.r0.z);
-    n0.z = mt_mix(p.a0.z, p.a0.w, p.r0.w);
-    n0.w = mt_mix(p.a0.w, p.a1.x, p.r1.x);
-    n1.x = mt_mix(p.a1.x, p.a1.y, p.r1.y);
-    n1.y = mt_mix(p.a1.y, p.a1.z, p.r1.z);
-    n1.z = mt_mix(p.a1.z, p.a1.w, p.r1.w);
-    n1.w = mt_mix(p.a1.w, p.a8, p.r2.x);
+    const bool two = (D == 2) && !(i & 8u);
+    u32x4 n[4];
+    mt_twist8(pf[0], n[0], n[1]);
+    n[2] = n[3] = u32x4{0u, 0u, 0u, 0u};
+    if (D == 2) mt_twist8(pf[D - 1], n[2], n[3]);
     if (wrap && buf.cnt) {
-        pn0 = n0, pn1 = n1, straddle = 1u;
-    } else {
-        *(u32x4*)(st + i) = n0;
-        *(u32x4*)(st + i + 4) = n1;
-    }
-    const uint64_t lo = (uint64_t)((mt_temper(n0.x) & 0xFFu) | ((mt_temper(n0.y) & 0xFFu) << 8) |
-                                   ((mt_temper(n0.z) & 0xFFu) << 16) | (mt_temper(n0.w) << 24));
-    const uint64_t hi = (uint64_t)((mt_temper(n1.x) & 0xFFu) | ((mt_temper(n1.y) & 0xFFu) << 8) |
-                                   ((mt_temper(n1.z) & 0xFFu) << 16) | (mt_temper(n1.w) << 24));
-    buf.append(lo | (hi << 32), 8u);
-    pos = i + 8u;
-    uint32_t c = mt_next_chunk(i);
 #pragma unroll
-    for (int k = 0; k + 1 < D; k++) {
-        pf[k] = pf[k + 1];
-        c = mt_next_chunk(c);
+        for (int k = 0; k < 2 * D; k++) pn[k] = n[k];
+        straddle = 1u;
+    } else {
+        *(u32x4*)(st + i) = n[0];
+        *(u32x4*)(st + i + 4) = n[1];
+        if (two) {
+            *(u32x4*)(st + i + 8) = n[2];
+            *(u32x4*)(st + i + 12) = n[3];
+        }
     }
-    pf[D - 1] = mt_prefetch(st, c);
+    buf.append(mt_bytes8(n[0], n[1]), 8u);
+    if (two) buf.append(mt_bytes8(n[2], n[3]), 8u);
+    pos = i + (two ? 16u : 8u);
+    // Keep the next loads below the last use of the inputs just consumed:
+    // hoisted above it, they get fresh registers and the loop's phi copies
+    // them back at once -- an s_waitcnt right behind the loads that made the
+    // prefetch worthless (seen in the gfx950 ISA).
+    asm volatile("" ::"v"(n[0].x), "v"(n[1].w), "v"(n[2].x), "v"(n[3].w) : "memory");
+    prefetch_next();
     return true;
 }
 
 using MtGen = MtGenT<1>;
+
+// numpy (key, pos) form of a state code, host and device: the caller has
+// finished the round in place when pos < 624 (mt_finish_round)
+__host__ __device__ __forceinline__ int mt_numpy_pos(uint32_t code) {
+    const uint32_t p = code & 0x7FFu, cnt = (code >> 16) & kMtCntMask;
+    if (p == 0u) return kMtN;  // previous round complete, next draw twists
+    return (int)(p - cnt);
+}
+__host__ __device__ __forceinline__ uint32_t mt_code_from_numpy(int pos) {
+    return (pos >= kMtN) ? 0u : ((uint32_t)kMtN | ((uint32_t)(kMtN - pos) << 16));
+}
 
 // ---- Philox4x32-10 counter-based stream -----------------------------------
 // word w of game s = philox({w/4 lo, w/4 hi, s lo, s hi}, seed)[w % 4]

@@ -93,8 +93,8 @@ __global__ __launch_bounds__(kBlock) void k_reset_to(DevState s, const int8_t* b
     store_game<N>(s, g, G);
 }
 
-// MT19937 refills whose inputs are in flight in k_play (one wave per SIMD
-// at B = 65 536: nothing else hides the latency)
+// MT19937 chunks (8 words) twisted per refill in k_play: 2 doubles the
+// lookahead of the refill's loads (one wave per SIMD: nothing else hides them)
 constexpr int kPlayPrefetch = 2;
 
 struct PlayArgs {
@@ -108,36 +108,22 @@ struct PlayArgs {
     int32_t* invalid;        // [B]
 };
 
-// Each wave owns a private LDS region: the lanes' deal decks, and -- when
-// the observation rows are 48 bytes -- a staging area where the wave's 64
-// rows are assembled so that they leave as 1-KB contiguous stores instead
-// of 64 scattered 16-B pieces per instruction.  (Both uses never overlap in
-// time within a step: observations first, the deal at the very end.)
-template <int N, int MODE>
-__global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= s.B) return;
+// The env-step loop of one lane (game g).  R supplies the random words
+// (topup/force, sechs_device.h).  Each wave
+// owns a private LDS region: the lanes' deal decks, and -- when the
+// observation rows are 48 bytes -- a staging area where the wave's 64 rows
+// are assembled so that they leave as 1-KB contiguous stores instead of 64
+// scattered 16-B pieces per instruction.  (Both uses never overlap in time
+// within a step: observations first, the deal at the very end.)
+template <int N, class R>
+__device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a, int64_t g, int lane, uint8_t* wave_lds,
+                                           Game<N>& G, R& rng, ByteBuf& buf, int32_t (&sum_res)[N], int32_t& episodes) {
     const int64_t B = s.B;
-    const int lane = threadIdx.x & 63;
-    uint8_t* wave_lds = lds_dyn + (threadIdx.x >> 6) * a.wave_lds;
     uint8_t* my_deck = wave_lds + lane * kDeckStride;
     const bool staged = a.obs && a.obs_stride == 48;
-    const int64_t g0 = g - lane;                       // first game of this wave
+    const int64_t g0 = g - lane;                           // first game of this wave
     const int wave_games = (int)min((int64_t)64, B - g0);  // = active lanes (lanes past B left)
-    Game<N> G;
-    load_game<N>(s, g, G);
-    typename RngOf<MODE, kPlayPrefetch>::T rng;
-    ByteBuf buf;
-    RngOf<MODE, kPlayPrefetch>::load(s, g, rng, buf);
-    // episode results stay in registers for the launch (one load, one store)
     const bool auto_reset = (a.flags & SN_AUTO_RESET) != 0;
-    int32_t sum_res[N], episodes = 0;
-    if (auto_reset) {
-#pragma unroll
-        for (int p = 0; p < N; p++) sum_res[p] = s.sum_res[(int64_t)p * B + g];
-        episodes = s.episodes[g];
-    }
     const bool summ = !(a.flags & SN_NO_SUMMARIES);
     int32_t* rew = a.rewards ? a.rewards + g * N : nullptr;
     uint8_t* act = a.actions_out ? a.actions_out + g * N : nullptr;
@@ -185,11 +171,9 @@ __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
         } else {
             // DrunkHamster for every seat in seat order (play.py:38-41):
             // legal[random_interval(n-1)], agents/random.py:9
+            rng_draws<N>(rng, buf, G.n - 1u, idx);
 #pragma unroll
-            for (int p = 0; p < N; p++) {
-                idx[p] = rng_interval(rng, buf, G.n - 1u);
-                card[p] = hand_get(G.hand[p], idx[p]);
-            }
+            for (int p = 0; p < N; p++) card[p] = hand_get(G.hand[p], idx[p]);
         }
         if (a.invalid) a.invalid[g] = bad;
         if (bad >= 0) {
@@ -242,13 +226,49 @@ __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
             deal_shuffle<N>(rng, buf, my_deck, s.C, G);
         }
     }
-    store_game<N>(s, g, G);
-    RngOf<MODE, kPlayPrefetch>::store(s, g, rng, buf);
-    if (auto_reset) {
+}
+
+// episode results stay in registers for the launch (one load, one store)
+template <int N>
+__device__ __forceinline__ void load_results(const DevState& s, int64_t g, int flags, int32_t (&sum_res)[N], int32_t& episodes) {
 #pragma unroll
-        for (int p = 0; p < N; p++) s.sum_res[(int64_t)p * B + g] = sum_res[p];
+    for (int p = 0; p < N; p++) sum_res[p] = 0;
+    episodes = 0;
+    if (flags & SN_AUTO_RESET) {
+#pragma unroll
+        for (int p = 0; p < N; p++) sum_res[p] = s.sum_res[(int64_t)p * s.B + g];
+        episodes = s.episodes[g];
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void store_results(const DevState& s, int64_t g, int flags, const int32_t (&sum_res)[N],
+                                              int32_t episodes) {
+    if (flags & SN_AUTO_RESET) {
+#pragma unroll
+        for (int p = 0; p < N; p++) s.sum_res[(int64_t)p * s.B + g] = sum_res[p];
         s.episodes[g] = episodes;
     }
+}
+
+template <int N, int MODE>
+__global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= s.B) return;
+    const int lane = threadIdx.x & 63;
+    uint8_t* wave_lds = lds_dyn + (threadIdx.x >> 6) * a.wave_lds;
+    Game<N> G;
+    load_game<N>(s, g, G);
+    typename RngOf<MODE, kPlayPrefetch>::T rng;
+    ByteBuf buf;
+    RngOf<MODE, kPlayPrefetch>::load(s, g, rng, buf);
+    int32_t sum_res[N], episodes;
+    load_results<N>(s, g, a.flags, sum_res, episodes);
+    play_steps<N>(s, a, g, lane, wave_lds, G, rng, buf, sum_res, episodes);
+    store_game<N>(s, g, G);
+    RngOf<MODE, kPlayPrefetch>::store(s, g, rng, buf);
+    store_results<N>(s, g, a.flags, sum_res, episodes);
 }
 
 // obs in any dtype, one thread per (game, seat)
@@ -555,16 +575,10 @@ sn_status sn_mt_get(sn_env* e, int64_t game, uint32_t* key, int32_t* pos) {
     uint32_t code = 0;
     HIP_TRY(hipMemcpy(key, e->s.mt + game * kMtN, sizeof(uint32_t) * kMtN, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(&code, e->s.mt_pos + game, sizeof(uint32_t), hipMemcpyDeviceToHost));
-    // decode (sechs_device.h MtRng): words [pos-cnt, pos) generated, unconsumed
-    const int p = (int)(code & 0x7FFu), cnt = (int)((code >> 16) & 0x3Fu);
-    if (code & kMtDirect) {
-        *pos = (int32_t)(p - cnt);
-    } else if (p == 0) {
-        *pos = kMtN;  // previous round complete, next draw twists
-    } else {
-        mt_finish_round(key, p);  // twist the rest of this round in place
-        *pos = (int32_t)(p - cnt);
-    }
+    // decode (sechs_device.h MtGenT): words [pos-cnt, pos) twisted, unconsumed
+    const int p = (int)(code & 0x7FFu);
+    if (p > 0 && p < kMtN) mt_finish_round(key, p);  // twist the rest of this round in place
+    *pos = (int32_t)mt_numpy_pos(code);
     return SN_OK;
 }
 
@@ -575,7 +589,7 @@ sn_status sn_mt_set(sn_env* e, int64_t game, const uint32_t* key, int32_t pos) {
     if (pos < 0 || pos > kMtN) return fail(SN_EINVAL, "pos must be in 0..624");
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipDeviceSynchronize());
-    uint32_t code = (pos == kMtN) ? 0u : (kMtDirect | (uint32_t)pos);
+    const uint32_t code = mt_code_from_numpy(pos);
     HIP_TRY(hipMemcpy(e->s.mt + game * kMtN, key, sizeof(uint32_t) * kMtN, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(e->s.mt_pos + game, &code, sizeof(uint32_t), hipMemcpyHostToDevice));
     return SN_OK;

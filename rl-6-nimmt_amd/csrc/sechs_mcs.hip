@@ -287,12 +287,10 @@ __global__ __launch_bounds__(kBlock) void k_mcs_play_exact(DevState s, ExactArgs
 
 // numpy form of a lane's MT state, in place (the device twin of sn_mt_get)
 __device__ int32_t mt_export(uint32_t* st, uint32_t code) {
-    const uint32_t p = code & 0x7FFu, cnt = (code >> 16) & 0x3Fu;
-    if (code & kMtDirect) return (int32_t)(p - cnt);
-    if (p == 0u) return kMtN;
-    for (uint32_t i = p; i < (uint32_t)kMtN; i++)
-        st[i] = mt_mix(st[i], st[(i + 1u) % kMtN], st[(i + kMtM) % kMtN]);
-    return (int32_t)(p - cnt);
+    const uint32_t p = code & 0x7FFu;
+    if (p > 0u && p < (uint32_t)kMtN)
+        for (uint32_t i = p; i < (uint32_t)kMtN; i++) st[i] = mt_mix(st[i], st[(i + 1u) % kMtN], st[(i + kMtM) % kMtN]);
+    return mt_numpy_pos(code);
 }
 
 struct DecideArgs {
@@ -318,7 +316,7 @@ __global__ __launch_bounds__(kBlock) void k_mcs_decide_exact(DecideArgs a) {
     const int32_t np_pos = a.mt_pos[d];
     MtGen gen;
     ByteBuf buf;
-    gen.load(st, np_pos >= kMtN ? 0u : (kMtDirect | (uint32_t)np_pos), buf);
+    gen.load(st, mt_code_from_numpy(np_pos), buf);
     u32x4 hs = {0u, 0u, 0u, 0u};
     for (int k = 0; k < kHand; k++) {
         const int c = a.hand[d * kHand + k];

@@ -140,14 +140,38 @@ __device__ __forceinline__ void deal_from(const D& deck, int C, Game<N>& G) {
 
 // np.random.shuffle(arange(C)) (legacy Fisher-Yates from the end,
 // j = random_interval(i)) in this lane's LDS slot, then deal.
+//
+// Word-synchronous form: instead of one rejection loop per draw, the lane
+// walks its words in order, 8 per pass (the buffered ones first, then fresh
+// refills), and every word advances the shuffle by at most one draw:
+// accepted (x <= i) -> swap(i, x), i -= 1; rejected -> nothing (a self-swap,
+// so the pass is branch-free).  That is exactly numpy's sequence of
+// masked-rejection draws, and all lanes of a wave consume their words in
+// lockstep (one refill per pass for every lane still shuffling).  A lane
+// that finishes inside a pass keeps the unused words for its next draws.
 template <int N, class R>
 __device__ __forceinline__ void deal_shuffle(R& rng, ByteBuf& buf, uint8_t* deck, int C, Game<N>& G) {
     for (int i = 0; i < C; i += 4) *(uint32_t*)(deck + i) = (uint32_t)i * 0x01010101u + 0x03020100u;
-    for (int i = C - 1; i >= 1; --i) {
-        const uint32_t j = rng_interval(rng, buf, (uint32_t)i);
-        const uint8_t di = deck[i], dj = deck[j];
-        deck[i] = dj;
-        deck[j] = di;
+    uint32_t i = (uint32_t)C - 1u;
+    while (i >= 1u) {
+        if (buf.cnt == 0u) rng.force(buf);
+        const uint32_t valid = min(buf.cnt, 8u);
+        const uint64_t w = buf.b0;
+        uint32_t used = 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < 8u; k++) {
+            const bool act = (k < valid) && (i >= 1u);
+            const uint32_t m = 0xFFFFFFFFu >> __builtin_clz(i | 1u);
+            const uint32_t x = (uint32_t)(w >> (8u * k)) & m;
+            const bool acc = act && (x <= i);
+            const uint32_t j = acc ? x : i;
+            const uint8_t di = deck[i], dj = deck[j];
+            deck[i] = dj;
+            deck[j] = di;
+            i -= acc ? 1u : 0u;
+            used = act ? k + 1u : used;
+        }
+        buf.drop(used);
     }
     deal_from<N>([&](int i) -> uint32_t { return deck[i]; }, C, G);
 }

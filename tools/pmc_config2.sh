@@ -9,9 +9,9 @@ TAG=${1:-cur}
 OUT=$R/gpurun_out/pmc_$TAG
 mkdir -p $OUT
 for mode in numpy philox; do
-  timeout -k 10 180 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_play --output-format csv -d $OUT/fetch_$mode -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-mcs --rng $mode > $OUT/fetch_$mode.log 2>&1
-  timeout -k 10 180 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_play --output-format csv -d $OUT/write_$mode -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-mcs --rng $mode > $OUT/write_$mode.log 2>&1
-  timeout -k 10 180 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS --kernel-include-regex k_play --output-format csv -d $OUT/sq_$mode -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-mcs --rng $mode > $OUT/sq_$mode.log 2>&1
+  timeout -k 10 180 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_play --output-format csv -d $OUT/fetch_$mode -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-mcs --no-puct --rng $mode > $OUT/fetch_$mode.log 2>&1
+  timeout -k 10 180 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_play --output-format csv -d $OUT/write_$mode -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-mcs --no-puct --rng $mode > $OUT/write_$mode.log 2>&1
+  timeout -k 10 180 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS --kernel-include-regex k_play --output-format csv -d $OUT/sq_$mode -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu --no-mcs --no-puct --rng $mode > $OUT/sq_$mode.log 2>&1
   python3 tools/pmc_traffic.py $OUT/fetch_$mode/run_counter_collection.csv $OUT/write_$mode/run_counter_collection.csv "k_play<4" $OUT/traffic_$mode.json "config2 $mode, 65536 games x 10 env-steps per launch"
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/stats -o run -- python3 bench.py --no-cpu > $OUT/stats.log 2>&1
