@@ -40,6 +40,12 @@ STEPS_PER_LAUNCH = 10
 # hands, board, lens, scores, rewards 4N, done 1 written) + 47N for the int8
 # observation the step emits.
 ALGO_BYTES_PER_STEP = (33 * N_PLAYERS + 57) + 47 * N_PLAYERS  # 377 B at N = 4
+# HBM bytes per k_play launch from rocprofv3 PMC passes of this kernel
+# (tools/pmc_config2.sh: FETCH_SIZE and WRITE_SIZE in separate passes, gfx950
+# corrections of MI355X_MICROARCH.md applied by tools/pmc_traffic.py).  PMC
+# counters cannot be read inside a plain run, so the committed summary of the
+# current kernel is reported beside the live timing.
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_v12_pmc_traffic_{rng}.json")
 
 
 def parse():
@@ -221,6 +227,14 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
     }
 
 
+def pmc_traffic(rng, games):
+    path = PMC_TRAFFIC.format(rng=rng)
+    if games != 65536 or not os.path.exists(path):
+        return None, None
+    rec = json.load(open(path))
+    return float(rec["traffic_bytes_per_launch"]), os.path.relpath(path, ROOT)
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
@@ -250,6 +264,7 @@ def main():
     value = total_steps / wall
     launch_steps = B * STEPS_PER_LAUNCH
     achieved = launch_steps * ALGO_BYTES_PER_STEP / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(args.rng, B) if not args.no_obs else (None, None)
     result = {
         "metric": "env-steps/sec at 65536 concurrent 4-player games, 1/2/4/8 MI355X",
         "value": value,
@@ -279,7 +294,10 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+            "traffic_source": traffic_src,
+            "traffic_gbs_at_live_kernel_ms": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
             "kernel": "k_play<4, RNG_NUMPY_MT>",
             "kernel_ms": kern_ms,
             "algo_bytes_per_env_step": ALGO_BYTES_PER_STEP,
