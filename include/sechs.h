@@ -127,6 +127,16 @@ sn_status sn_mt_set(sn_env* env, int64_t game, const uint32_t* key_host, int32_t
 /* philox word counter of game g [sync] */
 sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
 
+/* Tuning knobs of the numpy-compat DrunkHamster rollout (results never
+   depend on them; the tests run both ways):
+     SN_OPT_RING_WORDS   words each game's stream is twisted ahead per
+                         launch by k_mt_prep (multiple of 64, 64..512;
+                         0 = no ring, k_play twists lazily per lane).
+                         Default 256 for N <= 4, else 512.
+     SN_OPT_CHUNK_STEPS  env-steps per ring-fed launch (>= 1, default 10). */
+enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2 };
+sn_status sn_set_option(sn_env* env, int option, int value);
+
 /* ---- Monte-Carlo search, MCSAgent (agents/mcts.py:17-188) ------------- */
 
 /* Card memory of every seat (mcts.py:62-73), updated in place from the

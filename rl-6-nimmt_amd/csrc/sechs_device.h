@@ -30,7 +30,9 @@ constexpr int kMaxCards = 104;
 constexpr int kMtN = 624;
 constexpr int kMtM = 397;
 
-enum RngMode { RNG_PHILOX = 0, RNG_NUMPY_MT = 1 };
+// RNG_NUMPY_RING(_HBM): numpy-MT words pre-twisted by k_mt_prep, read from
+// an LDS copy of the ring (or straight from HBM when LDS is short); k_play only
+enum RngMode { RNG_PHILOX = 0, RNG_NUMPY_MT = 1, RNG_NUMPY_RING = 2, RNG_NUMPY_RING_HBM = 3 };
 
 // --------------------------------------------------------------------------
 // bull heads, env.py:224-239
@@ -429,6 +431,13 @@ __device__ __forceinline__ void rng_draws(G& gen, ByteBuf& buf, uint32_t max, ui
 //  (key, pos) form: np.random.seed(s) == init_genrand(s) with code 0, and an
 //  imported numpy (key, p) is code 624 | (624 - p) << 16.
 //
+// A code may also straddle a round (cnt > pos): k_mt_prep twists ahead in
+// place across the boundary while old-round words are still unconsumed.  The
+// unconsumed old words [624 - (cnt - pos), 624) are untouched; the old
+// round's words [0, pos) -- all consumed -- are recoverable from the new ones
+// (the twist is invertible given the old mt[0], kept in mt0[g]), which is
+// how sn_mt_get exports such a state.
+//
 // Round boundary.  A lane that reaches word 624 with words of the old round
 // still buffered twists the new round's chunk 0 into registers but holds the
 // store back ("straddle"): mt[0..8) keeps the old round's values until the
@@ -503,9 +512,15 @@ __device__ __forceinline__ uint64_t mt_bytes8(const u32x4& n0, const u32x4& n1) 
 
 // Replay of k (1..8) words that are already twisted (the unconsumed words of
 // the previous launch, or an imported numpy round); scalar, out of line.
+// `from` = pos - rem (mod 624): a state whose unconsumed words straddle a
+// round (k_mt_prep twists ahead across it) replays the old round's tail,
+// then the new round's head.
 static __device__ __noinline__ uint64_t mt_replay(const uint32_t* st, uint32_t from, uint32_t k) {
     uint64_t b = 0ull;
-    for (uint32_t i = 0; i < k; i++) b |= (uint64_t)(mt_temper(st[from + i]) & 0xFFu) << (8u * i);
+    for (uint32_t i = 0; i < k; i++) {
+        const uint32_t idx = (from + i >= (uint32_t)kMtN) ? from + i - kMtN : from + i;
+        b |= (uint64_t)(mt_temper(st[idx]) & 0xFFu) << (8u * i);
+    }
     return b;
 }
 
@@ -531,12 +546,13 @@ struct MtGenT {
         for (int k = 0; k < 2 * D; k++) *(u32x4*)(st + 4 * k) = pn[k];
         straddle = 0u;
     }
-    __device__ __forceinline__ void load(uint32_t* state, uint32_t code, ByteBuf& buf) {
+    // keep = true: continue after bytes already in buf (RingGen's fallback)
+    __device__ __forceinline__ void load(uint32_t* state, uint32_t code, ByteBuf& buf, bool keep = false) {
         st = state;
         pos = code & 0x7FFu;
         rem = (code >> 16) & kMtCntMask;
         straddle = 0u;
-        buf.clear();
+        if (!keep) buf.clear();
         prefetch_next();
     }
     // state code for mt_pos[]; commits or drops a held-back chunk
@@ -561,7 +577,7 @@ template <int D>
 __device__ __forceinline__ bool MtGenT<D>::gen(ByteBuf& buf) {
     if (rem) {
         const uint32_t k = min(8u, rem);
-        buf.append(mt_replay(st, pos - rem, k), k);
+        buf.append(mt_replay(st, (pos >= rem) ? pos - rem : pos + kMtN - rem, k), k);
         rem -= k;
         return true;
     }
@@ -604,10 +620,12 @@ using MtGen = MtGenT<1>;
 
 // numpy (key, pos) form of a state code, host and device: the caller has
 // finished the round in place when pos < 624 (mt_finish_round)
+// (a straddling code, cnt > pos, is in the previous round: its numpy key is
+// that round, restored by the caller -- sn_mt_get)
 __host__ __device__ __forceinline__ int mt_numpy_pos(uint32_t code) {
     const uint32_t p = code & 0x7FFu, cnt = (code >> 16) & kMtCntMask;
     if (p == 0u) return kMtN;  // previous round complete, next draw twists
-    return (int)(p - cnt);
+    return (cnt > p) ? (int)(kMtN + p - cnt) : (int)(p - cnt);
 }
 __host__ __device__ __forceinline__ uint32_t mt_code_from_numpy(int pos) {
     return (pos >= kMtN) ? 0u : ((uint32_t)kMtN | ((uint32_t)(kMtN - pos) << 16));

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -93,12 +94,132 @@ __global__ __launch_bounds__(kBlock) void k_reset_to(DevState s, const int8_t* b
     store_game<N>(s, g, G);
 }
 
+// numpy-MT twist-ahead for a k_play launch: one wave per game twists, in
+// place and 64 consecutive words per instruction (every load and store one
+// contiguous run), the game's stream far enough that ring_w words lie
+// twisted and unconsumed, and writes their tempered low bytes to the ring
+// (RingGen).  numpy's in-place twist order makes any 227 consecutive words
+// independent: word i reads mt[i], mt[i+1] (both still the previous round's)
+// and mt[i+397] (previous round, i < 227) or mt[i-227] (this round, twisted
+// 227 words earlier).  So the words this launch twists first (j < 227) have
+// every input in memory already: all their loads are issued before any
+// store (the wave keeps 3 * (NB + 1) loads in flight), and only words j >=
+// 227 (a nearly empty ring, or 512-word rings) wait for those stores.  The
+// twist pointer stays a multiple of 8 (MtGen's chunking).  Twisting word 0
+// of a new round while old words are unconsumed makes the code straddle;
+// the overwritten old mt[0] goes to mt0[g] so sn_mt_get can still export
+// numpy's key.
+constexpr int kPrepGamesPerWave = 4;
+
+template <int NB, int GPW, int DBG = 0>  // ring_w / 64, games per wave
+__global__ __launch_bounds__(kBlock) void k_mt_prep(DevState s) {
+    constexpr uint32_t W = 64u * NB;
+    constexpr uint32_t D = kMtN - kMtM;  // 227
+    const int64_t g0 = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * GPW;
+    if (g0 >= s.B) return;  // whole waves
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t rem[GPW], KT[GPW], T0[GPW], base[GPW];
+    uint32_t A[GPW][NB + 1], C[GPW][NB + 1];
+    // Word k of game q (k = 0 .. KT) sits at twist index base + k (mod 624):
+    // the first rem are twisted and unconsumed (re-tempered into the ring),
+    // the rest are twisted now.  All loads of all GPW games go out first.
+    // one load for the GPW state codes (lane q holds game g0 + q's): a
+    // per-game load here would make each game's wait drain the previous
+    // game's loads (vmcnt counts in order)
+    const uint32_t codes = (lane < (uint32_t)GPW) ? s.mt_pos[min(g0 + (int64_t)lane, s.B - 1)] : 0u;
+#pragma unroll
+    for (int q = 0; q < GPW; q++) {
+        const int64_t g = min(g0 + q, s.B - 1);  // a short last wave repeats its last game (loads only)
+        const uint32_t code = __builtin_amdgcn_readlane(codes, q);
+        const uint32_t T = code & 0x7FFu;
+        rem[q] = (code >> 16) & kMtCntMask;
+        const uint32_t add = (rem[q] >= W) ? 0u : ((W - rem[q] + 7u) & ~7u);
+        KT[q] = rem[q] + add;
+        T0[q] = (T == (uint32_t)kMtN) ? 0u : T;
+        base[q] = T0[q] + kMtN - rem[q];  // + k, mod 624
+        const uint32_t* st = s.mt + g * kMtN;
+#pragma unroll
+        for (int b = 0; b <= NB; b++) {
+            const uint32_t k = 64u * b + lane;
+            uint32_t idx = base[q] + k;
+            idx = (idx >= (uint32_t)kMtN) ? idx - kMtN : idx;
+            idx = (idx >= (uint32_t)kMtN) ? idx - kMtN : idx;
+            if (k <= KT[q]) A[q][b] = st[idx];
+            if (k >= rem[q] && k < KT[q] && k - rem[q] < D) C[q][b] = st[(idx < D) ? idx + kMtM : idx - D];
+        }
+    }
+    uint32_t* ring = (uint32_t*)s.ring;
+#pragma unroll
+    for (int q = 0; q < GPW; q++) {
+        const int64_t g = g0 + q;
+        if (g >= s.B) break;
+        uint32_t* st = s.mt + g * kMtN;
+        const uint32_t r = rem[q], kt = KT[q];
+#pragma unroll
+        for (int b = 0; b <= NB; b++) {
+            if (b == NB && kt <= W) break;
+            const uint32_t k = 64u * b + lane;
+            uint32_t idx = base[q] + k;
+            idx = (idx >= (uint32_t)kMtN) ? idx - kMtN : idx;
+            idx = (idx >= (uint32_t)kMtN) ? idx - kMtN : idx;
+            // mt[idx + 1] = word k + 1 = the next lane's A (lane 63: lane 0 of the next batch)
+            const uint32_t nxt = (b < NB) ? __shfl(A[q][b < NB ? b + 1 : b], 0) : 0u;
+            uint32_t bb = __shfl_down(A[q][b], 1);
+            bb = (lane == 63u) ? nxt : bb;
+            uint32_t v = A[q][b];
+            if (k >= r && k < kt && k - r < D) {
+                v = mt_mix(A[q][b], bb, C[q][b]);
+                if (!(DBG & 2)) st[idx] = v;
+                if (idx == 0u) s.mt0[g] = A[q][b];
+            }
+            if (b < NB) {  // ring bytes: 4 words per dword (lanes 4m..4m+3)
+                const uint32_t y = mt_temper(v) & 0xFFu;
+                const uint32_t d = y | (__shfl_down(y, 1) << 8) | (__shfl_down(y, 2) << 16) | (__shfl_down(y, 3) << 24);
+                if ((lane & 3u) == 0u && !(DBG & 1)) ring[(((int64_t)(k >> 4)) * s.B + g) * 4 + ((k >> 2) & 3u)] = d;
+                if ((DBG & 1) && d == 0x12345678u) ring[0] = d;
+            }
+        }
+        // words j >= 227 read words twisted just above: in order, after those stores
+        if (kt > r + D) {
+            for (uint32_t k0 = ((r + D) & ~63u); k0 < kt; k0 += 64u) {
+                const uint32_t k = k0 + lane;
+                uint32_t v = 0u;
+                if (k >= r + D && k < kt) {
+                    uint32_t idx = base[q] + k;
+                    idx = (idx >= (uint32_t)kMtN) ? idx - kMtN : idx;
+                    idx = (idx >= (uint32_t)kMtN) ? idx - kMtN : idx;
+                    const uint32_t a = st[idx];
+                    v = mt_mix(a, st[(idx + 1u == (uint32_t)kMtN) ? 0u : idx + 1u], st[(idx < D) ? idx + kMtM : idx - D]);
+                    st[idx] = v;
+                    if (idx == 0u) s.mt0[g] = a;
+                }
+                const uint32_t y = mt_temper(v) & 0xFFu;
+                const uint32_t d = y | (__shfl_down(y, 1) << 8) | (__shfl_down(y, 2) << 16) | (__shfl_down(y, 3) << 24);
+                if ((lane & 3u) == 0u && k < W && k + 3u >= r + D) {
+                    uint32_t* dst = ring + (((int64_t)(k >> 4)) * s.B + g) * 4 + ((k >> 2) & 3u);
+                    if (k >= r + D) {
+                        *dst = d;
+                    } else {  // dword shared with words stored above: merge the new bytes
+                        const uint32_t keep = (1u << (8u * (r + D - k))) - 1u;
+                        *dst = (*dst & keep) | (d & ~keep);
+                    }
+                }
+            }
+        }
+        if (lane == 0u && kt > r) {
+            const uint32_t Tn = T0[q] + (kt - r);
+            s.mt_pos[g] = ((Tn > (uint32_t)kMtN) ? Tn - kMtN : Tn) | (kt << 16);
+        }
+    }
+}
+
 // MT19937 chunks (8 words) twisted per refill in k_play: 2 doubles the
 // lookahead of the refill's loads (one wave per SIMD: nothing else hides them)
 constexpr int kPlayPrefetch = 2;
 
 struct PlayArgs {
     int steps, flags, obs_stride, wave_lds;  // wave_lds: bytes of LDS per wave (dynamic)
+    int ring_lds;            // bytes of that per lane for the LDS ring copy (RNG_NUMPY_RING), at the region's end
     int vec_out;             // rewards 16-B and actions 4-B aligned: one store per lane each (N == 4)
     const int32_t* actions;  // [B][N] (steps == 1) or NULL = DrunkHamster
     int32_t* rewards;        // [steps][B][N]
@@ -146,8 +267,16 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 const u32x4* src = (const u32x4*)wave_lds;
                 u32x4* dst = (u32x4*)(a.obs + ((int64_t)t * B + g0) * N * 48);
-                const int pieces = wave_games * N * 3;
-                for (int i = lane; i < pieces; i += wave_games) dst[i] = src[i];
+                if (wave_games == 64) {  // all reads, one wait, all stores
+                    u32x4 pc[3 * N];
+#pragma unroll
+                    for (int j = 0; j < 3 * N; j++) pc[j] = src[lane + 64 * j];
+#pragma unroll
+                    for (int j = 0; j < 3 * N; j++) dst[lane + 64 * j] = pc[j];
+                } else {
+                    const int pieces = wave_games * N * 3;
+                    for (int i = lane; i < pieces; i += wave_games) dst[i] = src[i];
+                }
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             } else {
 #pragma unroll
@@ -262,7 +391,12 @@ __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
     load_game<N>(s, g, G);
     typename RngOf<MODE, kPlayPrefetch>::T rng;
     ByteBuf buf;
-    RngOf<MODE, kPlayPrefetch>::load(s, g, rng, buf);
+    if constexpr (MODE == RNG_NUMPY_RING || MODE == RNG_NUMPY_RING_HBM) {
+        uint8_t* slot = wave_lds + a.wave_lds - 64 * a.ring_lds + lane * a.ring_lds;
+        RngOf<MODE, kPlayPrefetch>::load(s, g, rng, buf, slot);
+    } else {
+        RngOf<MODE, kPlayPrefetch>::load(s, g, rng, buf);
+    }
     int32_t sum_res[N], episodes;
     load_results<N>(s, g, a.flags, sum_res, episodes);
     play_steps<N>(s, a, g, lane, wave_lds, G, rng, buf, sum_res, episodes);
@@ -383,6 +517,7 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
         {(void**)&s.sum_res, sizeof(int32_t) * N * B},     {(void**)&s.episodes, sizeof(int32_t) * B},
         {(void**)&s.mt_pos, sizeof(uint32_t) * B},         {(void**)&s.ctr, sizeof(uint64_t) * B},
         {(void**)&s.mt, rng_mode == SN_RNG_NUMPY_MT ? sizeof(uint32_t) * kMtN * B : 4},
+        {(void**)&s.mt0, sizeof(uint32_t) * B},
     };
     for (auto& a : allocs) {
         if (hipMalloc(a.p, a.bytes) != hipSuccess) {
@@ -390,6 +525,14 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
             return fail(SN_ENOMEM, "hipMalloc of device state failed");
         }
         (void)hipMemset(*a.p, 0, a.bytes);
+    }
+    e->chunk_steps = 10;
+    if (rng_mode == SN_RNG_NUMPY_MT) {
+        const sn_status r = sn_set_option(e, SN_OPT_RING_WORDS, N <= 4 ? 256 : 512);
+        if (r != SN_OK) {
+            sn_destroy(e);
+            return r;
+        }
     }
     hipLaunchKernelGGL(k_seed, dim3(grid_for(B)), dim3(kBlock), 0, 0, s);
     hipError_t err = hipDeviceSynchronize();
@@ -406,11 +549,37 @@ sn_status sn_destroy(sn_env* e) {
     if (!e) return SN_OK;
     (void)hipSetDevice(e->device);
     DevState& s = e->s;
-    void* ps[] = {s.hand, s.row_lo, s.row_hi, s.score, s.sum_res, s.episodes, s.mt_pos, s.ctr, s.mt};
+    void* ps[] = {s.hand, s.row_lo, s.row_hi, s.score, s.sum_res, s.episodes, s.mt_pos, s.ctr, s.mt, s.mt0, s.ring};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     delete e;
     return SN_OK;
+}
+
+sn_status sn_set_option(sn_env* e, int option, int value) {
+    if (!e) return fail(SN_EINVAL, "env is NULL");
+    DevState& s = e->s;
+    switch (option) {
+        case SN_OPT_RING_WORDS: {
+            if (value < 0 || value > 512 || (value % 64)) return fail(SN_EINVAL, "ring words must be a multiple of 64 in 0..512");
+            if (value && s.rng_mode != SN_RNG_NUMPY_MT) return fail(SN_EINVAL, "the ring feeds numpy-compat mode only");
+            HIP_TRY(hipSetDevice(e->device));
+            HIP_TRY(hipDeviceSynchronize());
+            if (s.ring) (void)hipFree(s.ring);
+            s.ring = nullptr;
+            s.ring_w = 0;
+            if (value) {
+                if (hipMalloc((void**)&s.ring, (size_t)value * (size_t)s.B) != hipSuccess) return fail(SN_ENOMEM, "ring allocation failed");
+                s.ring_w = value;
+            }
+            return SN_OK;
+        }
+        case SN_OPT_CHUNK_STEPS:
+            if (value < 1) return fail(SN_EINVAL, "chunk steps must be >= 1");
+            e->chunk_steps = value;
+            return SN_OK;
+        default: return fail(SN_EINVAL, "unknown option");
+    }
 }
 
 sn_status sn_info(const sn_env* e, int64_t* B, int* N, int* C, int* mode) {
@@ -444,15 +613,62 @@ sn_status sn_reset_to(sn_env* e, const int8_t* board, const int8_t* hands, void*
     return SN_OK;
 }
 
-static sn_status launch_play(sn_env* e, PlayArgs a, hipStream_t st) {
+// LDS per CU (gfx950); a k_play block (4 waves) must fit in it
+constexpr int kLdsBytes = 160 * 1024;
+
+static sn_status launch_play_one(sn_env* e, PlayArgs a, hipStream_t st) {
     const DevState& s = e->s;
+    const bool ring = (s.rng_mode == SN_RNG_NUMPY_MT) && !a.actions && s.ring_w > 0;
     int wave = 64 * kDeckStride;
     if (a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15) == 0) wave = max(wave, 64 * s.N * 48);
+    a.ring_lds = 0;
+    const int ring_stride = ring_lds_stride(s.ring_w);
+    const bool ring_in_lds = ring && (wave + 64 * ring_stride) * (kBlock / 64) <= kLdsBytes;
+    if (ring_in_lds) {
+        a.ring_lds = ring_stride;
+        wave += 64 * ring_stride;
+    }
     a.wave_lds = wave;
     a.vec_out = ((((uintptr_t)a.rewards) & 15) == 0) && ((((uintptr_t)a.actions_out) & 3) == 0);
     const size_t shmem = (size_t)wave * (kBlock / 64);
     if (a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15)) return fail(SN_EINVAL, "obs with stride 48 must be 16-byte aligned");
-    if (s.rng_mode == SN_RNG_NUMPY_MT) {
+    if (ring) {
+        constexpr int GPW = kPrepGamesPerWave;
+        const dim3 pg((unsigned)((s.B + GPW * (kBlock / 64) - 1) / (GPW * (kBlock / 64))));
+        switch (s.ring_w / 64) {
+            case 1: hipLaunchKernelGGL((k_mt_prep<1, GPW>), pg, dim3(kBlock), 0, st, s); break;
+            case 2: hipLaunchKernelGGL((k_mt_prep<2, GPW>), pg, dim3(kBlock), 0, st, s); break;
+            case 3: hipLaunchKernelGGL((k_mt_prep<3, GPW>), pg, dim3(kBlock), 0, st, s); break;
+            case 4: {
+                static const int dbg = getenv("SECHS_PREP_DBG") ? atoi(getenv("SECHS_PREP_DBG")) : 0;
+                if (dbg == 1) hipLaunchKernelGGL((k_mt_prep<4, GPW, 1>), pg, dim3(kBlock), 0, st, s);
+                else if (dbg == 2) hipLaunchKernelGGL((k_mt_prep<4, GPW, 2>), pg, dim3(kBlock), 0, st, s);
+                else if (dbg == 3) hipLaunchKernelGGL((k_mt_prep<4, GPW, 3>), pg, dim3(kBlock), 0, st, s);
+                else if (dbg == 4) hipLaunchKernelGGL((k_mt_prep<4, 1>), dim3((unsigned)((s.B + 3) / 4)), dim3(kBlock), 0, st, s);
+                else if (dbg == 5) hipLaunchKernelGGL((k_mt_prep<4, 8>), dim3((unsigned)((s.B + 31) / 32)), dim3(kBlock), 0, st, s);
+                else hipLaunchKernelGGL((k_mt_prep<4, GPW>), pg, dim3(kBlock), 0, st, s);
+                break;
+            }
+            case 5: hipLaunchKernelGGL((k_mt_prep<5, GPW>), pg, dim3(kBlock), 0, st, s); break;
+            case 6: hipLaunchKernelGGL((k_mt_prep<6, GPW>), pg, dim3(kBlock), 0, st, s); break;
+            case 7: hipLaunchKernelGGL((k_mt_prep<7, GPW>), pg, dim3(kBlock), 0, st, s); break;
+            case 8: hipLaunchKernelGGL((k_mt_prep<8, GPW>), pg, dim3(kBlock), 0, st, s); break;
+            default: return fail(SN_EINVAL, "bad ring size");
+        }
+        if (ring_in_lds) {
+            SN_DISPATCH_N(s.N, {
+                HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_RING>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
+                hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_RING>), dim3(grid_for(s.B)), dim3(kBlock), shmem, st, s, a);
+            });
+        } else {
+            SN_DISPATCH_N(s.N, {
+                HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_RING_HBM>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
+                hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_RING_HBM>), dim3(grid_for(s.B)), dim3(kBlock), shmem, st, s, a);
+            });
+        }
+    } else if (s.rng_mode == SN_RNG_NUMPY_MT) {
         SN_DISPATCH_N(s.N, {
             HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_MT>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
@@ -466,6 +682,27 @@ static sn_status launch_play(sn_env* e, PlayArgs a, hipStream_t st) {
         });
     }
     HIP_TRY(hipGetLastError());
+    return SN_OK;
+}
+
+// A ring-fed (numpy-MT, in-kernel DrunkHamster) rollout runs in launches of
+// at most chunk_steps env-steps, each behind its own k_mt_prep, so that one
+// ring covers a launch's draws (a 4-player episode: 193.5 +- 9.3 words).
+static sn_status launch_play(sn_env* e, PlayArgs a, hipStream_t st) {
+    const DevState& s = e->s;
+    const bool ring = (s.rng_mode == SN_RNG_NUMPY_MT) && !a.actions && s.ring_w > 0;
+    if (!ring || a.steps <= e->chunk_steps) return launch_play_one(e, a, st);
+    const int64_t B = s.B, N = s.N;
+    for (int t0 = 0; t0 < a.steps; t0 += e->chunk_steps) {
+        PlayArgs c = a;
+        c.steps = min(e->chunk_steps, a.steps - t0);
+        if (a.rewards) c.rewards = a.rewards + (int64_t)t0 * B * N;
+        if (a.done) c.done = a.done + (int64_t)t0 * B;
+        if (a.actions_out) c.actions_out = a.actions_out + (int64_t)t0 * B * N;
+        if (a.obs) c.obs = a.obs + (int64_t)t0 * B * N * a.obs_stride;
+        const sn_status r = launch_play_one(e, c, st);
+        if (r != SN_OK) return r;
+    }
     return SN_OK;
 }
 
@@ -566,6 +803,29 @@ static void mt_finish_round(uint32_t* a, int p) {
     }
 }
 
+// Undo the twist of the new round's words [0, T): new[j] = src ^ (y >> 1) ^
+// (y & 1 ? A : 0) with y = (old[j] & UPPER) | (old[j+1] & LOWER) and src =
+// new[j-227] (j >= 227) or old[j+397] (j < 227: still in place, or itself
+// restored from the j >= 227 words when T > 397).  A's top bit is set and
+// y >> 1's is not, so the top bit of new[j] ^ src is y & 1 and y follows.
+// old[0]'s low 31 bits never enter the twist; they come from mt0.
+static uint32_t mt_untwist_y(uint32_t t) {
+    const uint32_t lsb = t >> 31;
+    if (lsb) t ^= 0x9908b0dfu;
+    return (t << 1) | lsb;
+}
+
+static void mt_unstraddle(uint32_t* a, int T, uint32_t old0) {
+    constexpr int D = kMtN - kMtM;  // 227
+    uint32_t y[kMtN];
+    for (int j = D; j < T; j++) y[j] = mt_untwist_y(a[j] ^ a[j - D]);
+    auto old_at = [&](int m) -> uint32_t {  // m >= 397
+        return (m < T) ? ((y[m] & 0x80000000u) | (y[m - 1] & 0x7fffffffu)) : a[m];
+    };
+    for (int j = 0; j < T && j < D; j++) y[j] = mt_untwist_y(a[j] ^ old_at(j + kMtM));
+    for (int j = 0; j < T; j++) a[j] = (y[j] & 0x80000000u) | ((j == 0 ? old0 : y[j - 1]) & 0x7fffffffu);
+}
+
 sn_status sn_mt_get(sn_env* e, int64_t game, uint32_t* key, int32_t* pos) {
     if (!e || !key || !pos) return fail(SN_EINVAL, "NULL argument");
     if (e->s.rng_mode != SN_RNG_NUMPY_MT) return fail(SN_EINVAL, "env is not in numpy-compat RNG mode");
@@ -576,8 +836,14 @@ sn_status sn_mt_get(sn_env* e, int64_t game, uint32_t* key, int32_t* pos) {
     HIP_TRY(hipMemcpy(key, e->s.mt + game * kMtN, sizeof(uint32_t) * kMtN, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(&code, e->s.mt_pos + game, sizeof(uint32_t), hipMemcpyDeviceToHost));
     // decode (sechs_device.h MtGenT): words [pos-cnt, pos) twisted, unconsumed
-    const int p = (int)(code & 0x7FFu);
-    if (p > 0 && p < kMtN) mt_finish_round(key, p);  // twist the rest of this round in place
+    const int p = (int)(code & 0x7FFu), cnt = (int)((code >> 16) & kMtCntMask);
+    if (cnt > p && p > 0) {  // straddling: still in the previous round, whose head [0, p) was overwritten
+        uint32_t old0 = 0;
+        HIP_TRY(hipMemcpy(&old0, e->s.mt0 + game, sizeof(uint32_t), hipMemcpyDeviceToHost));
+        mt_unstraddle(key, p, old0);
+    } else if (p > 0 && p < kMtN) {
+        mt_finish_round(key, p);  // twist the rest of this round in place
+    }
     *pos = (int32_t)mt_numpy_pos(code);
     return SN_OK;
 }

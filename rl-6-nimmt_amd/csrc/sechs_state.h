@@ -38,6 +38,10 @@ struct DevState {
     uint32_t* mt;
     uint32_t* mt_pos;
     uint64_t* ctr;
+    uint32_t* mt0;   // [B] old-round mt[0] saved by k_mt_prep (export of straddling codes)
+    u32x4* ring;     // [ring_w/16][B] low bytes of the words k_mt_prep twisted ahead
+    int ring_w;      // ring words per game (multiple of 64), 0 = no ring
+    int pad2_;
 };
 
 constexpr int kBlock = 256;
@@ -65,6 +69,112 @@ struct RngOf<RNG_PHILOX, PF> {
     }
     static __device__ __forceinline__ void store(const DevState& s, int64_t g, const T& r, const ByteBuf& buf) {
         s.ctr[g] = r.consumed(buf);
+    }
+};
+
+// numpy-MT words for k_play from the ring k_mt_prep filled just before the
+// launch: the low bytes of the next ring_w words of the game's stream, in
+// 16-B chunks interleaved over games (chunk q of game g at ring[q*B + g], so
+// a wave's lanes reading their q-th chunks read one contiguous 1-KB run).
+// LDS = true: the lane copies its ring to its LDS slot at launch start (16
+// coalesced loads per lane, one wait), so the step loop issues no global
+// loads at all -- a global load there would wait behind every observation
+// store still in flight (vmcnt counts loads and stores in issue order).
+// LDS = false: chunks come from HBM, the next one prefetched.  A lane that
+// runs the ring dry continues with MtGen from the in-place state (rare: the
+// ring is sized for a launch's draws + ~6.5 sd).
+template <bool LDS>
+struct RingGen {
+    const u32x4* base;    // ring + g
+    const uint8_t* lring;  // LDS copy (LDS = true)
+    uint32_t* st;
+    int64_t B;
+    u32x4 c0, c1;          // chunks q, q + 1 (LDS = false)
+    uint32_t q, nq, half;  // next chunk, chunks in the ring, next 8-B half of c0
+    uint32_t rb;           // ring bytes not yet handed out
+    uint32_t T, extra;     // twist position; twisted words past the ring
+    uint32_t on;           // MtGen fallback active
+    MtGenT<1> mt;
+
+    __device__ __forceinline__ void load(const DevState& s, int64_t g, ByteBuf& buf, uint8_t* lds_slot) {
+        const uint32_t code = s.mt_pos[g];
+        T = code & 0x7FFu;
+        const uint32_t rem = (code >> 16) & kMtCntMask;
+        rb = (uint32_t)s.ring_w;  // k_mt_prep left rem >= ring_w
+        extra = rem - rb;
+        st = s.mt + g * kMtN;
+        B = s.B;
+        base = s.ring + g;
+        nq = rb >> 4;
+        q = 0u, half = 0u, on = 0u;
+        if (LDS) {
+            lring = lds_slot;
+            for (uint32_t i = 0; i < nq; i++) {  // 8-B aligned slot: two ds_write_b64
+                const u32x4 c = base[(int64_t)i * B];
+                *(uint64_t*)(lds_slot + 16u * i) = (uint64_t)c.x | ((uint64_t)c.y << 32);
+                *(uint64_t*)(lds_slot + 16u * i + 8u) = (uint64_t)c.z | ((uint64_t)c.w << 32);
+            }
+        } else {
+            c0 = base[0];
+            c1 = base[B];
+        }
+        buf.clear();
+    }
+    __device__ __forceinline__ uint32_t save(const ByteBuf& buf) {
+        return on ? mt.save(buf) : (T | ((rb + extra + buf.cnt) << 16));
+    }
+    __device__ __forceinline__ bool gen(ByteBuf& buf) {
+        if (rb) {
+            uint64_t v;
+            if (LDS) {
+                v = *(const uint64_t*)(lring + 8u * (2u * q + half));
+                q += half;
+            } else {
+                v = half ? ((uint64_t)c0.z | ((uint64_t)c0.w << 32)) : ((uint64_t)c0.x | ((uint64_t)c0.y << 32));
+                if (half) {
+                    c0 = c1;
+                    q += 1u;
+                    c1 = base[(int64_t)min(q + 1u, nq - 1u) * B];
+                }
+            }
+            buf.append(v, 8u);
+            rb -= 8u;
+            half ^= 1u;
+            return true;
+        }
+        if (!on) {
+            mt.load(st, T | (extra << 16), buf, true);
+            on = 1u;
+        }
+        return mt.gen(buf);
+    }
+    __device__ __forceinline__ void topup(ByteBuf& buf) {
+        if (buf.cnt <= 24u) gen(buf);
+    }
+    __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf); }  // cnt == 0: always succeeds
+};
+
+// bytes of a lane's LDS ring slot (+8: odd 8-B stride, conflict-free ds_read_b64 rows)
+__host__ __device__ __forceinline__ int ring_lds_stride(int ring_w) { return ring_w + 8; }
+
+template <int PF>
+struct RngOf<RNG_NUMPY_RING, PF> {
+    using T = RingGen<true>;
+    static __device__ __forceinline__ void load(const DevState& s, int64_t g, T& r, ByteBuf& buf, uint8_t* slot) {
+        r.load(s, g, buf, slot);
+    }
+    static __device__ __forceinline__ void store(const DevState& s, int64_t g, T& r, const ByteBuf& buf) {
+        s.mt_pos[g] = r.save(buf);
+    }
+};
+template <int PF>
+struct RngOf<RNG_NUMPY_RING_HBM, PF> {
+    using T = RingGen<false>;
+    static __device__ __forceinline__ void load(const DevState& s, int64_t g, T& r, ByteBuf& buf, uint8_t*) {
+        r.load(s, g, buf, nullptr);
+    }
+    static __device__ __forceinline__ void store(const DevState& s, int64_t g, T& r, const ByteBuf& buf) {
+        s.mt_pos[g] = r.save(buf);
     }
 };
 
@@ -120,16 +230,41 @@ __device__ __forceinline__ void store_game(const DevState& s, int64_t g, const G
     s.row_hi[0 * B + g] = G.b.hi.x, s.row_hi[1 * B + g] = G.b.hi.y, s.row_hi[2 * B + g] = G.b.hi.z, s.row_hi[3 * B + g] = G.b.hi.w;
 }
 
+// 10-input sorting network: 29 compare-exchanges in 8 layers (Knuth, TAOCP
+// 5.3.4; checked by the 0-1 principle over all 2^10 inputs).  Branch-free
+// min/max in registers -- a wave sorts 64 hands in ~60 VALU.
+__device__ __forceinline__ void sort10(uint32_t (&v)[10]) {
+    constexpr int net[29][2] = {{0, 8}, {1, 9}, {2, 7}, {3, 5}, {4, 6}, {0, 2}, {1, 4}, {5, 8}, {7, 9}, {0, 3},
+                                {2, 4}, {5, 7}, {6, 9}, {0, 1}, {3, 6}, {8, 9}, {1, 5}, {2, 3}, {4, 8}, {6, 7},
+                                {1, 2}, {3, 5}, {4, 6}, {7, 8}, {2, 3}, {4, 5}, {6, 7}, {3, 4}, {5, 6}};
+#pragma unroll
+    for (int c = 0; c < 29; c++) {
+        const uint32_t a = v[net[c][0]], b = v[net[c][1]];
+        v[net[c][0]] = min(a, b);
+        v[net[c][1]] = max(a, b);
+    }
+}
+
+// sorted legal list from 10 distinct cards
+__device__ __forceinline__ Hand hand_from_cards(uint32_t (&v)[10]) {
+    sort10(v);
+    Hand h;
+    h.lo = (uint64_t)(v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24)) |
+           ((uint64_t)(v[4] | (v[5] << 8) | (v[6] << 16) | (v[7] << 24)) << 32);
+    h.hi = v[8] | (v[9] << 8) | 0xFFFF0000u;
+    return h;
+}
+
 // env.py:99-112 _deal from a dealt deck: hand p = sorted(deck[10p:10p+10]),
 // row r = [deck[C-1-r]]
 template <int N, class D>
 __device__ __forceinline__ void deal_from(const D& deck, int C, Game<N>& G) {
 #pragma unroll
     for (int p = 0; p < N; p++) {
-        u32x4 set = {0u, 0u, 0u, 0u};
+        uint32_t v[kHand];
 #pragma unroll
-        for (int k = 0; k < kHand; k++) set = set_bit(set, deck(kHand * p + k));
-        G.hand[p] = hand_from_set(set);
+        for (int k = 0; k < kHand; k++) v[k] = deck(kHand * p + k);
+        G.hand[p] = hand_from_cards(v);
         G.score[p] = 0;
     }
     const uint32_t r0 = deck(C - 1), r1 = deck(C - 2), r2 = deck(C - 3), r3 = deck(C - 4);
@@ -144,11 +279,18 @@ __device__ __forceinline__ void deal_from(const D& deck, int C, Game<N>& G) {
 // Word-synchronous form: instead of one rejection loop per draw, the lane
 // walks its words in order, 8 per pass (the buffered ones first, then fresh
 // refills), and every word advances the shuffle by at most one draw:
-// accepted (x <= i) -> swap(i, x), i -= 1; rejected -> nothing (a self-swap,
-// so the pass is branch-free).  That is exactly numpy's sequence of
-// masked-rejection draws, and all lanes of a wave consume their words in
-// lockstep (one refill per pass for every lane still shuffling).  A lane
-// that finishes inside a pass keeps the unused words for its next draws.
+// accepted (x <= i) -> swap(i, x), i -= 1; rejected -> nothing.  That is
+// exactly numpy's sequence of masked-rejection draws, and all lanes of a
+// wave consume their words in lockstep (one refill per pass for every lane
+// still shuffling).  A lane that finishes inside a pass keeps the unused
+// words for its next draws.
+//
+// One LDS round trip per pass: the (up to) 8 swaps' positions are known
+// before any deck value is (they depend on the words only), so the pass
+// issues all 16 reads at once, forwards in registers the values the pass
+// itself has already moved, and writes back in order.  A swap at step k
+// writes positions i_k (never read again: later positions are all < i_k)
+// and j_k; a later read aliases only an earlier j_k.
 template <int N, class R>
 __device__ __forceinline__ void deal_shuffle(R& rng, ByteBuf& buf, uint8_t* deck, int C, Game<N>& G) {
     for (int i = 0; i < C; i += 4) *(uint32_t*)(deck + i) = (uint32_t)i * 0x01010101u + 0x03020100u;
@@ -157,23 +299,58 @@ __device__ __forceinline__ void deal_shuffle(R& rng, ByteBuf& buf, uint8_t* deck
         if (buf.cnt == 0u) rng.force(buf);
         const uint32_t valid = min(buf.cnt, 8u);
         const uint64_t w = buf.b0;
-        uint32_t used = 0u;
+        uint32_t I[8], J[8], Jm[8];
+        uint32_t used = 0u, ii = i;
 #pragma unroll
         for (uint32_t k = 0; k < 8u; k++) {
-            const bool act = (k < valid) && (i >= 1u);
-            const uint32_t m = 0xFFFFFFFFu >> __builtin_clz(i | 1u);
+            const bool act = (k < valid) && (ii >= 1u);
+            const uint32_t m = 0xFFFFFFFFu >> __builtin_clz(ii | 1u);
             const uint32_t x = (uint32_t)(w >> (8u * k)) & m;
-            const bool acc = act && (x <= i);
-            const uint32_t j = acc ? x : i;
-            const uint8_t di = deck[i], dj = deck[j];
-            deck[i] = dj;
-            deck[j] = di;
-            i -= acc ? 1u : 0u;
+            const bool acc = act && (x <= ii);
+            I[k] = ii;
+            J[k] = acc ? x : ii;      // rejected / past the end: a no-op self-swap
+            Jm[k] = acc ? x : 0xFFu;  // positions this pass has written
+            ii -= acc ? 1u : 0u;
             used = act ? k + 1u : used;
         }
+        uint32_t DI[8], DJ[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            DI[k] = deck[I[k]];
+            DJ[k] = deck[J[k]];
+        }
+#pragma unroll
+        for (int k = 1; k < 8; k++)
+#pragma unroll
+            for (int q = 0; q < k; q++) {  // ascending: the latest write wins
+                DI[k] = (Jm[q] == I[k]) ? DI[q] : DI[k];
+                DJ[k] = (Jm[q] == J[k]) ? DI[q] : DJ[k];
+            }
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            deck[J[k]] = (uint8_t)DI[k];
+            deck[I[k]] = (uint8_t)DJ[k];
+        }
+        i = ii;
         buf.drop(used);
     }
-    deal_from<N>([&](int i) -> uint32_t { return deck[i]; }, C, G);
+    // deal: hands from the first 10N bytes (4-B aligned slot), rows from the end
+    constexpr int NW = (kHand * N + 3) / 4;
+    uint32_t dw[NW];
+#pragma unroll
+    for (int q = 0; q < NW; q++) dw[q] = *(const uint32_t*)(deck + 4 * q);
+#pragma unroll
+    for (int p = 0; p < N; p++) {
+        uint32_t v[kHand];
+#pragma unroll
+        for (int k = 0; k < kHand; k++) v[k] = (dw[(kHand * p + k) >> 2] >> (8 * ((kHand * p + k) & 3))) & 0xFFu;
+        G.hand[p] = hand_from_cards(v);
+        G.score[p] = 0;
+    }
+    const uint32_t r0 = deck[C - 1], r1 = deck[C - 2], r2 = deck[C - 3], r3 = deck[C - 4];
+    G.b.lo.x = r0, G.b.lo.y = r1, G.b.lo.z = r2, G.b.lo.w = r3;
+    G.b.hi.x = meta_row(r0), G.b.hi.y = meta_row(r1), G.b.hi.z = meta_row(r2), G.b.hi.w = meta_row(r3);
+    G.n = kHand;
 }
 
 // ---------------------------------------------------------------- observation
@@ -262,5 +439,6 @@ inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBloc
 
 struct sn_env {
     int device;
+    int chunk_steps;  // SN_OPT_CHUNK_STEPS
     sechs::DevState s;
 };

@@ -175,6 +175,13 @@ class VecSechsNimmtEnv:
         nat.check(nat.lib().sn_clear_results(self._h, self._stream()), "sn_clear_results")
 
     # ------------------------------------------------------------ numpy RNG bridge
+    def set_option(self, ring_words=None, chunk_steps=None):
+        """numpy-compat rollout tuning (include/sechs.h SN_OPT_*); results never depend on it"""
+        if ring_words is not None:
+            nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_RING_WORDS, int(ring_words)), "sn_set_option")
+        if chunk_steps is not None:
+            nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_CHUNK_STEPS, int(chunk_steps)), "sn_set_option")
+
     def get_mt_state(self, game=0):
         key = np.zeros(624, dtype=np.uint32)
         pos = ctypes.c_int32()

@@ -308,3 +308,41 @@ def test_mt_state_across_round_boundaries_every_step():
             k, p = _np_form(*env.get_mt_state(g))
             rk, rp = _np_form(np.frombuffer(bytes(rngs[g].mt), dtype=np.uint32), rngs[g].pos)
             assert p == rp and np.array_equal(k, rk), (t, g)
+
+
+@pytest.mark.parametrize("ring_words,chunk_steps", [(0, 10), (64, 10), (64, 1), (128, 3), (512, 25), (256, 7)])
+def test_ring_options_do_not_change_results(ring_words, chunk_steps):
+    """k_mt_prep's twist-ahead ring is an optimisation only: every ring size
+    (0 = lazy per-lane MT19937; 64 runs the ring dry inside every episode, so
+    the MtGen fallback continues mid-launch) and launch chunking give the
+    oracle's actions, rewards, obs and final numpy MT states."""
+    B, N, T, seed = 300, 4, 37, 21
+    env = venv(B, N, seed=seed, rng="numpy")
+    env.set_option(ring_words=ring_words, chunk_steps=chunk_steps)
+    env.reset()
+    ref = O.VecOracle(B, N, rng_mode=O.RNG_NUMPY_MT, seed=seed)
+    ref.reset()
+    out = env.rollout(T, want_actions=True, want_obs=True)
+    rr, rd, ra, ro = ref.rollout(T, want_obs=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(out["actions"].cpu().numpy(), ra)
+    assert np.array_equal(out["rewards"].cpu().numpy(), rr)
+    assert np.array_equal(out["done"].cpu().numpy(), rd)
+    assert np.array_equal(out["obs"].cpu().numpy()[..., :47], ro)
+    rngs = ref.v.contents.rngs
+    for g in range(0, B, 7):
+        k, p = _np_form(*env.get_mt_state(g))
+        rk, rp = _np_form(np.frombuffer(bytes(rngs[g].mt), dtype=np.uint32), rngs[g].pos)
+        assert p == rp and np.array_equal(k, rk), g
+
+
+def test_ring_option_validation():
+    env = venv(4, 4, rng="numpy")
+    for bad in (-64, 32, 576):
+        with pytest.raises(ValueError):
+            env.set_option(ring_words=bad)
+    with pytest.raises(ValueError):
+        env.set_option(chunk_steps=0)
+    penv = venv(4, 4, rng="philox")
+    with pytest.raises(ValueError):
+        penv.set_option(ring_words=256)

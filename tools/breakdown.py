@@ -5,6 +5,7 @@
   play1+deal   the 10th env-step + the auto-reset deal
   episode      one full bench launch (10 env-steps incl. the deal)
 for numpy-MT and Philox, with and without int8 obs.   usage: breakdown.py [B]
+(back-to-back launches, so small kernels are not inflated by host latency)
 """
 import json
 import os
@@ -20,16 +21,16 @@ from rl_6_nimmt.vec_env import VecSechsNimmtEnv  # noqa: E402
 
 
 def timed(fn, reps=20):
-    ts = []
-    for _ in range(reps):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        fn()
-        b.record()
-        ts.append((a, b))
+    """mean time of `reps` back-to-back calls (the queue stays full: kernel time, not host latency)"""
+    fn()
     torch.cuda.synchronize()
-    v = sorted(x.elapsed_time(y) for x, y in ts)
-    return v[len(v) // 2] * 1e3  # median, us
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) * 1e3 / reps  # us
 
 
 def main():
@@ -46,13 +47,10 @@ def main():
             r = {}
             r["episode"] = timed(lambda: env.rollout(10, out=out10))
             r["reset"] = timed(lambda: env.reset())
-            p9, p1 = [], []
-            for _ in range(10):
-                env.reset()
-                p9.append(timed(lambda: env.rollout(9, out=out9), reps=1))
-                p1.append(timed(lambda: env.rollout(1, out=out1), reps=1))
-            r["play9"] = sorted(p9)[5]
-            r["play1+deal"] = sorted(p1)[5]
+            t_r9 = timed(lambda: (env.reset(), env.rollout(9, out=out9)))
+            t_r91 = timed(lambda: (env.reset(), env.rollout(9, out=out9), env.rollout(1, out=out1)))
+            r["play9"] = t_r9 - r["reset"]
+            r["play1+deal"] = t_r91 - t_r9
             res[f"{rng}{'+obs' if obs else ''}"] = r
             print(rng, "obs" if obs else "no-obs", json.dumps({k: round(v, 1) for k, v in r.items()}), flush=True)
             env.close()
