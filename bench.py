@@ -8,10 +8,12 @@ Workload (BASELINE.json configs[1]): per GPU,
 B = 65 536 independent 4-player games of DrunkHamster self-play in
 numpy-compat RNG mode (game g replays np.random.seed(g) +
 GameSession(DrunkHamster() x 4) of the reference, episode after episode).
-One bench step = one launch of the fused rollout kernel that advances every
-game by one full episode (10 env-steps: policy draw, simultaneous-play
-resolution, scoring, per-seat int8 observation, auto-reset deal) and writes
-the whole trajectory (obs, actions, rewards, done) to HBM.  Inputs are
+One bench step = one rollout call that advances every game by one full
+episode (10 env-steps: policy draw, simultaneous-play resolution, scoring,
+per-seat int8 observation, auto-reset deal) and writes the whole trajectory
+(obs, actions, rewards, done) to HBM: in numpy mode two launches, k_mt_prep
+(each game's MT19937 stream twisted ahead, coalesced) and k_play (the game
+loop, drawing from an LDS copy of the prepared words).  Inputs are
 resident on the device before timing starts.
 
 Multi-GPU: game shards are independent (rank r owns global games
@@ -40,12 +42,13 @@ STEPS_PER_LAUNCH = 10
 # hands, board, lens, scores, rewards 4N, done 1 written) + 47N for the int8
 # observation the step emits.
 ALGO_BYTES_PER_STEP = (33 * N_PLAYERS + 57) + 47 * N_PLAYERS  # 377 B at N = 4
-# HBM bytes per k_play launch from rocprofv3 PMC passes of this kernel
-# (tools/pmc_config2.sh: FETCH_SIZE and WRITE_SIZE in separate passes, gfx950
-# corrections of MI355X_MICROARCH.md applied by tools/pmc_traffic.py).  PMC
-# counters cannot be read inside a plain run, so the committed summary of the
-# current kernel is reported beside the live timing.
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_v12_pmc_traffic_{rng}.json")
+# HBM bytes per bench step from rocprofv3 PMC passes of its kernels (numpy
+# mode: k_mt_prep + k_play; philox: k_play) -- tools/pmc_config2.sh: FETCH_SIZE
+# and WRITE_SIZE in separate passes, gfx950 corrections of MI355X_MICROARCH.md
+# applied by tools/pmc_traffic.py.  PMC counters cannot be read inside a plain
+# run, so the committed summary of the current kernels is reported beside the
+# live timing.
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_v13_pmc_traffic_{rng}.json")
 
 
 def parse():
@@ -295,10 +298,11 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+            "traffic_unit": "HBM bytes per bench step (PMC FETCH_SIZE x2 + WRITE_SIZE, summed over its kernels)",
             "traffic_source": traffic_src,
             "traffic_gbs_at_live_kernel_ms": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
-            "kernel": "k_play<4, RNG_NUMPY_MT>",
+            "kernel": ("k_mt_prep<4,4> + k_play<4, RNG_NUMPY_RING> (one bench step: MT19937 twist-ahead, then the "
+                       "10 env-steps; timed together)" if args.rng == "numpy" else "k_play<4, RNG_PHILOX>"),
             "kernel_ms": kern_ms,
             "algo_bytes_per_env_step": ALGO_BYTES_PER_STEP,
         },

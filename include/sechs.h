@@ -133,8 +133,12 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          launch by k_mt_prep (multiple of 64, 64..512;
                          0 = no ring, k_play twists lazily per lane).
                          Default 256 for N <= 4, else 512.
-     SN_OPT_CHUNK_STEPS  env-steps per ring-fed launch (>= 1, default 10). */
-enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2 };
+     SN_OPT_CHUNK_STEPS  env-steps per k_mt_prep-fed launch (>= 1, default 10).
+     SN_OPT_FUSED        0 (default): k_mt_prep + k_play.  1: when the ring
+                         has >= 256 words and the LDS fits (N <= 4 with int8
+                         obs), one k_play_fused launch with MT19937 producer
+                         waves beside the play waves (slower today). */
+enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_FUSED = 3 };
 sn_status sn_set_option(sn_env* env, int option, int value);
 
 /* ---- Monte-Carlo search, MCSAgent (agents/mcts.py:17-188) ------------- */

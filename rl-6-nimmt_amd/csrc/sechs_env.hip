@@ -32,6 +32,7 @@ __global__ void k_seed(DevState s) {
             st[i] = v;
         }
         s.mt_pos[g] = 0u;
+        s.ringn[g] = 0u;
     } else {
         s.ctr[g] = 0u;
     }
@@ -111,7 +112,7 @@ __global__ __launch_bounds__(kBlock) void k_reset_to(DevState s, const int8_t* b
 // numpy's key.
 constexpr int kPrepGamesPerWave = 4;
 
-template <int NB, int GPW, int DBG = 0>  // ring_w / 64, games per wave
+template <int NB, int GPW>  // ring_w / 64, games per wave
 __global__ __launch_bounds__(kBlock) void k_mt_prep(DevState s) {
     constexpr uint32_t W = 64u * NB;
     constexpr uint32_t D = kMtN - kMtM;  // 227
@@ -169,14 +170,13 @@ __global__ __launch_bounds__(kBlock) void k_mt_prep(DevState s) {
             uint32_t v = A[q][b];
             if (k >= r && k < kt && k - r < D) {
                 v = mt_mix(A[q][b], bb, C[q][b]);
-                if (!(DBG & 2)) st[idx] = v;
+                st[idx] = v;
                 if (idx == 0u) s.mt0[g] = A[q][b];
             }
             if (b < NB) {  // ring bytes: 4 words per dword (lanes 4m..4m+3)
                 const uint32_t y = mt_temper(v) & 0xFFu;
                 const uint32_t d = y | (__shfl_down(y, 1) << 8) | (__shfl_down(y, 2) << 16) | (__shfl_down(y, 3) << 24);
-                if ((lane & 3u) == 0u && !(DBG & 1)) ring[(((int64_t)(k >> 4)) * s.B + g) * 4 + ((k >> 2) & 3u)] = d;
-                if ((DBG & 1) && d == 0x12345678u) ring[0] = d;
+                if ((lane & 3u) == 0u) ring[(((int64_t)(k >> 4)) * s.B + g) * 4 + ((k >> 2) & 3u)] = d;
             }
         }
         // words j >= 227 read words twisted just above: in order, after those stores
@@ -210,6 +210,7 @@ __global__ __launch_bounds__(kBlock) void k_mt_prep(DevState s) {
             const uint32_t Tn = T0[q] + (kt - r);
             s.mt_pos[g] = ((Tn > (uint32_t)kMtN) ? Tn - kMtN : Tn) | (kt << 16);
         }
+        if (lane == 0u) s.ringn[g] = W;
     }
 }
 
@@ -227,6 +228,7 @@ struct PlayArgs {
     uint8_t* actions_out;    // [steps][B][N]
     int8_t* obs;             // [steps][B][N][obs_stride]
     int32_t* invalid;        // [B]
+    int debug;               // k_play_fused: print handshake counters (SECHS_FUSED_DEBUG)
 };
 
 // The env-step loop of one lane (game g).  R supplies the random words
@@ -405,6 +407,258 @@ __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
     store_results<N>(s, g, a.flags, sum_res, episodes);
 }
 
+// ============================================================================
+// k_play_fused: the numpy-MT DrunkHamster rollout with the MT19937 twist
+// running beside the game, in the same workgroup.
+//
+// A workgroup = 4 play waves (256 games, one per lane, exactly k_play's
+// step loop) + kFusedProducers producer waves.  The producers twist each
+// game's stream ahead in place, 64 consecutive words per instruction (the
+// coalesced form of k_mt_prep), and stream the tempered low bytes into the
+// game's LDS ring (kFusedRing bytes, circular); a play lane takes 8 bytes at
+// a time from its ring.  The play waves are latency/VALU-bound at one wave
+// per SIMD, the producers are memory-bound: sharing the SIMDs, each hides
+// the other's stalls.  Handshake, all in LDS, per game: head = bytes
+// published by the producer (multiples of 8, published after its byte
+// writes completed: s_waitcnt lgkmcnt(0)), tail = bytes taken by the play
+// lane (published after its read issued; LDS executes a wave's operations
+// in order, so the producer never overwrites bytes not yet read).  A play
+// lane whose ring is empty sleeps until head moves (bounded: a lost producer
+// cannot hang the GPU, it only corrupts that game's draws).  The words
+// still in a ring at the end (up to kFusedRing) go back to HBM (s.ring,
+// ringn) and are the first words of the next launch, so play starts at once.
+// Stream accounting is MtGen's: code = twist pointer | twisted-unconsumed
+// words << 16, the old mt[0] saved whenever a round is crossed (mt0).
+// ============================================================================
+constexpr int kFusedProducers = 4;
+constexpr int kFusedRing = 256;               // ring bytes (= words) per game
+constexpr int kFusedRingStride = kFusedRing + 8;
+constexpr int kFusedGroup = 16;               // games a producer wave twists per pass (loads in flight)
+constexpr int kFusedThreads = (4 + kFusedProducers) * 64;
+
+struct FusedShared {   // at the end of the dynamic LDS
+    uint32_t head[256], tail[256], cons[256];
+    uint32_t done;
+    uint32_t dbg[8];   // SECHS_FUSED_DEBUG: passes, batches, idle polls, play sleeps, ...
+};
+
+struct FusedRing {
+    const uint8_t* ring;
+    volatile uint32_t* headp;
+    volatile uint32_t* tailp;
+    uint32_t tail, head_seen, sleeps;
+
+    __device__ __forceinline__ void gen(ByteBuf& buf) {
+        if (head_seen - tail < 8u) {
+            for (uint32_t spin = 0;; spin++) {
+                head_seen = *headp;
+                if (head_seen - tail >= 8u || spin > (1u << 20)) break;
+                __builtin_amdgcn_s_sleep(1);
+                sleeps++;
+            }
+        }
+        asm volatile("" ::: "memory");  // the ring read stays behind the head read (LDS runs them in order)
+        const uint64_t v = *(const uint64_t*)(ring + (tail & (uint32_t)(kFusedRing - 1)));
+        tail += 8u;
+        *tailp = tail;
+        buf.append(v, 8u);
+    }
+    __device__ __forceinline__ void topup(ByteBuf& buf) {
+        if (buf.cnt <= 24u) gen(buf);
+    }
+    __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf); }
+};
+
+template <int N>
+__global__ __launch_bounds__(kFusedThreads) void k_play_fused(DevState s, PlayArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
+    const int wave = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    const int64_t gb = (int64_t)blockIdx.x * 256;  // first game of the block
+    uint8_t* rings = lds_dyn + 4 * a.wave_lds;
+    FusedShared* sh = (FusedShared*)(rings + 256 * kFusedRingStride);
+    constexpr uint32_t RW = kFusedRing;
+    constexpr uint32_t D = kMtN - kMtM;  // 227
+
+    // ---- launch start: play lanes copy the leftover words of the last launch
+    if (wave < 4) {
+        const uint32_t i = wave * 64 + lane;  // game in block
+        const int64_t g = gb + i;
+        uint32_t L = 0u;
+        if (g < s.B) {
+            L = min(s.ringn[g], RW);
+            uint8_t* r = rings + i * kFusedRingStride;
+            for (uint32_t c = 0; c * 16u < L; c++) {
+                const u32x4 v = s.ring[(int64_t)c * s.B + g];
+                *(uint64_t*)(r + 16u * c) = (uint64_t)v.x | ((uint64_t)v.y << 32);
+                *(uint64_t*)(r + 16u * c + 8u) = (uint64_t)v.z | ((uint64_t)v.w << 32);
+            }
+        }
+        sh->head[i] = L & ~7u;
+        sh->tail[i] = 0u;
+        sh->cons[i] = 0u;
+        if (threadIdx.x == 0) sh->done = 0u;
+        if (threadIdx.x < 8) sh->dbg[threadIdx.x] = 0u;
+    }
+    __syncthreads();
+
+    if (wave < 4) {
+        // ---- play waves: k_play's step loop, words from the ring
+        const uint32_t i = wave * 64 + lane;
+        const int64_t g = gb + i;
+        if (g < s.B) {
+            uint8_t* wave_lds = lds_dyn + wave * a.wave_lds;
+            Game<N> G;
+            load_game<N>(s, g, G);
+            FusedRing rng;
+            rng.ring = rings + i * kFusedRingStride;
+            rng.headp = &sh->head[i];
+            rng.tailp = &sh->tail[i];
+            rng.tail = 0u;
+            rng.head_seen = 0u;
+            rng.sleeps = 0u;
+            ByteBuf buf;
+            buf.clear();
+            int32_t sum_res[N], episodes;
+            load_results<N>(s, g, a.flags, sum_res, episodes);
+            play_steps<N>(s, a, g, (int)lane, wave_lds, G, rng, buf, sum_res, episodes);
+            store_game<N>(s, g, G);
+            store_results<N>(s, g, a.flags, sum_res, episodes);
+            sh->cons[i] = rng.tail - buf.cnt;
+            if (a.debug) atomicAdd(&sh->dbg[3], rng.sleeps);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0u) atomicAdd(&sh->done, 1u);
+    } else {
+        // ---- producer waves: lane l owns game p + P*l of the block
+        constexpr int P = kFusedProducers;
+        constexpr int GPL = 256 / P;  // games per producer wave (<= 64)
+        const int p = wave - 4;
+        const uint32_t i = (uint32_t)p + (uint32_t)P * lane;  // my game (lanes < GPL)
+        const int64_t g = gb + i;
+        const bool mine = lane < (uint32_t)GPL && g < s.B;
+        uint32_t T = 0u, rem0 = 0u, made = 0u;
+        if (mine) {
+            const uint32_t code = s.mt_pos[g];
+            T = code & 0x7FFu;
+            rem0 = (code >> 16) & kMtCntMask;
+            made = min(s.ringn[g], RW);
+        }
+        const uint32_t T0 = (T == (uint32_t)kMtN) ? 0u : T;
+        uint32_t rot = 0u;
+        volatile uint32_t* vdone = &sh->done;
+        volatile uint32_t* vtail = sh->tail;
+        while (true) {
+            const bool fin = *vdone >= 4u;
+            const uint32_t tl = mine ? vtail[i] : 0u;
+            // room for a batch, keeping the <= 32 bytes the lane has taken but
+            // not consumed (its ByteBuf) intact: they are saved at the end
+            const bool want = mine && !fin && (made - tl) <= RW - 64u - 32u;
+            uint64_t mask = __ballot(want);
+            if (!mask) {
+                if (fin) break;
+                if (a.debug && lane == 0u) atomicAdd(&sh->dbg[2], 1u);
+                __builtin_amdgcn_s_sleep(2);
+                continue;
+            }
+            mask = (mask >> rot) | (rot ? (mask << (64u - rot)) : 0ull);  // fairness: rotate the start
+            int cnt = 0;
+            uint32_t ql[kFusedGroup];
+#pragma unroll
+            for (int q = 0; q < kFusedGroup; q++) {
+                ql[q] = ql[0];  // past cnt: a duplicate of the first (loads only, results unused)
+                if (mask) {
+                    ql[q] = ((uint32_t)__builtin_ctzll(mask) + rot) & 63u;
+                    mask &= mask - 1ull;
+                    cnt = q + 1;
+                }
+            }
+            rot = (rot + 17u) & 63u;
+            if (a.debug && lane == 0u) {
+                atomicAdd(&sh->dbg[0], 1u);
+                atomicAdd(&sh->dbg[1], (uint32_t)cnt);
+            }
+            // batch of game q: words [made, made + n); n < 64 only for the batch
+            // that starts twisting, so that the twist pointer stays 8-aligned.
+            // Branch-free: every lane loads three valid words for every game,
+            // so all 3 * kFusedGroup loads are in flight before the first use.
+            uint32_t A[kFusedGroup], Bv[kFusedGroup], Cv[kFusedGroup], IX[kFusedGroup], NQ[kFusedGroup];
+#pragma unroll
+            for (int q = 0; q < kFusedGroup; q++) {
+                const uint32_t l = ql[q];
+                const uint32_t gi = (uint32_t)p + (uint32_t)P * l;
+                const uint32_t* st = s.mt + (gb + gi) * kMtN;
+                const uint32_t mq = __builtin_amdgcn_readlane(made, l), rq = __builtin_amdgcn_readlane(rem0, l);
+                const uint32_t Tq = __builtin_amdgcn_readlane(T, l), T0q = __builtin_amdgcn_readlane(T0, l);
+                const uint32_t k = mq + lane;
+                NQ[q] = (mq + 64u <= rq) ? 64u : 64u - ((mq + 64u - rq) & 7u);
+                const bool re = k < rq;  // twisted by an earlier launch: stream index T - rem0 + k (mod 624)
+                const uint32_t idx = re ? (Tq + kMtN - rq + k) % (uint32_t)kMtN : (T0q + (k - rq)) % (uint32_t)kMtN;
+                IX[q] = (re || lane >= NQ[q]) ? 0xFFFFu : idx;
+                A[q] = st[idx];
+                Bv[q] = st[(idx + 1u == (uint32_t)kMtN) ? 0u : idx + 1u];
+                Cv[q] = st[(idx < D) ? idx + kMtM : idx - D];
+            }
+#pragma unroll
+            for (int q = 0; q < kFusedGroup; q++) {
+                if (q < cnt) {
+                    const uint32_t l = ql[q];
+                    const uint32_t gi = (uint32_t)p + (uint32_t)P * l;
+                    const uint32_t mq = __builtin_amdgcn_readlane(made, l);
+                    const bool tw = IX[q] != 0xFFFFu;
+                    const uint32_t v = tw ? mt_mix(A[q], Bv[q], Cv[q]) : A[q];
+                    if (tw) {
+                        s.mt[(gb + gi) * kMtN + IX[q]] = v;
+                        if (IX[q] == 0u) s.mt0[gb + gi] = A[q];
+                    }
+                    if (lane < NQ[q]) rings[gi * kFusedRingStride + ((mq + lane) & (RW - 1u))] = (uint8_t)(mt_temper(v) & 0xFFu);
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // bytes land before their head
+#pragma unroll
+            for (int q = 0; q < kFusedGroup; q++) {
+                if (q < cnt) {
+                    const uint32_t l = ql[q];
+                    const uint32_t gi = (uint32_t)p + (uint32_t)P * l;
+                    if (lane == 0u) ((volatile uint32_t*)sh->head)[gi] = __builtin_amdgcn_readlane(made, l) + NQ[q];
+                    made += (lane == l) ? NQ[q] : 0u;
+                }
+            }
+        }
+        if (a.debug && lane == 0u && p == 0 && (blockIdx.x % 64) == 0)
+            printf("fused blk %d: passes %u batches %u idle %u play-sleeps %u\n", (int)blockIdx.x, sh->dbg[0], sh->dbg[1],
+                   sh->dbg[2], sh->dbg[3]);
+        // all play lanes are done (their cons[] written): state code and leftovers
+        if (mine) {
+            const uint32_t consumed = ((volatile uint32_t*)sh->cons)[i];
+            const uint32_t twisted = (made > rem0) ? made - rem0 : 0u;
+            uint32_t Tn = T;
+            if (twisted) {
+                Tn = T0 + twisted;
+                while (Tn > (uint32_t)kMtN) Tn -= kMtN;
+            }
+            const uint32_t rem = max(made, rem0) - consumed;
+            s.mt_pos[g] = Tn | (rem << 16);
+            const uint32_t L = min(made - consumed, (uint32_t)s.ring_w);
+            s.ringn[g] = L;
+            // bytes [consumed, consumed + L) of the ring -> chunks 0.. of s.ring
+            const uint8_t* r = rings + i * kFusedRingStride;
+            for (uint32_t c = 0; c * 16u < L; c++) {
+                uint32_t w[4];
+#pragma unroll
+                for (int d = 0; d < 4; d++) {
+                    uint32_t x = 0u;
+#pragma unroll
+                    for (int b = 0; b < 4; b++)
+                        x |= (uint32_t)r[(consumed + 16u * c + 4u * d + b) & (RW - 1u)] << (8 * b);
+                    w[d] = x;
+                }
+                s.ring[(int64_t)c * s.B + g] = u32x4{w[0], w[1], w[2], w[3]};
+            }
+        }
+    }
+}
+
 // obs in any dtype, one thread per (game, seat)
 template <typename T>
 __global__ void k_obs(DevState s, T* out, int stride, int summ) {
@@ -517,7 +771,7 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
         {(void**)&s.sum_res, sizeof(int32_t) * N * B},     {(void**)&s.episodes, sizeof(int32_t) * B},
         {(void**)&s.mt_pos, sizeof(uint32_t) * B},         {(void**)&s.ctr, sizeof(uint64_t) * B},
         {(void**)&s.mt, rng_mode == SN_RNG_NUMPY_MT ? sizeof(uint32_t) * kMtN * B : 4},
-        {(void**)&s.mt0, sizeof(uint32_t) * B},
+        {(void**)&s.mt0, sizeof(uint32_t) * B},   {(void**)&s.ringn, sizeof(uint32_t) * B},
     };
     for (auto& a : allocs) {
         if (hipMalloc(a.p, a.bytes) != hipSuccess) {
@@ -527,6 +781,7 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
         (void)hipMemset(*a.p, 0, a.bytes);
     }
     e->chunk_steps = 10;
+    e->fused = 0;  // SN_OPT_FUSED: measured slower than k_mt_prep + k_play so far
     if (rng_mode == SN_RNG_NUMPY_MT) {
         const sn_status r = sn_set_option(e, SN_OPT_RING_WORDS, N <= 4 ? 256 : 512);
         if (r != SN_OK) {
@@ -549,7 +804,7 @@ sn_status sn_destroy(sn_env* e) {
     if (!e) return SN_OK;
     (void)hipSetDevice(e->device);
     DevState& s = e->s;
-    void* ps[] = {s.hand, s.row_lo, s.row_hi, s.score, s.sum_res, s.episodes, s.mt_pos, s.ctr, s.mt, s.mt0, s.ring};
+    void* ps[] = {s.hand, s.row_lo, s.row_hi, s.score, s.sum_res, s.episodes, s.mt_pos, s.ctr, s.mt, s.mt0, s.ring, s.ringn};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     delete e;
@@ -577,6 +832,10 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
         case SN_OPT_CHUNK_STEPS:
             if (value < 1) return fail(SN_EINVAL, "chunk steps must be >= 1");
             e->chunk_steps = value;
+            return SN_OK;
+        case SN_OPT_FUSED:
+            if (value != 0 && value != 1) return fail(SN_EINVAL, "fused must be 0 or 1");
+            e->fused = value;
             return SN_OK;
         default: return fail(SN_EINVAL, "unknown option");
     }
@@ -639,16 +898,7 @@ static sn_status launch_play_one(sn_env* e, PlayArgs a, hipStream_t st) {
             case 1: hipLaunchKernelGGL((k_mt_prep<1, GPW>), pg, dim3(kBlock), 0, st, s); break;
             case 2: hipLaunchKernelGGL((k_mt_prep<2, GPW>), pg, dim3(kBlock), 0, st, s); break;
             case 3: hipLaunchKernelGGL((k_mt_prep<3, GPW>), pg, dim3(kBlock), 0, st, s); break;
-            case 4: {
-                static const int dbg = getenv("SECHS_PREP_DBG") ? atoi(getenv("SECHS_PREP_DBG")) : 0;
-                if (dbg == 1) hipLaunchKernelGGL((k_mt_prep<4, GPW, 1>), pg, dim3(kBlock), 0, st, s);
-                else if (dbg == 2) hipLaunchKernelGGL((k_mt_prep<4, GPW, 2>), pg, dim3(kBlock), 0, st, s);
-                else if (dbg == 3) hipLaunchKernelGGL((k_mt_prep<4, GPW, 3>), pg, dim3(kBlock), 0, st, s);
-                else if (dbg == 4) hipLaunchKernelGGL((k_mt_prep<4, 1>), dim3((unsigned)((s.B + 3) / 4)), dim3(kBlock), 0, st, s);
-                else if (dbg == 5) hipLaunchKernelGGL((k_mt_prep<4, 8>), dim3((unsigned)((s.B + 31) / 32)), dim3(kBlock), 0, st, s);
-                else hipLaunchKernelGGL((k_mt_prep<4, GPW>), pg, dim3(kBlock), 0, st, s);
-                break;
-            }
+            case 4: hipLaunchKernelGGL((k_mt_prep<4, GPW>), pg, dim3(kBlock), 0, st, s); break;
             case 5: hipLaunchKernelGGL((k_mt_prep<5, GPW>), pg, dim3(kBlock), 0, st, s); break;
             case 6: hipLaunchKernelGGL((k_mt_prep<6, GPW>), pg, dim3(kBlock), 0, st, s); break;
             case 7: hipLaunchKernelGGL((k_mt_prep<7, GPW>), pg, dim3(kBlock), 0, st, s); break;
@@ -688,8 +938,39 @@ static sn_status launch_play_one(sn_env* e, PlayArgs a, hipStream_t st) {
 // A ring-fed (numpy-MT, in-kernel DrunkHamster) rollout runs in launches of
 // at most chunk_steps env-steps, each behind its own k_mt_prep, so that one
 // ring covers a launch's draws (a 4-player episode: 193.5 +- 9.3 words).
+// the fused producer/consumer launch (k_play_fused), if it applies and fits
+static bool try_launch_fused(sn_env* e, PlayArgs a, hipStream_t st, sn_status* rc) {
+    const DevState& s = e->s;
+    if (!e->fused || s.rng_mode != SN_RNG_NUMPY_MT || a.actions || s.ring_w < kFusedRing) return false;
+    int wave = 64 * kDeckStride;
+    if (a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15) == 0) wave = max(wave, 64 * s.N * 48);
+    if (a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15)) return false;
+    const size_t shmem = (size_t)4 * wave + (size_t)256 * kFusedRingStride + sizeof(FusedShared);
+    if (shmem > (size_t)kLdsBytes) return false;
+    a.wave_lds = wave;
+    a.ring_lds = 0;
+    a.vec_out = ((((uintptr_t)a.rewards) & 15) == 0) && ((((uintptr_t)a.actions_out) & 3) == 0);
+    static const int dbg = getenv("SECHS_FUSED_DEBUG") ? 1 : 0;
+    a.debug = dbg;
+    const dim3 grid((unsigned)((s.B + 255) / 256));
+    *rc = SN_OK;
+    SN_DISPATCH_N(s.N, {
+        if (hipFuncSetAttribute((const void*)k_play_fused<NN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem) !=
+            hipSuccess) {
+            *rc = fail(SN_EHIP, "k_play_fused: LDS attribute");
+            return true;
+        }
+        hipLaunchKernelGGL((k_play_fused<NN>), grid, dim3(kFusedThreads), shmem, st, s, a);
+    });
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) *rc = fail(SN_EHIP, std::string("k_play_fused: ") + hipGetErrorString(err));
+    return true;
+}
+
 static sn_status launch_play(sn_env* e, PlayArgs a, hipStream_t st) {
     const DevState& s = e->s;
+    sn_status frc;
+    if (try_launch_fused(e, a, st, &frc)) return frc;
     const bool ring = (s.rng_mode == SN_RNG_NUMPY_MT) && !a.actions && s.ring_w > 0;
     if (!ring || a.steps <= e->chunk_steps) return launch_play_one(e, a, st);
     const int64_t B = s.B, N = s.N;
@@ -858,6 +1139,7 @@ sn_status sn_mt_set(sn_env* e, int64_t game, const uint32_t* key, int32_t pos) {
     const uint32_t code = mt_code_from_numpy(pos);
     HIP_TRY(hipMemcpy(e->s.mt + game * kMtN, key, sizeof(uint32_t) * kMtN, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(e->s.mt_pos + game, &code, sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemset(e->s.ringn + game, 0, sizeof(uint32_t)));  // buffered words belong to the old stream
     return SN_OK;
 }
 

@@ -42,6 +42,7 @@ struct DevState {
     u32x4* ring;     // [ring_w/16][B] low bytes of the words k_mt_prep twisted ahead
     int ring_w;      // ring words per game (multiple of 64), 0 = no ring
     int pad2_;
+    uint32_t* ringn; // [B] ring bytes valid for the next launch (the stream's next words); 0 = none
 };
 
 constexpr int kBlock = 256;
@@ -59,6 +60,7 @@ struct RngOf<RNG_NUMPY_MT, PF> {
     }
     static __device__ __forceinline__ void store(const DevState& s, int64_t g, T& r, const ByteBuf& buf) {
         s.mt_pos[g] = r.save(buf);
+        s.ringn[g] = 0u;  // words consumed outside the ring: its bytes are stale
     }
 };
 template <int PF>
@@ -165,6 +167,7 @@ struct RngOf<RNG_NUMPY_RING, PF> {
     }
     static __device__ __forceinline__ void store(const DevState& s, int64_t g, T& r, const ByteBuf& buf) {
         s.mt_pos[g] = r.save(buf);
+        s.ringn[g] = 0u;
     }
 };
 template <int PF>
@@ -175,6 +178,7 @@ struct RngOf<RNG_NUMPY_RING_HBM, PF> {
     }
     static __device__ __forceinline__ void store(const DevState& s, int64_t g, T& r, const ByteBuf& buf) {
         s.mt_pos[g] = r.save(buf);
+        s.ringn[g] = 0u;
     }
 };
 
@@ -440,5 +444,6 @@ inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBloc
 struct sn_env {
     int device;
     int chunk_steps;  // SN_OPT_CHUNK_STEPS
+    int fused;        // SN_OPT_FUSED
     sechs::DevState s;
 };

@@ -175,8 +175,10 @@ class VecSechsNimmtEnv:
         nat.check(nat.lib().sn_clear_results(self._h, self._stream()), "sn_clear_results")
 
     # ------------------------------------------------------------ numpy RNG bridge
-    def set_option(self, ring_words=None, chunk_steps=None):
+    def set_option(self, ring_words=None, chunk_steps=None, fused=None):
         """numpy-compat rollout tuning (include/sechs.h SN_OPT_*); results never depend on it"""
+        if fused is not None:
+            nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_FUSED, int(bool(fused))), "sn_set_option")
         if ring_words is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_RING_WORDS, int(ring_words)), "sn_set_option")
         if chunk_steps is not None:

@@ -310,15 +310,17 @@ def test_mt_state_across_round_boundaries_every_step():
             assert p == rp and np.array_equal(k, rk), (t, g)
 
 
-@pytest.mark.parametrize("ring_words,chunk_steps", [(0, 10), (64, 10), (64, 1), (128, 3), (512, 25), (256, 7)])
-def test_ring_options_do_not_change_results(ring_words, chunk_steps):
-    """k_mt_prep's twist-ahead ring is an optimisation only: every ring size
-    (0 = lazy per-lane MT19937; 64 runs the ring dry inside every episode, so
-    the MtGen fallback continues mid-launch) and launch chunking give the
-    oracle's actions, rewards, obs and final numpy MT states."""
+@pytest.mark.parametrize("ring_words,chunk_steps,fused", [(0, 10, 1), (64, 10, 1), (64, 1, 1), (128, 3, 1),
+                                                           (512, 25, 1), (256, 7, 1), (256, 10, 0), (512, 4, 0), (256, 10, 1)])
+def test_ring_options_do_not_change_results(ring_words, chunk_steps, fused):
+    """The twist-ahead paths are optimisations only: every ring size (0 =
+    lazy per-lane MT19937; 64 runs k_mt_prep's ring dry inside every
+    episode, so the MtGen fallback continues mid-launch), launch chunking,
+    and the fused producer/consumer kernel (ring >= 256) give the oracle's
+    actions, rewards, obs and final numpy MT states."""
     B, N, T, seed = 300, 4, 37, 21
     env = venv(B, N, seed=seed, rng="numpy")
-    env.set_option(ring_words=ring_words, chunk_steps=chunk_steps)
+    env.set_option(ring_words=ring_words, chunk_steps=chunk_steps, fused=fused)
     env.reset()
     ref = O.VecOracle(B, N, rng_mode=O.RNG_NUMPY_MT, seed=seed)
     ref.reset()
@@ -346,3 +348,53 @@ def test_ring_option_validation():
     penv = venv(4, 4, rng="philox")
     with pytest.raises(ValueError):
         penv.set_option(ring_words=256)
+
+
+def test_fused_then_other_paths_interleave():
+    """Leftover ring words carried between fused launches are dropped when
+    anything else consumes the stream (per-step API, reset, prep path, numpy
+    state import): every mix stays bit-exact with the oracle."""
+    B, N, seed = 130, 4, 5
+    env = venv(B, N, seed=seed, rng="numpy")
+    env.reset()
+    ref = O.VecOracle(B, N, rng_mode=O.RNG_NUMPY_MT, seed=seed)
+    ref.reset()
+    rngs = ref.v.contents.rngs
+    plan = [("roll", 13), ("step", 1), ("roll", 4), ("reset", 0), ("roll", 9), ("prep", 6), ("roll", 21),
+            ("import", 0), ("roll", 12), ("roll", 1), ("roll", 30)]
+    for what, T in plan:
+        if what == "roll":
+            env.set_option(fused=1)
+            out = env.rollout(T, want_actions=True)
+            rr, rd, ra, _ = ref.rollout(T)
+            torch.cuda.synchronize()
+            assert np.array_equal(out["actions"].cpu().numpy(), ra), what
+            assert np.array_equal(out["rewards"].cpu().numpy(), rr), what
+        elif what == "prep":
+            env.set_option(fused=0)
+            out = env.rollout(T, want_actions=True)
+            rr, rd, ra, _ = ref.rollout(T)
+            torch.cuda.synchronize()
+            assert np.array_equal(out["actions"].cpu().numpy(), ra), what
+        elif what == "step":  # external actions (lazy MtGen path; deals of finished games draw words)
+            for _ in range(12):
+                acts = env.hands().cpu().numpy()[:, :, 0].astype(np.int32)
+                rew, done, inv = env.step(torch.from_numpy(acts), auto_reset=True)
+                r_rew, r_done, r_inv = ref.step(acts, auto_reset=True)
+                assert np.array_equal(rew.cpu().numpy(), r_rew)
+        elif what == "reset":
+            env.reset()
+            ref.reset()
+        elif what == "import":
+            rs = np.random.RandomState(77)
+            rs.randint(0, 2**32, size=300, dtype=np.uint64)
+            key, pos = rs.get_state()[1:3]
+            for g in (0, 5, 129):
+                env.set_mt_state(key, pos, game=g)
+                for i in range(624):
+                    rngs[g].mt[i] = int(key[i])
+                rngs[g].pos = int(pos)
+    for g in range(0, B, 3):
+        k, p = _np_form(*env.get_mt_state(g))
+        rk, rp = _np_form(np.frombuffer(bytes(rngs[g].mt), dtype=np.uint32), rngs[g].pos)
+        assert p == rp and np.array_equal(k, rk), g
