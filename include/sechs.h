@@ -134,12 +134,15 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          0 = no ring, k_play twists lazily per lane).
                          Default 256 for N <= 4, else 512.
      SN_OPT_CHUNK_STEPS  env-steps per k_mt_prep-fed launch (>= 1, default 10).
-     SN_OPT_FUSED        0 (default): k_mt_prep + k_play.  1: when the ring
-                         has >= 256 words and the LDS fits (N <= 4 with int8
-                         obs), one k_play_fused launch with MT19937 producer
-                         waves beside the play waves (slower today). */
-enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_FUSED = 3 };
+     SN_OPT_PIPELINE     1 (default): DrunkHamster rollouts in numpy mode keep
+                         each stream twisted ~600 words ahead with k_mt_ahead
+                         on a side stream, concurrently with the previous
+                         launch's k_play (N <= 6); 0: the paths above. */
+enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3 };
 sn_status sn_set_option(sn_env* env, int option, int value);
+/* pipelined rollouts whose draws ran past the twisted words (must be 0; a
+   nonzero count means those games' draws are wrong) [sync] */
+sn_status sn_pipe_errors(sn_env* env, uint32_t* count);
 
 /* ---- Monte-Carlo search, MCSAgent (agents/mcts.py:17-188) ------------- */
 

@@ -32,7 +32,6 @@ __global__ void k_seed(DevState s) {
             st[i] = v;
         }
         s.mt_pos[g] = 0u;
-        s.ringn[g] = 0u;
     } else {
         s.ctr[g] = 0u;
     }
@@ -210,8 +209,127 @@ __global__ __launch_bounds__(kBlock) void k_mt_prep(DevState s) {
             const uint32_t Tn = T0[q] + (kt - r);
             s.mt_pos[g] = ((Tn > (uint32_t)kMtN) ? Tn - kMtN : Tn) | (kt << 16);
         }
-        if (lane == 0u) s.ringn[g] = W;
     }
+}
+
+// ============================================================================
+// Pipelined numpy-MT twist-ahead (SN_OPT_PIPELINE, the default for numpy-mode
+// DrunkHamster rollouts).  k_mt_ahead keeps each game's stream twisted
+// kPipeLead words past the consumer position of the play launch before last,
+// writing the tempered low bytes into a per-game circular ring indexed by
+// absolute stream position (pring).  It reads only state no running kernel
+// writes (pabsc of the launch before last, its own ptend / ptp), and the
+// ring slots it fills are never the ones the running k_play reads (lead +
+// one launch < kPipeRing), so it runs on a side stream CONCURRENTLY with
+// k_play (launch i+1's twist beside launch i's game loop: memory-bound work
+// beside latency-bound work, on the same CUs).  One wave per game; 64
+// consecutive words per instruction; the first 224 words have all inputs in
+// memory (loads first), later ones follow in order (word j reads j - 227).
+// INIT: start from the MtGen state code (re-temper its twisted-unconsumed
+// words into the ring first).
+// ============================================================================
+struct AheadArgs {
+    int cin;   // pabsc parity holding the consumer position to lead (INIT: written)
+    int tin;   // ptend parity of the previous prep (steady)
+    int tout;  // ptend parity written
+};
+
+template <bool INIT>
+__global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
+    constexpr uint32_t D = kMtN - kMtM;  // 227
+    constexpr uint32_t P1 = 224;          // words twisted before any store (all inputs already in memory)
+    const int64_t g = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (g >= s.B) return;  // whole waves
+    const uint32_t lane = threadIdx.x & 63u;
+    const int64_t B = s.B;
+    uint32_t* st = s.mt + g * kMtN;
+    uint8_t* ring = (uint8_t*)s.pring;
+    uint32_t Tp, t0, c;
+    if (INIT) {
+        const uint32_t code = s.mt_pos[g];
+        Tp = code & 0x7FFu;
+        const uint32_t rem = (code >> 16) & kMtCntMask;
+        t0 = 0u;
+        c = 0u - rem;
+        for (uint32_t k0 = 0; k0 < rem; k0 += 64u) {  // twisted, unconsumed: stream index Tp - rem + k (mod 624)
+            const uint32_t k = k0 + lane;
+            if (k < rem) {
+                const uint32_t v = st[(Tp + kMtN - rem + k) % (uint32_t)kMtN];
+                const uint32_t ri = (c + k) & (uint32_t)(kPipeRing - 1);
+                ring[((int64_t)(ri >> 4) * B + g) * 16 + (ri & 15u)] = (uint8_t)(mt_temper(v) & 0xFFu);
+            }
+        }
+        if (lane == 0u) s.pabsc[(int64_t)a.cin * B + g] = c;
+    } else {
+        Tp = s.ptp[g];
+        t0 = s.ptend[(int64_t)a.tin * B + g];
+        c = s.pabsc[(int64_t)a.cin * B + g];
+    }
+    const uint32_t lead = t0 - c;
+    const uint32_t n = (lead < (uint32_t)kPipeLead) ? (((uint32_t)kPipeLead - lead) & ~7u) : 0u;
+    const uint32_t T0 = (Tp == (uint32_t)kMtN) ? 0u : Tp;
+    auto ring_dword = [&](uint32_t j, uint32_t v) {  // t0 is 8-aligned: lanes 4m..4m+3 share one dword
+        const uint32_t y = mt_temper(v) & 0xFFu;
+        const uint32_t d = y | (__shfl_down(y, 1) << 8) | (__shfl_down(y, 2) << 16) | (__shfl_down(y, 3) << 24);
+        const uint32_t ri = (t0 + j) & (uint32_t)(kPipeRing - 1);
+        if ((lane & 3u) == 0u && j < n) *(uint32_t*)(ring + ((int64_t)(ri >> 4) * B + g) * 16 + (ri & 12u)) = d;
+    };
+    // phase 1: words 0 .. min(n, 224)
+    uint32_t A[4], Bv[4], Cv[4], IX[4];
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        const uint32_t j = 64u * b + lane;
+        IX[b] = 0xFFFFu;
+        if (j < n && j < P1) {
+            const uint32_t idx = (T0 + j) % (uint32_t)kMtN;
+            IX[b] = idx;
+            A[b] = st[idx];
+            Bv[b] = st[(idx + 1u == (uint32_t)kMtN) ? 0u : idx + 1u];
+            Cv[b] = st[(idx < D) ? idx + kMtM : idx - D];
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        if (64u * b >= min(n, P1)) break;
+        const uint32_t j = 64u * b + lane;
+        uint32_t v = 0u;
+        if (IX[b] != 0xFFFFu) {
+            v = mt_mix(A[b], Bv[b], Cv[b]);
+            st[IX[b]] = v;
+            if (IX[b] == 0u) s.mt0[g] = A[b];
+        }
+        ring_dword(j, v);
+    }
+    // phase 2: words 224 .. n, in order (their inputs include words just twisted)
+    for (uint32_t j0 = P1; j0 < n; j0 += 64u) {
+        const uint32_t j = j0 + lane;
+        uint32_t v = 0u;
+        if (j < n) {
+            const uint32_t idx = (T0 + j) % (uint32_t)kMtN;
+            const uint32_t aa = st[idx];
+            v = mt_mix(aa, st[(idx + 1u == (uint32_t)kMtN) ? 0u : idx + 1u], st[(idx < D) ? idx + kMtM : idx - D]);
+            st[idx] = v;
+            if (idx == 0u) s.mt0[g] = aa;
+        }
+        ring_dword(j, v);
+    }
+    if (lane == 0u) {
+        uint32_t Tn = Tp;
+        if (n) {
+            Tn = T0 + n;
+            while (Tn > (uint32_t)kMtN) Tn -= kMtN;
+        }
+        s.ptp[g] = Tn;
+        s.ptend[(int64_t)a.tout * B + g] = t0 + n;
+    }
+}
+
+// state code of a pipelined handle (for MtGen users and sn_mt_get):
+// twist pointer | (twisted end - consumer) << 16
+__global__ void k_pipe_code(DevState s, int cin, int tin) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= s.B) return;
+    s.mt_pos[g] = s.ptp[g] | ((s.ptend[(int64_t)tin * s.B + g] - s.pabsc[(int64_t)cin * s.B + g]) << 16);
 }
 
 // MT19937 chunks (8 words) twisted per refill in k_play: 2 doubles the
@@ -220,7 +338,8 @@ constexpr int kPlayPrefetch = 2;
 
 struct PlayArgs {
     int steps, flags, obs_stride, wave_lds;  // wave_lds: bytes of LDS per wave (dynamic)
-    int ring_lds;            // bytes of that per lane for the LDS ring copy (RNG_NUMPY_RING), at the region's end
+    int ring_lds;            // bytes of that per lane for the LDS ring copy (RNG_NUMPY_RING/PIPE), at the region's end
+    int pipe_cin, pipe_cout, pipe_t;  // RNG_NUMPY_PIPE: pabsc parity read / written, ptend parity read
     int vec_out;             // rewards 16-B and actions 4-B aligned: one store per lane each (N == 4)
     const int32_t* actions;  // [B][N] (steps == 1) or NULL = DrunkHamster
     int32_t* rewards;        // [steps][B][N]
@@ -228,7 +347,6 @@ struct PlayArgs {
     uint8_t* actions_out;    // [steps][B][N]
     int8_t* obs;             // [steps][B][N][obs_stride]
     int32_t* invalid;        // [B]
-    int debug;               // k_play_fused: print handshake counters (SECHS_FUSED_DEBUG)
 };
 
 // The env-step loop of one lane (game g).  R supplies the random words
@@ -391,272 +509,27 @@ __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
     uint8_t* wave_lds = lds_dyn + (threadIdx.x >> 6) * a.wave_lds;
     Game<N> G;
     load_game<N>(s, g, G);
-    typename RngOf<MODE, kPlayPrefetch>::T rng;
-    ByteBuf buf;
-    if constexpr (MODE == RNG_NUMPY_RING || MODE == RNG_NUMPY_RING_HBM) {
-        uint8_t* slot = wave_lds + a.wave_lds - 64 * a.ring_lds + lane * a.ring_lds;
-        RngOf<MODE, kPlayPrefetch>::load(s, g, rng, buf, slot);
-    } else {
-        RngOf<MODE, kPlayPrefetch>::load(s, g, rng, buf);
-    }
     int32_t sum_res[N], episodes;
     load_results<N>(s, g, a.flags, sum_res, episodes);
-    play_steps<N>(s, a, g, lane, wave_lds, G, rng, buf, sum_res, episodes);
-    store_game<N>(s, g, G);
-    RngOf<MODE, kPlayPrefetch>::store(s, g, rng, buf);
-    store_results<N>(s, g, a.flags, sum_res, episodes);
-}
-
-// ============================================================================
-// k_play_fused: the numpy-MT DrunkHamster rollout with the MT19937 twist
-// running beside the game, in the same workgroup.
-//
-// A workgroup = 4 play waves (256 games, one per lane, exactly k_play's
-// step loop) + kFusedProducers producer waves.  The producers twist each
-// game's stream ahead in place, 64 consecutive words per instruction (the
-// coalesced form of k_mt_prep), and stream the tempered low bytes into the
-// game's LDS ring (kFusedRing bytes, circular); a play lane takes 8 bytes at
-// a time from its ring.  The play waves are latency/VALU-bound at one wave
-// per SIMD, the producers are memory-bound: sharing the SIMDs, each hides
-// the other's stalls.  Handshake, all in LDS, per game: head = bytes
-// published by the producer (multiples of 8, published after its byte
-// writes completed: s_waitcnt lgkmcnt(0)), tail = bytes taken by the play
-// lane (published after its read issued; LDS executes a wave's operations
-// in order, so the producer never overwrites bytes not yet read).  A play
-// lane whose ring is empty sleeps until head moves (bounded: a lost producer
-// cannot hang the GPU, it only corrupts that game's draws).  The words
-// still in a ring at the end (up to kFusedRing) go back to HBM (s.ring,
-// ringn) and are the first words of the next launch, so play starts at once.
-// Stream accounting is MtGen's: code = twist pointer | twisted-unconsumed
-// words << 16, the old mt[0] saved whenever a round is crossed (mt0).
-// ============================================================================
-constexpr int kFusedProducers = 4;
-constexpr int kFusedRing = 256;               // ring bytes (= words) per game
-constexpr int kFusedRingStride = kFusedRing + 8;
-constexpr int kFusedGroup = 16;               // games a producer wave twists per pass (loads in flight)
-constexpr int kFusedThreads = (4 + kFusedProducers) * 64;
-
-struct FusedShared {   // at the end of the dynamic LDS
-    uint32_t head[256], tail[256], cons[256];
-    uint32_t done;
-    uint32_t dbg[8];   // SECHS_FUSED_DEBUG: passes, batches, idle polls, play sleeps, ...
-};
-
-struct FusedRing {
-    const uint8_t* ring;
-    volatile uint32_t* headp;
-    volatile uint32_t* tailp;
-    uint32_t tail, head_seen, sleeps;
-
-    __device__ __forceinline__ void gen(ByteBuf& buf) {
-        if (head_seen - tail < 8u) {
-            for (uint32_t spin = 0;; spin++) {
-                head_seen = *headp;
-                if (head_seen - tail >= 8u || spin > (1u << 20)) break;
-                __builtin_amdgcn_s_sleep(1);
-                sleeps++;
-            }
-        }
-        asm volatile("" ::: "memory");  // the ring read stays behind the head read (LDS runs them in order)
-        const uint64_t v = *(const uint64_t*)(ring + (tail & (uint32_t)(kFusedRing - 1)));
-        tail += 8u;
-        *tailp = tail;
-        buf.append(v, 8u);
-    }
-    __device__ __forceinline__ void topup(ByteBuf& buf) {
-        if (buf.cnt <= 24u) gen(buf);
-    }
-    __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf); }
-};
-
-template <int N>
-__global__ __launch_bounds__(kFusedThreads) void k_play_fused(DevState s, PlayArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
-    const int wave = threadIdx.x >> 6;
-    const uint32_t lane = threadIdx.x & 63u;
-    const int64_t gb = (int64_t)blockIdx.x * 256;  // first game of the block
-    uint8_t* rings = lds_dyn + 4 * a.wave_lds;
-    FusedShared* sh = (FusedShared*)(rings + 256 * kFusedRingStride);
-    constexpr uint32_t RW = kFusedRing;
-    constexpr uint32_t D = kMtN - kMtM;  // 227
-
-    // ---- launch start: play lanes copy the leftover words of the last launch
-    if (wave < 4) {
-        const uint32_t i = wave * 64 + lane;  // game in block
-        const int64_t g = gb + i;
-        uint32_t L = 0u;
-        if (g < s.B) {
-            L = min(s.ringn[g], RW);
-            uint8_t* r = rings + i * kFusedRingStride;
-            for (uint32_t c = 0; c * 16u < L; c++) {
-                const u32x4 v = s.ring[(int64_t)c * s.B + g];
-                *(uint64_t*)(r + 16u * c) = (uint64_t)v.x | ((uint64_t)v.y << 32);
-                *(uint64_t*)(r + 16u * c + 8u) = (uint64_t)v.z | ((uint64_t)v.w << 32);
-            }
-        }
-        sh->head[i] = L & ~7u;
-        sh->tail[i] = 0u;
-        sh->cons[i] = 0u;
-        if (threadIdx.x == 0) sh->done = 0u;
-        if (threadIdx.x < 8) sh->dbg[threadIdx.x] = 0u;
-    }
-    __syncthreads();
-
-    if (wave < 4) {
-        // ---- play waves: k_play's step loop, words from the ring
-        const uint32_t i = wave * 64 + lane;
-        const int64_t g = gb + i;
-        if (g < s.B) {
-            uint8_t* wave_lds = lds_dyn + wave * a.wave_lds;
-            Game<N> G;
-            load_game<N>(s, g, G);
-            FusedRing rng;
-            rng.ring = rings + i * kFusedRingStride;
-            rng.headp = &sh->head[i];
-            rng.tailp = &sh->tail[i];
-            rng.tail = 0u;
-            rng.head_seen = 0u;
-            rng.sleeps = 0u;
-            ByteBuf buf;
-            buf.clear();
-            int32_t sum_res[N], episodes;
-            load_results<N>(s, g, a.flags, sum_res, episodes);
-            play_steps<N>(s, a, g, (int)lane, wave_lds, G, rng, buf, sum_res, episodes);
-            store_game<N>(s, g, G);
-            store_results<N>(s, g, a.flags, sum_res, episodes);
-            sh->cons[i] = rng.tail - buf.cnt;
-            if (a.debug) atomicAdd(&sh->dbg[3], rng.sleeps);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0u) atomicAdd(&sh->done, 1u);
+    ByteBuf buf;
+    if constexpr (MODE == RNG_NUMPY_PIPE) {
+        RingPipe rng;
+        rng.load(s, g, buf, wave_lds + a.wave_lds - 64 * a.ring_lds + lane * a.ring_lds, a.pipe_cin, a.pipe_t);
+        play_steps<N>(s, a, g, lane, wave_lds, G, rng, buf, sum_res, episodes);
+        s.pabsc[(int64_t)a.pipe_cout * s.B + g] = rng.consumed(buf);
     } else {
-        // ---- producer waves: lane l owns game p + P*l of the block
-        constexpr int P = kFusedProducers;
-        constexpr int GPL = 256 / P;  // games per producer wave (<= 64)
-        const int p = wave - 4;
-        const uint32_t i = (uint32_t)p + (uint32_t)P * lane;  // my game (lanes < GPL)
-        const int64_t g = gb + i;
-        const bool mine = lane < (uint32_t)GPL && g < s.B;
-        uint32_t T = 0u, rem0 = 0u, made = 0u;
-        if (mine) {
-            const uint32_t code = s.mt_pos[g];
-            T = code & 0x7FFu;
-            rem0 = (code >> 16) & kMtCntMask;
-            made = min(s.ringn[g], RW);
+        typename RngOf<MODE, kPlayPrefetch>::T rng;
+        if constexpr (MODE == RNG_NUMPY_RING || MODE == RNG_NUMPY_RING_HBM) {
+            uint8_t* slot = wave_lds + a.wave_lds - 64 * a.ring_lds + lane * a.ring_lds;
+            RngOf<MODE, kPlayPrefetch>::load(s, g, rng, buf, slot);
+        } else {
+            RngOf<MODE, kPlayPrefetch>::load(s, g, rng, buf);
         }
-        const uint32_t T0 = (T == (uint32_t)kMtN) ? 0u : T;
-        uint32_t rot = 0u;
-        volatile uint32_t* vdone = &sh->done;
-        volatile uint32_t* vtail = sh->tail;
-        while (true) {
-            const bool fin = *vdone >= 4u;
-            const uint32_t tl = mine ? vtail[i] : 0u;
-            // room for a batch, keeping the <= 32 bytes the lane has taken but
-            // not consumed (its ByteBuf) intact: they are saved at the end
-            const bool want = mine && !fin && (made - tl) <= RW - 64u - 32u;
-            uint64_t mask = __ballot(want);
-            if (!mask) {
-                if (fin) break;
-                if (a.debug && lane == 0u) atomicAdd(&sh->dbg[2], 1u);
-                __builtin_amdgcn_s_sleep(2);
-                continue;
-            }
-            mask = (mask >> rot) | (rot ? (mask << (64u - rot)) : 0ull);  // fairness: rotate the start
-            int cnt = 0;
-            uint32_t ql[kFusedGroup];
-#pragma unroll
-            for (int q = 0; q < kFusedGroup; q++) {
-                ql[q] = ql[0];  // past cnt: a duplicate of the first (loads only, results unused)
-                if (mask) {
-                    ql[q] = ((uint32_t)__builtin_ctzll(mask) + rot) & 63u;
-                    mask &= mask - 1ull;
-                    cnt = q + 1;
-                }
-            }
-            rot = (rot + 17u) & 63u;
-            if (a.debug && lane == 0u) {
-                atomicAdd(&sh->dbg[0], 1u);
-                atomicAdd(&sh->dbg[1], (uint32_t)cnt);
-            }
-            // batch of game q: words [made, made + n); n < 64 only for the batch
-            // that starts twisting, so that the twist pointer stays 8-aligned.
-            // Branch-free: every lane loads three valid words for every game,
-            // so all 3 * kFusedGroup loads are in flight before the first use.
-            uint32_t A[kFusedGroup], Bv[kFusedGroup], Cv[kFusedGroup], IX[kFusedGroup], NQ[kFusedGroup];
-#pragma unroll
-            for (int q = 0; q < kFusedGroup; q++) {
-                const uint32_t l = ql[q];
-                const uint32_t gi = (uint32_t)p + (uint32_t)P * l;
-                const uint32_t* st = s.mt + (gb + gi) * kMtN;
-                const uint32_t mq = __builtin_amdgcn_readlane(made, l), rq = __builtin_amdgcn_readlane(rem0, l);
-                const uint32_t Tq = __builtin_amdgcn_readlane(T, l), T0q = __builtin_amdgcn_readlane(T0, l);
-                const uint32_t k = mq + lane;
-                NQ[q] = (mq + 64u <= rq) ? 64u : 64u - ((mq + 64u - rq) & 7u);
-                const bool re = k < rq;  // twisted by an earlier launch: stream index T - rem0 + k (mod 624)
-                const uint32_t idx = re ? (Tq + kMtN - rq + k) % (uint32_t)kMtN : (T0q + (k - rq)) % (uint32_t)kMtN;
-                IX[q] = (re || lane >= NQ[q]) ? 0xFFFFu : idx;
-                A[q] = st[idx];
-                Bv[q] = st[(idx + 1u == (uint32_t)kMtN) ? 0u : idx + 1u];
-                Cv[q] = st[(idx < D) ? idx + kMtM : idx - D];
-            }
-#pragma unroll
-            for (int q = 0; q < kFusedGroup; q++) {
-                if (q < cnt) {
-                    const uint32_t l = ql[q];
-                    const uint32_t gi = (uint32_t)p + (uint32_t)P * l;
-                    const uint32_t mq = __builtin_amdgcn_readlane(made, l);
-                    const bool tw = IX[q] != 0xFFFFu;
-                    const uint32_t v = tw ? mt_mix(A[q], Bv[q], Cv[q]) : A[q];
-                    if (tw) {
-                        s.mt[(gb + gi) * kMtN + IX[q]] = v;
-                        if (IX[q] == 0u) s.mt0[gb + gi] = A[q];
-                    }
-                    if (lane < NQ[q]) rings[gi * kFusedRingStride + ((mq + lane) & (RW - 1u))] = (uint8_t)(mt_temper(v) & 0xFFu);
-                }
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // bytes land before their head
-#pragma unroll
-            for (int q = 0; q < kFusedGroup; q++) {
-                if (q < cnt) {
-                    const uint32_t l = ql[q];
-                    const uint32_t gi = (uint32_t)p + (uint32_t)P * l;
-                    if (lane == 0u) ((volatile uint32_t*)sh->head)[gi] = __builtin_amdgcn_readlane(made, l) + NQ[q];
-                    made += (lane == l) ? NQ[q] : 0u;
-                }
-            }
-        }
-        if (a.debug && lane == 0u && p == 0 && (blockIdx.x % 64) == 0)
-            printf("fused blk %d: passes %u batches %u idle %u play-sleeps %u\n", (int)blockIdx.x, sh->dbg[0], sh->dbg[1],
-                   sh->dbg[2], sh->dbg[3]);
-        // all play lanes are done (their cons[] written): state code and leftovers
-        if (mine) {
-            const uint32_t consumed = ((volatile uint32_t*)sh->cons)[i];
-            const uint32_t twisted = (made > rem0) ? made - rem0 : 0u;
-            uint32_t Tn = T;
-            if (twisted) {
-                Tn = T0 + twisted;
-                while (Tn > (uint32_t)kMtN) Tn -= kMtN;
-            }
-            const uint32_t rem = max(made, rem0) - consumed;
-            s.mt_pos[g] = Tn | (rem << 16);
-            const uint32_t L = min(made - consumed, (uint32_t)s.ring_w);
-            s.ringn[g] = L;
-            // bytes [consumed, consumed + L) of the ring -> chunks 0.. of s.ring
-            const uint8_t* r = rings + i * kFusedRingStride;
-            for (uint32_t c = 0; c * 16u < L; c++) {
-                uint32_t w[4];
-#pragma unroll
-                for (int d = 0; d < 4; d++) {
-                    uint32_t x = 0u;
-#pragma unroll
-                    for (int b = 0; b < 4; b++)
-                        x |= (uint32_t)r[(consumed + 16u * c + 4u * d + b) & (RW - 1u)] << (8 * b);
-                    w[d] = x;
-                }
-                s.ring[(int64_t)c * s.B + g] = u32x4{w[0], w[1], w[2], w[3]};
-            }
-        }
+        play_steps<N>(s, a, g, lane, wave_lds, G, rng, buf, sum_res, episodes);
+        RngOf<MODE, kPlayPrefetch>::store(s, g, rng, buf);
     }
+    store_game<N>(s, g, G);
+    store_results<N>(s, g, a.flags, sum_res, episodes);
 }
 
 // obs in any dtype, one thread per (game, seat)
@@ -771,7 +644,7 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
         {(void**)&s.sum_res, sizeof(int32_t) * N * B},     {(void**)&s.episodes, sizeof(int32_t) * B},
         {(void**)&s.mt_pos, sizeof(uint32_t) * B},         {(void**)&s.ctr, sizeof(uint64_t) * B},
         {(void**)&s.mt, rng_mode == SN_RNG_NUMPY_MT ? sizeof(uint32_t) * kMtN * B : 4},
-        {(void**)&s.mt0, sizeof(uint32_t) * B},   {(void**)&s.ringn, sizeof(uint32_t) * B},
+        {(void**)&s.mt0, sizeof(uint32_t) * B},
     };
     for (auto& a : allocs) {
         if (hipMalloc(a.p, a.bytes) != hipSuccess) {
@@ -781,7 +654,30 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
         (void)hipMemset(*a.p, 0, a.bytes);
     }
     e->chunk_steps = 10;
-    e->fused = 0;  // SN_OPT_FUSED: measured slower than k_mt_prep + k_play so far
+    e->pipe = 1;
+    e->pvalid = 0;
+    e->pcount = 0;
+    if (rng_mode == SN_RNG_NUMPY_MT) {
+        struct {
+            void** p;
+            size_t bytes;
+        } pal[] = {{(void**)&s.pring, (size_t)kPipeRing * B}, {(void**)&s.pabsc, sizeof(uint32_t) * 2 * B},
+                   {(void**)&s.ptend, sizeof(uint32_t) * 2 * B}, {(void**)&s.ptp, sizeof(uint32_t) * B},
+                   {(void**)&s.perr, sizeof(uint32_t)}};
+        for (auto& a : pal) {
+            if (hipMalloc(a.p, a.bytes) != hipSuccess) {
+                sn_destroy(e);
+                return fail(SN_ENOMEM, "hipMalloc of the MT pipeline failed");
+            }
+            (void)hipMemset(*a.p, 0, a.bytes);
+        }
+        if (hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&e->ev_prep, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e->ev_main, hipEventDisableTiming) != hipSuccess) {
+            sn_destroy(e);
+            return fail(SN_EHIP, "stream/event creation failed");
+        }
+    }
     if (rng_mode == SN_RNG_NUMPY_MT) {
         const sn_status r = sn_set_option(e, SN_OPT_RING_WORDS, N <= 4 ? 256 : 512);
         if (r != SN_OK) {
@@ -804,7 +700,12 @@ sn_status sn_destroy(sn_env* e) {
     if (!e) return SN_OK;
     (void)hipSetDevice(e->device);
     DevState& s = e->s;
-    void* ps[] = {s.hand, s.row_lo, s.row_hi, s.score, s.sum_res, s.episodes, s.mt_pos, s.ctr, s.mt, s.mt0, s.ring, s.ringn};
+    (void)hipDeviceSynchronize();  // no k_mt_ahead may still be in flight
+    if (e->ev_prep) (void)hipEventDestroy(e->ev_prep);
+    if (e->ev_main) (void)hipEventDestroy(e->ev_main);
+    if (e->side) (void)hipStreamDestroy(e->side);
+    void* ps[] = {s.hand, s.row_lo, s.row_hi, s.score, s.sum_res, s.episodes, s.mt_pos, s.ctr, s.mt, s.mt0, s.ring,
+                  s.pring, s.pabsc, s.ptend, s.ptp, s.perr};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     delete e;
@@ -814,6 +715,7 @@ sn_status sn_destroy(sn_env* e) {
 sn_status sn_set_option(sn_env* e, int option, int value) {
     if (!e) return fail(SN_EINVAL, "env is NULL");
     DevState& s = e->s;
+    if (sn_pipe_sync(e, 0) != SN_OK) return SN_EHIP;
     switch (option) {
         case SN_OPT_RING_WORDS: {
             if (value < 0 || value > 512 || (value % 64)) return fail(SN_EINVAL, "ring words must be a multiple of 64 in 0..512");
@@ -833,9 +735,9 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
             if (value < 1) return fail(SN_EINVAL, "chunk steps must be >= 1");
             e->chunk_steps = value;
             return SN_OK;
-        case SN_OPT_FUSED:
-            if (value != 0 && value != 1) return fail(SN_EINVAL, "fused must be 0 or 1");
-            e->fused = value;
+        case SN_OPT_PIPELINE:
+            if (value != 0 && value != 1) return fail(SN_EINVAL, "pipeline must be 0 or 1");
+            e->pipe = value;
             return SN_OK;
         default: return fail(SN_EINVAL, "unknown option");
     }
@@ -853,6 +755,7 @@ sn_status sn_info(const sn_env* e, int64_t* B, int* N, int* C, int* mode) {
 sn_status sn_reset(sn_env* e, const uint8_t* decks, void* stream) {
     if (!e) return fail(SN_EINVAL, "env is NULL");
     hipStream_t st = (hipStream_t)stream;
+    if (sn_pipe_sync(e, st) != SN_OK) return SN_EHIP;
     const DevState& s = e->s;
     if (s.rng_mode == SN_RNG_NUMPY_MT) {
         SN_DISPATCH_N(s.N, hipLaunchKernelGGL((k_reset<NN, RNG_NUMPY_MT>), dim3(grid_for(s.B)), dim3(kBlock), 0, st, s, decks));
@@ -938,39 +841,82 @@ static sn_status launch_play_one(sn_env* e, PlayArgs a, hipStream_t st) {
 // A ring-fed (numpy-MT, in-kernel DrunkHamster) rollout runs in launches of
 // at most chunk_steps env-steps, each behind its own k_mt_prep, so that one
 // ring covers a launch's draws (a 4-player episode: 193.5 +- 9.3 words).
-// the fused producer/consumer launch (k_play_fused), if it applies and fits
-static bool try_launch_fused(sn_env* e, PlayArgs a, hipStream_t st, sn_status* rc) {
-    const DevState& s = e->s;
-    if (!e->fused || s.rng_mode != SN_RNG_NUMPY_MT || a.actions || s.ring_w < kFusedRing) return false;
+sn_status sn_pipe_sync(sn_env* e, hipStream_t st) {
+    if (!e || !e->pvalid) return SN_OK;
+    HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));
+    const int p = (int)(e->pcount & 1u);
+    hipLaunchKernelGGL(k_pipe_code, dim3(grid_for(e->s.B)), dim3(kBlock), 0, st, e->s, 1 - p, p);
+    HIP_TRY(hipGetLastError());
+    e->pvalid = 0;
+    return SN_OK;
+}
+
+// LDS a pipelined k_play block needs (obs staging / deck + the RingPipe windows)
+static size_t pipe_lds(const DevState& s, const PlayArgs& a, int* wave_out) {
     int wave = 64 * kDeckStride;
     if (a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15) == 0) wave = max(wave, 64 * s.N * 48);
-    if (a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15)) return false;
-    const size_t shmem = (size_t)4 * wave + (size_t)256 * kFusedRingStride + sizeof(FusedShared);
-    if (shmem > (size_t)kLdsBytes) return false;
+    wave += 64 * kPipeSlot;
+    *wave_out = wave;
+    return (size_t)wave * (kBlock / 64);
+}
+
+// The pipelined numpy-MT rollout: per launch of <= 10 env-steps, k_play (on
+// the caller's stream) draws from words k_mt_ahead twisted during the
+// previous launch, while the next k_mt_ahead runs on the side stream.
+static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
+    DevState& s = e->s;
+    int wave;
+    const size_t shmem = pipe_lds(s, a, &wave);
     a.wave_lds = wave;
-    a.ring_lds = 0;
+    a.ring_lds = kPipeSlot;
     a.vec_out = ((((uintptr_t)a.rewards) & 15) == 0) && ((((uintptr_t)a.actions_out) & 3) == 0);
-    static const int dbg = getenv("SECHS_FUSED_DEBUG") ? 1 : 0;
-    a.debug = dbg;
-    const dim3 grid((unsigned)((s.B + 255) / 256));
-    *rc = SN_OK;
-    SN_DISPATCH_N(s.N, {
-        if (hipFuncSetAttribute((const void*)k_play_fused<NN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem) !=
-            hipSuccess) {
-            *rc = fail(SN_EHIP, "k_play_fused: LDS attribute");
-            return true;
-        }
-        hipLaunchKernelGGL((k_play_fused<NN>), grid, dim3(kFusedThreads), shmem, st, s, a);
-    });
-    const hipError_t err = hipGetLastError();
-    if (err != hipSuccess) *rc = fail(SN_EHIP, std::string("k_play_fused: ") + hipGetErrorString(err));
-    return true;
+    const dim3 pg((unsigned)((s.B + kBlock / 64 - 1) / (kBlock / 64)));
+    if (!e->pvalid) {  // start the pipeline from mt_pos: twist kPipeLead ahead, synchronously
+        const int p = (int)(e->pcount & 1u);
+        hipLaunchKernelGGL(k_mt_ahead<true>, pg, dim3(kBlock), 0, st, s, AheadArgs{1 - p, 0, p});
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(e->ev_prep, st));
+        e->pvalid = 1;
+    }
+    const int64_t B = s.B, N = s.N;
+    const int chunk = min(e->chunk_steps, 10);
+    for (int t0 = 0; t0 < a.steps; t0 += chunk) {
+        PlayArgs c = a;
+        c.steps = min(chunk, a.steps - t0);
+        if (a.rewards) c.rewards = a.rewards + (int64_t)t0 * B * N;
+        if (a.done) c.done = a.done + (int64_t)t0 * B;
+        if (a.actions_out) c.actions_out = a.actions_out + (int64_t)t0 * B * N;
+        if (a.obs) c.obs = a.obs + (int64_t)t0 * B * N * a.obs_stride;
+        const int p = (int)(e->pcount & 1u);
+        c.pipe_cin = 1 - p, c.pipe_cout = p, c.pipe_t = p;
+        HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));  // this launch's words are twisted
+        HIP_TRY(hipEventRecord(e->ev_main, st));         // the previous launch's consumption is final
+        SN_DISPATCH_N(s.N, {
+            HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_PIPE>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
+            hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_PIPE>), dim3(grid_for(s.B)), dim3(kBlock), shmem, st, s, c);
+        });
+        HIP_TRY(hipGetLastError());
+        // the next launch's twist, beside this one: leads the consumer of the launch before
+        HIP_TRY(hipStreamWaitEvent(e->side, e->ev_main, 0));
+        hipLaunchKernelGGL(k_mt_ahead<false>, pg, dim3(kBlock), 0, e->side, s, AheadArgs{1 - p, p, 1 - p});
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(e->ev_prep, e->side));
+        e->pcount++;
+    }
+    return SN_OK;
 }
 
 static sn_status launch_play(sn_env* e, PlayArgs a, hipStream_t st) {
     const DevState& s = e->s;
-    sn_status frc;
-    if (try_launch_fused(e, a, st, &frc)) return frc;
+    if (s.rng_mode == SN_RNG_NUMPY_MT && !a.actions && e->pipe) {
+        int wave;
+        if (pipe_lds(s, a, &wave) <= (size_t)kLdsBytes) return launch_pipe(e, a, st);
+    }
+    {
+        const sn_status r = sn_pipe_sync(e, st);
+        if (r != SN_OK) return r;
+    }
     const bool ring = (s.rng_mode == SN_RNG_NUMPY_MT) && !a.actions && s.ring_w > 0;
     if (!ring || a.steps <= e->chunk_steps) return launch_play_one(e, a, st);
     const int64_t B = s.B, N = s.N;
@@ -1112,6 +1058,7 @@ sn_status sn_mt_get(sn_env* e, int64_t game, uint32_t* key, int32_t* pos) {
     if (e->s.rng_mode != SN_RNG_NUMPY_MT) return fail(SN_EINVAL, "env is not in numpy-compat RNG mode");
     if (game < 0 || game >= e->s.B) return fail(SN_EINVAL, "game out of range");
     HIP_TRY(hipSetDevice(e->device));
+    if (sn_pipe_sync(e, 0) != SN_OK) return SN_EHIP;
     HIP_TRY(hipDeviceSynchronize());
     uint32_t code = 0;
     HIP_TRY(hipMemcpy(key, e->s.mt + game * kMtN, sizeof(uint32_t) * kMtN, hipMemcpyDeviceToHost));
@@ -1135,11 +1082,21 @@ sn_status sn_mt_set(sn_env* e, int64_t game, const uint32_t* key, int32_t pos) {
     if (game < 0 || game >= e->s.B) return fail(SN_EINVAL, "game out of range");
     if (pos < 0 || pos > kMtN) return fail(SN_EINVAL, "pos must be in 0..624");
     HIP_TRY(hipSetDevice(e->device));
+    if (sn_pipe_sync(e, 0) != SN_OK) return SN_EHIP;
     HIP_TRY(hipDeviceSynchronize());
     const uint32_t code = mt_code_from_numpy(pos);
     HIP_TRY(hipMemcpy(e->s.mt + game * kMtN, key, sizeof(uint32_t) * kMtN, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(e->s.mt_pos + game, &code, sizeof(uint32_t), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemset(e->s.ringn + game, 0, sizeof(uint32_t)));  // buffered words belong to the old stream
+    return SN_OK;
+}
+
+sn_status sn_pipe_errors(sn_env* e, uint32_t* count) {
+    if (!e || !count) return fail(SN_EINVAL, "NULL argument");
+    *count = 0;
+    if (!e->s.perr) return SN_OK;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(count, e->s.perr, sizeof(uint32_t), hipMemcpyDeviceToHost));
     return SN_OK;
 }
 

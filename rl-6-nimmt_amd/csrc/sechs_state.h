@@ -42,8 +42,17 @@ struct DevState {
     u32x4* ring;     // [ring_w/16][B] low bytes of the words k_mt_prep twisted ahead
     int ring_w;      // ring words per game (multiple of 64), 0 = no ring
     int pad2_;
-    uint32_t* ringn; // [B] ring bytes valid for the next launch (the stream's next words); 0 = none
+    // pipelined twist-ahead (k_mt_ahead / RingPipe, sechs_env.hip):
+    u32x4* pring;    // [kPipeRing/16][B] 16-B chunks: byte of absolute stream word p at p mod kPipeRing
+    uint32_t* pabsc; // [2][B] consumer position after a play launch (by launch parity)
+    uint32_t* ptend; // [2][B] end of the twisted words after a prep launch (by launch parity)
+    uint32_t* ptp;   // [B] twist pointer (MtGen's pos field), owned by k_mt_ahead
+    uint32_t* perr;  // [1] play lanes that ran past the twisted words (must stay 0)
 };
+
+constexpr int kPipeRing = 1024;  // ring bytes per game (>= lead + one launch)
+constexpr int kPipeLead = 600;   // words k_mt_ahead keeps twisted ahead of the consumer (<= 624)
+constexpr int kPipeWin = 304;    // of them, copied to LDS per lane at a k_play launch
 
 constexpr int kBlock = 256;
 constexpr int kDeckStride = 108;  // 27 dwords: odd dword stride -> conflict-free LDS lanes
@@ -60,7 +69,6 @@ struct RngOf<RNG_NUMPY_MT, PF> {
     }
     static __device__ __forceinline__ void store(const DevState& s, int64_t g, T& r, const ByteBuf& buf) {
         s.mt_pos[g] = r.save(buf);
-        s.ringn[g] = 0u;  // words consumed outside the ring: its bytes are stale
     }
 };
 template <int PF>
@@ -85,18 +93,66 @@ struct RngOf<RNG_PHILOX, PF> {
 // LDS = false: chunks come from HBM, the next one prefetched.  A lane that
 // runs the ring dry continues with MtGen from the in-place state (rare: the
 // ring is sized for a launch's draws + ~6.5 sd).
+// Past the ring (rare): the next 8 words of the stream from the in-place
+// state -- `extra` twisted words first, then numpy's in-place twist of the
+// next 8 (T stays 8-aligned; a crossed round saves the old mt[0]).  Out of
+// line and by value, so the hot inlined paths carry none of it.
+struct RingSlow {
+    uint64_t bytes;
+    uint32_t T, extra;
+};
+
+static __device__ __noinline__ RingSlow ring_slow8(uint32_t* st, uint32_t* mt0, uint32_t T, uint32_t extra) {
+    RingSlow r;
+    r.bytes = 0ull;
+    if (extra) {  // replay: words [T - extra, T) mod 624
+        const uint32_t from = (T >= extra) ? T - extra : T + kMtN - extra;
+        const uint32_t k = min(8u, extra);
+        for (uint32_t i = 0; i < k; i++) {
+            const uint32_t idx = (from + i >= (uint32_t)kMtN) ? from + i - kMtN : from + i;
+            r.bytes |= (uint64_t)(mt_temper(st[idx]) & 0xFFu) << (8u * i);
+        }
+        r.T = T, r.extra = extra - k;
+        r.extra |= k << 16;  // count of bytes in r.bytes (< 8 only when replaying a short tail)
+        return r;
+    }
+    const uint32_t i0 = (T == (uint32_t)kMtN) ? 0u : T;
+    for (uint32_t i = 0; i < 8u; i++) {
+        const uint32_t idx = i0 + i;
+        const uint32_t a = st[idx];
+        const uint32_t v = mt_mix(a, st[(idx + 1u == (uint32_t)kMtN) ? 0u : idx + 1u],
+                                  st[(idx < (uint32_t)(kMtN - kMtM)) ? idx + kMtM : idx - (uint32_t)(kMtN - kMtM)]);
+        if (idx == 0u) *mt0 = a;
+        st[idx] = v;
+        r.bytes |= (uint64_t)(mt_temper(v) & 0xFFu) << (8u * i);
+    }
+    r.T = i0 + 8u;
+    r.extra = 8u << 16;
+    return r;
+}
+
+// numpy-MT words for k_play from the ring k_mt_prep filled just before the
+// launch: the low bytes of the next ring_w words of the game's stream, in
+// 16-B chunks interleaved over games (chunk q of game g at ring[q*B + g], so
+// a wave's lanes reading their q-th chunks read one contiguous 1-KB run).
+// LDS = true: the lane copies its ring to its LDS slot at launch start (16
+// coalesced loads per lane, one wait), so the step loop issues no global
+// loads at all -- a global load there would wait behind every observation
+// store still in flight (vmcnt counts loads and stores in issue order).
+// LDS = false: chunks come from HBM, the next one prefetched.  A lane that
+// runs the ring dry continues with ring_slow8 (rare: the ring is sized for a
+// launch's draws + ~6.5 sd).
 template <bool LDS>
 struct RingGen {
-    const u32x4* base;    // ring + g
+    const u32x4* base;     // ring + g
     const uint8_t* lring;  // LDS copy (LDS = true)
     uint32_t* st;
+    uint32_t* mt0;
     int64_t B;
     u32x4 c0, c1;          // chunks q, q + 1 (LDS = false)
     uint32_t q, nq, half;  // next chunk, chunks in the ring, next 8-B half of c0
     uint32_t rb;           // ring bytes not yet handed out
     uint32_t T, extra;     // twist position; twisted words past the ring
-    uint32_t on;           // MtGen fallback active
-    MtGenT<1> mt;
 
     __device__ __forceinline__ void load(const DevState& s, int64_t g, ByteBuf& buf, uint8_t* lds_slot) {
         const uint32_t code = s.mt_pos[g];
@@ -105,10 +161,11 @@ struct RingGen {
         rb = (uint32_t)s.ring_w;  // k_mt_prep left rem >= ring_w
         extra = rem - rb;
         st = s.mt + g * kMtN;
+        mt0 = s.mt0 + g;
         B = s.B;
         base = s.ring + g;
         nq = rb >> 4;
-        q = 0u, half = 0u, on = 0u;
+        q = 0u, half = 0u;
         if (LDS) {
             lring = lds_slot;
             for (uint32_t i = 0; i < nq; i++) {  // 8-B aligned slot: two ds_write_b64
@@ -122,9 +179,7 @@ struct RingGen {
         }
         buf.clear();
     }
-    __device__ __forceinline__ uint32_t save(const ByteBuf& buf) {
-        return on ? mt.save(buf) : (T | ((rb + extra + buf.cnt) << 16));
-    }
+    __device__ __forceinline__ uint32_t save(const ByteBuf& buf) { return T | ((rb + extra + buf.cnt) << 16); }
     __device__ __forceinline__ bool gen(ByteBuf& buf) {
         if (rb) {
             uint64_t v;
@@ -144,17 +199,96 @@ struct RingGen {
             half ^= 1u;
             return true;
         }
-        if (!on) {
-            mt.load(st, T | (extra << 16), buf, true);
-            on = 1u;
-        }
-        return mt.gen(buf);
+        const RingSlow r = ring_slow8(st, mt0, T, extra);
+        T = r.T;
+        extra = r.extra & 0xFFFFu;
+        buf.append(r.bytes, r.extra >> 16);
+        return true;
     }
     __device__ __forceinline__ void topup(ByteBuf& buf) {
         if (buf.cnt <= 24u) gen(buf);
     }
     __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf); }  // cnt == 0: always succeeds
 };
+
+// numpy-MT words for k_play from the pipelined ring: k_mt_ahead twisted the
+// stream up to `tend` (>= ~400 words past the consumer) while the previous
+// k_play ran.  The first kPipeWin of those bytes are copied to LDS at start
+// (21 coalesced 1-KB loads per wave); reads are 8 bytes at any byte offset
+// (two aligned ds_read_b64 + funnel shift).  Past the window the bytes come
+// from HBM; past `tend` a lane would need words the next k_mt_ahead is
+// twisting concurrently: it counts an error (perr) and draws zero bytes
+// instead -- ~18 standard deviations past one launch's draws.
+struct PipeSlow {
+    uint64_t bytes;
+    uint32_t k;
+};
+
+static __device__ __noinline__ PipeSlow pipe_slow(const uint8_t* ring, int64_t B, int64_t g, uint32_t pos, uint32_t left,
+                                                  uint32_t* err) {
+    PipeSlow r;
+    r.bytes = 0ull;
+    r.k = min(8u, left);
+    for (uint32_t i = 0; i < r.k; i++) {
+        const uint32_t ri = (pos + i) & (uint32_t)(kPipeRing - 1);
+        r.bytes |= (uint64_t)ring[((int64_t)(ri >> 4) * B + g) * 16 + (ri & 15u)] << (8u * i);
+    }
+    if (r.k == 0u) {
+        atomicAdd(err, 1u);
+        r.k = 8u;
+    }
+    return r;
+}
+
+struct RingPipe {
+    const uint8_t* slot;  // LDS window: chunk-aligned copy starting at the consumer's chunk
+    const uint8_t* ring;
+    uint32_t* err;
+    int64_t B, g;
+    uint32_t c0, off, take, win, avail;
+
+    __device__ __forceinline__ void load(const DevState& s, int64_t gg, ByteBuf& buf, uint8_t* lds_slot, int cin, int tpar) {
+        g = gg, B = s.B;
+        c0 = s.pabsc[(int64_t)cin * B + g];
+        avail = s.ptend[(int64_t)tpar * B + g] - c0;
+        win = min(avail, (uint32_t)kPipeWin);
+        off = c0 & 15u;
+        slot = lds_slot;
+        ring = (const uint8_t*)s.pring;
+        err = s.perr;
+        take = 0u;
+        const uint32_t q0 = (c0 & (uint32_t)(kPipeRing - 1)) >> 4;
+        const uint32_t nch = (off + win + 15u) >> 4;
+        for (uint32_t i = 0; i < nch; i++) {
+            const u32x4 c = s.pring[(int64_t)((q0 + i) & (uint32_t)(kPipeRing / 16 - 1)) * B + g];
+            *(uint64_t*)(lds_slot + 16u * i) = (uint64_t)c.x | ((uint64_t)c.y << 32);
+            *(uint64_t*)(lds_slot + 16u * i + 8u) = (uint64_t)c.z | ((uint64_t)c.w << 32);
+        }
+        buf.clear();
+    }
+    __device__ __forceinline__ uint32_t consumed(const ByteBuf& buf) const { return c0 + take - buf.cnt; }
+    __device__ __forceinline__ bool gen(ByteBuf& buf) {
+        if (take + 8u <= win) {
+            const uint32_t p = off + take, a8 = p & ~7u, sh = 8u * (p & 7u);
+            const uint64_t lo = *(const uint64_t*)(slot + a8);
+            const uint64_t hi = *(const uint64_t*)(slot + a8 + 8u);
+            buf.append(sh ? ((lo >> sh) | (hi << (64u - sh))) : lo, 8u);
+            take += 8u;
+            return true;
+        }
+        const PipeSlow r = pipe_slow(ring, B, g, c0 + take, (avail > take) ? avail - take : 0u, err);
+        buf.append(r.bytes, r.k);
+        take += r.k;
+        return true;
+    }
+    __device__ __forceinline__ void topup(ByteBuf& buf) {
+        if (buf.cnt <= 24u) gen(buf);
+    }
+    __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf); }
+};
+
+// bytes of a lane's LDS window for RingPipe (chunk-aligned copy + 8 for the funnel's second read)
+constexpr int kPipeSlot = ((kPipeWin + 15 + 15) / 16) * 16 + 8;
 
 // bytes of a lane's LDS ring slot (+8: odd 8-B stride, conflict-free ds_read_b64 rows)
 __host__ __device__ __forceinline__ int ring_lds_stride(int ring_w) { return ring_w + 8; }
@@ -167,7 +301,6 @@ struct RngOf<RNG_NUMPY_RING, PF> {
     }
     static __device__ __forceinline__ void store(const DevState& s, int64_t g, T& r, const ByteBuf& buf) {
         s.mt_pos[g] = r.save(buf);
-        s.ringn[g] = 0u;
     }
 };
 template <int PF>
@@ -178,7 +311,6 @@ struct RngOf<RNG_NUMPY_RING_HBM, PF> {
     }
     static __device__ __forceinline__ void store(const DevState& s, int64_t g, T& r, const ByteBuf& buf) {
         s.mt_pos[g] = r.save(buf);
-        s.ringn[g] = 0u;
     }
 };
 
@@ -363,32 +495,40 @@ __device__ __forceinline__ void deal_shuffle(R& rng, ByteBuf& buf, uint8_t* deck
 // hand bytes, bytes 10..47 are the same for every seat (game words).
 template <bool SUMM>
 __device__ __forceinline__ void game_words(int N, const Board& b, uint32_t& w2hi, uint32_t (&w)[9]) {
-    uint32_t bytes[48];
-#pragma unroll
-    for (int i = 0; i < 48; i++) bytes[i] = 0u;
+    // Built a row at a time as 6-byte groups (no per-byte selects): row r =
+    // its packed cards 0..3 with the bytes past len forced to 0xFF (-1), card
+    // 4 or 0xFF, then 0xFF; the four groups form the 24 board bytes X.
     const uint32_t lo[4] = {b.lo.x, b.lo.y, b.lo.z, b.lo.w};
     const uint32_t hi[4] = {b.hi.x, b.hi.y, b.hi.z, b.hi.w};
-    int pos = 10;
-    bytes[pos++] = (uint32_t)N & 0xFFu;
-    if (SUMM) {
-#pragma unroll
-        for (int r = 0; r < kRows; r++) bytes[pos++] = len_of(hi[r]);
-#pragma unroll
-        for (int r = 0; r < kRows; r++) bytes[pos++] = end_of(hi[r]);
-#pragma unroll
-        for (int r = 0; r < kRows; r++) bytes[pos++] = heads_in(hi[r]);
-    }
+    uint64_t G[4];
 #pragma unroll
     for (int r = 0; r < kRows; r++) {
-        const uint32_t len = len_of(hi[r]);
-#pragma unroll
-        for (int i = 0; i < kThreshold; i++, pos++)
-            bytes[pos] = (i < 5 && (uint32_t)i < len) ? card_at(lo[r], hi[r], i < 5 ? i : 0) : 0xFFu;
+        const uint32_t len = len_of(hi[r]);  // 1..5
+        const uint32_t r4 = lo[r] | ((len >= 4u) ? 0u : (0xFFFFFFFFu << (8u * len)));
+        const uint32_t b4 = (len == 5u) ? (hi[r] & 0xFFu) : 0xFFu;
+        G[r] = (uint64_t)r4 | ((uint64_t)(b4 | 0xFF00u) << 32);
     }
-    w2hi = (bytes[10] << 16) | (bytes[11] << 24);
-#pragma unroll
-    for (int k = 0; k < 9; k++)
-        w[k] = bytes[12 + 4 * k] | (bytes[13 + 4 * k] << 8) | (bytes[14 + 4 * k] << 16) | (bytes[15 + 4 * k] << 24);
+    const uint64_t X0 = G[0] | (G[1] << 48), X1 = (G[1] >> 16) | (G[2] << 32), X2 = (G[2] >> 32) | (G[3] << 16);
+    const uint64_t Y0 = (X0 >> 8) | (X1 << 56), Y1 = (X1 >> 8) | (X2 << 56), Y2 = X2 >> 8;  // X bytes 1..23 + 0
+    const uint32_t nb = (uint32_t)N & 0xFFu;
+    if (SUMM) {  // [10] N, [11..14] lens, [15..18] ends, [19..22] heads, [23..46] X, [47] 0
+        const uint32_t L = ((hi[0] >> 8) & 0xFFu) | (hi[1] & 0xFF00u) | ((hi[2] << 8) & 0xFF0000u) | ((hi[3] << 16) & 0xFF000000u);
+        const uint32_t H = ((hi[0] >> 16) & 0xFFu) | ((hi[1] >> 8) & 0xFF00u) | (hi[2] & 0xFF0000u) | ((hi[3] << 8) & 0xFF000000u);
+        const uint32_t E = (hi[0] >> 24) | ((hi[1] >> 16) & 0xFF00u) | ((hi[2] >> 8) & 0xFF0000u) | (hi[3] & 0xFF000000u);
+        w2hi = (nb << 16) | (L << 24);
+        w[0] = (L >> 8) | (E << 24);
+        w[1] = (E >> 8) | (H << 24);
+        w[2] = (H >> 8) | ((uint32_t)X0 << 24);
+        w[3] = (uint32_t)Y0, w[4] = (uint32_t)(Y0 >> 32);
+        w[5] = (uint32_t)Y1, w[6] = (uint32_t)(Y1 >> 32);
+        w[7] = (uint32_t)Y2, w[8] = (uint32_t)(Y2 >> 32);
+    } else {  // [10] N, [11..34] X, zeros
+        w2hi = (nb << 16) | ((uint32_t)X0 << 24);
+        w[0] = (uint32_t)Y0, w[1] = (uint32_t)(Y0 >> 32);
+        w[2] = (uint32_t)Y1, w[3] = (uint32_t)(Y1 >> 32);
+        w[4] = (uint32_t)Y2, w[5] = (uint32_t)(Y2 >> 32);
+        w[6] = w[7] = w[8] = 0u;
+    }
 }
 
 // one seat's obs row of `stride` bytes (stride % 4 == 0, >= L)
@@ -444,6 +584,17 @@ inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBloc
 struct sn_env {
     int device;
     int chunk_steps;  // SN_OPT_CHUNK_STEPS
-    int fused;        // SN_OPT_FUSED
+    int pipe;         // SN_OPT_PIPELINE
     sechs::DevState s;
+    // pipelined twist-ahead (sechs_env.hip launch_pipe): a k_mt_ahead for the
+    // next play launch may be in flight on `side` (ev_prep) after a rollout
+    int pvalid;         // ring + ptend/pabsc/ptp are the live RNG state (mt_pos is stale)
+    uint64_t pcount;    // play launches so far (parity selects the pabsc / ptend buffers)
+    hipStream_t side;
+    hipEvent_t ev_prep, ev_main;
 };
+
+// Every entry point that reads or writes a handle's numpy-MT state other
+// than the pipelined rollout itself calls this first (on its stream): waits
+// for an in-flight k_mt_ahead and folds the pipeline back into mt_pos.
+extern "C" sn_status sn_pipe_sync(sn_env* e, hipStream_t st);

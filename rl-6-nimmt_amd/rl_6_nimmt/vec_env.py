@@ -175,14 +175,20 @@ class VecSechsNimmtEnv:
         nat.check(nat.lib().sn_clear_results(self._h, self._stream()), "sn_clear_results")
 
     # ------------------------------------------------------------ numpy RNG bridge
-    def set_option(self, ring_words=None, chunk_steps=None, fused=None):
+    def set_option(self, ring_words=None, chunk_steps=None, pipeline=None):
         """numpy-compat rollout tuning (include/sechs.h SN_OPT_*); results never depend on it"""
-        if fused is not None:
-            nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_FUSED, int(bool(fused))), "sn_set_option")
+        if pipeline is not None:
+            nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPELINE, int(bool(pipeline))), "sn_set_option")
         if ring_words is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_RING_WORDS, int(ring_words)), "sn_set_option")
         if chunk_steps is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_CHUNK_STEPS, int(chunk_steps)), "sn_set_option")
+
+    def pipe_errors(self):
+        """draws of pipelined rollouts that ran past the twisted words (must be 0) [sync]"""
+        c = ctypes.c_uint32()
+        nat.check(nat.lib().sn_pipe_errors(self._h, ctypes.byref(c)), "sn_pipe_errors")
+        return c.value
 
     def get_mt_state(self, game=0):
         key = np.zeros(624, dtype=np.uint32)

@@ -310,17 +310,18 @@ def test_mt_state_across_round_boundaries_every_step():
             assert p == rp and np.array_equal(k, rk), (t, g)
 
 
-@pytest.mark.parametrize("ring_words,chunk_steps,fused", [(0, 10, 1), (64, 10, 1), (64, 1, 1), (128, 3, 1),
-                                                           (512, 25, 1), (256, 7, 1), (256, 10, 0), (512, 4, 0), (256, 10, 1)])
-def test_ring_options_do_not_change_results(ring_words, chunk_steps, fused):
+@pytest.mark.parametrize("ring_words,chunk_steps,pipeline", [(0, 10, 0), (64, 10, 0), (64, 1, 0), (128, 3, 0),
+                                                              (512, 25, 0), (256, 7, 0), (256, 10, 1), (256, 3, 1),
+                                                              (0, 1, 1), (512, 25, 1)])
+def test_ring_options_do_not_change_results(ring_words, chunk_steps, pipeline):
     """The twist-ahead paths are optimisations only: every ring size (0 =
     lazy per-lane MT19937; 64 runs k_mt_prep's ring dry inside every
-    episode, so the MtGen fallback continues mid-launch), launch chunking,
-    and the fused producer/consumer kernel (ring >= 256) give the oracle's
-    actions, rewards, obs and final numpy MT states."""
+    episode, so the slow path continues mid-launch), launch chunking, and
+    the pipelined k_mt_ahead (concurrent with the previous k_play) give the
+    oracle's actions, rewards, obs and final numpy MT states."""
     B, N, T, seed = 300, 4, 37, 21
     env = venv(B, N, seed=seed, rng="numpy")
-    env.set_option(ring_words=ring_words, chunk_steps=chunk_steps, fused=fused)
+    env.set_option(ring_words=ring_words, chunk_steps=chunk_steps, pipeline=pipeline)
     env.reset()
     ref = O.VecOracle(B, N, rng_mode=O.RNG_NUMPY_MT, seed=seed)
     ref.reset()
@@ -336,6 +337,7 @@ def test_ring_options_do_not_change_results(ring_words, chunk_steps, fused):
         k, p = _np_form(*env.get_mt_state(g))
         rk, rp = _np_form(np.frombuffer(bytes(rngs[g].mt), dtype=np.uint32), rngs[g].pos)
         assert p == rp and np.array_equal(k, rk), g
+    assert env.pipe_errors() == 0
 
 
 def test_ring_option_validation():
@@ -350,9 +352,10 @@ def test_ring_option_validation():
         penv.set_option(ring_words=256)
 
 
-def test_fused_then_other_paths_interleave():
-    """Leftover ring words carried between fused launches are dropped when
-    anything else consumes the stream (per-step API, reset, prep path, numpy
+def test_pipeline_then_other_paths_interleave():
+    """The pipelined twist-ahead state (ring, a k_mt_ahead in flight) is
+    folded back into the MT state whenever anything else touches the stream
+    (per-step API with external actions, reset, the k_mt_prep path, numpy
     state import): every mix stays bit-exact with the oracle."""
     B, N, seed = 130, 4, 5
     env = venv(B, N, seed=seed, rng="numpy")
@@ -364,14 +367,14 @@ def test_fused_then_other_paths_interleave():
             ("import", 0), ("roll", 12), ("roll", 1), ("roll", 30)]
     for what, T in plan:
         if what == "roll":
-            env.set_option(fused=1)
+            env.set_option(pipeline=1)
             out = env.rollout(T, want_actions=True)
             rr, rd, ra, _ = ref.rollout(T)
             torch.cuda.synchronize()
             assert np.array_equal(out["actions"].cpu().numpy(), ra), what
             assert np.array_equal(out["rewards"].cpu().numpy(), rr), what
         elif what == "prep":
-            env.set_option(fused=0)
+            env.set_option(pipeline=0)
             out = env.rollout(T, want_actions=True)
             rr, rd, ra, _ = ref.rollout(T)
             torch.cuda.synchronize()

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof_${1:-cur}
 mkdir -p $OUT
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 30 --warmup 2 --no-cpu --no-mcs --no-puct --rng ${2:-numpy} > $OUT/bench.json 2> $OUT/prof.err || { tail -20 $OUT/prof.err; exit 1; }
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 30 --warmup 2 --no-cpu --no-mcs --no-puct --rng ${2:-numpy} ${3:-} > $OUT/bench.json 2> $OUT/prof.err || { tail -20 $OUT/prof.err; exit 1; }
 python3 - $OUT/prof/run_kernel_stats.csv <<'PY'
 import csv, sys
 for r in csv.DictReader(open(sys.argv[1])):
