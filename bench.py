@@ -11,10 +11,11 @@ GameSession(DrunkHamster() x 4) of the reference, episode after episode).
 One bench step = one rollout call that advances every game by one full
 episode (10 env-steps: policy draw, simultaneous-play resolution, scoring,
 per-seat int8 observation, auto-reset deal) and writes the whole trajectory
-(obs, actions, rewards, done) to HBM: in numpy mode two launches, k_mt_prep
-(each game's MT19937 stream twisted ahead, coalesced) and k_play (the game
-loop, drawing from an LDS copy of the prepared words).  Inputs are
-resident on the device before timing starts.
+(obs, actions, rewards, done) to HBM: in numpy mode k_play (the game loop,
+drawing from an LDS copy of pre-twisted MT19937 words) with, on a side
+stream and concurrently, k_mt_ahead twisting every game's stream ~600 words
+ahead for the next launch.  Inputs are resident on the device before timing
+starts; the timed region includes both kernels.
 
 Multi-GPU: game shards are independent (rank r owns global games
 [r*B, (r+1)*B), streams keyed by the global id), so there is no collective
@@ -43,12 +44,12 @@ STEPS_PER_LAUNCH = 10
 # observation the step emits.
 ALGO_BYTES_PER_STEP = (33 * N_PLAYERS + 57) + 47 * N_PLAYERS  # 377 B at N = 4
 # HBM bytes per bench step from rocprofv3 PMC passes of its kernels (numpy
-# mode: k_mt_prep + k_play; philox: k_play) -- tools/pmc_config2.sh: FETCH_SIZE
+# mode: k_mt_ahead + k_play; philox: k_play) -- tools/pmc_config2.sh: FETCH_SIZE
 # and WRITE_SIZE in separate passes, gfx950 corrections of MI355X_MICROARCH.md
 # applied by tools/pmc_traffic.py.  PMC counters cannot be read inside a plain
 # run, so the committed summary of the current kernels is reported beside the
 # live timing.
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_v13_pmc_traffic_{rng}.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_v15_pmc_traffic_{rng}.json")
 
 
 def parse():
@@ -110,7 +111,18 @@ def time_rollouts(env, out, steps, warmup, world):
     barrier(world)
     t1 = time.perf_counter()
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    return t1 - t0, kern_ms
+    if env.rng != "numpy":
+        return t1 - t0, kern_ms, {"k_play": kern_ms, "launches": steps}
+    # numpy mode: the two kernels of a step run on two streams, so each gets
+    # HIP events on its own stream -- in a second pass of the same `steps`
+    # launches right after the timed one (the extra per-launch events on both
+    # streams slow the pipelined step by ~10 %, so they stay out of `value`)
+    env.time_kernels(steps)
+    for i in range(steps):
+        env.rollout(STEPS_PER_LAUNCH, out=out)
+    play_ms, ahead_ms, n = env.kernel_times()
+    env.time_kernels(0)
+    return t1 - t0, kern_ms, {"k_play": play_ms, "k_mt_ahead": ahead_ms, "launches": n}
 
 
 def make_out(env, games, with_obs):
@@ -230,12 +242,45 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
     }
 
 
+def bench_customed(games, episodes=5):
+    """BASELINE config 4, policy/value-net variant: PUCTCustomedAgent
+    (mcts.py:325-451) in every seat of `games` 4-player games -- per
+    decision one 2-head MLP forward (bf16, PyTorch-ROCm) over the root
+    candidates, the move = first argmax of the value head.  `episodes` whole
+    games back to back; units: env-steps and decisions (one seat's move)."""
+    from rl_6_nimmt.puct import BatchedPUCTCustomed, make_actor_value
+    from rl_6_nimmt.vec_env import VecSechsNimmtEnv
+
+    env = VecSechsNimmtEnv(games, N_PLAYERS, seed=3, rng="philox")
+    torch.manual_seed(0)
+    eng = BatchedPUCTCustomed(env, make_actor_value(), seed=4, net_dtype=torch.bfloat16)
+    eng.play_episode()  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tot = None
+    for _ in range(episodes):
+        total, _ = eng.play_episode()
+        tot = total if tot is None else tot + total
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    return {
+        "workload": f"config4 (policy/value net): {games} x 4-player games, all seats PUCTCustomedAgent, bf16 2-head "
+                    f"MLP 48-100-100-2 via PyTorch-ROCm, {episodes} games",
+        "value": 10 * games * episodes / wall,
+        "unit": "env-steps/s",
+        "decisions_per_s": 10 * N_PLAYERS * games * episodes / wall,
+        "wall_s": wall,
+        "mean_score_per_seat": (tot.double() / episodes).mean(dim=0).tolist(),
+    }
+
+
 def pmc_traffic(rng, games):
     path = PMC_TRAFFIC.format(rng=rng)
     if games != 65536 or not os.path.exists(path):
         return None, None
     rec = json.load(open(path))
-    return float(rec["traffic_bytes_per_launch"]), os.path.relpath(path, ROOT)
+    per_kernel = {k: v["traffic_bytes_per_dispatch"] for k, v in rec["kernels"].items()}
+    return per_kernel, os.path.relpath(path, ROOT)
 
 
 def main():
@@ -247,8 +292,13 @@ def main():
     env = VecSechsNimmtEnv(B, N_PLAYERS, seed=0, game_offset=rank * B, rng=args.rng)
     env.reset()
     out = make_out(env, B, not args.no_obs)
-    wall, kern_ms = time_rollouts(env, out, args.steps, args.warmup, world)
+    wall, kern_ms, kt = time_rollouts(env, out, args.steps, args.warmup, world)
 
+    # pipelined draws must never have run past the twisted words (checked
+    # after the timed region; a nonzero count would void the parity claim)
+    pipe_errors = env.pipe_errors() if args.rng == "numpy" else 0
+    if pipe_errors:
+        raise SystemExit(f"bench: {pipe_errors} pipelined MT19937 draws ran past the twisted words")
     # tournament score gather over RCCL (outside the timed region)
     sums, eps = env.results()
     tot = sums.to(torch.float64).sum(dim=0)
@@ -258,16 +308,25 @@ def main():
         walls = torch.tensor([wall], dtype=torch.float64, device=env.device)
         dist.all_reduce(walls, op=dist.ReduceOp.MAX)
         wall = float(walls.item())
-        kms = torch.tensor([kern_ms], dtype=torch.float64, device=env.device)
+        kms = torch.tensor([kern_ms, kt["k_play"], kt.get("k_mt_ahead", 0.0)], dtype=torch.float64, device=env.device)
         dist.all_reduce(kms, op=dist.ReduceOp.MAX)
-        kern_ms = float(kms.item())
+        kern_ms, kt["k_play"] = float(kms[0].item()), float(kms[1].item())
+        if "k_mt_ahead" in kt:
+            kt["k_mt_ahead"] = float(kms[2].item())
         dist.all_reduce(tot)
 
     total_steps = world * B * STEPS_PER_LAUNCH * args.steps
     value = total_steps / wall
     launch_steps = B * STEPS_PER_LAUNCH
-    achieved = launch_steps * ALGO_BYTES_PER_STEP / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(args.rng, B) if not args.no_obs else (None, None)
+    # dominant kernel = k_play (the game loop); its algorithmic bytes are the
+    # SURVEY.md §8(d) 377 B per env-step x the 655 360 env-steps of a launch,
+    # its duration the live HIP-event mean on its own stream (numpy mode: the
+    # twist-ahead k_mt_ahead runs concurrently on a side stream and is
+    # reported beside it; the whole step is `step_ms`)
+    play_ms = kt["k_play"]
+    achieved = launch_steps * ALGO_BYTES_PER_STEP / (play_ms * 1e-3) / 1e9
+    per_kernel, traffic_src = pmc_traffic(args.rng, B) if not args.no_obs else (None, None)
+    traffic = per_kernel.get("k_play<4") if per_kernel else None
     result = {
         "metric": "env-steps/sec at 65536 concurrent 4-player games, 1/2/4/8 MI355X",
         "value": value,
@@ -298,13 +357,22 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "traffic_unit": "HBM bytes per bench step (PMC FETCH_SIZE x2 + WRITE_SIZE, summed over its kernels)",
+            "traffic_unit": "HBM bytes per k_play launch (PMC FETCH_SIZE x2 + WRITE_SIZE, separate passes)",
             "traffic_source": traffic_src,
-            "traffic_gbs_at_live_kernel_ms": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
-            "kernel": ("k_mt_prep<4,4> + k_play<4, RNG_NUMPY_RING> (one bench step: MT19937 twist-ahead, then the "
-                       "10 env-steps; timed together)" if args.rng == "numpy" else "k_play<4, RNG_PHILOX>"),
-            "kernel_ms": kern_ms,
+            "kernel": f"k_play<4, {'RNG_NUMPY_PIPE' if args.rng == 'numpy' else 'RNG_PHILOX'}>: 10 env-steps of 65536 games",
+            "kernel_ms": play_ms,
+            "kernel_ms_source": ("HIP events around each k_play launch on its stream (sn_kernel_times), over a second "
+                                 "pass of the same launches right after the timed one" if args.rng == "numpy" else
+                                 "HIP events around each timed launch on the launch stream"),
             "algo_bytes_per_env_step": ALGO_BYTES_PER_STEP,
+            "algo_bytes_per_launch": launch_steps * ALGO_BYTES_PER_STEP,
+            "step_ms": kern_ms,
+            "step_frac": launch_steps * ALGO_BYTES_PER_STEP / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "concurrent": ({"kernel": "k_mt_ahead<false> (side stream, next launch's MT19937 twist-ahead)",
+                            "kernel_ms": kt.get("k_mt_ahead"),
+                            "traffic": per_kernel.get("k_mt_ahead") if per_kernel else None}
+                           if args.rng == "numpy" else None),
+            "step_traffic": sum(per_kernel.values()) if per_kernel else None,
         },
         "episodes_checksum": {"episodes": int(eps.sum().item()) * world, "mean_score_per_seat": (tot / (eps.sum().item() * world)).tolist()},
     }
@@ -314,10 +382,11 @@ def main():
         result["extra_config3_mcs"] = bench_mcs(args.mcs_games, args.mcs_rollouts)
     if world == 1 and not args.no_puct:
         result["extra_config4_puct"] = bench_puct(args.puct_games)
+        result["extra_config4_customed"] = bench_customed(args.puct_games)
     if args.extras and world == 1:
         env2 = VecSechsNimmtEnv(B, N_PLAYERS, seed=0, rng="philox")
         env2.reset()
-        w2, k2 = time_rollouts(env2, out, args.steps, args.warmup, world)
+        w2, k2, _ = time_rollouts(env2, out, args.steps, args.warmup, world)
         result["extra_philox"] = {"value": B * STEPS_PER_LAUNCH * args.steps / w2, "kernel_ms": k2}
     if rank == 0:
         print(json.dumps(result), flush=True)

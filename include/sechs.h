@@ -137,12 +137,19 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
      SN_OPT_PIPELINE     1 (default): DrunkHamster rollouts in numpy mode keep
                          each stream twisted ~600 words ahead with k_mt_ahead
                          on a side stream, concurrently with the previous
-                         launch's k_play (N <= 6); 0: the paths above. */
-enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3 };
+                         launch's k_play (N <= 6); 0: the paths above.
+     SN_OPT_TIMING       n > 0: record HIP events around the next n
+                         pipelined k_play / k_mt_ahead launches, each on the
+                         stream it runs on (read with sn_kernel_times);
+                         0 (default): off. */
+enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3, SN_OPT_TIMING = 4 };
 sn_status sn_set_option(sn_env* env, int option, int value);
 /* pipelined rollouts whose draws ran past the twisted words (must be 0; a
    nonzero count means those games' draws are wrong) [sync] */
 sn_status sn_pipe_errors(sn_env* env, uint32_t* count);
+/* mean launch duration (ms) of the pipelined k_play and k_mt_ahead launches
+   recorded since SN_OPT_TIMING was set; *n = launches recorded [sync] */
+sn_status sn_kernel_times(sn_env* env, float* play_ms, float* ahead_ms, int32_t* n);
 
 /* ---- Monte-Carlo search, MCSAgent (agents/mcts.py:17-188) ------------- */
 
@@ -229,6 +236,23 @@ sn_status sn_puct_rows(sn_env* env, const sn_puct* q, int n_cur, void* rows, int
 sn_status sn_puct_step(sn_env* env, const sn_puct* q, const float* logits, int t, int n_cur, void* stream);
 /* best_index [D] (optional): index of the chosen card in the root legal list */
 sn_status sn_puct_choose(sn_env* env, const sn_puct* q, int32_t* actions, int32_t* best_index, void* stream);
+/* PUCTCustomedAgent (agents/mcts.py:325-451, replaces _mcts /
+   _play_out_with_NN / _choose_action_mc_func :356-395): no rollouts.  heads
+   [D*n][2] f32 = the 2-head net (policy logit, value) on the
+   sn_puct_root_rows rows; per decision: best = first argmax of the values,
+   actions [B][N] (deciding seats) = legal[best], best_index [D],
+   log_prob [D] = log softmax(policy)[best], value [D] = values[best] (the
+   "outcome" learn() regresses).  Optional outputs may be NULL. */
+sn_status sn_pcv_choose(sn_env* env, const sn_puct* q, const float* heads, int32_t* actions, int32_t* best_index,
+                        float* log_prob, float* value, void* stream);
+/* BatchedReinforceAgent.forward (agents/policy.py:137-156) for every
+   deciding seat of q->seats_mask at hand size q->n: logits [D*n] f32 = the
+   policy MLP on the sn_puct_root_rows rows; samples Categorical(softmax)
+   with Philox (key q->seed ^ q->step; torch's CPU generator is not
+   reproducible on the device), actions [B][N] (deciding seats) = legal[k],
+   index [D] = k, log_prob [D], entropy [D] (optional, may be NULL). */
+sn_status sn_policy_sample(sn_env* env, const sn_puct* q, const float* logits, int32_t* actions, int32_t* index,
+                           float* log_prob, float* entropy, void* stream);
 /* _compute_pucts + argmax (mcts.py:282-315) for D given states: n [D],
    stats [D][24] (sums[10], counts[10], total, min, max), hist [D][172]
    outcome counts (value v at bin v+171), probs [D][10] f32 -> pucts [D][10]

@@ -696,6 +696,8 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
     return SN_OK;
 }
 
+static void free_timing(sn_env* e);
+
 sn_status sn_destroy(sn_env* e) {
     if (!e) return SN_OK;
     (void)hipSetDevice(e->device);
@@ -704,12 +706,21 @@ sn_status sn_destroy(sn_env* e) {
     if (e->ev_prep) (void)hipEventDestroy(e->ev_prep);
     if (e->ev_main) (void)hipEventDestroy(e->ev_main);
     if (e->side) (void)hipStreamDestroy(e->side);
+    free_timing(e);
     void* ps[] = {s.hand, s.row_lo, s.row_hi, s.score, s.sum_res, s.episodes, s.mt_pos, s.ctr, s.mt, s.mt0, s.ring,
                   s.pring, s.pabsc, s.ptend, s.ptp, s.perr};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     delete e;
     return SN_OK;
+}
+
+static void free_timing(sn_env* e) {
+    for (int i = 0; i < 4 * e->tcap; i++)
+        if (e->tev[i]) (void)hipEventDestroy(e->tev[i]);
+    delete[] e->tev;
+    e->tev = nullptr;
+    e->tcap = e->tn = 0;
 }
 
 sn_status sn_set_option(sn_env* e, int option, int value) {
@@ -738,6 +749,17 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
         case SN_OPT_PIPELINE:
             if (value != 0 && value != 1) return fail(SN_EINVAL, "pipeline must be 0 or 1");
             e->pipe = value;
+            return SN_OK;
+        case SN_OPT_TIMING:
+            if (value < 0 || value > 4096) return fail(SN_EINVAL, "timing launches must be in 0..4096");
+            HIP_TRY(hipSetDevice(e->device));
+            HIP_TRY(hipDeviceSynchronize());
+            free_timing(e);
+            if (value) {
+                e->tev = new hipEvent_t[4 * value]();
+                e->tcap = value;
+                for (int i = 0; i < 4 * value; i++) HIP_TRY(hipEventCreate(&e->tev[i]));
+            }
             return SN_OK;
         default: return fail(SN_EINVAL, "unknown option");
     }
@@ -891,16 +913,21 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         c.pipe_cin = 1 - p, c.pipe_cout = p, c.pipe_t = p;
         HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));  // this launch's words are twisted
         HIP_TRY(hipEventRecord(e->ev_main, st));         // the previous launch's consumption is final
+        hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
+        if (tv) HIP_TRY(hipEventRecord(tv[0], st));
         SN_DISPATCH_N(s.N, {
             HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_PIPE>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
             hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_PIPE>), dim3(grid_for(s.B)), dim3(kBlock), shmem, st, s, c);
         });
         HIP_TRY(hipGetLastError());
+        if (tv) HIP_TRY(hipEventRecord(tv[1], st));
         // the next launch's twist, beside this one: leads the consumer of the launch before
         HIP_TRY(hipStreamWaitEvent(e->side, e->ev_main, 0));
+        if (tv) HIP_TRY(hipEventRecord(tv[2], e->side));
         hipLaunchKernelGGL(k_mt_ahead<false>, pg, dim3(kBlock), 0, e->side, s, AheadArgs{1 - p, p, 1 - p});
         HIP_TRY(hipGetLastError());
+        if (tv) HIP_TRY(hipEventRecord(tv[3], e->side));
         HIP_TRY(hipEventRecord(e->ev_prep, e->side));
         e->pcount++;
     }
@@ -1087,6 +1114,23 @@ sn_status sn_mt_set(sn_env* e, int64_t game, const uint32_t* key, int32_t pos) {
     const uint32_t code = mt_code_from_numpy(pos);
     HIP_TRY(hipMemcpy(e->s.mt + game * kMtN, key, sizeof(uint32_t) * kMtN, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(e->s.mt_pos + game, &code, sizeof(uint32_t), hipMemcpyHostToDevice));
+    return SN_OK;
+}
+
+sn_status sn_kernel_times(sn_env* e, float* play_ms, float* ahead_ms, int32_t* n) {
+    if (!e || !play_ms || !ahead_ms || !n) return fail(SN_EINVAL, "NULL argument");
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipDeviceSynchronize());
+    double sp = 0.0, sa = 0.0;
+    for (int i = 0; i < e->tn; i++) {
+        float a = 0.f, b = 0.f;
+        HIP_TRY(hipEventElapsedTime(&a, e->tev[4 * i], e->tev[4 * i + 1]));
+        HIP_TRY(hipEventElapsedTime(&b, e->tev[4 * i + 2], e->tev[4 * i + 3]));
+        sp += a, sa += b;
+    }
+    *n = e->tn;
+    *play_ms = e->tn ? (float)(sp / e->tn) : 0.f;
+    *ahead_ms = e->tn ? (float)(sa / e->tn) : 0.f;
     return SN_OK;
 }
 

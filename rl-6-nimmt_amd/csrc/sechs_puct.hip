@@ -335,6 +335,68 @@ __global__ void k_puct_choose(DevState s, PuctArgs a, int32_t* actions, int32_t*
     if (best_index) best_index[d] = best;
 }
 
+// PUCTCustomedAgent (mcts.py:325-451): no rollouts; the 2-head net's value
+// head picks the move (_choose_action_mc_func, mcts.py:385-395: the first
+// argmax of the values over the legal list), its policy head gives the
+// move's log-probability (Categorical(softmax(policy)).log_prob) and the
+// chosen value is the step's "outcome".  heads = [D*n][2] f32 (policy, value)
+// in sn_puct_root_rows order.  One lane per decision.
+__global__ void k_pcv_choose(DevState s, PuctArgs a, const float* heads, int32_t* actions, int32_t* best_index,
+                             float* log_prob, float* value) {
+    const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= a.D) return;
+    int64_t g;
+    int p;
+    dec_to_gp(a, d, g, p);
+    const Hand h = load_hand(s, p, g);
+    const float2* x = (const float2*)heads + d * a.n;
+    float bv = x[0].y, m = x[0].x;
+    int best = 0;
+    for (int k = 1; k < a.n; k++) {
+        const float2 v = x[k];
+        if (v.y > bv) bv = v.y, best = k;
+        m = fmaxf(m, v.x);
+    }
+    float sum = 0.f;
+    for (int k = 0; k < a.n; k++) sum += expf(x[k].x - m);
+    actions[g * s.N + p] = (int32_t)hand_get(h, (uint32_t)best);
+    if (best_index) best_index[d] = best;
+    if (log_prob) log_prob[d] = (x[best].x - m) - logf(sum);
+    if (value) value[d] = bv;
+}
+
+// BatchedReinforceAgent.forward (agents/policy.py:137-156) for every
+// deciding seat: Categorical(softmax(logits)).sample() with a Philox uniform
+// keyed (seed ^ step, game, seat; rollout tag 0xFFFFF, never a PUCT
+// rollout's), plus log_prob and entropy of the distribution.  logits
+// [D*n] f32 in sn_puct_root_rows order.  One lane per decision.
+__global__ void k_policy_sample(DevState s, PuctArgs a, const float* logits, int32_t* actions, int32_t* index,
+                                float* log_prob, float* entropy) {
+    const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= a.D) return;
+    int64_t g;
+    int p;
+    dec_to_gp(a, d, g, p);
+    const Hand h = load_hand(s, p, g);
+    const float* x = logits + d * a.n;
+    const uint64_t gid = s.game_offset + (uint64_t)g;
+    const uint64_t stream = ((uint64_t)(uint32_t)gid << 32) | ((uint64_t)p << 28) | (0xFFFFFull << 8);
+    const int k = sample_softmax(x, a.n, philox_uniform(a.seed_lo ^ a.step, a.seed_hi, stream, 0u));
+    float m = x[0];
+    for (int j = 1; j < a.n; j++) m = fmaxf(m, x[j]);
+    float sum = 0.f, sx = 0.f;
+    for (int j = 0; j < a.n; j++) {
+        const float e = expf(x[j] - m);
+        sum += e;
+        sx += e * (x[j] - m);
+    }
+    const float lse = logf(sum);
+    actions[g * s.N + p] = (int32_t)hand_get(h, (uint32_t)k);
+    if (index) index[d] = k;
+    if (log_prob) log_prob[d] = (x[k] - m) - lse;
+    if (entropy) entropy[d] = lse - sx / sum;  // -sum p log p
+}
+
 // test hook for the formula fixtures (F5): stats/hist/probs given per decision
 __global__ void k_puct_score(int64_t D, int n_max, const int32_t* n, const int32_t* stats, const int32_t* hist,
                              const float* probs, double c_puct, double* pucts, int32_t* choice) {
@@ -438,6 +500,31 @@ sn_status sn_puct_choose(sn_env* e, const sn_puct* q, int32_t* actions, int32_t*
     if (st != SN_OK) return st;
     hipLaunchKernelGGL(k_puct_choose, dim3(grid_for(a.D)), dim3(kBlock), 0, (hipStream_t)stream, e->s, a, actions,
                        best_index);
+    HIP_TRY(hipGetLastError());
+    return SN_OK;
+}
+
+sn_status sn_pcv_choose(sn_env* e, const sn_puct* q, const float* heads, int32_t* actions, int32_t* best_index,
+                        float* log_prob, float* value, void* stream) {
+    if (!heads || !actions) return set_error(SN_EINVAL, "NULL argument");
+    PuctArgs a{};
+    sn_status st = puct_args(e, q, a);
+    if (st != SN_OK) return st;
+    if (a.n < 1) return set_error(SN_EINVAL, "hand size must be >= 1");
+    hipLaunchKernelGGL(k_pcv_choose, dim3(grid_for(a.D)), dim3(kBlock), 0, (hipStream_t)stream, e->s, a, heads,
+                       actions, best_index, log_prob, value);
+    HIP_TRY(hipGetLastError());
+    return SN_OK;
+}
+
+sn_status sn_policy_sample(sn_env* e, const sn_puct* q, const float* logits, int32_t* actions, int32_t* index,
+                           float* log_prob, float* entropy, void* stream) {
+    if (!logits || !actions) return set_error(SN_EINVAL, "NULL argument");
+    PuctArgs a{};
+    sn_status st = puct_args(e, q, a);
+    if (st != SN_OK) return st;
+    hipLaunchKernelGGL(k_policy_sample, dim3(grid_for(a.D)), dim3(kBlock), 0, (hipStream_t)stream, e->s, a, logits,
+                       actions, index, log_prob, entropy);
     HIP_TRY(hipGetLastError());
     return SN_OK;
 }

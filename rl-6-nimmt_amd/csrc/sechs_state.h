@@ -592,6 +592,10 @@ struct sn_env {
     uint64_t pcount;    // play launches so far (parity selects the pabsc / ptend buffers)
     hipStream_t side;
     hipEvent_t ev_prep, ev_main;
+    // SN_OPT_TIMING: per-launch event pairs (k_play start/end on the launch
+    // stream, k_mt_ahead start/end on `side`), tcap pairs, tn recorded
+    hipEvent_t* tev;
+    int tcap, tn;
 };
 
 // Every entry point that reads or writes a handle's numpy-MT state other

@@ -20,7 +20,7 @@ SN_OK, SN_EINVAL, SN_EHIP, SN_ENOMEM, SN_EUNSUPPORTED = 0, 1, 2, 3, 4
 SN_RNG_PHILOX, SN_RNG_NUMPY_MT = 0, 1
 SN_I8, SN_I16, SN_I32, SN_I64, SN_F32 = 1, 2, 3, 4, 5
 SN_AUTO_RESET, SN_NO_SUMMARIES = 1, 2
-SN_OPT_RING_WORDS, SN_OPT_CHUNK_STEPS, SN_OPT_PIPELINE = 1, 2, 3
+SN_OPT_RING_WORDS, SN_OPT_CHUNK_STEPS, SN_OPT_PIPELINE, SN_OPT_TIMING = 1, 2, 3, 4
 
 class SnPuct(ctypes.Structure):
     """sn_puct (include/sechs.h)"""
@@ -67,6 +67,7 @@ SIGNATURES = {
     "sn_philox_counter": ([_P, _I64, _P], _I),
     "sn_set_option": ([_P, _I, _I], _I),
     "sn_pipe_errors": ([_P, _P], _I),
+    "sn_kernel_times": ([_P, _P, _P, _P], _I),
     "sn_mcs_memorize": ([_P, _P, _I, _P], _I),
     "sn_mcs_rollouts": ([_P, _P, _I, _U64, ctypes.c_uint32, _P, _P], _I),
     "sn_mcs_rollouts_ex": ([_P, _P, _I, _U64, ctypes.c_uint32, _P, _P, _P], _I),
@@ -79,6 +80,8 @@ SIGNATURES = {
     "sn_puct_rows": ([_P, _P, _I, _P, _I, _P], _I),
     "sn_puct_step": ([_P, _P, _P, _I, _I, _P], _I),
     "sn_puct_choose": ([_P, _P, _P, _P, _P], _I),
+    "sn_pcv_choose": ([_P, _P, _P, _P, _P, _P, _P, _P], _I),
+    "sn_policy_sample": ([_P, _P, _P, _P, _P, _P, _P, _P], _I),
     "sn_puct_score": ([_I64, _P, _P, _P, _P, ctypes.c_double, _P, _P, _P], _I),
 }
 

@@ -119,6 +119,7 @@ class MCSAgent(BaseMCAgent):
 # policy-guided search ("Alpha0.5"): mcts.py:191-323
 # ---------------------------------------------------------------------------
 from torch import nn  # noqa: E402
+from torch.distributions import Categorical  # noqa: E402
 
 from ..utils.nets import MultiHeadedMLP  # noqa: E402
 from ..utils.preprocessing import SechsNimmtStateNormalization  # noqa: E402
@@ -140,7 +141,11 @@ class PolicyMCSAgent(BaseMCAgent):
         self.actor = MultiHeadedMLP(self.state_length + 1, hidden_sizes=hidden_sizes, head_sizes=(1,),
                                     activation=activation, head_activations=(None,))
         self.softmax = nn.Softmax(dim=0)
+        # the search key is drawn without moving torch's global stream, so
+        # seeded constructions init the same weights as the reference's
+        rng = torch.random.get_rng_state()
         self.search_seed = int(torch.randint(0, 2**62, (1,)).item())
+        torch.random.set_rng_state(rng)
         self._engine = None
         self._decisions = 0
 
@@ -249,3 +254,68 @@ class PUCTAgent(PolicyMCSAgent):
         if len(every) < 10:
             return 0.0, -10.0, -5.0  # quirk Q8: the "mean" is a median, with this fallback
         return np.max(every), np.min(every), np.median(every)
+
+
+class PUCTCustomedAgent(PUCTAgent):
+    """PUCTAgent with a 2-head net (policy logit, value) and no rollouts
+    (mcts.py:325-451): every move -- the root included, since the reference
+    calls _choose_action_mc with opponent=True (mcts.py:372-374) -- is the
+    first argmax of the value head over the legal cards; info carries
+    log pi(move) from the policy head and the chosen value as "outcome".
+    The reference draws a random environment first (_draw_env) whose other
+    hands it never reads; the same numpy shuffle is made here so the global
+    stream stays in step with the reference's.  The net is evaluated on the
+    host (the agent's device); the batched form is puct.BatchedPUCTCustomed
+    (sn_puct_root_rows -> MLP -> sn_pcv_choose on the GPU)."""
+
+    def __init__(self, hidden_sizes=(100, 100), activation=nn.ReLU(), **kwargs):
+        super().__init__(hidden_sizes=hidden_sizes, activation=activation, **kwargs)
+        self.actor = MultiHeadedMLP(self.state_length + 1, hidden_sizes=hidden_sizes, head_sizes=(2,),
+                                    activation=activation, head_activations=(None,))
+        self.MSELoss = nn.MSELoss()
+
+    def forward(self, state, legal_actions, *args, **kwargs):
+        n = len(legal_actions)
+        if n == self.handsize:
+            self._initialize_game(state)
+        self._memorize_cards(state, legal_actions)
+        action, info = self._mcts(legal_actions, state)
+        if n == 1:  # mcts.py:347-349
+            return legal_actions[0], {"log_prob": torch.tensor(0.0).to(self.device, self.dtype), "outcome": info["outcome"]}
+        return action, info
+
+    def _mcts(self, legal_actions, state):
+        cards = list(self.available_cards)
+        np.random.shuffle(cards)  # _draw_env -> _deal_hands (mcts.py:116-127): only its draws matter
+        probs, values = self._compute_policy_and_value(legal_actions, state)
+        action_id = torch.argmax(values)
+        log_prob = Categorical(probs).log_prob(action_id)
+        return int(legal_actions[action_id]), {"log_prob": log_prob, "outcome": values[action_id]}
+
+    def _compute_policy_and_value(self, legal_actions, state):
+        state = torch.as_tensor(state).to(self.device, self.dtype).reshape(-1)
+        cards = torch.tensor(legal_actions, device=self.device).to(self.dtype)[:, None]
+        batch = torch.cat((cards, state[None, :].expand(len(legal_actions), -1)), dim=1)
+        (out,) = self.actor(self.preprocessor(batch))
+        return self.softmax(out[:, 0]).flatten(), out[:, 1].flatten()
+
+    def learn(self, state, reward, action, done, next_state, next_reward, episode_end, num_episode, legal_actions,
+              *args, **kwargs):
+        self.history.store(log_prob=kwargs["log_prob"], outcome=kwargs["outcome"], reward=reward * self.r_factor)
+        if not episode_end or not self.training:
+            return 0.0
+        loss = self._train()
+        self.history.clear()
+        return loss
+
+    def _train(self):
+        rollout = self.history.rollout()
+        log_probs = torch.stack(rollout["log_prob"], dim=0)
+        outcome = torch.stack(rollout["outcome"], dim=0)
+        reward_sum = sum(rollout["reward"]) / self.r_factor
+        outcome_loss = self.MSELoss(outcome, torch.full(outcome.shape, fill_value=reward_sum))
+        policy_loss = -torch.sum(log_probs)
+        loss = outcome_loss + policy_loss
+        logger.info("loss: %s, policy_loss: %s, outcome_loss: %s", loss.item(), policy_loss.item(), outcome_loss.item())
+        self._gradient_step(loss)
+        return loss.item()

@@ -161,6 +161,94 @@ class BatchedPUCT:
         return loss
 
 
+def make_actor_value(hidden_sizes=(100, 100), activation=None):
+    """PUCTCustomedAgent's net (mcts.py:334-335): MultiHeadedMLP(48, (100, 100), (2,)) -- column 0 the
+    policy logit, column 1 the value"""
+    return MultiHeadedMLP(ROW, hidden_sizes=hidden_sizes, head_sizes=(2,), activation=activation or nn.ReLU(),
+                          head_activations=(None,))
+
+
+class BatchedPUCTCustomed(BatchedPUCT):
+    """PUCTCustomedAgent (agents/mcts.py:325-451) for every deciding seat of
+    a batch of games.  The reference's "search" draws an environment and
+    evaluates the 2-head net once on the root candidates -- no rollouts
+    (_play_out_with_NN, mcts.py:366-376): the move is the first argmax of
+    the value head, its log-probability comes from the policy head and the
+    chosen value is the step's outcome.  Per decision batch: one
+    sn_puct_root_rows launch (normalised rows straight from the device
+    state), one MLP forward (PyTorch-ROCm), one sn_pcv_choose launch.
+
+    Training (mcts.py:421-451) from stored rows instead of retained graphs:
+    per (game, deciding seat), loss = MSE(values of the chosen moves,
+    reward_sum) - sum(log pi(chosen)), with reward_sum = the rewards of the
+    first 9 steps (GameSession hands learn() the previous step's reward,
+    play.py:29,57,72, so the last step's never reaches the agent); the batch
+    loss is the sum over games (the reference steps Adam after every game)."""
+
+    def __init__(self, env, actor, seats_mask=None, net_dtype=torch.bfloat16, seed=0):
+        super().__init__(env, actor, seed=seed, seats_mask=seats_mask, puct_root=False, net_dtype=net_dtype)
+        D = self.D
+        self.log_prob = torch.zeros((D,), dtype=torch.float32, device=env.device)
+        self.value = torch.zeros((D,), dtype=torch.float32, device=env.device)
+
+    def decide(self, n, memorize=False, record=False):
+        """every deciding seat at hand size n; returns actions [B, N] int32"""
+        L, h, st = nat.lib(), self.env._h, self.env._stream()
+        bf16 = int(self.net_dtype == torch.bfloat16)
+        q = self._params(n)
+        self.sync_net()
+        rows = torch.empty((self.D * n, ROW), dtype=self.net_dtype, device=self.env.device)
+        nat.check(L.sn_puct_root_rows(h, ctypes_ref(q), nat.ptr(rows), bf16, st), "sn_puct_root_rows")
+        with torch.no_grad():
+            (heads,) = self._net(rows)
+        self.rows_evaluated += rows.shape[0]
+        heads = heads.float().contiguous()
+        nat.check(L.sn_pcv_choose(h, ctypes_ref(q), nat.ptr(heads), nat.ptr(self.actions), nat.ptr(self.best_index),
+                                  nat.ptr(self.log_prob), nat.ptr(self.value), st), "sn_pcv_choose")
+        if record:
+            self.decisions.append((rows.float(), n, self.best_index.clone()))
+        self.step_id += 1
+        return self.actions
+
+    def play_episode(self, others=None, record=False):
+        """one whole game of every env game; returns (summed rewards [B, N]
+        int32, per-step rewards [10, B, N] int32)"""
+        env = self.env
+        env.reset()
+        per_step = torch.zeros((10, env.num_games, env.num_players), dtype=torch.int32, device=env.device)
+        for t in range(10):
+            acts = self.decide(10 - t, record=record)
+            if self.M < env.num_players:
+                keep = torch.tensor([(self.seats_mask >> p) & 1 for p in range(env.num_players)], device=env.device,
+                                    dtype=torch.bool)
+                acts = torch.where(keep[None, :], acts, self._random_moves())
+            rew, done, inv = env.step(acts)
+            per_step[t] = rew
+        self.episode_rewards = per_step
+        return per_step.sum(dim=0), per_step
+
+    def _decider_rewards(self, per_step):
+        seats = [p for p in range(self.env.num_players) if (self.seats_mask >> p) & 1]
+        return per_step[:, :, seats].reshape(per_step.shape[0], -1)  # [10, D] in decision order
+
+    def loss(self, per_step=None):
+        """reference loss of the recorded episode (mcts.py:431-451), summed over games"""
+        per_step = self.episode_rewards if per_step is None else per_step
+        dev_actor = self.actor.to(self.env.device)
+        target = self._decider_rewards(per_step)[:-1].sum(dim=0).float()  # [D]
+        logps, values = [], []
+        for rows, n, best in self.decisions:
+            (out,) = dev_actor(rows)
+            out = out.reshape(-1, n, 2)
+            logp = torch.log_softmax(out[:, :, 0], dim=1)
+            logps.append(logp.gather(1, best.long()[:, None])[:, 0])
+            values.append(out[:, :, 1].gather(1, best.long()[:, None])[:, 0])
+        logps, values = torch.stack(logps, dim=1), torch.stack(values, dim=1)  # [D, steps]
+        outcome_loss = ((values - target[:, None]) ** 2).mean(dim=1)
+        policy_loss = -logps.sum(dim=1)
+        return (outcome_loss + policy_loss).sum()
+
+
 def ctypes_ref(q):
     import ctypes
 

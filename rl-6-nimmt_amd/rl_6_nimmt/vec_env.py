@@ -184,6 +184,17 @@ class VecSechsNimmtEnv:
         if chunk_steps is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_CHUNK_STEPS, int(chunk_steps)), "sn_set_option")
 
+    def time_kernels(self, launches):
+        """record HIP events around the next `launches` pipelined k_play /
+        k_mt_ahead launches, each on its own stream (0 = off)"""
+        nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_TIMING, int(launches)), "sn_set_option")
+
+    def kernel_times(self):
+        """(mean k_play ms, mean k_mt_ahead ms, launches recorded) [sync]"""
+        a, b, n = ctypes.c_float(), ctypes.c_float(), ctypes.c_int32()
+        nat.check(nat.lib().sn_kernel_times(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)), "sn_kernel_times")
+        return a.value, b.value, n.value
+
     def pipe_errors(self):
         """draws of pipelined rollouts that ran past the twisted words (must be 0) [sync]"""
         c = ctypes.c_uint32()

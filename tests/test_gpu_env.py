@@ -352,6 +352,31 @@ def test_ring_option_validation():
         penv.set_option(ring_words=256)
 
 
+def test_kernel_timing_is_observational():
+    """SN_OPT_TIMING only records events: rollouts stay bit-exact with the
+    oracle, every timed launch is counted (capped at the requested number)
+    and both kernels report a positive duration."""
+    B, N, seed = 500, 4, 9
+    env = venv(B, N, seed=seed, rng="numpy")
+    env.reset()
+    ref = O.VecOracle(B, N, rng_mode=O.RNG_NUMPY_MT, seed=seed)
+    ref.reset()
+    env.time_kernels(3)
+    for T in (10, 10, 10, 10):
+        out = env.rollout(T, want_actions=True)
+        rr, rd, ra, _ = ref.rollout(T)
+        torch.cuda.synchronize()
+        assert np.array_equal(out["actions"].cpu().numpy(), ra)
+        assert np.array_equal(out["rewards"].cpu().numpy(), rr)
+    play_ms, ahead_ms, n = env.kernel_times()
+    assert n == 3 and play_ms > 0 and ahead_ms > 0
+    env.time_kernels(0)
+    assert env.kernel_times()[2] == 0
+    with pytest.raises(ValueError):
+        env.time_kernels(-1)
+    assert env.pipe_errors() == 0
+
+
 def test_pipeline_then_other_paths_interleave():
     """The pipelined twist-ahead state (ring, a k_mt_ahead in flight) is
     folded back into the MT state whenever anything else touches the stream

@@ -27,6 +27,12 @@ Fixture families (SURVEY.md §4 "What the build must add"):
   F6 normalization.json  SechsNimmtStateNormalization vectors
   F7 positions.json      Tournament._compute_relative/absolute_positions vectors
   F8 puct_policy.npz     PUCTAgent policy-net weights + _compute_policy outputs
+  F9 customed_games.json seeded GameSession(PUCTCustomedAgent, DrunkHamster...)
+     customed_weights.npz  training games: actions, log-probs, value outcomes,
+                           losses, and the 2-head net before / after each game
+  F10 reinforce_games.json seeded GameSession(BatchedReinforceAgent, ...)
+      reinforce_weights.npz  training games: actions, log-probs, entropies,
+                           losses, final weights
 """
 import argparse
 import json
@@ -542,6 +548,116 @@ def gen_puct(ref, out):
 
 
 # ----------------------------------------------------------------------------
+# F9: PUCTCustomedAgent (policy + value head, no rollouts) in training sessions
+# ----------------------------------------------------------------------------
+def gen_customed(ref, out):
+    import torch
+    from rl_6_nimmt.agents import DrunkHamster, PUCTCustomedAgent
+    from rl_6_nimmt.play import GameSession
+
+    specs = [("CRRR", s, 2) for s in range(4)] + [("CR", 7, 2), ("RCR", 11, 1), ("CC", 5, 2)]
+    sessions, arrays = [], {}
+    for si, (seats, seed, n_games) in enumerate(specs):
+        torch.manual_seed(seed)
+        agents = [PUCTCustomedAgent(mc_max=200) if ch == "C" else DrunkHamster() for ch in seats]
+        for a, ch in zip(agents, seats):
+            if ch == "C":
+                a.train()
+        trace = {i: {"info": [], "loss": []} for i, ch in enumerate(seats) if ch == "C"}
+        for i in trace:
+            ag = agents[i]
+            for k, v in ag.actor.state_dict().items():
+                arrays[f"s{si}_a{i}_init_{k}"] = v.detach().numpy().astype(np.float32)
+            fwd, lrn = ag.forward, ag.learn
+
+            def fwd_rec(state, legal_actions, *a, _fwd=fwd, _i=i, **k):
+                act, info = _fwd(state, legal_actions, *a, **k)
+                trace[_i]["info"].append([int(act), float(info["log_prob"]), float(info["outcome"])])
+                return act, info
+
+            def lrn_rec(*a, _lrn=lrn, _i=i, **k):
+                loss = _lrn(*a, **k)
+                if k.get("episode_end"):
+                    trace[_i]["loss"].append(float(loss))
+                return loss
+
+            ag.forward, ag.learn = fwd_rec, lrn_rec
+        np.random.seed(seed)
+        sess = GameSession(*agents)
+        for _ in range(n_games):
+            sess.play_game()
+        for i in trace:
+            for k, v in agents[i].actor.state_dict().items():
+                arrays[f"s{si}_a{i}_final_{k}"] = v.detach().numpy().astype(np.float32)
+        sessions.append({"seats": seats, "seed": seed, "games": n_games,
+                         "results": [[int(x) for x in r] for r in sess.results],
+                         "trace": {str(i): t for i, t in trace.items()}})
+    np.savez_compressed(os.path.join(out, "customed_weights.npz"), **arrays)
+    with open(os.path.join(out, "customed_games.json"), "w") as f:
+        json.dump({"protocol": "torch.manual_seed(seed); agents (C = PUCTCustomedAgent(mc_max=200) in train mode, "
+                               "R = DrunkHamster); np.random.seed(seed); GameSession(*agents).play_game() x games. "
+                               "trace[seat].info = per forward [action, log_prob, outcome]; loss = learn() at episode end",
+                   "sessions": sessions}, f)
+
+
+# ----------------------------------------------------------------------------
+# F10: BatchedReinforceAgent (REINFORCE) in training sessions
+# ----------------------------------------------------------------------------
+def gen_reinforce(ref, out):
+    import torch
+    from rl_6_nimmt.agents import BatchedReinforceAgent, DrunkHamster
+    from rl_6_nimmt.play import GameSession
+
+    specs = [("PRRR", 0, 3, {}), ("PR", 4, 2, {"r_factor": 0.1, "entropy_weight": 0.05}),
+             ("PP", 9, 2, {"gamma": 0.9}), ("RPRRP", 2, 1, {})]
+    sessions, arrays = [], {}
+    for si, (seats, seed, n_games, kw) in enumerate(specs):
+        torch.manual_seed(seed)
+        agents = [BatchedReinforceAgent(**kw) if ch == "P" else DrunkHamster() for ch in seats]
+        trace = {}
+        for i, ch in enumerate(seats):
+            if ch != "P":
+                continue
+            ag = agents[i]
+            ag.train()
+            if si == 0:
+                for k, v in ag.actor.state_dict().items():
+                    arrays[f"s{si}_a{i}_init_{k}"] = v.detach().numpy().astype(np.float32)
+            trace[i] = {"info": [], "loss": []}
+            fwd, lrn = ag.forward, ag.learn
+
+            def fwd_rec(state, legal_actions, *a, _fwd=fwd, _i=i, **k):
+                act, info = _fwd(state, legal_actions, *a, **k)
+                trace[_i]["info"].append([int(act), float(info["log_prob"]), float(info["entropy"])])
+                return act, info
+
+            def lrn_rec(*a, _lrn=lrn, _i=i, **k):
+                losses = _lrn(*a, **k)
+                if k.get("episode_end"):
+                    trace[_i]["loss"].append([float(x) for x in losses])
+                return losses
+
+            ag.forward, ag.learn = fwd_rec, lrn_rec
+        np.random.seed(seed)
+        sess = GameSession(*agents)
+        for _ in range(n_games):
+            sess.play_game()
+        for i in trace:
+            for k, v in agents[i].actor.state_dict().items():
+                arrays[f"s{si}_a{i}_final_{k}"] = v.detach().numpy().astype(np.float32)
+        sessions.append({"seats": seats, "seed": seed, "games": n_games, "kwargs": kw,
+                         "results": [[int(x) for x in r] for r in sess.results],
+                         "trace": {str(i): t for i, t in trace.items()}})
+    np.savez_compressed(os.path.join(out, "reinforce_weights.npz"), **arrays)
+    with open(os.path.join(out, "reinforce_games.json"), "w") as f:
+        json.dump({"protocol": "torch.manual_seed(seed); agents (P = BatchedReinforceAgent(**kwargs) in train mode, "
+                               "R = DrunkHamster); np.random.seed(seed); GameSession(*agents).play_game() x games. "
+                               "trace[seat].info = per forward [action, log_prob, entropy]; loss = learn() at "
+                               "episode end ([actor, 0, entropy])",
+                   "sessions": sessions}, f)
+
+
+# ----------------------------------------------------------------------------
 # F7: tournament positions
 # ----------------------------------------------------------------------------
 def gen_positions(ref, out):
@@ -576,6 +692,8 @@ def main():
         ("puct", gen_puct),
         ("positions", gen_positions),
         ("mcs", gen_mcs),
+        ("customed", gen_customed),
+        ("reinforce", gen_reinforce),
     ]
     for name, fn in steps:
         if args.only and name not in args.only.split(","):

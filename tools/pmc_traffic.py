@@ -34,6 +34,8 @@ def main():
     for k in kernels.split("|"):
         f = per_dispatch(fetch_csv, k, "FETCH_SIZE")
         w = per_dispatch(write_csv, k, "WRITE_SIZE")
+        if not f or not w:  # a kernel this path does not launch
+            continue
         f_kb, w_kb = sum(f) / len(f), sum(w) / len(w)
         b = 2.0 * f_kb * 1024.0 + w_kb * 1024.0
         rec["kernels"][k] = {"dispatches": {"fetch": len(f), "write": len(w)}, "fetch_size_kb_raw": f_kb,
