@@ -60,6 +60,7 @@ def parse():
     ap.add_argument("--games", type=int, default=65536, help="games per GPU")
     ap.add_argument("--rng", default="numpy", choices=["numpy", "philox"])
     ap.add_argument("--no-obs", action="store_true", help="do not emit observations (not the headline)")
+    ap.add_argument("--pipe-gpw", type=int, default=64, choices=[32, 64], help="games per k_play wave (pipelined path)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--extras", action="store_true", help="also time the philox mode and the per-step API")
@@ -290,6 +291,8 @@ def main():
 
     B = args.games
     env = VecSechsNimmtEnv(B, N_PLAYERS, seed=0, game_offset=rank * B, rng=args.rng)
+    if args.rng == "numpy":
+        env.set_option(pipe_gpw=args.pipe_gpw)
     env.reset()
     out = make_out(env, B, not args.no_obs)
     wall, kern_ms, kt = time_rollouts(env, out, args.steps, args.warmup, world)

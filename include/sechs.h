@@ -141,8 +141,11 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
      SN_OPT_TIMING       n > 0: record HIP events around the next n
                          pipelined k_play / k_mt_ahead launches, each on the
                          stream it runs on (read with sn_kernel_times);
-                         0 (default): off. */
-enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3, SN_OPT_TIMING = 4 };
+                         0 (default): off.
+     SN_OPT_PIPE_GPW     games per k_play wave on the pipelined path: 64
+                         (one per lane) or 32 (half the LDS per wave, two
+                         waves per SIMD). */
+enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3, SN_OPT_TIMING = 4, SN_OPT_PIPE_GPW = 5 };
 sn_status sn_set_option(sn_env* env, int option, int value);
 /* pipelined rollouts whose draws ran past the twisted words (must be 0; a
    nonzero count means those games' draws are wrong) [sync] */

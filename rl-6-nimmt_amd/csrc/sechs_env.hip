@@ -356,14 +356,14 @@ struct PlayArgs {
 // are assembled so that they leave as 1-KB contiguous stores instead of 64
 // scattered 16-B pieces per instruction.  (Both uses never overlap in time
 // within a step: observations first, the deal at the very end.)
-template <int N, class R>
+template <int N, class R, int GPW = 64>
 __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a, int64_t g, int lane, uint8_t* wave_lds,
                                            Game<N>& G, R& rng, ByteBuf& buf, int32_t (&sum_res)[N], int32_t& episodes) {
     const int64_t B = s.B;
     uint8_t* my_deck = wave_lds + lane * kDeckStride;
     const bool staged = a.obs && a.obs_stride == 48;
     const int64_t g0 = g - lane;                           // first game of this wave
-    const int wave_games = (int)min((int64_t)64, B - g0);  // = active lanes (lanes past B left)
+    const int wave_games = (int)min((int64_t)GPW, B - g0);  // = active lanes (lanes past B left)
     const bool auto_reset = (a.flags & SN_AUTO_RESET) != 0;
     const bool summ = !(a.flags & SN_NO_SUMMARIES);
     int32_t* rew = a.rewards ? a.rewards + g * N : nullptr;
@@ -387,12 +387,12 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 const u32x4* src = (const u32x4*)wave_lds;
                 u32x4* dst = (u32x4*)(a.obs + ((int64_t)t * B + g0) * N * 48);
-                if (wave_games == 64) {  // all reads, one wait, all stores
+                if (wave_games == GPW) {  // all reads, one wait, all stores
                     u32x4 pc[3 * N];
 #pragma unroll
-                    for (int j = 0; j < 3 * N; j++) pc[j] = src[lane + 64 * j];
+                    for (int j = 0; j < 3 * N; j++) pc[j] = src[lane + GPW * j];
 #pragma unroll
-                    for (int j = 0; j < 3 * N; j++) dst[lane + 64 * j] = pc[j];
+                    for (int j = 0; j < 3 * N; j++) dst[lane + GPW * j] = pc[j];
                 } else {
                     const int pieces = wave_games * N * 3;
                     for (int i = lane; i < pieces; i += wave_games) dst[i] = src[i];
@@ -500,12 +500,16 @@ __device__ __forceinline__ void store_results(const DevState& s, int64_t g, int 
     }
 }
 
-template <int N, int MODE>
+// GPW = games per wave: 64 (one game per lane), or 32 for the pipelined
+// path (lanes 32..63 idle) -- half the LDS per wave, so two blocks fit a CU
+// and a SIMD holds two waves to hide each other's latency
+template <int N, int MODE, int GPW = 64>
 __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= s.B) return;
     const int lane = threadIdx.x & 63;
+    if (GPW < 64 && lane >= GPW) return;
+    const int64_t g = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * GPW + lane;
+    if (g >= s.B) return;
     uint8_t* wave_lds = lds_dyn + (threadIdx.x >> 6) * a.wave_lds;
     Game<N> G;
     load_game<N>(s, g, G);
@@ -514,8 +518,8 @@ __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
     ByteBuf buf;
     if constexpr (MODE == RNG_NUMPY_PIPE) {
         RingPipe rng;
-        rng.load(s, g, buf, wave_lds + a.wave_lds - 64 * a.ring_lds + lane * a.ring_lds, a.pipe_cin, a.pipe_t);
-        play_steps<N>(s, a, g, lane, wave_lds, G, rng, buf, sum_res, episodes);
+        rng.load(s, g, buf, wave_lds + a.wave_lds - GPW * a.ring_lds + lane * a.ring_lds, a.pipe_cin, a.pipe_t);
+        play_steps<N, RingPipe, GPW>(s, a, g, lane, wave_lds, G, rng, buf, sum_res, episodes);
         s.pabsc[(int64_t)a.pipe_cout * s.B + g] = rng.consumed(buf);
     } else {
         typename RngOf<MODE, kPlayPrefetch>::T rng;
@@ -655,6 +659,7 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
     }
     e->chunk_steps = 10;
     e->pipe = 1;
+    e->pipe_gpw = 64;
     e->pvalid = 0;
     e->pcount = 0;
     if (rng_mode == SN_RNG_NUMPY_MT) {
@@ -749,6 +754,10 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
         case SN_OPT_PIPELINE:
             if (value != 0 && value != 1) return fail(SN_EINVAL, "pipeline must be 0 or 1");
             e->pipe = value;
+            return SN_OK;
+        case SN_OPT_PIPE_GPW:
+            if (value != 32 && value != 64) return fail(SN_EINVAL, "games per wave must be 32 or 64");
+            e->pipe_gpw = value;
             return SN_OK;
         case SN_OPT_TIMING:
             if (value < 0 || value > 4096) return fail(SN_EINVAL, "timing launches must be in 0..4096");
@@ -874,10 +883,10 @@ sn_status sn_pipe_sync(sn_env* e, hipStream_t st) {
 }
 
 // LDS a pipelined k_play block needs (obs staging / deck + the RingPipe windows)
-static size_t pipe_lds(const DevState& s, const PlayArgs& a, int* wave_out) {
-    int wave = 64 * kDeckStride;
-    if (a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15) == 0) wave = max(wave, 64 * s.N * 48);
-    wave += 64 * kPipeSlot;
+static size_t pipe_lds(const DevState& s, const PlayArgs& a, int gpw, int* wave_out) {
+    int wave = gpw * kDeckStride;
+    if (a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15) == 0) wave = max(wave, gpw * s.N * 48);
+    wave += gpw * kPipeSlot;
     *wave_out = wave;
     return (size_t)wave * (kBlock / 64);
 }
@@ -888,7 +897,8 @@ static size_t pipe_lds(const DevState& s, const PlayArgs& a, int* wave_out) {
 static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     DevState& s = e->s;
     int wave;
-    const size_t shmem = pipe_lds(s, a, &wave);
+    const int gpw = e->pipe_gpw;
+    const size_t shmem = pipe_lds(s, a, gpw, &wave);
     a.wave_lds = wave;
     a.ring_lds = kPipeSlot;
     a.vec_out = ((((uintptr_t)a.rewards) & 15) == 0) && ((((uintptr_t)a.actions_out) & 3) == 0);
@@ -916,9 +926,16 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
         if (tv) HIP_TRY(hipEventRecord(tv[0], st));
         SN_DISPATCH_N(s.N, {
-            HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_PIPE>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
-            hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_PIPE>), dim3(grid_for(s.B)), dim3(kBlock), shmem, st, s, c);
+            if (gpw == 32) {
+                HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_PIPE, 32>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
+                hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_PIPE, 32>), dim3((unsigned)((s.B + 32 * (kBlock / 64) - 1) / (32 * (kBlock / 64)))),
+                                   dim3(kBlock), shmem, st, s, c);
+            } else {
+                HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_PIPE>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
+                hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_PIPE>), dim3(grid_for(s.B)), dim3(kBlock), shmem, st, s, c);
+            }
         });
         HIP_TRY(hipGetLastError());
         if (tv) HIP_TRY(hipEventRecord(tv[1], st));
@@ -938,7 +955,7 @@ static sn_status launch_play(sn_env* e, PlayArgs a, hipStream_t st) {
     const DevState& s = e->s;
     if (s.rng_mode == SN_RNG_NUMPY_MT && !a.actions && e->pipe) {
         int wave;
-        if (pipe_lds(s, a, &wave) <= (size_t)kLdsBytes) return launch_pipe(e, a, st);
+        if (pipe_lds(s, a, e->pipe_gpw, &wave) <= (size_t)kLdsBytes) return launch_pipe(e, a, st);
     }
     {
         const sn_status r = sn_pipe_sync(e, st);

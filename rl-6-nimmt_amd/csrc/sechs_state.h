@@ -585,6 +585,7 @@ struct sn_env {
     int device;
     int chunk_steps;  // SN_OPT_CHUNK_STEPS
     int pipe;         // SN_OPT_PIPELINE
+    int pipe_gpw;     // SN_OPT_PIPE_GPW: games per k_play wave on the pipelined path (32 or 64)
     sechs::DevState s;
     // pipelined twist-ahead (sechs_env.hip launch_pipe): a k_mt_ahead for the
     // next play launch may be in flight on `side` (ev_prep) after a rollout

@@ -175,8 +175,10 @@ class VecSechsNimmtEnv:
         nat.check(nat.lib().sn_clear_results(self._h, self._stream()), "sn_clear_results")
 
     # ------------------------------------------------------------ numpy RNG bridge
-    def set_option(self, ring_words=None, chunk_steps=None, pipeline=None):
+    def set_option(self, ring_words=None, chunk_steps=None, pipeline=None, pipe_gpw=None):
         """numpy-compat rollout tuning (include/sechs.h SN_OPT_*); results never depend on it"""
+        if pipe_gpw is not None:
+            nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPE_GPW, int(pipe_gpw)), "sn_set_option")
         if pipeline is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPELINE, int(bool(pipeline))), "sn_set_option")
         if ring_words is not None:

@@ -310,10 +310,12 @@ def test_mt_state_across_round_boundaries_every_step():
             assert p == rp and np.array_equal(k, rk), (t, g)
 
 
-@pytest.mark.parametrize("ring_words,chunk_steps,pipeline", [(0, 10, 0), (64, 10, 0), (64, 1, 0), (128, 3, 0),
-                                                              (512, 25, 0), (256, 7, 0), (256, 10, 1), (256, 3, 1),
-                                                              (0, 1, 1), (512, 25, 1)])
-def test_ring_options_do_not_change_results(ring_words, chunk_steps, pipeline):
+@pytest.mark.parametrize("ring_words,chunk_steps,pipeline,gpw", [(0, 10, 0, 64), (64, 10, 0, 64), (64, 1, 0, 64),
+                                                                  (128, 3, 0, 64), (512, 25, 0, 64), (256, 7, 0, 64),
+                                                                  (256, 10, 1, 64), (256, 3, 1, 64), (0, 1, 1, 64),
+                                                                  (512, 25, 1, 64), (256, 10, 1, 32), (0, 3, 1, 32),
+                                                                  (0, 25, 1, 32)])
+def test_ring_options_do_not_change_results(ring_words, chunk_steps, pipeline, gpw):
     """The twist-ahead paths are optimisations only: every ring size (0 =
     lazy per-lane MT19937; 64 runs k_mt_prep's ring dry inside every
     episode, so the slow path continues mid-launch), launch chunking, and
@@ -321,7 +323,7 @@ def test_ring_options_do_not_change_results(ring_words, chunk_steps, pipeline):
     oracle's actions, rewards, obs and final numpy MT states."""
     B, N, T, seed = 300, 4, 37, 21
     env = venv(B, N, seed=seed, rng="numpy")
-    env.set_option(ring_words=ring_words, chunk_steps=chunk_steps, pipeline=pipeline)
+    env.set_option(ring_words=ring_words, chunk_steps=chunk_steps, pipeline=pipeline, pipe_gpw=gpw)
     env.reset()
     ref = O.VecOracle(B, N, rng_mode=O.RNG_NUMPY_MT, seed=seed)
     ref.reset()
