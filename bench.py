@@ -162,6 +162,18 @@ def cpu_baseline(budget_s, rng):
         v.rollout(STEPS_PER_LAUNCH, want_obs=True, want_actions=True, nthreads=1)
     dt = time.perf_counter() - t
     steps = games * episodes * STEPS_PER_LAUNCH
+    # the same restatement with OpenMP over this job's CPU share (16 threads
+    # on the GPU box), ~3 s on the full 65 536 games
+    threads = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    vm = O.VecOracle(65536, N_PLAYERS, rng_mode=mode, seed=0)
+    vm.reset()
+    vm.rollout(STEPS_PER_LAUNCH, want_obs=True, want_actions=True, nthreads=threads)  # first touch of the outputs
+    t = time.perf_counter()
+    eps_mt = 0
+    while eps_mt == 0 or time.perf_counter() - t < 3.0:
+        vm.rollout(STEPS_PER_LAUNCH, want_obs=True, want_actions=True, nthreads=threads)
+        eps_mt += 1
+    dt_mt = time.perf_counter() - t
     return {
         "value": steps / dt,
         "unit": "env-steps/s",
@@ -170,6 +182,8 @@ def cpu_baseline(budget_s, rng):
         "sample": f"{games} games x {episodes} episodes x 10 env-steps ({steps} env-steps, {dt:.1f} s) of the same "
                   f"workload (DrunkHamster self-play, {rng} RNG, int8 obs + actions + rewards written) on the "
                   f"oracle's single-threaded C restatement of env.py",
+        "multi_thread": {"value": 65536 * eps_mt * STEPS_PER_LAUNCH / dt_mt, "cores": threads,
+                         "sample": f"65536 games x {eps_mt} episodes, OpenMP"},
     }
 
 
