@@ -228,6 +228,23 @@ __global__ __launch_bounds__(kBlock) void k_mt_prep(DevState s) {
 // INIT: start from the MtGen state code (re-temper its twisted-unconsumed
 // words into the ring first).
 // ============================================================================
+#ifndef SECHS_NT_OBS
+#define SECHS_NT_OBS 1
+#endif
+#ifndef SECHS_NT_MORE
+#define SECHS_NT_MORE 1
+#endif
+// streaming (non-temporal) stores for what no later kernel finds in L2
+// anyway (the 155 MB of trajectory outputs and the MT words / ring bytes a
+// launch writes): measured 5.77 -> 6.4 G env-steps/s.  Non-temporal LOADS
+// of the MT state were measured slower (5.5 G/s: consecutive lanes share
+// lines through L2), so loads stay normal.
+template <class T>
+__device__ __forceinline__ void st_nt(T* p, T v, bool nt) {
+    if (nt) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 struct AheadArgs {
     int cin;   // pabsc parity holding the consumer position to lead (INIT: written)
     int tin;   // ptend parity of the previous prep (steady)
@@ -272,7 +289,7 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
         const uint32_t y = mt_temper(v) & 0xFFu;
         const uint32_t d = y | (__shfl_down(y, 1) << 8) | (__shfl_down(y, 2) << 16) | (__shfl_down(y, 3) << 24);
         const uint32_t ri = (t0 + j) & (uint32_t)(kPipeRing - 1);
-        if ((lane & 3u) == 0u && j < n) *(uint32_t*)(ring + ((int64_t)(ri >> 4) * B + g) * 16 + (ri & 12u)) = d;
+        if ((lane & 3u) == 0u && j < n) st_nt((uint32_t*)(ring + ((int64_t)(ri >> 4) * B + g) * 16 + (ri & 12u)), d, SECHS_NT_MORE);
     };
     // phase 1: words 0 .. min(n, 224)
     uint32_t A[4], Bv[4], Cv[4], IX[4];
@@ -295,7 +312,7 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
         uint32_t v = 0u;
         if (IX[b] != 0xFFFFu) {
             v = mt_mix(A[b], Bv[b], Cv[b]);
-            st[IX[b]] = v;
+            st_nt(&st[IX[b]], v, SECHS_NT_MORE);
             if (IX[b] == 0u) s.mt0[g] = A[b];
         }
         ring_dword(j, v);
@@ -392,7 +409,10 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
 #pragma unroll
                     for (int j = 0; j < 3 * N; j++) pc[j] = src[lane + GPW * j];
 #pragma unroll
-                    for (int j = 0; j < 3 * N; j++) dst[lane + GPW * j] = pc[j];
+                    for (int j = 0; j < 3 * N; j++) {
+                        if (SECHS_NT_OBS) __builtin_nontemporal_store(pc[j], &dst[lane + GPW * j]);
+                        else dst[lane + GPW * j] = pc[j];
+                    }
                 } else {
                     const int pieces = wave_games * N * 3;
                     for (int i = lane; i < pieces; i += wave_games) dst[i] = src[i];
@@ -447,7 +467,7 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
         const bool done = (G.n == 0u);  // env.py:246-249
         if (rew) {
             if (N == 4 && a.vec_out) {  // one 16-B store per lane: 1 KB contiguous per wave
-                *(u32x4*)rew = u32x4{-pen[0], -pen[1 % N], -pen[2 % N], -pen[3 % N]};
+                st_nt((u32x4*)rew, u32x4{-pen[0], -pen[1 % N], -pen[2 % N], -pen[3 % N]}, SECHS_NT_MORE);
             } else {
 #pragma unroll
                 for (int p = 0; p < N; p++) rew[p] = -(int32_t)pen[p];
@@ -456,7 +476,8 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
         }
         if (act) {
             if (N == 4 && a.vec_out) {
-                *(uint32_t*)act = card[0] | (card[1 % N] << 8) | (card[2 % N] << 16) | (card[3 % N] << 24);
+                st_nt((uint32_t*)act, (uint32_t)(card[0] | (card[1 % N] << 8) | (card[2 % N] << 16) | (card[3 % N] << 24)),
+                      SECHS_NT_MORE);
             } else {
 #pragma unroll
                 for (int p = 0; p < N; p++) act[p] = (uint8_t)card[p];
