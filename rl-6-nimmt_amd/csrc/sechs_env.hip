@@ -389,17 +389,16 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
     int8_t* ob = a.obs ? a.obs + g * N * a.obs_stride : nullptr;
     for (int t = 0; t < a.steps; t++) {
         if (ob) {
-            uint32_t w2hi, gw[9];
-            if (summ) game_words<true>(N, G.b, w2hi, gw);
-            else game_words<false>(N, G.b, w2hi, gw);
+            uint32_t w2hi;
+            const GameWords gw = summ ? game_words<true>(N, G.b, w2hi) : game_words<false>(N, G.b, w2hi);
             if (staged) {
                 u32x4* row = (u32x4*)(wave_lds + lane * N * 48);
 #pragma unroll
                 for (int p = 0; p < N; p++) {
                     const Hand& h = G.hand[p];
-                    row[3 * p + 0] = u32x4{(uint32_t)h.lo, (uint32_t)(h.lo >> 32), (h.hi & 0xFFFFu) | w2hi, gw[0]};
-                    row[3 * p + 1] = u32x4{gw[1], gw[2], gw[3], gw[4]};
-                    row[3 * p + 2] = u32x4{gw[5], gw[6], gw[7], gw[8]};
+                    row[3 * p + 0] = u32x4{(uint32_t)h.lo, (uint32_t)(h.lo >> 32), (h.hi & 0xFFFFu) | w2hi, gw.w0};
+                    row[3 * p + 1] = gw.a;
+                    row[3 * p + 2] = gw.b;
                 }
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 const u32x4* src = (const u32x4*)wave_lds;
@@ -569,9 +568,9 @@ __global__ void k_obs(DevState s, T* out, int stride, int summ) {
     const int p = (int)(i - g * s.N);
     const Hand h = load_hand(s, p, g);
     const Board b = load_board(s, g);
-    uint32_t w2hi, gw[9];
-    if (summ) game_words<true>(s.N, b, w2hi, gw);
-    else game_words<false>(s.N, b, w2hi, gw);
+    uint32_t w2hi;
+    const GameWords gwv = summ ? game_words<true>(s.N, b, w2hi) : game_words<false>(s.N, b, w2hi);
+    const uint32_t gw[9] = {gwv.w0, gwv.a.x, gwv.a.y, gwv.a.z, gwv.a.w, gwv.b.x, gwv.b.y, gwv.b.z, gwv.b.w};
     const uint32_t all[12] = {(uint32_t)h.lo, (uint32_t)(h.lo >> 32), (h.hi & 0xFFFFu) | w2hi,
                               gw[0], gw[1], gw[2], gw[3], gw[4], gw[5], gw[6], gw[7], gw[8]};
     T* dst = out + i * stride;

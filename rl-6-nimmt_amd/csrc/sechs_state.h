@@ -493,8 +493,12 @@ __device__ __forceinline__ void deal_shuffle(R& rng, ByteBuf& buf, uint8_t* deck
 // env.py:188-212.  A seat's 48-byte row = [hand asc, -1 pad to 10][N]
 // [lens][ends][heads][4x6 board, -1 pad][0 pad]; bytes 0..9 are the seat's
 // hand bytes, bytes 10..47 are the same for every seat (game words).
+struct GameWords {  // obs bytes 10..47 as words: w0 (bytes 12..15), a (16..31), b (32..47)
+    uint32_t w0;
+    u32x4 a, b;
+};
 template <bool SUMM>
-__device__ __forceinline__ void game_words(int N, const Board& b, uint32_t& w2hi, uint32_t (&w)[9]) {
+__device__ __forceinline__ GameWords game_words(int N, const Board& b, uint32_t& w2hi) {
     // Built a row at a time as 6-byte groups (no per-byte selects): row r =
     // its packed cards 0..3 with the bytes past len forced to 0xFF (-1), card
     // 4 or 0xFF, then 0xFF; the four groups form the 24 board bytes X.
@@ -516,35 +520,35 @@ __device__ __forceinline__ void game_words(int N, const Board& b, uint32_t& w2hi
         const uint32_t H = ((hi[0] >> 16) & 0xFFu) | ((hi[1] >> 8) & 0xFF00u) | (hi[2] & 0xFF0000u) | ((hi[3] << 8) & 0xFF000000u);
         const uint32_t E = (hi[0] >> 24) | ((hi[1] >> 16) & 0xFF00u) | ((hi[2] >> 8) & 0xFF0000u) | (hi[3] & 0xFF000000u);
         w2hi = (nb << 16) | (L << 24);
-        w[0] = (L >> 8) | (E << 24);
-        w[1] = (E >> 8) | (H << 24);
-        w[2] = (H >> 8) | ((uint32_t)X0 << 24);
-        w[3] = (uint32_t)Y0, w[4] = (uint32_t)(Y0 >> 32);
-        w[5] = (uint32_t)Y1, w[6] = (uint32_t)(Y1 >> 32);
-        w[7] = (uint32_t)Y2, w[8] = (uint32_t)(Y2 >> 32);
+        GameWords r;
+        r.w0 = (L >> 8) | (E << 24);
+        r.a = u32x4{(E >> 8) | (H << 24), (H >> 8) | ((uint32_t)X0 << 24), (uint32_t)Y0, (uint32_t)(Y0 >> 32)};
+        r.b = u32x4{(uint32_t)Y1, (uint32_t)(Y1 >> 32), (uint32_t)Y2, (uint32_t)(Y2 >> 32)};
+        return r;
     } else {  // [10] N, [11..34] X, zeros
         w2hi = (nb << 16) | ((uint32_t)X0 << 24);
-        w[0] = (uint32_t)Y0, w[1] = (uint32_t)(Y0 >> 32);
-        w[2] = (uint32_t)Y1, w[3] = (uint32_t)(Y1 >> 32);
-        w[4] = (uint32_t)Y2, w[5] = (uint32_t)(Y2 >> 32);
-        w[6] = w[7] = w[8] = 0u;
+        GameWords r;
+        r.w0 = (uint32_t)Y0;
+        r.a = u32x4{(uint32_t)(Y0 >> 32), (uint32_t)Y1, (uint32_t)(Y1 >> 32), (uint32_t)Y2};
+        r.b = u32x4{(uint32_t)(Y2 >> 32), 0u, 0u, 0u};
+        return r;
     }
 }
 
 // one seat's obs row of `stride` bytes (stride % 4 == 0, >= L)
-__device__ __forceinline__ void store_obs_row(int8_t* dst, const Hand& h, uint32_t w2hi, const uint32_t (&gw)[9],
+__device__ __forceinline__ void store_obs_row(int8_t* dst, const Hand& h, uint32_t w2hi, const GameWords& gw,
                                               int stride) {
     const uint32_t w0 = (uint32_t)h.lo, w1 = (uint32_t)(h.lo >> 32), w2 = (h.hi & 0xFFFFu) | w2hi;
     if ((stride & 15) == 0 && (((uintptr_t)dst) & 15) == 0) {  // stride >= 48 here
         u32x4* d = (u32x4*)dst;
-        d[0] = u32x4{w0, w1, w2, gw[0]};
-        d[1] = u32x4{gw[1], gw[2], gw[3], gw[4]};
-        d[2] = u32x4{gw[5], gw[6], gw[7], gw[8]};
+        d[0] = u32x4{w0, w1, w2, gw.w0};
+        d[1] = gw.a;
+        d[2] = gw.b;
         for (int i = 3; i < (stride >> 4); i++) d[i] = u32x4{0u, 0u, 0u, 0u};
     } else {
         uint32_t* d = (uint32_t*)dst;
         const int nw = stride >> 2;
-        const uint32_t all[12] = {w0, w1, w2, gw[0], gw[1], gw[2], gw[3], gw[4], gw[5], gw[6], gw[7], gw[8]};
+        const uint32_t all[12] = {w0, w1, w2, gw.w0, gw.a.x, gw.a.y, gw.a.z, gw.a.w, gw.b.x, gw.b.y, gw.b.z, gw.b.w};
 #pragma unroll
         for (int i = 0; i < 12; i++)
             if (i < nw) d[i] = all[i];
