@@ -161,3 +161,45 @@ def test_puct_formulas_golden():
         ref = [np.nan if v is None else v for v in c["pucts"]]
         assert np.array_equal(np.asarray(pucts), np.asarray(ref), equal_nan=True)
         assert [float(v) for v in a._normalize_q(outcomes)] == c["normalize_q"]
+
+
+def test_customed_and_reinforce_seeded_init_match_reference():
+    """Host-side agents (no GPU): seeded constructions give the reference's
+    initial weights (golden F9/F10), so seeded scripts train the same nets."""
+    import torch
+
+    from rl_6_nimmt.agents import AGENTS, BatchedReinforceAgent, PUCTCustomedAgent
+
+    assert AGENTS["reinforce"] is BatchedReinforceAgent
+    W = np.load(os.path.join(GOLDEN, "customed_weights.npz"))
+    spec = json.load(open(os.path.join(GOLDEN, "customed_games.json")))
+    for si, sess in enumerate(spec["sessions"][:3]):
+        torch.manual_seed(sess["seed"])
+        agents = [PUCTCustomedAgent(mc_max=200) if c == "C" else None for c in sess["seats"]]
+        for i, a in enumerate(agents):
+            if a is None:
+                continue
+            for k, v in a.actor.state_dict().items():
+                assert torch.equal(v, torch.from_numpy(W[f"s{si}_a{i}_init_{k}"])), (si, i, k)
+            assert a.actor.head_nets[0][0].out_features == 2
+    W = np.load(os.path.join(GOLDEN, "reinforce_weights.npz"))
+    spec = json.load(open(os.path.join(GOLDEN, "reinforce_games.json")))
+    sess = spec["sessions"][0]
+    torch.manual_seed(sess["seed"])
+    a = BatchedReinforceAgent(**sess["kwargs"])
+    for k, v in a.actor.state_dict().items():
+        assert torch.equal(v, torch.from_numpy(W[f"s0_a0_init_{k}"])), k
+
+
+def test_discounted_returns_formula():
+    """utils/various.py:41-50: G_t = r_t + gamma G_{t+1}"""
+    from rl_6_nimmt.agents.policy import compute_discounted_returns
+
+    r = [0.0, -3.0, 0.0, -5.0, -1.0]
+    g = compute_discounted_returns(r, 0.9).numpy()
+    want = np.zeros(5)
+    acc = 0.0
+    for t in range(4, -1, -1):
+        acc = r[t] + 0.9 * acc
+        want[t] = acc
+    assert np.allclose(g, want, rtol=0, atol=1e-6)
