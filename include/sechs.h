@@ -42,6 +42,8 @@ typedef enum {
     SN_EHIP = 2,         /* HIP runtime error */
     SN_ENOMEM = 3,       /* device allocation failed */
     SN_EUNSUPPORTED = 4, /* valid in the reference but not built here */
+    SN_ERNG = 5,         /* a pipelined numpy-MT draw ran past the twisted words (sticky: every
+                            rollout of this handle since then is invalid; see sn_pipe_errors) */
 } sn_status;
 
 /* random word sources; both drive numpy's legacy masked-rejection
@@ -144,11 +146,19 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          0 (default): off.
      SN_OPT_PIPE_GPW     games per k_play wave on the pipelined path: 64
                          (one per lane) or 32 (half the LDS per wave, two
-                         waves per SIMD). */
-enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3, SN_OPT_TIMING = 4, SN_OPT_PIPE_GPW = 5 };
+                         waves per SIMD).
+     SN_OPT_PIPE_LEAD    words k_mt_ahead keeps twisted past the consumer
+                         (64..600, default 600).  TEST KNOB: below 600 the
+                         overrun bound of sn_pipe_errors no longer holds;
+                         it exists to exercise the SN_ERNG path. */
+enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3, SN_OPT_TIMING = 4, SN_OPT_PIPE_GPW = 5,
+       SN_OPT_PIPE_LEAD = 6 };
 sn_status sn_set_option(sn_env* env, int option, int value);
 /* pipelined rollouts whose draws ran past the twisted words (must be 0; a
-   nonzero count means those games' draws are wrong) [sync] */
+   nonzero count means those games' draws are wrong) [sync].  The count is
+   also mirrored asynchronously into pinned host memory after every
+   pipelined rollout: sn_rollout returns SN_ERNG once a completed rollout
+   has counted one (sticky for the handle). */
 sn_status sn_pipe_errors(sn_env* env, uint32_t* count);
 /* mean launch duration (ms) of the pipelined k_play and k_mt_ahead launches
    recorded since SN_OPT_TIMING was set; *n = launches recorded [sync] */

@@ -249,6 +249,8 @@ struct AheadArgs {
     int cin;   // pabsc parity holding the consumer position to lead (INIT: written)
     int tin;   // ptend parity of the previous prep (steady)
     int tout;  // ptend parity written
+    int lead;  // words to keep twisted past the consumer (kPipeLead; smaller only to test the overrun path)
+    uint32_t* perr_mirror;  // host-mapped copy of *perr, refreshed at launch start (off the play stream)
 };
 
 template <bool INIT>
@@ -259,6 +261,11 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
     if (g >= s.B) return;  // whole waves
     const uint32_t lane = threadIdx.x & 63u;
     const int64_t B = s.B;
+    // publish the overrun count so far (every k_play before the running one)
+    // to the host without a sync; sn_rollout reads it at entry
+    if (g == 0 && lane == 0u && a.perr_mirror)
+        __hip_atomic_store(a.perr_mirror, __hip_atomic_load(s.perr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t* st = s.mt + g * kMtN;
     uint8_t* ring = (uint8_t*)s.pring;
     uint32_t Tp, t0, c;
@@ -282,8 +289,11 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
         t0 = s.ptend[(int64_t)a.tin * B + g];
         c = s.pabsc[(int64_t)a.cin * B + g];
     }
-    const uint32_t lead = t0 - c;
-    const uint32_t n = (lead < (uint32_t)kPipeLead) ? (((uint32_t)kPipeLead - lead) & ~7u) : 0u;
+    // signed: a consumer past the twisted end means a play lane overran
+    // (counted there too); twist nothing rather than underflow the lead
+    const int32_t lead = (int32_t)(t0 - c);
+    if (lead < 0 && lane == 0u) atomicAdd(s.perr, 1u);
+    const uint32_t n = (lead >= 0 && lead < a.lead) ? (((uint32_t)(a.lead - lead)) & ~7u) : 0u;
     const uint32_t T0 = (Tp == (uint32_t)kMtN) ? 0u : Tp;
     auto ring_dword = [&](uint32_t j, uint32_t v) {  // t0 is 8-aligned: lanes 4m..4m+3 share one dword
         const uint32_t y = mt_temper(v) & 0xFFu;
@@ -346,7 +356,9 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
 __global__ void k_pipe_code(DevState s, int cin, int tin) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= s.B) return;
-    s.mt_pos[g] = s.ptp[g] | ((s.ptend[(int64_t)tin * s.B + g] - s.pabsc[(int64_t)cin * s.B + g]) << 16);
+    const int32_t rem = (int32_t)(s.ptend[(int64_t)tin * s.B + g] - s.pabsc[(int64_t)cin * s.B + g]);
+    if (rem < 0) atomicAdd(s.perr, 1u);  // an overrun (already counted): the stream is lost
+    s.mt_pos[g] = s.ptp[g] | ((uint32_t)max(rem, 0) << 16);
 }
 
 // MT19937 chunks (8 words) twisted per refill in k_play: 2 doubles the
@@ -683,6 +695,7 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
     e->chunk_steps = 10;
     e->pipe = 1;
     e->pipe_gpw = 64;
+    e->pipe_lead = kPipeLead;
     e->pvalid = 0;
     e->pcount = 0;
     if (rng_mode == SN_RNG_NUMPY_MT) {
@@ -701,10 +714,17 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
         }
         if (hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&e->ev_prep, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&e->ev_main, hipEventDisableTiming) != hipSuccess) {
+            hipEventCreateWithFlags(&e->ev_main, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e->ev_play, hipEventDisableTiming) != hipSuccess) {
             sn_destroy(e);
             return fail(SN_EHIP, "stream/event creation failed");
         }
+        if (hipHostMalloc((void**)&e->perr_host, sizeof(uint32_t), hipHostMallocMapped) != hipSuccess ||
+            hipHostGetDevicePointer((void**)&e->perr_host_dev, e->perr_host, 0) != hipSuccess) {
+            sn_destroy(e);
+            return fail(SN_ENOMEM, "pinned overrun mirror allocation failed");
+        }
+        *e->perr_host = 0u;
     }
     if (rng_mode == SN_RNG_NUMPY_MT) {
         const sn_status r = sn_set_option(e, SN_OPT_RING_WORDS, N <= 4 ? 256 : 512);
@@ -733,6 +753,8 @@ sn_status sn_destroy(sn_env* e) {
     (void)hipDeviceSynchronize();  // no k_mt_ahead may still be in flight
     if (e->ev_prep) (void)hipEventDestroy(e->ev_prep);
     if (e->ev_main) (void)hipEventDestroy(e->ev_main);
+    if (e->ev_play) (void)hipEventDestroy(e->ev_play);
+    if (e->perr_host) (void)hipHostFree(e->perr_host);
     if (e->side) (void)hipStreamDestroy(e->side);
     free_timing(e);
     void* ps[] = {s.hand, s.row_lo, s.row_hi, s.score, s.sum_res, s.episodes, s.mt_pos, s.ctr, s.mt, s.mt0, s.ring,
@@ -781,6 +803,10 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
         case SN_OPT_PIPE_GPW:
             if (value != 32 && value != 64) return fail(SN_EINVAL, "games per wave must be 32 or 64");
             e->pipe_gpw = value;
+            return SN_OK;
+        case SN_OPT_PIPE_LEAD:
+            if (value < 64 || value > kPipeLead) return fail(SN_EINVAL, "pipe lead must be in 64..600");
+            e->pipe_lead = value;
             return SN_OK;
         case SN_OPT_TIMING:
             if (value < 0 || value > 4096) return fail(SN_EINVAL, "timing launches must be in 0..4096");
@@ -897,6 +923,10 @@ static sn_status launch_play_one(sn_env* e, PlayArgs a, hipStream_t st) {
 // ring covers a launch's draws (a 4-player episode: 193.5 +- 9.3 words).
 sn_status sn_pipe_sync(sn_env* e, hipStream_t st) {
     if (!e || !e->pvalid) return SN_OK;
+    // k_pipe_code reads the last k_play's consumer position (pabsc) and the
+    // last k_mt_ahead's twisted end: wait for both, whatever stream `st` is
+    // (the null stream does not order behind a non-blocking caller stream)
+    HIP_TRY(hipStreamWaitEvent(st, e->ev_play, 0));
     HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));
     const int p = (int)(e->pcount & 1u);
     hipLaunchKernelGGL(k_pipe_code, dim3(grid_for(e->s.B)), dim3(kBlock), 0, st, e->s, 1 - p, p);
@@ -904,6 +934,17 @@ sn_status sn_pipe_sync(sn_env* e, hipStream_t st) {
     e->pvalid = 0;
     return SN_OK;
 }
+
+// Longest pipelined launch for N players.  k_mt_ahead leaves 593..600 words
+// twisted past the consumer position of the launch BEFORE the running one,
+// so two consecutive launches must draw <= 592 words.  With auto-reset, 2c
+// consecutive env-steps hold at most ceil(2c/10) deals (103 draws each,
+// ~146 words) and each hand size at most that often; the exact tail of the
+// summed geometric word counts (tools/pipe_tail.py) gives, per game and
+// launch pair, P(> 592 words) = 2e-31 at N = 4 with 10-step launches
+// (two episodes) but 1.4e-25 at N = 5 and 4.5e-5 at N = 10; with 5-step
+// launches (one episode per pair) it is <= 6.1e-73 for every N <= 10.
+static int pipe_max_chunk(int N) { return N <= 4 ? 10 : 5; }
 
 // LDS a pipelined k_play block needs (obs staging / deck + the RingPipe windows)
 static size_t pipe_lds(const DevState& s, const PlayArgs& a, int gpw, int* wave_out) {
@@ -928,13 +969,13 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     const dim3 pg((unsigned)((s.B + kBlock / 64 - 1) / (kBlock / 64)));
     if (!e->pvalid) {  // start the pipeline from mt_pos: twist kPipeLead ahead, synchronously
         const int p = (int)(e->pcount & 1u);
-        hipLaunchKernelGGL(k_mt_ahead<true>, pg, dim3(kBlock), 0, st, s, AheadArgs{1 - p, 0, p});
+        hipLaunchKernelGGL(k_mt_ahead<true>, pg, dim3(kBlock), 0, st, s, AheadArgs{1 - p, 0, p, e->pipe_lead, e->perr_host_dev});
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(e->ev_prep, st));
         e->pvalid = 1;
     }
     const int64_t B = s.B, N = s.N;
-    const int chunk = min(e->chunk_steps, 10);
+    const int chunk = min(e->chunk_steps, pipe_max_chunk(s.N));
     for (int t0 = 0; t0 < a.steps; t0 += chunk) {
         PlayArgs c = a;
         c.steps = min(chunk, a.steps - t0);
@@ -961,11 +1002,12 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
             }
         });
         HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(e->ev_play, st));  // sn_pipe_sync orders behind the last k_play
         if (tv) HIP_TRY(hipEventRecord(tv[1], st));
         // the next launch's twist, beside this one: leads the consumer of the launch before
         HIP_TRY(hipStreamWaitEvent(e->side, e->ev_main, 0));
         if (tv) HIP_TRY(hipEventRecord(tv[2], e->side));
-        hipLaunchKernelGGL(k_mt_ahead<false>, pg, dim3(kBlock), 0, e->side, s, AheadArgs{1 - p, p, 1 - p});
+        hipLaunchKernelGGL(k_mt_ahead<false>, pg, dim3(kBlock), 0, e->side, s, AheadArgs{1 - p, p, 1 - p, e->pipe_lead, e->perr_host_dev});
         HIP_TRY(hipGetLastError());
         if (tv) HIP_TRY(hipEventRecord(tv[3], e->side));
         HIP_TRY(hipEventRecord(e->ev_prep, e->side));
@@ -1021,6 +1063,9 @@ sn_status sn_rollout(sn_env* e, int steps, int32_t* rewards, uint8_t* done, uint
     if (obs && (obs_stride < L || (obs_stride & 3))) return fail(SN_EINVAL, "obs_stride must be a multiple of 4 and >= obs length");
     if (obs && (((uintptr_t)obs) & 3)) return fail(SN_EINVAL, "obs must be 4-byte aligned");
     if (steps == 0) return SN_OK;
+    if (e->perr_host && __atomic_load_n(e->perr_host, __ATOMIC_RELAXED))
+        return fail(SN_ERNG, "a pipelined numpy-MT draw ran past the twisted words; this handle's rollouts are invalid "
+                             "from that launch on (sn_pipe_errors)");
     PlayArgs a{};
     a.steps = steps;
     a.flags = flags;
@@ -1181,6 +1226,7 @@ sn_status sn_pipe_errors(sn_env* e, uint32_t* count) {
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(count, e->s.perr, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (e->perr_host && *count) __atomic_store_n(e->perr_host, *count, __ATOMIC_RELAXED);
     return SN_OK;
 }
 

@@ -212,13 +212,17 @@ struct RingGen {
 };
 
 // numpy-MT words for k_play from the pipelined ring: k_mt_ahead twisted the
-// stream up to `tend` (>= ~400 words past the consumer) while the previous
-// k_play ran.  The first kPipeWin of those bytes are copied to LDS at start
-// (21 coalesced 1-KB loads per wave); reads are 8 bytes at any byte offset
-// (two aligned ds_read_b64 + funnel shift).  Past the window the bytes come
-// from HBM; past `tend` a lane would need words the next k_mt_ahead is
-// twisting concurrently: it counts an error (perr) and draws zero bytes
-// instead -- ~18 standard deviations past one launch's draws.
+// stream up to `tend` (593..600 words past the consumer position of the
+// launch before) while the previous k_play ran.  The first kPipeWin of those
+// bytes are copied to LDS at start (21 coalesced 1-KB loads per wave); reads
+// are 8 bytes at any byte offset (two aligned ds_read_b64 + funnel shift).
+// Past the window the bytes come from HBM.  A top-up (prefetch) never reads
+// past `tend`; a draw that NEEDS a word past it would need one the next
+// k_mt_ahead is twisting concurrently: it counts an error (perr, sticky,
+// surfaced as SN_ERNG by sn_rollout) and draws zero bytes.  The host caps
+// the launch length per player count (pipe_max_chunk, sechs_env.hip) so that
+// two launches' draws exceed 592 words with probability < 1e-25 per game
+// (exact tail of the geometric word counts).
 struct PipeSlow {
     uint64_t bytes;
     uint32_t k;
@@ -250,7 +254,11 @@ struct RingPipe {
     __device__ __forceinline__ void load(const DevState& s, int64_t gg, ByteBuf& buf, uint8_t* lds_slot, int cin, int tpar) {
         g = gg, B = s.B;
         c0 = s.pabsc[(int64_t)cin * B + g];
-        avail = s.ptend[(int64_t)tpar * B + g] - c0;
+        // signed: a consumer past the twisted end (an earlier overrun) must
+        // not read as a huge window of stale ring bytes
+        const int32_t av = (int32_t)(s.ptend[(int64_t)tpar * B + g] - c0);
+        if (av < 0) atomicAdd(s.perr, 1u);
+        avail = (av < 0) ? 0u : (uint32_t)av;
         win = min(avail, (uint32_t)kPipeWin);
         off = c0 & 15u;
         slot = lds_slot;
@@ -267,7 +275,8 @@ struct RingPipe {
         buf.clear();
     }
     __device__ __forceinline__ uint32_t consumed(const ByteBuf& buf) const { return c0 + take - buf.cnt; }
-    __device__ __forceinline__ bool gen(ByteBuf& buf) {
+    // forced = the buffer is empty and a draw needs a word now
+    __device__ __forceinline__ bool gen(ByteBuf& buf, bool forced) {
         if (take + 8u <= win) {
             const uint32_t p = off + take, a8 = p & ~7u, sh = 8u * (p & 7u);
             const uint64_t lo = *(const uint64_t*)(slot + a8);
@@ -276,15 +285,17 @@ struct RingPipe {
             take += 8u;
             return true;
         }
-        const PipeSlow r = pipe_slow(ring, B, g, c0 + take, (avail > take) ? avail - take : 0u, err);
+        const uint32_t left = (avail > take) ? avail - take : 0u;
+        if (left == 0u && !forced) return false;  // prefetch stops at the twisted end
+        const PipeSlow r = pipe_slow(ring, B, g, c0 + take, left, err);
         buf.append(r.bytes, r.k);
         take += r.k;
         return true;
     }
     __device__ __forceinline__ void topup(ByteBuf& buf) {
-        if (buf.cnt <= 24u) gen(buf);
+        if (buf.cnt <= 24u) gen(buf, false);
     }
-    __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf); }
+    __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf, true); }
 };
 
 // bytes of a lane's LDS window for RingPipe (chunk-aligned copy + 8 for the funnel's second read)
@@ -590,13 +601,16 @@ struct sn_env {
     int chunk_steps;  // SN_OPT_CHUNK_STEPS
     int pipe;         // SN_OPT_PIPELINE
     int pipe_gpw;     // SN_OPT_PIPE_GPW: games per k_play wave on the pipelined path (32 or 64)
+    int pipe_lead;    // SN_OPT_PIPE_LEAD: words k_mt_ahead keeps twisted ahead (kPipeLead; tests lower it)
     sechs::DevState s;
     // pipelined twist-ahead (sechs_env.hip launch_pipe): a k_mt_ahead for the
     // next play launch may be in flight on `side` (ev_prep) after a rollout
     int pvalid;         // ring + ptend/pabsc/ptp are the live RNG state (mt_pos is stale)
     uint64_t pcount;    // play launches so far (parity selects the pabsc / ptend buffers)
     hipStream_t side;
-    hipEvent_t ev_prep, ev_main;
+    hipEvent_t ev_prep, ev_main, ev_play;  // ev_play: after the last pipelined k_play (caller's stream)
+    uint32_t* perr_host;                    // pinned, device-mapped mirror of s.perr (PlayArgs::perr_mirror)
+    uint32_t* perr_host_dev;
     // SN_OPT_TIMING: per-launch event pairs (k_play start/end on the launch
     // stream, k_mt_ahead start/end on `side`), tcap pairs, tn recorded
     hipEvent_t* tev;

@@ -16,11 +16,11 @@ import torch  # noqa: F401  (must precede the dlopen below, see module doc)
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("SECHS_LIB", os.path.join(_PKG_ROOT, "libsechs.so"))
 
-SN_OK, SN_EINVAL, SN_EHIP, SN_ENOMEM, SN_EUNSUPPORTED = 0, 1, 2, 3, 4
+SN_OK, SN_EINVAL, SN_EHIP, SN_ENOMEM, SN_EUNSUPPORTED, SN_ERNG = 0, 1, 2, 3, 4, 5
 SN_RNG_PHILOX, SN_RNG_NUMPY_MT = 0, 1
 SN_I8, SN_I16, SN_I32, SN_I64, SN_F32 = 1, 2, 3, 4, 5
 SN_AUTO_RESET, SN_NO_SUMMARIES = 1, 2
-SN_OPT_RING_WORDS, SN_OPT_CHUNK_STEPS, SN_OPT_PIPELINE, SN_OPT_TIMING, SN_OPT_PIPE_GPW = 1, 2, 3, 4, 5
+SN_OPT_RING_WORDS, SN_OPT_CHUNK_STEPS, SN_OPT_PIPELINE, SN_OPT_TIMING, SN_OPT_PIPE_GPW, SN_OPT_PIPE_LEAD = 1, 2, 3, 4, 5, 6
 
 class SnPuct(ctypes.Structure):
     """sn_puct (include/sechs.h)"""
@@ -90,6 +90,11 @@ class NativeError(RuntimeError):
     pass
 
 
+class PipeOverrunError(NativeError):
+    """A pipelined numpy-MT draw ran past the twisted words (SN_ERNG): the
+    handle's rollouts from that launch on are not the reference's."""
+
+
 _lib = None
 
 
@@ -118,6 +123,8 @@ def check(status, what=""):
             raise ValueError(f"{what}: {msg}")
         if status == SN_EUNSUPPORTED:
             raise NotImplementedError(f"{what}: {msg}")
+        if status == SN_ERNG:
+            raise PipeOverrunError(f"{what}: {msg}")
         raise NativeError(f"{what} failed ({status}): {msg}")
 
 

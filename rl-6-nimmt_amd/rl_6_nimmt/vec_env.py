@@ -111,10 +111,16 @@ class VecSechsNimmtEnv:
         return rew, done.bool(), inv
 
     def rollout(self, steps, want_rewards=True, want_done=True, want_actions=False, want_obs=False, obs_stride=None,
-                out=None):
+                out=None, check=False):
         """Fused DrunkHamster self-play for `steps` env-steps with auto-reset.
         Returns dict of tensors: rewards int32 [T,B,N], done uint8 [T,B],
-        actions uint8 [T,B,N], obs int8 [T,B,N,obs_stride] (pre-action)."""
+        actions uint8 [T,B,N], obs int8 [T,B,N,obs_stride] (pre-action).
+
+        numpy mode: a pipelined draw past the twisted words (probability
+        < 1e-25 per game and launch pair) raises
+        PipeOverrunError -- at the next call without a sync (the library
+        mirrors the count to pinned host memory), or at once with
+        check=True (synchronises)."""
         B, N, T = self.num_games, self.num_players, int(steps)
         stride = obs_stride or ((self.obs_len + 15) // 16 * 16)
         if out is None:
@@ -135,6 +141,10 @@ class VecSechsNimmtEnv:
                                  self._flags(True), self._stream()),
             "sn_rollout",
         )
+        if check and self.rng == "numpy":
+            n = self.pipe_errors()
+            if n:
+                raise nat.PipeOverrunError(f"sn_rollout: {n} pipelined MT19937 draws ran past the twisted words")
         return out
 
     # ------------------------------------------------------------ views
@@ -175,8 +185,11 @@ class VecSechsNimmtEnv:
         nat.check(nat.lib().sn_clear_results(self._h, self._stream()), "sn_clear_results")
 
     # ------------------------------------------------------------ numpy RNG bridge
-    def set_option(self, ring_words=None, chunk_steps=None, pipeline=None, pipe_gpw=None):
-        """numpy-compat rollout tuning (include/sechs.h SN_OPT_*); results never depend on it"""
+    def set_option(self, ring_words=None, chunk_steps=None, pipeline=None, pipe_gpw=None, pipe_lead=None):
+        """numpy-compat rollout tuning (include/sechs.h SN_OPT_*); results never depend on it
+        (except pipe_lead < 600, a test knob that makes overruns -- PipeOverrunError -- likely)"""
+        if pipe_lead is not None:
+            nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPE_LEAD, int(pipe_lead)), "sn_set_option")
         if pipe_gpw is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPE_GPW, int(pipe_gpw)), "sn_set_option")
         if pipeline is not None:

@@ -57,6 +57,8 @@ def test_rollout_matches_oracle(rng, N, C, summ):
     assert np.array_equal(e.cpu().numpy(), ref.episodes())
     for dt in (torch.int8, torch.int16, torch.int64, torch.float32):
         assert np.array_equal(env.obs(dt).cpu().numpy(), ref.obs(summ).astype(np.int64).astype(dt_np(dt)))
+    if rng == "numpy":
+        assert env.pipe_errors() == 0
 
 
 def dt_np(dt):
@@ -73,18 +75,23 @@ def _pad_hands(hands, N):
 
 @pytest.mark.parametrize("rng", ["numpy", "philox"])
 def test_full_size_episode_matches_oracle(rng):
-    """BASELINE config 2 size: 65 536 x 4-player games, one full episode, bit-exact."""
+    """BASELINE config 2 size: 65 536 x 4-player games, one full episode with
+    the int8 observations the headline emits, bit-exact."""
     B, N = 65536, 4
     env = venv(B, N, seed=0, rng=rng)
     env.reset()
-    out = env.rollout(10, want_actions=True)
+    out = env.rollout(10, want_actions=True, want_obs=True, check=True)
     ref = O.VecOracle(B, N, rng_mode=RNG[rng], seed=0)
     ref.reset()
-    rr, rd, ra, _ = ref.rollout(10, nthreads=8)
+    rr, rd, ra, ro = ref.rollout(10, want_obs=True, nthreads=16)
     torch.cuda.synchronize()
     assert np.array_equal(out["actions"].cpu().numpy(), ra)
     assert np.array_equal(out["rewards"].cpu().numpy(), rr)
     assert np.array_equal(out["done"].cpu().numpy(), rd)
+    o = out["obs"].cpu().numpy()
+    assert np.array_equal(o[..., :47], ro)
+    assert not o[..., 47:].any()
+    del o, ro
     # size-independent properties: every game ends after exactly 10 steps, the
     # 104-card deck holds 171 heads, so no episode can cost more than that
     d = out["done"].cpu().numpy()
@@ -428,3 +435,66 @@ def test_pipeline_then_other_paths_interleave():
         k, p = _np_form(*env.get_mt_state(g))
         rk, rp = _np_form(np.frombuffer(bytes(rngs[g].mt), dtype=np.uint32), rngs[g].pos)
         assert p == rp and np.array_equal(k, rk), g
+
+
+@pytest.mark.parametrize("N", [9, 10])
+def test_pipelined_many_players_full_size(N):
+    """The default pipelined numpy-MT path at 65 536 games and 9 / 10
+    players without observations (the case whose LDS fits the pipelined
+    k_play and whose launch pairs draw the most words): 3 episodes = 6
+    launches (5 env-steps each at N >= 5, sechs_env.hip pipe_max_chunk),
+    bit-exact against the oracle, no overrun."""
+    B, seed = 65536, 3
+    env = venv(B, N, seed=seed, rng="numpy")
+    env.reset()
+    ref = O.VecOracle(B, N, rng_mode=O.RNG_NUMPY_MT, seed=seed)
+    ref.reset()
+    for ep in range(3):
+        out = env.rollout(10, want_actions=True, check=True)
+        rr, rd, ra, _ = ref.rollout(10, nthreads=16)
+        torch.cuda.synchronize()
+        assert np.array_equal(out["actions"].cpu().numpy(), ra), ep
+        assert np.array_equal(out["rewards"].cpu().numpy(), rr), ep
+        assert np.array_equal(out["done"].cpu().numpy(), rd), ep
+    assert env.pipe_errors() == 0
+    s, e = env.results()
+    assert np.array_equal(s.cpu().numpy(), ref.sum_results())
+
+
+@pytest.mark.parametrize("N,chunk", [(9, 10), (10, 10), (10, 3), (5, 7), (6, 10)])
+def test_pipelined_many_players_chunks(N, chunk):
+    """pipelined rollouts at N >= 5 with requested launch lengths above and
+    below the per-N cap: bit-exact, final numpy MT states equal, no overrun"""
+    B, T, seed = 2000, 37, 8
+    env = venv(B, N, seed=seed, rng="numpy")
+    env.set_option(chunk_steps=chunk, pipeline=1)
+    env.reset()
+    ref = O.VecOracle(B, N, rng_mode=O.RNG_NUMPY_MT, seed=seed)
+    ref.reset()
+    out = env.rollout(T, want_actions=True, check=True)
+    rr, rd, ra, _ = ref.rollout(T)
+    torch.cuda.synchronize()
+    assert np.array_equal(out["actions"].cpu().numpy(), ra)
+    assert np.array_equal(out["rewards"].cpu().numpy(), rr)
+    rngs = ref.v.contents.rngs
+    for g in range(0, B, 97):
+        k, p = _np_form(*env.get_mt_state(g))
+        rk, rp = _np_form(np.frombuffer(bytes(rngs[g].mt), dtype=np.uint32), rngs[g].pos)
+        assert p == rp and np.array_equal(k, rk), g
+    assert env.pipe_errors() == 0
+
+
+def test_pipelined_overrun_is_an_error():
+    """With the lead lowered below a launch pair's draws (test knob), lanes
+    overrun: the count is nonzero, rollout(check=True) raises at once, and
+    the next rollout raises from the asynchronous mirror (sticky)."""
+    from rl_6_nimmt._native import PipeOverrunError
+
+    env = venv(4096, 10, seed=1, rng="numpy")
+    env.set_option(pipe_lead=128)
+    env.reset()
+    with pytest.raises(PipeOverrunError):
+        env.rollout(20, check=True)
+    assert env.pipe_errors() > 0
+    with pytest.raises(PipeOverrunError):
+        env.rollout(10)
