@@ -26,6 +26,7 @@ import argparse
 import json
 import os
 import sys
+import subprocess
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -95,32 +96,34 @@ def barrier(world):
 
 def time_rollouts(env, out, steps, warmup, world):
     """Warm up, then time exactly `steps` launches between barrier+sync on
-    both sides.  Returns (wall seconds, mean per-launch kernel ms measured
-    with HIP events on the launch stream)."""
+    both sides (nothing else enqueued in between: per-launch timing events
+    on the stream cost the pipelined step ~30 %).  Returns (wall seconds,
+    mean per-launch ms from HIP events around each launch in a second pass of
+    the same `steps` launches, per-kernel times)."""
     for _ in range(warmup):
         env.rollout(STEPS_PER_LAUNCH, out=out)
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    for i in range(steps):
+        env.rollout(STEPS_PER_LAUNCH, out=out)
+    torch.cuda.synchronize()
+    barrier(world)
+    t1 = time.perf_counter()
+    # second pass: HIP events around each launch on the launch stream, and
+    # (numpy mode) inside the library around each kernel on its own stream
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if env.rng == "numpy":
+        env.time_kernels(steps)
     for i in range(steps):
         ev[i][0].record()
         env.rollout(STEPS_PER_LAUNCH, out=out)
         ev[i][1].record()
     torch.cuda.synchronize()
-    barrier(world)
-    t1 = time.perf_counter()
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if env.rng != "numpy":
         return t1 - t0, kern_ms, {"k_play": kern_ms, "launches": steps}
-    # numpy mode: the two kernels of a step run on two streams, so each gets
-    # HIP events on its own stream -- in a second pass of the same `steps`
-    # launches right after the timed one (the extra per-launch events on both
-    # streams slow the pipelined step by ~10 %, so they stay out of `value`)
-    env.time_kernels(steps)
-    for i in range(steps):
-        env.rollout(STEPS_PER_LAUNCH, out=out)
     play_ms, ahead_ms, n = env.kernel_times()
     env.time_kernels(0)
     return t1 - t0, kern_ms, {"k_play": play_ms, "k_mt_ahead": ahead_ms, "launches": n}
@@ -162,9 +165,13 @@ def cpu_baseline(budget_s, rng):
         v.rollout(STEPS_PER_LAUNCH, want_obs=True, want_actions=True, nthreads=1)
     dt = time.perf_counter() - t
     steps = games * episodes * STEPS_PER_LAUNCH
-    # the same restatement with OpenMP over this job's CPU share (16 threads
-    # on the GPU box), ~3 s on the full 65 536 games
-    threads = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    # the same restatement with OpenMP over this job's CPU share (SURVEY.md
+    # §8(d)), ~3 s on the full 65 536 games: as many threads as this process
+    # may run on, capped by OMP_NUM_THREADS when the job sets it
+    host = host_cpu_info()
+    threads = host["affinity_cpus"]
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        threads = max(1, min(threads, int(os.environ["OMP_NUM_THREADS"])))
     vm = O.VecOracle(65536, N_PLAYERS, rng_mode=mode, seed=0)
     vm.reset()
     vm.rollout(STEPS_PER_LAUNCH, want_obs=True, want_actions=True, nthreads=threads)  # first touch of the outputs
@@ -184,7 +191,37 @@ def cpu_baseline(budget_s, rng):
                   f"oracle's single-threaded C restatement of env.py",
         "multi_thread": {"value": 65536 * eps_mt * STEPS_PER_LAUNCH / dt_mt, "cores": threads,
                          "sample": f"65536 games x {eps_mt} episodes, OpenMP"},
+        "host": host,
     }
+
+
+def host_cpu_info():
+    """What the CPU baseline ran on: logical CPUs of the machine, the CPUs
+    this process may use (its affinity mask, the job's share on the GPU box),
+    OMP_NUM_THREADS, and the CPU model (lscpu / /proc/cpuinfo)."""
+    model = None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except (OSError, subprocess.SubprocessError):
+        pass
+    if model is None:
+        try:
+            for line in open("/proc/cpuinfo"):
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+        except OSError:
+            pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "affinity_cpus": aff,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 def bench_mcs(games, rollouts, episodes=1):

@@ -163,6 +163,14 @@ sn_status sn_pipe_errors(sn_env* env, uint32_t* count);
 /* mean launch duration (ms) of the pipelined k_play and k_mt_ahead launches
    recorded since SN_OPT_TIMING was set; *n = launches recorded [sync] */
 sn_status sn_kernel_times(sn_env* env, float* play_ms, float* ahead_ms, int32_t* n);
+/* Diagnostics (no reference counterpart): shader-clock cycles every k_play
+   wave spent per phase of its step loop since the last call, summed over
+   waves -- out[0..8] = prologue, obs, draws, resolve, output stores, deck
+   shuffle targets, epilogue, hand sorting, deck shuffle swaps; out[9] =
+   waves.  Only the libsechs_prof.so build
+   (-DSECHS_PHASE_PROF) records them; the product build returns
+   SN_EUNSUPPORTED [sync]. */
+sn_status sn_debug_phases(uint64_t* out, int n);
 
 /* ---- Monte-Carlo search, MCSAgent (agents/mcts.py:17-188) ------------- */
 

@@ -387,9 +387,20 @@ __device__ __forceinline__ uint32_t rng_interval(G& gen, ByteBuf& buf, uint32_t 
 
 // K draws with the same max (DrunkHamster for every seat of one step,
 // agents/random.py:9 called in seat order, play.py:38-41): the accepted
-// bytes of one 8-word window are the next draws in order, so the common
-// case takes all K from one SWAR compare; draws the window could not
-// supply fall back to rng_interval.
+// bytes of one 16-word window are the next draws in order, so the common
+// case takes all K from two SWAR compares (an 8-word window leaves some
+// lane of a wave short of K accepts at most steps, and the wave then runs
+// the scalar fallback for all); draws the window could not supply fall back
+// to rng_interval.
+__device__ __forceinline__ void buf_drop16(ByteBuf& buf, uint32_t k) {
+    if (k >= 8u) {
+        buf.b0 = buf.b1, buf.b1 = buf.b2, buf.b2 = buf.b3, buf.b3 = 0ull;
+        buf.cnt -= 8u;
+        k -= 8u;
+    }
+    buf.drop(k);
+}
+
 template <int K, class G>
 __device__ __forceinline__ void rng_draws(G& gen, ByteBuf& buf, uint32_t max, uint32_t (&out)[K]) {
     if (max == 0u) {
@@ -397,25 +408,33 @@ __device__ __forceinline__ void rng_draws(G& gen, ByteBuf& buf, uint32_t max, ui
         for (int k = 0; k < K; k++) out[k] = 0u;
         return;
     }
-    if (__any(buf.cnt < 8u)) gen.topup(buf);
+    if (__any(buf.cnt < 16u)) gen.topup(buf);
+    if (__any(buf.cnt < 16u)) gen.topup(buf);
     if (buf.cnt == 0u) gen.force(buf);
     const uint32_t mask = 0xFFFFFFFFu >> __builtin_clz(max);
-    const uint32_t valid = min(buf.cnt, 8u);
-    const uint64_t vmask = (valid >= 8u) ? ~0ull : ((1ull << (8u * valid)) - 1ull);
-    const uint64_t x = buf.b0 & (0x0101010101010101ull * (uint64_t)mask);
-    uint64_t t = swar_le_mask(x, max) & vmask;
+    const uint64_t mb = 0x0101010101010101ull * (uint64_t)mask;
+    const uint32_t valid = min(buf.cnt, 16u);
+    const uint32_t v0 = min(valid, 8u), v1 = valid - v0;
+    const uint64_t vm0 = (v0 >= 8u) ? ~0ull : ((1ull << (8u * v0)) - 1ull);
+    const uint64_t vm1 = (v1 >= 8u) ? ~0ull : ((1ull << (8u * v1)) - 1ull);
+    const uint64_t x0 = buf.b0 & mb, x1 = buf.b1 & mb;
+    uint64_t t0 = swar_le_mask(x0, max) & vm0, t1 = swar_le_mask(x1, max) & vm1;
     uint32_t got = 0u, last = 0u;
 #pragma unroll
     for (int k = 0; k < K; k++) {
-        const bool has = t != 0ull;
-        const uint32_t pos = (uint32_t)__builtin_ctzll(t | (1ull << 63));  // bit index (8*byte + 7)
-        out[k] = (uint32_t)(x >> (pos & 56u)) & 0xFFu;
-        t &= t - 1ull;
+        const bool in0 = t0 != 0ull;
+        const bool has = in0 || t1 != 0ull;
+        const uint32_t p0 = (uint32_t)__builtin_ctzll(t0 | (1ull << 63));
+        const uint32_t p1 = (uint32_t)__builtin_ctzll(t1 | (1ull << 63));
+        const uint32_t pos = in0 ? p0 : 64u + p1;  // bit index (8*byte + 7) in the 16-byte window
+        out[k] = (uint32_t)((in0 ? x0 : x1) >> (pos & 56u)) & 0xFFu;
+        t0 = in0 ? (t0 & (t0 - 1ull)) : t0;
+        t1 = in0 ? t1 : (t1 & (t1 - 1ull));
         last = has ? pos : last;
         got += has ? 1u : 0u;
     }
     // consumed: through the K-th accepted word, or the whole window
-    buf.drop(got == (uint32_t)K ? (last >> 3) + 1u : valid);
+    buf_drop16(buf, got == (uint32_t)K ? (last >> 3) + 1u : valid);
 #pragma unroll
     for (int k = 0; k < K; k++)
         if ((uint32_t)k >= got) out[k] = rng_interval(gen, buf, max);

@@ -41,7 +41,7 @@ __global__ void k_seed(DevState s) {
 
 template <int N, int MODE>
 __global__ __launch_bounds__(kBlock) void k_reset(DevState s, const uint8_t* decks) {
-    __shared__ uint8_t lds_deck[kBlock * kDeckStride];
+    __shared__ uint8_t lds_deck[kBlock * kDealStride];
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= s.B) return;
     Game<N> G;
@@ -52,7 +52,9 @@ __global__ __launch_bounds__(kBlock) void k_reset(DevState s, const uint8_t* dec
         typename RngOf<MODE>::T rng;
         ByteBuf buf;
         RngOf<MODE>::load(s, g, rng, buf);
-        deal_shuffle<N>(rng, buf, lds_deck + threadIdx.x * kDeckStride, s.C, G);
+        uint8_t* slot = lds_deck + threadIdx.x * kDealStride;
+        deck_shuffle2(rng, buf, slot, s.C);
+        deal_from_deck<N>(slot, s.C, G);
         RngOf<MODE>::store(s, g, rng, buf);
     }
     store_game<N>(s, g, G);
@@ -361,6 +363,41 @@ __global__ void k_pipe_code(DevState s, int cin, int tin) {
     s.mt_pos[g] = s.ptp[g] | ((uint32_t)max(rem, 0) << 16);
 }
 
+// ---- k_play phase profiler (diagnostics; built only with -DSECHS_PHASE_PROF,
+// the libsechs_prof.so variant).  Each wave accumulates shader-clock cycles
+// per phase of its step loop and adds them to g_phase at exit; the clock
+// reads add lgkmcnt waits at the phase marks, so the split is indicative.
+enum { PH_PROLOGUE = 0, PH_OBS, PH_DRAW, PH_RESOLVE, PH_STORE, PH_DEAL, PH_EPILOGUE, PH_HANDS, PH_APPLY, PH_N };
+#ifdef SECHS_PHASE_PROF
+__device__ unsigned long long g_phase[PH_N + 1];
+struct PhaseProf {
+    uint64_t t, acc[PH_N];
+    __device__ __forceinline__ void start() {
+        t = __builtin_readcyclecounter();
+#pragma unroll
+        for (int k = 0; k < PH_N; k++) acc[k] = 0ull;
+    }
+    __device__ __forceinline__ void mark(int k) {
+        const uint64_t n = __builtin_readcyclecounter();
+        acc[k] += n - t;
+        t = n;
+    }
+    __device__ __forceinline__ void flush(int lane) {
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < PH_N; k++) atomicAdd(&g_phase[k], (unsigned long long)acc[k]);
+            atomicAdd(&g_phase[PH_N], 1ull);
+        }
+    }
+};
+#else
+struct PhaseProf {
+    __device__ __forceinline__ void start() {}
+    __device__ __forceinline__ void mark(int) {}
+    __device__ __forceinline__ void flush(int) {}
+};
+#endif
+
 // MT19937 chunks (8 words) twisted per refill in k_play: 2 doubles the
 // lookahead of the refill's loads (one wave per SIMD: nothing else hides them)
 constexpr int kPlayPrefetch = 2;
@@ -387,9 +424,10 @@ struct PlayArgs {
 // within a step: observations first, the deal at the very end.)
 template <int N, class R, int GPW = 64>
 __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a, int64_t g, int lane, uint8_t* wave_lds,
-                                           Game<N>& G, R& rng, ByteBuf& buf, int32_t (&sum_res)[N], int32_t& episodes) {
+                                           Game<N>& G, R& rng, ByteBuf& buf, int32_t (&sum_res)[N], int32_t& episodes,
+                                           PhaseProf& pp) {
     const int64_t B = s.B;
-    uint8_t* my_deck = wave_lds + lane * kDeckStride;
+    uint8_t* my_deck = wave_lds + lane * kDealStride;
     const bool staged = a.obs && a.obs_stride == 48;
     const int64_t g0 = g - lane;                           // first game of this wave
     const int wave_games = (int)min((int64_t)GPW, B - g0);  // = active lanes (lanes past B left)
@@ -435,6 +473,7 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
             }
             ob += B * N * a.obs_stride;
         }
+        pp.mark(PH_OBS);
         uint32_t card[N], pen[N], idx[N];
         int bad = -1;
         if (G.n == 0u) {
@@ -455,6 +494,7 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
 #pragma unroll
             for (int p = 0; p < N; p++) card[p] = hand_get(G.hand[p], idx[p]);
         }
+        pp.mark(PH_DRAW);
         if (a.invalid) a.invalid[g] = bad;
         if (bad >= 0) {
             if (rew) {
@@ -476,6 +516,7 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
         for (int p = 0; p < N; p++) G.score[p] += (int32_t)pen[p];
         G.n -= 1u;
         const bool done = (G.n == 0u);  // env.py:246-249
+        pp.mark(PH_RESOLVE);
         if (rew) {
             if (N == 4 && a.vec_out) {  // one 16-B store per lane: 1 KB contiguous per wave
                 st_nt((u32x4*)rew, u32x4{-pen[0], -pen[1 % N], -pen[2 % N], -pen[3 % N]}, SECHS_NT_MORE);
@@ -499,12 +540,20 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
             st_nt(dn, (uint8_t)(done ? 1 : 0), SECHS_NT_MORE);
             dn += B;
         }
+        pp.mark(PH_STORE);
         if (done && auto_reset) {
             // GameSession.results.append(scores) then the next play_game()
 #pragma unroll
             for (int p = 0; p < N; p++) sum_res[p] -= G.score[p];
             episodes += 1;
-            deal_shuffle<N>(rng, buf, my_deck, s.C, G);
+            // deck_shuffle2 in its two phases (marked apart for the profiler)
+            shuffle_targets(rng, buf, my_deck + kDeckStride, s.C);
+            pp.mark(PH_DEAL);
+            for (int i = 0; i < s.C; i += 4) *(uint32_t*)(my_deck + i) = (uint32_t)i * 0x01010101u + 0x03020100u;
+            shuffle_apply(my_deck, my_deck + kDeckStride, s.C);
+            pp.mark(PH_APPLY);
+            deal_from_deck<N>(my_deck, s.C, G);
+            pp.mark(PH_HANDS);
         }
     }
 }
@@ -535,17 +584,18 @@ __device__ __forceinline__ void store_results(const DevState& s, int64_t g, int 
 // GPW = games per wave: 64 (one game per lane), or 32 for the pipelined
 // path (lanes 32..63 idle) -- half the LDS per wave, so two blocks fit a CU
 // and a SIMD holds two waves to hide each other's latency
-template <int N, int MODE, int GPW = 64>
-__global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
-    const int lane = threadIdx.x & 63;
+template <int N, int MODE, int GPW>
+__device__ __forceinline__ void play_body(const DevState& s, const PlayArgs& a, uint8_t* lds_dyn, int tid) {
+    const int lane = tid & 63;
     if (GPW < 64 && lane >= GPW) return;
-    // issue priority over the co-resident k_mt_ahead waves (side stream):
-    // the game loop is one latency-bound wave per SIMD (measured +1.7 %)
+    // issue priority over the co-resident k_mt_ahead waves: the game loop
+    // is one latency-bound wave per SIMD (measured +1.7 %)
     __builtin_amdgcn_s_setprio(1);
-    const int64_t g = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * GPW + lane;
+    const int64_t g = ((int64_t)blockIdx.x * (kBlock / 64) + (tid >> 6)) * GPW + lane;
     if (g >= s.B) return;
-    uint8_t* wave_lds = lds_dyn + (threadIdx.x >> 6) * a.wave_lds;
+    uint8_t* wave_lds = lds_dyn + (tid >> 6) * a.wave_lds;
+    PhaseProf pp;
+    pp.start();
     Game<N> G;
     load_game<N>(s, g, G);
     int32_t sum_res[N], episodes;
@@ -554,7 +604,8 @@ __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
     if constexpr (MODE == RNG_NUMPY_PIPE) {
         RingPipe rng;
         rng.load(s, g, buf, wave_lds + a.wave_lds - GPW * a.ring_lds + lane * a.ring_lds, a.pipe_cin, a.pipe_t);
-        play_steps<N, RingPipe, GPW>(s, a, g, lane, wave_lds, G, rng, buf, sum_res, episodes);
+        pp.mark(PH_PROLOGUE);
+        play_steps<N, RingPipe, GPW>(s, a, g, lane, wave_lds, G, rng, buf, sum_res, episodes, pp);
         s.pabsc[(int64_t)a.pipe_cout * s.B + g] = rng.consumed(buf);
     } else {
         typename RngOf<MODE, kPlayPrefetch>::T rng;
@@ -564,11 +615,20 @@ __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
         } else {
             RngOf<MODE, kPlayPrefetch>::load(s, g, rng, buf);
         }
-        play_steps<N>(s, a, g, lane, wave_lds, G, rng, buf, sum_res, episodes);
+        pp.mark(PH_PROLOGUE);
+        play_steps<N>(s, a, g, lane, wave_lds, G, rng, buf, sum_res, episodes, pp);
         RngOf<MODE, kPlayPrefetch>::store(s, g, rng, buf);
     }
     store_game<N>(s, g, G);
     store_results<N>(s, g, a.flags, sum_res, episodes);
+    pp.mark(PH_EPILOGUE);
+    pp.flush(lane);
+}
+
+template <int N, int MODE, int GPW = 64>
+__global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
+    play_body<N, MODE, GPW>(s, a, lds_dyn, (int)threadIdx.x);
 }
 
 // obs in any dtype, one thread per (game, seat)
@@ -861,7 +921,7 @@ constexpr int kLdsBytes = 160 * 1024;
 static sn_status launch_play_one(sn_env* e, PlayArgs a, hipStream_t st) {
     const DevState& s = e->s;
     const bool ring = (s.rng_mode == SN_RNG_NUMPY_MT) && !a.actions && s.ring_w > 0;
-    int wave = 64 * kDeckStride;
+    int wave = 64 * kDealStride;
     if (a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15) == 0) wave = max(wave, 64 * s.N * 48);
     a.ring_lds = 0;
     const int ring_stride = ring_lds_stride(s.ring_w);
@@ -948,7 +1008,7 @@ static int pipe_max_chunk(int N) { return N <= 4 ? 10 : 5; }
 
 // LDS a pipelined k_play block needs (obs staging / deck + the RingPipe windows)
 static size_t pipe_lds(const DevState& s, const PlayArgs& a, int gpw, int* wave_out) {
-    int wave = gpw * kDeckStride;
+    int wave = gpw * kDealStride;
     if (a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15) == 0) wave = max(wave, gpw * s.N * 48);
     wave += gpw * kPipeSlot;
     *wave_out = wave;
@@ -1002,7 +1062,6 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
             }
         });
         HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(e->ev_play, st));  // sn_pipe_sync orders behind the last k_play
         if (tv) HIP_TRY(hipEventRecord(tv[1], st));
         // the next launch's twist, beside this one: leads the consumer of the launch before
         HIP_TRY(hipStreamWaitEvent(e->side, e->ev_main, 0));
@@ -1013,6 +1072,7 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         HIP_TRY(hipEventRecord(e->ev_prep, e->side));
         e->pcount++;
     }
+    HIP_TRY(hipEventRecord(e->ev_play, st));  // sn_pipe_sync orders behind the last k_play
     return SN_OK;
 }
 
@@ -1217,6 +1277,22 @@ sn_status sn_kernel_times(sn_env* e, float* play_ms, float* ahead_ms, int32_t* n
     *play_ms = e->tn ? (float)(sp / e->tn) : 0.f;
     *ahead_ms = e->tn ? (float)(sa / e->tn) : 0.f;
     return SN_OK;
+}
+
+sn_status sn_debug_phases(uint64_t* out, int n) {
+    if (!out || n < 1) return fail(SN_EINVAL, "NULL argument");
+#ifdef SECHS_PHASE_PROF
+    unsigned long long h[PH_N + 1];
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)));
+    for (int k = 0; k < n; k++) out[k] = (k <= PH_N) ? (uint64_t)h[k] : 0ull;
+    const unsigned long long z[PH_N + 1] = {};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)));
+    return SN_OK;
+#else
+    for (int k = 0; k < n; k++) out[k] = 0ull;
+    return fail(SN_EUNSUPPORTED, "built without SECHS_PHASE_PROF (make libsechs_prof.so)");
+#endif
 }
 
 sn_status sn_pipe_errors(sn_env* e, uint32_t* count) {

@@ -56,6 +56,7 @@ constexpr int kPipeWin = 304;    // of them, copied to LDS per lane at a k_play 
 
 constexpr int kBlock = 256;
 constexpr int kDeckStride = 108;  // 27 dwords: odd dword stride -> conflict-free LDS lanes
+constexpr int kDealStride = 212;  // deck (108) + swap targets (104): 53 dwords, odd as well
 
 // ---------------------------------------------------------------- rng glue
 // PF = MT19937 refills prefetched ahead (MtGenT); Philox ignores it.
@@ -298,6 +299,63 @@ struct RingPipe {
     __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf, true); }
 };
 
+// Phase (A) of deck_shuffle2 on the pipelined ring: the words are read
+// straight from the LDS window by stream position (no byte buffer: appending
+// and dropping a variable number of bytes is a long 64-bit shift chain), the
+// next pass's 8 bytes prefetched while this pass decodes.  Same words, same
+// targets as the generic form.
+__device__ __forceinline__ uint64_t pipe_peek8(const RingPipe& r, uint32_t t) {
+    const uint32_t p = r.off + t, a8 = p & ~7u, sh = 8u * (p & 7u);
+    const uint64_t lo = *(const uint64_t*)(r.slot + a8);
+    const uint64_t hi = *(const uint64_t*)(r.slot + a8 + 8u);
+    return sh ? ((lo >> sh) | (hi << (64u - sh))) : lo;
+}
+
+__device__ __forceinline__ void shuffle_targets(RingPipe& rng, ByteBuf& buf, uint8_t* jslot, int C) {
+    uint32_t t = rng.take - buf.cnt;  // next unconsumed byte (buffered bytes are re-read from the window)
+    buf.clear();
+    uint32_t i = (uint32_t)C - 1u;
+    uint64_t w = 0ull;
+    uint32_t valid = 8u;
+    if (t + 8u <= rng.win) {
+        w = pipe_peek8(rng, t);
+    } else {
+        const uint32_t left = (rng.avail > t) ? rng.avail - t : 0u;
+        const PipeSlow r = pipe_slow(rng.ring, rng.B, rng.g, rng.c0 + t, left, rng.err);
+        w = r.bytes, valid = r.k;
+    }
+    while (i >= 1u) {
+        const uint32_t tn = t + 8u;
+        const bool fast_next = tn + 8u <= rng.win;
+        const uint64_t wn = fast_next ? pipe_peek8(rng, tn) : 0ull;  // speculative: a full pass
+        uint32_t used = 0u, ii = i;
+#pragma unroll
+        for (uint32_t q = 0; q < 8u; q++) {
+            const bool act = (q < valid) && (ii >= 1u);
+            const uint32_t m = 0xFFFFFFFFu >> __builtin_clz(ii | 1u);
+            const uint32_t x = (uint32_t)(w >> (8u * q)) & m;
+            const bool acc = act && (x <= ii);
+            jslot[acc ? (uint32_t)C - 1u - ii : 103u] = (uint8_t)x;
+            ii -= acc ? 1u : 0u;
+            used = act ? q + 1u : used;
+        }
+        i = ii;
+        t += used;
+        if (i >= 1u) {
+            if (used == 8u && fast_next) {
+                w = wn, valid = 8u;
+            } else if (t + 8u <= rng.win) {
+                w = pipe_peek8(rng, t), valid = 8u;
+            } else {
+                const uint32_t left = (rng.avail > t) ? rng.avail - t : 0u;
+                const PipeSlow r = pipe_slow(rng.ring, rng.B, rng.g, rng.c0 + t, left, rng.err);
+                w = r.bytes, valid = r.k;
+            }
+        }
+    }
+    rng.take = t;
+}
+
 // bytes of a lane's LDS window for RingPipe (chunk-aligned copy + 8 for the funnel's second read)
 constexpr int kPipeSlot = ((kPipeWin + 15 + 15) / 16) * 16 + 8;
 
@@ -438,11 +496,15 @@ __device__ __forceinline__ void deal_from(const D& deck, int C, Game<N>& G) {
 // itself has already moved, and writes back in order.  A swap at step k
 // writes positions i_k (never read again: later positions are all < i_k)
 // and j_k; a later read aliases only an earlier j_k.
-template <int N, class R>
-__device__ __forceinline__ void deal_shuffle(R& rng, ByteBuf& buf, uint8_t* deck, int C, Game<N>& G) {
+template <class R>
+__device__ __forceinline__ uint32_t deck_shuffle(R& rng, ByteBuf& buf, uint8_t* deck, int C) {
+    uint32_t passes = 0u;
     for (int i = 0; i < C; i += 4) *(uint32_t*)(deck + i) = (uint32_t)i * 0x01010101u + 0x03020100u;
     uint32_t i = (uint32_t)C - 1u;
     while (i >= 1u) {
+        // a full 8-word window every pass (a pass over fewer words is a
+        // wasted LDS round trip for the whole wave)
+        if (__any(buf.cnt < 8u)) rng.topup(buf);
         if (buf.cnt == 0u) rng.force(buf);
         const uint32_t valid = min(buf.cnt, 8u);
         const uint64_t w = buf.b0;
@@ -480,8 +542,116 @@ __device__ __forceinline__ void deal_shuffle(R& rng, ByteBuf& buf, uint8_t* deck
         }
         i = ii;
         buf.drop(used);
+        passes++;
     }
-    // deal: hands from the first 10N bytes (4-B aligned slot), rows from the end
+    return passes;
+}
+
+// Two-phase form of the same shuffle (deck_shuffle2, used by k_play and
+// k_reset).  The swap targets depend on the words only, never on the deck,
+// and the positions do not even depend on the words: step k swaps position
+// i = C-1-k with j_k.  So
+//  (A) shuffle_targets walks the words as above (8 per pass, full windows)
+//      and only records j_k in the lane's target slot (one branch-free byte
+//      store per word; a rejected word stores to a dummy byte);
+//  (B) shuffle_apply then performs the swaps 8 steps per LDS round trip in
+//      lockstep over the wave: the i side of a batch sits at the same
+//      positions in every lane (conflict-free reads and writes), the values a
+//      batch itself moves are forwarded in registers, and a batch is exactly
+//      8 swaps (a pass of (A) averages ~5.6 accepted words).
+// Same words consumed, same permutation: pinned by every deal parity test.
+template <class R>
+__device__ __forceinline__ void shuffle_targets(R& rng, ByteBuf& buf, uint8_t* jslot, int C) {
+    uint32_t i = (uint32_t)C - 1u;
+    while (i >= 1u) {
+        if (__any(buf.cnt < 8u)) rng.topup(buf);
+        if (buf.cnt == 0u) rng.force(buf);
+        const uint32_t valid = min(buf.cnt, 8u);
+        const uint64_t w = buf.b0;
+        uint32_t used = 0u, ii = i;
+#pragma unroll
+        for (uint32_t q = 0; q < 8u; q++) {
+            const bool act = (q < valid) && (ii >= 1u);
+            const uint32_t m = 0xFFFFFFFFu >> __builtin_clz(ii | 1u);
+            const uint32_t x = (uint32_t)(w >> (8u * q)) & m;
+            const bool acc = act && (x <= ii);
+            jslot[acc ? (uint32_t)C - 1u - ii : 103u] = (uint8_t)x;  // step C-1-i; 103 = dummy (C-2 <= 102)
+            ii -= acc ? 1u : 0u;
+            used = act ? q + 1u : used;
+        }
+        i = ii;
+        buf.drop(used);
+    }
+}
+
+__device__ __forceinline__ void shuffle_apply(uint8_t* deck, const uint8_t* jslot, int C) {
+    // C % 8 == 0 (104 cards): every batch's i side is the 4-aligned run
+    // [i0-7, i0] and its targets the 4-aligned run jslot[k0, k0+8), so they
+    // move as dwords
+    const bool al = (C & 7) == 0;
+    for (int i0 = C - 1; i0 >= 1; i0 -= 8) {  // wave-uniform: steps i0, i0-1, .. (at most 8, all >= 1)
+        const int ns = min(8, i0);
+        const int k0 = C - 1 - i0;
+        uint32_t I[8], J[8], DI[8], DJ[8];
+        if (al) {
+            const uint32_t j0 = *(const uint32_t*)(jslot + k0), j1 = *(const uint32_t*)(jslot + k0 + 4);
+            const uint32_t d0 = *(const uint32_t*)(deck + i0 - 7), d1 = *(const uint32_t*)(deck + i0 - 3);
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                I[q] = (q < ns) ? (uint32_t)(i0 - q) : 0u;
+                J[q] = (q < ns) ? (((q < 4 ? j0 : j1) >> (8 * (q & 3))) & 0xFFu) : 0u;
+                // position i0 - q is byte 7 - q of the run: d1 holds bytes 4..7
+                // (the padded last batch has i0 = 7: its pad position 0 is byte 0 of the run)
+                DI[q] = ((q < 4 ? d1 : d0) >> (8 * (3 - (q & 3)))) & 0xFFu;
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) DJ[q] = deck[J[q]];
+        } else {
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                // a batch past step i = 1 pads with self-swaps of position 0 (no-ops)
+                I[q] = (q < ns) ? (uint32_t)(i0 - q) : 0u;
+                J[q] = (q < ns) ? (uint32_t)jslot[k0 + q] : 0u;
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                DI[q] = deck[I[q]];
+                DJ[q] = deck[J[q]];
+            }
+        }
+        // forwarding: within the batch only position j_m (m < q) was written
+        // (with DI[m]); the i side is never read again (later j, i < i_m)
+#pragma unroll
+        for (int q = 1; q < 8; q++)
+#pragma unroll
+            for (int m = 0; m < q; m++) {  // ascending: the latest write wins
+                DI[q] = (J[m] == I[q]) ? DI[m] : DI[q];
+                DJ[q] = (J[m] == J[q]) ? DI[m] : DJ[q];
+            }
+#pragma unroll
+        for (int q = 0; q < 8; q++) deck[J[q]] = (uint8_t)DI[q];
+        if (al && ns == 8) {  // the final values of positions i0-7 .. i0
+            *(uint32_t*)(deck + i0 - 3) = DJ[3] | (DJ[2] << 8) | (DJ[1] << 16) | (DJ[0] << 24);
+            *(uint32_t*)(deck + i0 - 7) = DJ[7] | (DJ[6] << 8) | (DJ[5] << 16) | (DJ[4] << 24);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 8; q++) deck[I[q]] = (uint8_t)DJ[q];
+        }
+    }
+}
+
+// deck (kDeckStride bytes) followed by the swap-target slot
+template <class R>
+__device__ __forceinline__ void deck_shuffle2(R& rng, ByteBuf& buf, uint8_t* slot, int C) {
+    shuffle_targets(rng, buf, slot + kDeckStride, C);
+    for (int i = 0; i < C; i += 4) *(uint32_t*)(slot + i) = (uint32_t)i * 0x01010101u + 0x03020100u;
+    shuffle_apply(slot, slot + kDeckStride, C);
+}
+
+// env.py:99-112 _deal from the shuffled deck in this lane's LDS slot
+template <int N>
+__device__ __forceinline__ void deal_from_deck(const uint8_t* deck, int C, Game<N>& G) {
+    // hands from the first 10N bytes (4-B aligned slot), rows from the end
     constexpr int NW = (kHand * N + 3) / 4;
     uint32_t dw[NW];
 #pragma unroll
@@ -498,6 +668,12 @@ __device__ __forceinline__ void deal_shuffle(R& rng, ByteBuf& buf, uint8_t* deck
     G.b.lo.x = r0, G.b.lo.y = r1, G.b.lo.z = r2, G.b.lo.w = r3;
     G.b.hi.x = meta_row(r0), G.b.hi.y = meta_row(r1), G.b.hi.z = meta_row(r2), G.b.hi.w = meta_row(r3);
     G.n = kHand;
+}
+
+template <int N, class R>
+__device__ __forceinline__ void deal_shuffle(R& rng, ByteBuf& buf, uint8_t* deck, int C, Game<N>& G) {
+    deck_shuffle(rng, buf, deck, C);
+    deal_from_deck<N>(deck, C, G);
 }
 
 // ---------------------------------------------------------------- observation
@@ -579,6 +755,16 @@ inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBloc
     } while (0)
 
 // instantiate BODY with constexpr int NN = N_ for N in 1..10
+// (SECHS_DEV_ONLY_N: a development build that instantiates one player count
+// only, to iterate on kernels without the full 3-minute compile)
+#ifdef SECHS_DEV_ONLY_N
+#define SN_DISPATCH_N(N_, BODY)                                                              \
+    if ((N_) == SECHS_DEV_ONLY_N) {                                                          \
+        constexpr int NN = SECHS_DEV_ONLY_N;                                                 \
+        BODY;                                                                                \
+    } else                                                                                   \
+        return ::sechs::set_error(SN_EUNSUPPORTED, "development build: one player count only");
+#else
 #define SN_DISPATCH_N(N_, BODY)                                                          \
     switch (N_) {                                                                        \
         case 1: { constexpr int NN = 1; BODY; } break;                                   \
@@ -593,6 +779,7 @@ inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBloc
         case 10: { constexpr int NN = 10; BODY; } break;                                 \
         default: return ::sechs::set_error(SN_EINVAL, "num_players out of range");      \
     }
+#endif
 
 }  // namespace sechs
 

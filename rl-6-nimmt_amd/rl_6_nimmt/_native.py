@@ -68,6 +68,7 @@ SIGNATURES = {
     "sn_set_option": ([_P, _I, _I], _I),
     "sn_pipe_errors": ([_P, _P], _I),
     "sn_kernel_times": ([_P, _P, _P, _P], _I),
+    "sn_debug_phases": ([_P, _I], _I),
     "sn_mcs_memorize": ([_P, _P, _I, _P], _I),
     "sn_mcs_rollouts": ([_P, _P, _I, _U64, ctypes.c_uint32, _P, _P], _I),
     "sn_mcs_rollouts_ex": ([_P, _P, _I, _U64, ctypes.c_uint32, _P, _P, _P], _I),

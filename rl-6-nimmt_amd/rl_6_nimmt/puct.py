@@ -33,6 +33,9 @@ def make_actor(hidden_sizes=(100, 100), activation=None):
 class BatchedPUCT:
     def __init__(self, env, actor, mc_per_card=10, mc_max=100, c_puct=2.0, seed=0, seats_mask=None, puct_root=True,
                  net_dtype=torch.bfloat16, mcs_num_cards=104):
+        # `actor` stays where the caller keeps it (the drop-in agents run it
+        # on the host): inference uses a device copy in net_dtype (sync_net),
+        # the training losses run on the actor's own device (actor_device).
         self.env, self.actor = env, actor
         self.mc_per_card, self.mc_max, self.c_puct = mc_per_card, mc_max, float(c_puct)
         self.seed = int(seed)
@@ -68,6 +71,9 @@ class BatchedPUCT:
             net.eval()
             self._net, self._net_version = net, version
         return self._net
+
+    def actor_device(self):
+        return next(self.actor.parameters()).device
 
     def _logits(self, rows):
         with torch.no_grad():
@@ -117,9 +123,19 @@ class BatchedPUCT:
         nat.check(L.sn_puct_choose(h, ctypes_ref(q), nat.ptr(self.actions), nat.ptr(self.best_index), st),
                   "sn_puct_choose")
         if record and n > 1:
-            self.decisions.append((rows.float(), n, self.best_index.clone()))
+            self.decisions.append((self._train_rows(q, n, rows), n, self.best_index.clone()))
         self.step_id += 1
         return self.actions
+
+    def _train_rows(self, q, n, rows):
+        """the root rows of a recorded decision in fp32, as the reference's
+        training forward sees them (inference may run on bf16 rows)"""
+        if rows.dtype == torch.float32:
+            return rows.clone()
+        r32 = torch.empty((self.D * n, ROW), dtype=torch.float32, device=self.env.device)
+        nat.check(nat.lib().sn_puct_root_rows(self.env._h, ctypes_ref(q), nat.ptr(r32), 0, self.env._stream()),
+                  "sn_puct_root_rows")
+        return r32
 
     def play_episode(self, others=None, record=False):
         """One whole game of every env game; deciding seats search, the other
@@ -151,13 +167,14 @@ class BatchedPUCT:
         """-sum over recorded decisions of log pi(chosen root move) under the
         current weights (the reference stores log(probs[best]) from the
         rollout that first chose it -- same weights during an episode, so the
-        same value)."""
-        dev_actor = self.actor.to(self.env.device)
-        loss = torch.zeros((), device=self.env.device)
+        same value).  n == 1 decisions play without search and add log 1 = 0
+        (mcts.py:50-51), so they are not recorded."""
+        dev = self.actor_device()
+        loss = torch.zeros((), device=dev)
         for rows, n, best in self.decisions:
-            (logits,) = dev_actor(rows)
+            (logits,) = self.actor(rows.to(dev))
             logp = torch.log_softmax(logits.reshape(-1, n), dim=1)
-            loss = loss - logp.gather(1, best.long()[:, None]).sum()
+            loss = loss - logp.gather(1, best.to(dev).long()[:, None]).sum()
         return loss
 
 
@@ -206,7 +223,7 @@ class BatchedPUCTCustomed(BatchedPUCT):
         nat.check(L.sn_pcv_choose(h, ctypes_ref(q), nat.ptr(heads), nat.ptr(self.actions), nat.ptr(self.best_index),
                                   nat.ptr(self.log_prob), nat.ptr(self.value), st), "sn_pcv_choose")
         if record:
-            self.decisions.append((rows.float(), n, self.best_index.clone()))
+            self.decisions.append((self._train_rows(q, n, rows), n, self.best_index.clone()))
         self.step_id += 1
         return self.actions
 
@@ -234,15 +251,16 @@ class BatchedPUCTCustomed(BatchedPUCT):
     def loss(self, per_step=None):
         """reference loss of the recorded episode (mcts.py:431-451), summed over games"""
         per_step = self.episode_rewards if per_step is None else per_step
-        dev_actor = self.actor.to(self.env.device)
-        target = self._decider_rewards(per_step)[:-1].sum(dim=0).float()  # [D]
+        dev = self.actor_device()
+        target = self._decider_rewards(per_step)[:-1].sum(dim=0).float().to(dev)  # [D]
         logps, values = [], []
         for rows, n, best in self.decisions:
-            (out,) = dev_actor(rows)
+            (out,) = self.actor(rows.to(dev))
             out = out.reshape(-1, n, 2)
+            best = best.to(dev).long()[:, None]
             logp = torch.log_softmax(out[:, :, 0], dim=1)
-            logps.append(logp.gather(1, best.long()[:, None])[:, 0])
-            values.append(out[:, :, 1].gather(1, best.long()[:, None])[:, 0])
+            logps.append(logp.gather(1, best)[:, 0])
+            values.append(out[:, :, 1].gather(1, best)[:, 0])
         logps, values = torch.stack(logps, dim=1), torch.stack(values, dim=1)  # [D, steps]
         outcome_loss = ((values - target[:, None]) ** 2).mean(dim=1)
         policy_loss = -logps.sum(dim=1)

@@ -47,7 +47,7 @@ class BatchedReinforce(BatchedPUCT):
         nat.check(L.sn_policy_sample(h, ctypes_ref(q), nat.ptr(logits), nat.ptr(self.actions), nat.ptr(self.best_index),
                                      nat.ptr(self.log_prob), nat.ptr(self.entropy), st), "sn_policy_sample")
         if record:
-            self.decisions.append((rows.float(), n, self.best_index.clone()))
+            self.decisions.append((self._train_rows(q, n, rows), n, self.best_index.clone()))
         self.step_id += 1
         return self.actions
 
@@ -85,17 +85,17 @@ class BatchedReinforce(BatchedPUCT):
     def loss(self, per_step=None):
         """policy.py:174-196 summed over games, on the recorded rows"""
         per_step = self.episode_rewards if per_step is None else per_step
-        dev_actor = self.actor.to(self.env.device)
+        dev = self.actor_device()
         logps, ents = [], []
         for rows, n, idx in self.decisions:
-            (logits,) = dev_actor(rows)
+            (logits,) = self.actor(rows.to(dev))
             logp = torch.log_softmax(logits.reshape(-1, n), dim=1)
-            logps.append(logp.gather(1, idx.long()[:, None])[:, 0])
+            logps.append(logp.gather(1, idx.to(dev).long()[:, None])[:, 0])
             ents.append(-(logp.exp() * logp).sum(dim=1))
         logps, ents = torch.stack(logps, dim=1), torch.stack(ents, dim=1)  # [D, T]
         T = logps.shape[1]
-        G = self.returns(per_step)[:, :T]
-        disc = torch.exp(np.log(self.gamma) * torch.linspace(0, T - 1, T)).to(self.env.device)
+        G = self.returns(per_step)[:, :T].to(dev)
+        disc = torch.exp(np.log(self.gamma) * torch.linspace(0, T - 1, T)).to(dev)
         actor_loss = -(disc[None, :] * G * logps).sum()
         entropy_loss = -ents.sum()
         return self.actor_weight * actor_loss + self.entropy_weight * entropy_loss

@@ -109,3 +109,44 @@ def test_stratified_engine_matches_oracle(N):
                 assert acts[g, p] == G.hands[p][best]
         rew, done, inv = env.step(torch.from_numpy(acts))
         assert (inv.cpu().numpy() == -1).all()
+
+
+def test_stratified_engine_matches_oracle_at_bench_rollouts():
+    """BASELINE config 3's search size -- 256 playouts per legal move -- on a
+    256-game subset of the bench's batch (4 MCS seats, philox), every
+    decision of every seat bit-exact against the oracle's stratified MCS
+    (the oracle runs in parallel threads: its C calls release the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from rl_6_nimmt.mcs import BatchedMCS
+    from rl_6_nimmt.vec_env import VecSechsNimmtEnv
+
+    B, N, R, seed = 256, 4, 256, 0xBEEF
+    env = VecSechsNimmtEnv(B, N, seed=1, rng="philox")
+    env.reset()
+    mcs = BatchedMCS(env, rollouts=R, seed=seed)
+    mem = [[[] for _ in range(N)] for _ in range(B)]
+    pool = ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1))
+    for step in range(10):
+        board, hands = env.board().cpu().numpy(), env.hands().cpu().numpy()
+        acts = mcs.decide(step_id=step).cpu().numpy()
+        sums = mcs.sums.cpu().numpy().reshape(B, N, 10)
+        games = [_oracle_game(board[g], hands[g], N) for g in range(B)]
+        for g in range(B):
+            for p in range(N):
+                mem[g][p] = O.mcs_memorize(mem[g][p], games[g], p)
+
+        def one(gp):
+            g, p = gp
+            return O.mcs_stratified(games[g], p, mem[g][p], R, seed, step, g)
+
+        refs = list(pool.map(one, [(g, p) for g in range(B) for p in range(N)]))
+        for i, ref in enumerate(refs):
+            g, p = divmod(i, N)
+            assert np.array_equal(sums[g, p], ref), (step, g, p)
+            n = len(games[g].hands[p])
+            best = int(np.argmax(ref[:n])) if n > 1 else 0
+            assert acts[g, p] == games[g].hands[p][best], (step, g, p)
+        rew, done, inv = env.step(torch.from_numpy(acts))
+        assert (inv.cpu().numpy() == -1).all()
+    pool.shutdown()

@@ -112,6 +112,111 @@ def test_root_probs_match_reference_policy():
         assert np.allclose(probs[p], z["probs"][p], atol=1e-5), p
 
 
+def test_root_probs_bf16_match_reference_policy():
+    """The bench's net dtype: bf16 rows, weights and activations (8-bit
+    mantissa, ~0.4 % relative per rounding) against the reference's fp32
+    probabilities (golden F8).  Tolerance |dp| <= 3e-3 on these ~0.1
+    probabilities: 3x the worst error of the same bf16 forward on the host
+    CPU (1.05e-3)."""
+    z = np.load(os.path.join(GOLDEN, "puct_policy.npz"))
+    weights = {k: torch.from_numpy(z[k]) for k in z.files if "net" in k}
+    env, eng = _engine(B=1, weights=weights, dtype=torch.bfloat16)
+    b = np.full((1, 4, 6), -1, dtype=np.int8)
+    s = z["states"][0]
+    for r in range(4):
+        row = [c for c in s[23 + 6 * r: 29 + 6 * r] if c >= 0]
+        b[0, r, : len(row)] = row
+    h = np.stack([z["legal"][p] for p in range(4)])[None].astype(np.int8)
+    env.reset_to(torch.from_numpy(b), torch.from_numpy(h))
+    eng.decide(10)
+    probs = eng.root_probs.cpu().numpy()
+    for p in range(4):
+        assert np.allclose(probs[p], z["probs"][p], rtol=0, atol=3e-3), (p, np.abs(probs[p] - z["probs"][p]).max())
+        assert abs(probs[p].sum() - 1.0) < 1e-5
+
+
+def test_playout_sampling_follows_the_policy():
+    """k_puct_step's Categorical(probs).sample() (mcts.py:209-217) with
+    Philox uniforms: the same position in every game, the root move SAMPLED
+    (puct_root=False), 64 playouts per decision -> 131 072 samples of the
+    root policy; per-move frequencies within 5 standard errors of
+    softmax(logits) computed on the host from the same fp32 net."""
+    from rl_6_nimmt.utils.preprocessing import SechsNimmtStateNormalization
+    from rl_6_nimmt.puct import BatchedPUCT, make_actor
+    from rl_6_nimmt.vec_env import VecSechsNimmtEnv
+
+    B = 2048
+    env = VecSechsNimmtEnv(B, 4, seed=21, rng="philox")
+    env.reset()
+    b = env.board()[:1].expand(B, -1, -1).contiguous()
+    h = env.hands()[:1].expand(B, -1, -1).contiguous()
+    env.reset_to(b, h)
+    torch.manual_seed(3)
+    actor = make_actor()
+    with torch.no_grad():  # a peaked policy, so the check has teeth
+        actor.head_nets[0][0].weight.mul_(40.0)
+    eng = BatchedPUCT(env, actor, mc_per_card=10, mc_max=64, seed=5, seats_mask=0b0001, puct_root=False,
+                      net_dtype=torch.float32)
+    eng.decide(10)
+    visits = eng.stats.cpu().numpy()[:, 10:20].sum(axis=0).astype(np.float64)
+    total = visits.sum()
+    assert total == B * 64
+    obs = env.obs(torch.int64).float().cpu()[0, 0]
+    hand = h[0, 0].long().cpu()
+    x = torch.cat((hand.float()[:, None], obs[None, :].expand(10, -1)), dim=1)
+    with torch.no_grad():
+        (logits,) = actor(SechsNimmtStateNormalization(action=True)(x))
+    probs = torch.softmax(logits.flatten().double(), 0).numpy()
+    assert probs.max() > 3 * probs.min(), probs  # far from uniform
+    assert np.allclose(eng.root_probs.cpu().numpy()[0], probs, atol=1e-5)
+    freq = visits / total
+    se = np.sqrt(probs * (1 - probs) / total)
+    assert np.all(np.abs(freq - probs) <= 5 * se + 1e-7), (freq, probs)
+
+
+def test_policy_loss_matches_reference_training_loss():
+    """BatchedPUCT.policy_loss == PolicyMCSAgent._train (mcts.py:245-261):
+    -sum over the episode's searched decisions of log pi(chosen root move),
+    pi = softmax(actor(SechsNimmtStateNormalization([card, obs]))) with the
+    reference's fp32 rows (mcts.py:219-228) -- value and gradient, although
+    the search ran a bf16 net (training rows are recorded in fp32)."""
+    from rl_6_nimmt.utils.preprocessing import SechsNimmtStateNormalization
+
+    env, eng = _engine(B=32, dtype=torch.bfloat16, mc_max=8, mc_per_card=2, seed=13)
+    env.reset()
+    norm = SechsNimmtStateNormalization(action=True)
+    seen = []
+    for t in range(10):
+        n = 10 - t
+        obs = env.obs(torch.int64).float().cpu()
+        hands = env.hands().long().cpu()
+        acts = eng.decide(n, record=True)
+        if n > 1:
+            seen.append((obs, hands, n, eng.best_index.cpu().clone()))
+        rew, done, inv = env.step(acts)
+        assert (inv.cpu() == -1).all()
+    assert len(eng.decisions) == 9
+    loss = eng.policy_loss()
+    grads = torch.autograd.grad(loss, list(eng.actor.parameters()))
+    loss = loss.detach()
+    ref = torch.zeros(())
+    N = env.num_players
+    for obs, hands, n, best in seen:
+        for g in range(env.num_games):
+            for p in range(N):
+                x = torch.cat((hands[g, p, :n].float()[:, None], obs[g, p][None, :].expand(n, -1)), dim=1)
+                (logits,) = eng.actor(norm(x))
+                probs = torch.softmax(logits, dim=0).flatten()
+                ref = ref - torch.log(probs[int(best[g * N + p])])
+    rgrads = torch.autograd.grad(ref, list(eng.actor.parameters()))
+    ref = ref.detach()
+    assert abs(float(loss) - float(ref)) <= 1e-5 * abs(float(ref)), (float(loss), float(ref))
+    # (the head bias's gradient is a sum of softmax residuals that is 0 in
+    # exact arithmetic: compare at an absolute floor of 1e-4)
+    for a, r in zip(grads, rgrads):
+        assert torch.allclose(a.cpu(), r, rtol=1e-4, atol=1e-4), (a, r)
+
+
 def test_search_statistics_consistent():
     env, eng = _engine(B=32, mc_max=12, mc_per_card=2)
     for t in range(10):
@@ -278,12 +383,12 @@ def test_batched_customed_matches_host_agent_math(mask):
             d = g * len(seats) + j
             vals, lps = [], []
             for rows, n, best in eng.decisions:
-                (out,) = actor(rows[d * n:(d + 1) * n])
+                (out,) = actor(rows[d * n:(d + 1) * n].cpu())
                 k = int(best[d])
                 vals.append(out[k, 1])
                 lps.append(torch.log_softmax(out[:, 0], 0)[k])
             target = float(per_step[:-1, g, p].sum())
-            ref = ref + torch.nn.functional.mse_loss(torch.stack(vals), torch.full((10,), target, device=env.device)) \
+            ref = ref + torch.nn.functional.mse_loss(torch.stack(vals), torch.full((10,), target)) \
                 - torch.stack(lps).sum()
     assert abs(float(loss) - float(ref)) <= 1e-4 * abs(float(ref)), (float(loss), float(ref))
 

@@ -148,7 +148,7 @@ def test_batched_reinforce_sample_outputs_and_loss(mask):
             G = compute_discounted_returns(seen, 0.95)
             lps, ents = [], []
             for rows, n, idx in eng.decisions:
-                (logits,) = actor(rows[d * n:(d + 1) * n])
+                (logits,) = actor(rows[d * n:(d + 1) * n].cpu())
                 logp = torch.log_softmax(logits.flatten(), 0)
                 lps.append(logp[int(idx[d])])
                 ents.append(-(logp.exp() * logp).sum())

@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Quick N=4 parity check for kernel iteration (test infrastructure: uses the
+oracle as the checker).  Full-size k_play rollouts -- numpy-MT (pipelined,
+the bench path) and philox, with int8 obs -- against oracle.VecOracle.
+Usage: SECHS_LIB=... python tools/dev_parity.py [games] [steps]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "rl-6-nimmt_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from oracle import oracle as O  # noqa: E402
+from rl_6_nimmt.vec_env import VecSechsNimmtEnv  # noqa: E402
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    T = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+    N = 4
+    for rng, mode in (("numpy", O.RNG_NUMPY_MT), ("philox", O.RNG_PHILOX)):
+        for want_obs in (True, False):
+            env = VecSechsNimmtEnv(B, N, seed=11, rng=rng, device="cuda:0")
+            env.reset()
+            ref = O.VecOracle(B, N, rng_mode=mode, seed=11)
+            ref.reset()
+            ok = True
+            for chunk in (10, 10, T - 20):
+                out = env.rollout(chunk, want_actions=True, want_obs=want_obs)
+                rr, rd, ra, ro = ref.rollout(chunk, want_obs=want_obs, nthreads=8)
+                torch.cuda.synchronize()
+                ok &= np.array_equal(out["rewards"].cpu().numpy(), rr)
+                ok &= np.array_equal(out["actions"].cpu().numpy(), ra)
+                ok &= np.array_equal(out["done"].cpu().numpy(), rd)
+                if want_obs:
+                    ok &= np.array_equal(out["obs"].cpu().numpy()[..., :47], ro)
+            perr = env.pipe_errors() if rng == "numpy" else 0
+            print(f"parity {rng} obs={want_obs} B={B} T={T}: {'OK' if ok and perr == 0 else 'FAIL'} perr={perr}",
+                  flush=True)
+            if not ok or perr:
+                sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()
