@@ -172,6 +172,40 @@ sn_status sn_kernel_times(sn_env* env, float* play_ms, float* ahead_ms, int32_t*
    SN_EUNSUPPORTED [sync]. */
 sn_status sn_debug_phases(uint64_t* out, int n);
 
+/* ---- Batched tournament (tournament.py:132-177) ------------------------
+   A tournament handle plays one league game per game slot at a time: slot
+   g is the reference's `np.random.seed(seed + game_offset + g); t =
+   Tournament(min_players, max_players) over num_agents DrunkHamster
+   agents; t.play_game() x games` -- every game first draws its seats
+   (_choose_players: num_players = choice(range(min, max+1)), agents =
+   choice(num_agents, num_players, replace=False)), then GameSession deals
+   and plays it, all from the slot's own stream.  The handle's num_players
+   is max_players; seats past a game's player count hold empty hands and
+   play nothing.  In-kernel DrunkHamster seats only (the search agents play
+   through the drop-in Tournament).  Elo (order dependent) is replayed on
+   the host from the records (sn_elo_replay). */
+/* turn a handle (num_players = max_players, 2..6) into a tournament of
+   num_agents (max_players..16) agents; 0 agents turns it back.  The next
+   sn_reset draws every slot's first seats and deals [sync]. */
+sn_status sn_league_config(sn_env* env, int num_agents, int min_players, int max_players);
+/* play steps/10 whole games per slot (auto-reset: each finished game's
+   slot draws its next seats and deals).  records: [steps/10][B][1 + N]
+   int32 per finished game: seats word (k | agent(seat p) << (4 + 4p)),
+   then the N results (GameSession.results[0]: -penalties; 0 past k).
+   rewards/done/actions/obs as sn_rollout (may be NULL). */
+sn_status sn_league_rollout(sn_env* env, int steps, int32_t* rewards, uint8_t* done, uint8_t* actions, int8_t* obs,
+                            int obs_stride, int32_t* records, void* stream);
+/* the seats word of every slot's current game, [B] uint32 */
+sn_status sn_league_seats(sn_env* env, uint32_t* out, void* stream);
+/* Sequential multiplayer Elo over game records in the given order (host
+   memory, no GPU): records [G][1 + max_players] int32 as sn_league_rollout
+   writes them; elos [num_agents] float64 in/out (initial ratings in).
+   Places are Tournament._compute_absolute_positions of the k results,
+   ratings update by the multiplayer Elo of rl_6_nimmt/elo.py (multi_elo's
+   scheme; parity unpinned: multi_elo is absent). */
+sn_status sn_elo_replay(const int32_t* records_host, int64_t num_games, int max_players, int num_agents, double elo_k,
+                        double* elos_host);
+
 /* ---- Monte-Carlo search, MCSAgent (agents/mcts.py:17-188) ------------- */
 
 /* Card memory of every seat (mcts.py:62-73), updated in place from the

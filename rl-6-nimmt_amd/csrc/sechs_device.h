@@ -202,7 +202,9 @@ __device__ __forceinline__ uint32_t place_card(Board& b, uint32_t c) {
 
 // simultaneous play, env.py:120-136: cards in ascending order, each placed
 // in turn.  card[p] must be legal.  pen[p] = bull heads seat p takes.
-template <int N>
+// SKIP: seats whose card is 0xFF (absent: a tournament game with fewer
+// players than the handle's seats) play nothing.
+template <int N, bool SKIP = false>
 __device__ __forceinline__ void resolve(Board& b, const uint32_t (&card)[N], uint32_t (&pen)[N]) {
     uint32_t key[N];
 #pragma unroll
@@ -218,6 +220,7 @@ __device__ __forceinline__ void resolve(Board& b, const uint32_t (&card)[N], uin
     for (int p = 0; p < N; p++) pen[p] = 0u;
 #pragma unroll
     for (int k = 0; k < N; k++) {
+        if (SKIP && (key[k] >> 4) >= 0xFFu) break;  // absent seats sort last
         const uint32_t penalty = place_card(b, key[k] >> 4);
         const uint32_t p = key[k] & 15u;
 #pragma unroll

@@ -6,6 +6,7 @@
 // numpy-compat mode, the MT19937 words (8 per refill, 16-B accesses).
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -39,7 +40,7 @@ __global__ void k_seed(DevState s) {
     s.episodes[g] = 0;
 }
 
-template <int N, int MODE>
+template <int N, int MODE, bool LG = false>
 __global__ __launch_bounds__(kBlock) void k_reset(DevState s, const uint8_t* decks) {
     __shared__ uint8_t lds_deck[kBlock * kDealStride];
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -52,9 +53,17 @@ __global__ __launch_bounds__(kBlock) void k_reset(DevState s, const uint8_t* dec
         typename RngOf<MODE>::T rng;
         ByteBuf buf;
         RngOf<MODE>::load(s, g, rng, buf);
+        uint32_t lg = 0u;
+        if (LG) lg = league_draw(rng, buf, s.lg_K, s.lg_lo, s.lg_hi);  // Tournament.play_game: seats, then the deal
         uint8_t* slot = lds_deck + threadIdx.x * kDealStride;
         deck_shuffle2(rng, buf, slot, s.C);
         deal_from_deck<N>(slot, s.C, G);
+        if (LG) {
+#pragma unroll
+            for (int p = 0; p < N; p++)
+                if ((uint32_t)p >= (lg & 15u)) G.hand[p].lo = ~0ull, G.hand[p].hi = ~0u;
+            s.lgs[g] = lg;
+        }
         RngOf<MODE>::store(s, g, rng, buf);
     }
     store_game<N>(s, g, G);
@@ -413,6 +422,8 @@ struct PlayArgs {
     uint8_t* actions_out;    // [steps][B][N]
     int8_t* obs;             // [steps][B][N][obs_stride]
     int32_t* invalid;        // [B]
+    int32_t* league_rec;     // league: [episodes][B][1 + N] per finished game: seats word, results
+    int step0;               // league: env-steps of this rollout before this launch (episode index of a record)
 };
 
 // The env-step loop of one lane (game g).  R supplies the random words
@@ -422,10 +433,10 @@ struct PlayArgs {
 // are assembled so that they leave as 1-KB contiguous stores instead of 64
 // scattered 16-B pieces per instruction.  (Both uses never overlap in time
 // within a step: observations first, the deal at the very end.)
-template <int N, class R, int GPW = 64>
+template <int N, class R, int GPW = 64, bool LG = false>
 __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a, int64_t g, int lane, uint8_t* wave_lds,
                                            Game<N>& G, R& rng, ByteBuf& buf, int32_t (&sum_res)[N], int32_t& episodes,
-                                           PhaseProf& pp) {
+                                           PhaseProf& pp, uint32_t& lg) {
     const int64_t B = s.B;
     uint8_t* my_deck = wave_lds + lane * kDealStride;
     const bool staged = a.obs && a.obs_stride == 48;
@@ -438,9 +449,11 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
     uint8_t* dn = a.done ? a.done + g : nullptr;
     int8_t* ob = a.obs ? a.obs + g * N * a.obs_stride : nullptr;
     for (int t = 0; t < a.steps; t++) {
+        const uint32_t kp = LG ? (lg & 15u) : (uint32_t)N;  // players of this game
         if (ob) {
             uint32_t w2hi;
-            const GameWords gw = summ ? game_words<true>(N, G.b, w2hi) : game_words<false>(N, G.b, w2hi);
+            const int nobs = LG ? (int)kp : N;
+            const GameWords gw = summ ? game_words<true>(nobs, G.b, w2hi) : game_words<false>(nobs, G.b, w2hi);
             if (staged) {
                 u32x4* row = (u32x4*)(wave_lds + lane * N * 48);
 #pragma unroll
@@ -490,7 +503,12 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
         } else {
             // DrunkHamster for every seat in seat order (play.py:38-41):
             // legal[random_interval(n-1)], agents/random.py:9
-            rng_draws<N>(rng, buf, G.n - 1u, idx);
+            if (LG && !__all(kp == (uint32_t)N)) {  // a tournament game with fewer players
+#pragma unroll
+                for (int p = 0; p < N; p++) idx[p] = ((uint32_t)p < kp) ? rng_interval(rng, buf, G.n - 1u) : 0u;
+            } else {
+                rng_draws<N>(rng, buf, G.n - 1u, idx);
+            }
 #pragma unroll
             for (int p = 0; p < N; p++) card[p] = hand_get(G.hand[p], idx[p]);
         }
@@ -511,7 +529,7 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
         }
 #pragma unroll
         for (int p = 0; p < N; p++) hand_del(G.hand[p], idx[p]);
-        resolve<N>(G.b, card, pen);
+        resolve<N, LG>(G.b, card, pen);  // absent seats' cards are 0xFF (empty hands)
 #pragma unroll
         for (int p = 0; p < N; p++) G.score[p] += (int32_t)pen[p];
         G.n -= 1u;
@@ -541,11 +559,18 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
             dn += B;
         }
         pp.mark(PH_STORE);
+        if (LG && done && a.league_rec) {  // the finished game's record: seats word, results (-penalty)
+            int32_t* rec = a.league_rec + ((int64_t)((a.step0 + t) / kHand) * B + g) * (1 + N);
+            rec[0] = (int32_t)lg;
+#pragma unroll
+            for (int p = 0; p < N; p++) rec[1 + p] = -G.score[p];
+        }
         if (done && auto_reset) {
             // GameSession.results.append(scores) then the next play_game()
 #pragma unroll
             for (int p = 0; p < N; p++) sum_res[p] -= G.score[p];
             episodes += 1;
+            if (LG) lg = league_draw(rng, buf, s.lg_K, s.lg_lo, s.lg_hi);  // Tournament.play_game: seats first
             // deck_shuffle2 in its two phases (marked apart for the profiler)
             shuffle_targets(rng, buf, my_deck + kDeckStride, s.C);
             pp.mark(PH_DEAL);
@@ -553,6 +578,12 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
             shuffle_apply(my_deck, my_deck + kDeckStride, s.C);
             pp.mark(PH_APPLY);
             deal_from_deck<N>(my_deck, s.C, G);
+            if (LG) {  // a k-player env deals k hands (env.py:108)
+                const uint32_t k2 = lg & 15u;
+#pragma unroll
+                for (int p = 0; p < N; p++)
+                    if ((uint32_t)p >= k2) G.hand[p].lo = ~0ull, G.hand[p].hi = ~0u;
+            }
             pp.mark(PH_HANDS);
         }
     }
@@ -584,7 +615,7 @@ __device__ __forceinline__ void store_results(const DevState& s, int64_t g, int 
 // GPW = games per wave: 64 (one game per lane), or 32 for the pipelined
 // path (lanes 32..63 idle) -- half the LDS per wave, so two blocks fit a CU
 // and a SIMD holds two waves to hide each other's latency
-template <int N, int MODE, int GPW>
+template <int N, int MODE, int GPW, bool LG = false>
 __device__ __forceinline__ void play_body(const DevState& s, const PlayArgs& a, uint8_t* lds_dyn, int tid) {
     const int lane = tid & 63;
     if (GPW < 64 && lane >= GPW) return;
@@ -600,12 +631,13 @@ __device__ __forceinline__ void play_body(const DevState& s, const PlayArgs& a, 
     load_game<N>(s, g, G);
     int32_t sum_res[N], episodes;
     load_results<N>(s, g, a.flags, sum_res, episodes);
+    uint32_t lg = LG ? s.lgs[g] : 0u;
     ByteBuf buf;
     if constexpr (MODE == RNG_NUMPY_PIPE) {
         RingPipe rng;
         rng.load(s, g, buf, wave_lds + a.wave_lds - GPW * a.ring_lds + lane * a.ring_lds, a.pipe_cin, a.pipe_t);
         pp.mark(PH_PROLOGUE);
-        play_steps<N, RingPipe, GPW>(s, a, g, lane, wave_lds, G, rng, buf, sum_res, episodes, pp);
+        play_steps<N, RingPipe, GPW, LG>(s, a, g, lane, wave_lds, G, rng, buf, sum_res, episodes, pp, lg);
         s.pabsc[(int64_t)a.pipe_cout * s.B + g] = rng.consumed(buf);
     } else {
         typename RngOf<MODE, kPlayPrefetch>::T rng;
@@ -616,19 +648,21 @@ __device__ __forceinline__ void play_body(const DevState& s, const PlayArgs& a, 
             RngOf<MODE, kPlayPrefetch>::load(s, g, rng, buf);
         }
         pp.mark(PH_PROLOGUE);
-        play_steps<N>(s, a, g, lane, wave_lds, G, rng, buf, sum_res, episodes, pp);
+        play_steps<N, typename RngOf<MODE, kPlayPrefetch>::T, 64, LG>(s, a, g, lane, wave_lds, G, rng, buf, sum_res,
+                                                                      episodes, pp, lg);
         RngOf<MODE, kPlayPrefetch>::store(s, g, rng, buf);
     }
     store_game<N>(s, g, G);
     store_results<N>(s, g, a.flags, sum_res, episodes);
+    if (LG) s.lgs[g] = lg;
     pp.mark(PH_EPILOGUE);
     pp.flush(lane);
 }
 
-template <int N, int MODE, int GPW = 64>
+template <int N, int MODE, int GPW = 64, bool LG = false>
 __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
-    play_body<N, MODE, GPW>(s, a, lds_dyn, (int)threadIdx.x);
+    play_body<N, MODE, GPW, LG>(s, a, lds_dyn, (int)threadIdx.x);
 }
 
 // obs in any dtype, one thread per (game, seat)
@@ -818,7 +852,7 @@ sn_status sn_destroy(sn_env* e) {
     if (e->side) (void)hipStreamDestroy(e->side);
     free_timing(e);
     void* ps[] = {s.hand, s.row_lo, s.row_hi, s.score, s.sum_res, s.episodes, s.mt_pos, s.ctr, s.mt, s.mt0, s.ring,
-                  s.pring, s.pabsc, s.ptend, s.ptp, s.perr};
+                  s.pring, s.pabsc, s.ptend, s.ptp, s.perr, s.lgs};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     delete e;
@@ -897,7 +931,21 @@ sn_status sn_reset(sn_env* e, const uint8_t* decks, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     if (sn_pipe_sync(e, st) != SN_OK) return SN_EHIP;
     const DevState& s = e->s;
-    if (s.rng_mode == SN_RNG_NUMPY_MT) {
+    if (s.lg_K) {  // a batched tournament: every game draws its seats, then deals (tournament.py:132-138)
+        if (decks) return fail(SN_EINVAL, "a tournament handle deals from its own streams (decks must be NULL)");
+        if (s.rng_mode == SN_RNG_NUMPY_MT) {
+            SN_DISPATCH_N(s.N, {
+                if constexpr (NN >= 2 && NN <= kLeagueMaxPlayers)
+                    hipLaunchKernelGGL((k_reset<NN, RNG_NUMPY_MT, true>), dim3(grid_for(s.B)), dim3(kBlock), 0, st, s, decks);
+            });
+        } else {
+            SN_DISPATCH_N(s.N, {
+                if constexpr (NN >= 2 && NN <= kLeagueMaxPlayers)
+                    hipLaunchKernelGGL((k_reset<NN, RNG_PHILOX, true>), dim3(grid_for(s.B)), dim3(kBlock), 0, st, s, decks);
+            });
+        }
+        e->lg_phase = 0;
+    } else if (s.rng_mode == SN_RNG_NUMPY_MT) {
         SN_DISPATCH_N(s.N, hipLaunchKernelGGL((k_reset<NN, RNG_NUMPY_MT>), dim3(grid_for(s.B)), dim3(kBlock), 0, st, s, decks));
     } else {
         SN_DISPATCH_N(s.N, hipLaunchKernelGGL((k_reset<NN, RNG_PHILOX>), dim3(grid_for(s.B)), dim3(kBlock), 0, st, s, decks));
@@ -969,9 +1017,17 @@ static sn_status launch_play_one(sn_env* e, PlayArgs a, hipStream_t st) {
         });
     } else {
         SN_DISPATCH_N(s.N, {
-            HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_PHILOX>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)shmem));
-            hipLaunchKernelGGL((k_play<NN, RNG_PHILOX>), dim3(grid_for(s.B)), dim3(kBlock), shmem, st, s, a);
+            if (s.lg_K) {
+                if constexpr (NN >= 2 && NN <= kLeagueMaxPlayers) {
+                    HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_PHILOX, 64, true>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
+                    hipLaunchKernelGGL((k_play<NN, RNG_PHILOX, 64, true>), dim3(grid_for(s.B)), dim3(kBlock), shmem, st, s, a);
+                }
+            } else {
+                HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_PHILOX>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)shmem));
+                hipLaunchKernelGGL((k_play<NN, RNG_PHILOX>), dim3(grid_for(s.B)), dim3(kBlock), shmem, st, s, a);
+            }
         });
     }
     HIP_TRY(hipGetLastError());
@@ -1039,6 +1095,7 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     for (int t0 = 0; t0 < a.steps; t0 += chunk) {
         PlayArgs c = a;
         c.steps = min(chunk, a.steps - t0);
+        c.step0 = a.step0 + t0;
         if (a.rewards) c.rewards = a.rewards + (int64_t)t0 * B * N;
         if (a.done) c.done = a.done + (int64_t)t0 * B;
         if (a.actions_out) c.actions_out = a.actions_out + (int64_t)t0 * B * N;
@@ -1055,6 +1112,12 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
                 hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_PIPE, 32>), dim3((unsigned)((s.B + 32 * (kBlock / 64) - 1) / (32 * (kBlock / 64)))),
                                    dim3(kBlock), shmem, st, s, c);
+            } else if (s.lg_K) {
+                if constexpr (NN >= 2 && NN <= kLeagueMaxPlayers) {
+                    HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_PIPE, 64, true>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
+                    hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_PIPE, 64, true>), dim3(grid_for(s.B)), dim3(kBlock), shmem, st, s, c);
+                }
             } else {
                 HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_PIPE>,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
@@ -1078,6 +1141,17 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
 
 static sn_status launch_play(sn_env* e, PlayArgs a, hipStream_t st) {
     const DevState& s = e->s;
+    if (s.lg_K) {  // tournament handles: in-kernel DrunkHamster seats, pipelined numpy-MT or philox
+        if (a.actions) return fail(SN_EUNSUPPORTED, "a tournament handle plays in-kernel DrunkHamster seats only (sn_rollout)");
+        if (!(a.flags & SN_AUTO_RESET)) return fail(SN_EINVAL, "a tournament handle rolls out with SN_AUTO_RESET");
+        if (s.rng_mode == SN_RNG_NUMPY_MT) {
+            int wave;
+            if (!e->pipe || e->pipe_gpw != 64 || pipe_lds(s, a, 64, &wave) > (size_t)kLdsBytes)
+                return fail(SN_EUNSUPPORTED, "tournament rollouts need the pipelined numpy-MT path (64 games per wave)");
+            return launch_pipe(e, a, st);
+        }
+        return launch_play_one(e, a, st);
+    }
     if (s.rng_mode == SN_RNG_NUMPY_MT && !a.actions && e->pipe) {
         int wave;
         if (pipe_lds(s, a, e->pipe_gpw, &wave) <= (size_t)kLdsBytes) return launch_pipe(e, a, st);
@@ -1105,6 +1179,7 @@ static sn_status launch_play(sn_env* e, PlayArgs a, hipStream_t st) {
 sn_status sn_step(sn_env* e, const int32_t* actions, int32_t* rewards, uint8_t* done, int32_t* invalid, int flags,
                   void* stream) {
     if (!e) return fail(SN_EINVAL, "env is NULL");
+    if (e->s.lg_K) return fail(SN_EUNSUPPORTED, "a tournament handle plays whole games with sn_league_rollout");
     PlayArgs a{};
     a.steps = 1;
     a.flags = flags;
@@ -1134,7 +1209,105 @@ sn_status sn_rollout(sn_env* e, int steps, int32_t* rewards, uint8_t* done, uint
     a.done = done;
     a.actions_out = actions;
     a.obs = obs;
+    const sn_status r = launch_play(e, a, (hipStream_t)stream);
+    if (r == SN_OK && e->s.lg_K) e->lg_phase = (e->lg_phase + steps) % kHand;
+    return r;
+}
+
+sn_status sn_league_config(sn_env* e, int num_agents, int min_players, int max_players) {
+    if (!e) return fail(SN_EINVAL, "env is NULL");
+    DevState& s = e->s;
+    HIP_TRY(hipSetDevice(e->device));
+    if (num_agents == 0) {
+        HIP_TRY(hipDeviceSynchronize());
+        if (s.lgs) (void)hipFree(s.lgs);
+        s.lgs = nullptr;
+        s.lg_K = s.lg_lo = s.lg_hi = 0;
+        return SN_OK;
+    }
+    if (max_players != s.N) return fail(SN_EINVAL, "max_players must equal the handle's num_players");
+    if (min_players < 2 || min_players > max_players || max_players > kLeagueMaxPlayers)
+        return fail(SN_EINVAL, "need 2 <= min_players <= max_players <= 6");
+    if (num_agents < max_players || num_agents > kLeagueMaxAgents)
+        return fail(SN_EINVAL, "need max_players <= num_agents <= 16 (tournament.py:170 asserts len(self) >= num_players)");
+    if (!s.lgs && hipMalloc((void**)&s.lgs, sizeof(uint32_t) * s.B) != hipSuccess) return fail(SN_ENOMEM, "league state");
+    HIP_TRY(hipMemset(s.lgs, 0, sizeof(uint32_t) * s.B));
+    s.lg_K = num_agents, s.lg_lo = min_players, s.lg_hi = max_players;
+    e->lg_phase = -1;  // sn_reset deals the first games
+    return SN_OK;
+}
+
+sn_status sn_league_rollout(sn_env* e, int steps, int32_t* rewards, uint8_t* done, uint8_t* actions, int8_t* obs,
+                            int obs_stride, int32_t* records, void* stream) {
+    if (!e) return fail(SN_EINVAL, "env is NULL");
+    if (!e->s.lg_K) return fail(SN_EINVAL, "not a tournament handle (sn_league_config)");
+    if (e->lg_phase != 0) return fail(SN_EINVAL, "tournament rollouts start right after sn_reset or a whole number of games");
+    if (steps % kHand) return fail(SN_EINVAL, "tournament rollouts play whole games (steps a multiple of 10)");
+    if (steps < 0) return fail(SN_EINVAL, "steps must be >= 0");
+    if (obs && (obs_stride < 47 || (obs_stride & 3))) return fail(SN_EINVAL, "obs_stride must be a multiple of 4 and >= 47");
+    if (steps == 0) return SN_OK;
+    if (e->perr_host && __atomic_load_n(e->perr_host, __ATOMIC_RELAXED))
+        return fail(SN_ERNG, "a pipelined numpy-MT draw ran past the twisted words (sn_pipe_errors)");
+    PlayArgs a{};
+    a.steps = steps;
+    a.flags = SN_AUTO_RESET;
+    a.obs_stride = obs_stride;
+    a.rewards = rewards;
+    a.done = done;
+    a.actions_out = actions;
+    a.obs = obs;
+    a.league_rec = records;
     return launch_play(e, a, (hipStream_t)stream);
+}
+
+// Host replay (no GPU): the reference scores a tournament game's Elo right
+// after it (tournament.py:157-164), one game at a time; rl_6_nimmt/elo.py
+// restates multi_elo's multiplayer Elo (parity unpinned).  Same operation
+// order as elo.calc_elo, so the doubles match the Python replay bit for bit.
+sn_status sn_elo_replay(const int32_t* rec, int64_t G, int NP, int K, double elo_k, double* elos) {
+    if ((!rec && G > 0) || !elos) return fail(SN_EINVAL, "NULL argument");
+    if (NP < 2 || NP > kLeagueMaxPlayers || K < 1 || K > kLeagueMaxAgents) return fail(SN_EINVAL, "bad sizes");
+    for (int64_t i = 0; i < G; i++) {
+        const int32_t* r = rec + i * (1 + NP);
+        const uint32_t w = (uint32_t)r[0];
+        const int k = (int)(w & 15u);
+        if (k < 2 || k > NP) return fail(SN_EINVAL, "record " + std::to_string(i) + ": bad player count");
+        int a[kLeagueMaxPlayers];
+        double place[kLeagueMaxPlayers], old[kLeagueMaxPlayers], nw[kLeagueMaxPlayers];
+        for (int p = 0; p < k; p++) {
+            a[p] = (int)((w >> (4 + 4 * p)) & 15u);
+            if (a[p] >= K) return fail(SN_EINVAL, "record " + std::to_string(i) + ": agent id out of range");
+            old[p] = elos[a[p]];
+        }
+        for (int p = 0; p < k; p++) {  // Tournament._compute_absolute_positions: 1-based, ties averaged
+            int greater = 0, equal = 0;
+            for (int q = 0; q < k; q++) {
+                greater += r[1 + q] > r[1 + p];
+                equal += r[1 + q] == r[1 + p];
+            }
+            place[p] = (double)greater + 0.5 * (double)(1 + equal);
+        }
+        const double kk = elo_k / (double)(k - 1);
+        for (int p = 0; p < k; p++) {
+            double delta = 0.0;
+            for (int q = 0; q < k; q++) {
+                if (q == p) continue;
+                const double actual = place[p] < place[q] ? 1.0 : (place[p] == place[q] ? 0.5 : 0.0);
+                const double expected = 1.0 / (1.0 + std::pow(10.0, (old[q] - old[p]) / 400.0));
+                delta += kk * (actual - expected);
+            }
+            nw[p] = old[p] + delta;
+        }
+        for (int p = 0; p < k; p++) elos[a[p]] = nw[p];
+    }
+    return SN_OK;
+}
+
+sn_status sn_league_seats(sn_env* e, uint32_t* out, void* stream) {
+    if (!e || !out) return fail(SN_EINVAL, "NULL argument");
+    if (!e->s.lg_K) return fail(SN_EINVAL, "not a tournament handle (sn_league_config)");
+    HIP_TRY(hipMemcpyAsync(out, e->s.lgs, sizeof(uint32_t) * e->s.B, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return SN_OK;
 }
 
 sn_status sn_obs(sn_env* e, void* out, int dtype, int stride, int flags, void* stream) {

@@ -48,6 +48,10 @@ struct DevState {
     uint32_t* ptend; // [2][B] end of the twisted words after a prep launch (by launch parity)
     uint32_t* ptp;   // [B] twist pointer (MtGen's pos field), owned by k_mt_ahead
     uint32_t* perr;  // [1] play lanes that ran past the twisted words (must stay 0)
+    // batched tournament (sn_league_config): per game the current game's
+    // player count k and seat agents, k | agent(seat p) << (4 + 4p)
+    uint32_t* lgs;   // [B]
+    int lg_K, lg_lo, lg_hi, lg_pad;
 };
 
 constexpr int kPipeRing = 1024;  // ring bytes per game (>= lead + one launch)
@@ -55,6 +59,8 @@ constexpr int kPipeLead = 600;   // words k_mt_ahead keeps twisted ahead of the 
 constexpr int kPipeWin = 304;    // of them, copied to LDS per lane at a k_play launch
 
 constexpr int kBlock = 256;
+constexpr int kLeagueMaxPlayers = 6;  // tournament handles: 2..6 seats (agent ids packed 4 bits per seat)
+constexpr int kLeagueMaxAgents = 16;
 constexpr int kDeckStride = 108;  // 27 dwords: odd dword stride -> conflict-free LDS lanes
 constexpr int kDealStride = 212;  // deck (108) + swap targets (104): 53 dwords, odd as well
 
@@ -382,6 +388,27 @@ struct RngOf<RNG_NUMPY_RING_HBM, PF> {
         s.mt_pos[g] = r.save(buf);
     }
 };
+
+// ---------------------------------------------------------------- tournament seat draw
+// Tournament._choose_players (tournament.py:166-177) on the game's stream,
+// right before its deal: num_players = np.random.choice(range(lo, hi+1)) =
+// lo + random_interval(hi - lo) (no draw when lo == hi), then
+// np.random.choice(K, num_players, replace=False) = permutation(K)[:k]
+// (numpy legacy: shuffle(arange(K)), j = random_interval(i) for i = K-1..1).
+// Returns k | agent(seat p) << (4 + 4p); K <= 16, k <= 6.
+template <class R>
+__device__ __forceinline__ uint32_t league_draw(R& rng, ByteBuf& buf, int K, int lo, int hi) {
+    const uint32_t k = (uint32_t)lo + rng_interval(rng, buf, (uint32_t)(hi - lo));
+    uint64_t perm = 0xFEDCBA9876543210ull;  // nibble i = i
+    for (int i = K - 1; i >= 1; i--) {
+        const uint32_t j = rng_interval(rng, buf, (uint32_t)i);
+        const uint32_t si = 4u * (uint32_t)i, sj = 4u * j;
+        const uint64_t a = (perm >> si) & 15ull, b = (perm >> sj) & 15ull;
+        perm &= ~((15ull << si) | (15ull << sj));
+        perm |= (b << si) | (a << sj);
+    }
+    return k | (uint32_t)((perm & ((1ull << (4u * k)) - 1ull)) << 4);
+}
 
 // ---------------------------------------------------------------- game in VGPRs
 template <int N>
@@ -789,6 +816,7 @@ struct sn_env {
     int pipe;         // SN_OPT_PIPELINE
     int pipe_gpw;     // SN_OPT_PIPE_GPW: games per k_play wave on the pipelined path (32 or 64)
     int pipe_lead;    // SN_OPT_PIPE_LEAD: words k_mt_ahead keeps twisted ahead (kPipeLead; tests lower it)
+    int lg_phase;     // tournament handle: env-steps since the games were dealt, mod 10 (-1: not dealt yet)
     sechs::DevState s;
     // pipelined twist-ahead (sechs_env.hip launch_pipe): a k_mt_ahead for the
     // next play launch may be in flight on `side` (ev_prep) after a rollout

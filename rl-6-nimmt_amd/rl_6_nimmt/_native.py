@@ -69,6 +69,10 @@ SIGNATURES = {
     "sn_pipe_errors": ([_P, _P], _I),
     "sn_kernel_times": ([_P, _P, _P, _P], _I),
     "sn_debug_phases": ([_P, _I], _I),
+    "sn_league_config": ([_P, _I, _I, _I], _I),
+    "sn_league_rollout": ([_P, _I, _P, _P, _P, _P, _I, _P, _P], _I),
+    "sn_league_seats": ([_P, _P, _P], _I),
+    "sn_elo_replay": ([_P, _I64, _I, _I, ctypes.c_double, _P], _I),
     "sn_mcs_memorize": ([_P, _P, _I, _P], _I),
     "sn_mcs_rollouts": ([_P, _P, _I, _U64, ctypes.c_uint32, _P, _P], _I),
     "sn_mcs_rollouts_ex": ([_P, _P, _I, _U64, ctypes.c_uint32, _P, _P, _P], _I),

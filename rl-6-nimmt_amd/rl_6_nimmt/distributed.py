@@ -7,7 +7,9 @@ data path).  After a block of games:
   * `reduce_agent_stats`: all_reduce(SUM) of per-agent accumulators;
   * `gather_game_records`: all_gather of per-game records (global id, seat
     -> agent, score) so rank 0 can replay the order-dependent Elo updates
-    (tournament.py:157-164) in global game-id order.
+    (tournament.py:157-164) in global game-id order;
+  * `gather_league_records`: the same for the batched tournament's records
+    (league.py), which carry no id column: rank order is global slot order.
 Works with any torch.distributed backend (nccl = RCCL on the GPUs, gloo on CPU).
 """
 import numpy as np
@@ -36,6 +38,18 @@ def gather_game_records(records):
         records = torch.cat(parts, dim=0)
     order = torch.argsort(records[:, 0].to(torch.int64), stable=True)
     return records[order]
+
+
+def gather_league_records(records):
+    """Batched-tournament records of this rank, int32 [games, slots, 1 + N]
+    (rank r owns global slots [r*slots, (r+1)*slots)), all_gather'ed (RCCL on
+    the GPUs) into [games, world*slots, 1 + N]: round major, then global slot
+    id -- the canonical order of the Elo replay (league.replay_league_elo)."""
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        parts = [torch.empty_like(records) for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, records.contiguous())
+        records = torch.cat(parts, dim=1)
+    return records
 
 
 def replay_elo(records, num_agents, num_players, elo_initial=1600.0, elo_k=32.0):

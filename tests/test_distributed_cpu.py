@@ -85,3 +85,63 @@ def test_two_rank_gather_equals_single_process():
             ref_stats[row[1 + p], 1] += row[1 + N + p]
     assert np.array_equal(stats, ref_stats)
     assert np.allclose(elos, replay_elo(ref, 6, N))
+
+
+# ---------------------------------------------------------------- batched tournament records
+LK, LN, LG = 5, 4, 3
+
+
+def _league_records(offset, count):
+    """synthetic league records [games, count, 1 + N] for global slots
+    offset.., a pure function of (round, global slot id) like the device's"""
+    rec = np.zeros((LG, count, 1 + LN), dtype=np.int32)
+    for e in range(LG):
+        for j in range(count):
+            rng = np.random.RandomState(1000 * e + offset + j)
+            k = int(rng.randint(2, LN + 1))
+            ids = rng.permutation(LK)[:k]
+            w = k
+            for p, a in enumerate(ids):
+                w |= int(a) << (4 + 4 * p)
+            rec[e, j, 0] = w
+            rec[e, j, 1: 1 + k] = -rng.randint(0, 12, size=k)
+    return torch.from_numpy(rec)
+
+
+def _league_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rl_6_nimmt.distributed import gather_league_records, reduce_agent_stats, shard
+    from rl_6_nimmt.league import league_agent_stats, replay_league_elo
+
+    off, cnt = shard(rank, world, B)
+    rec = _league_records(off, cnt)
+    stats = reduce_agent_stats(league_agent_stats(rec, LK, LN))
+    allrec = gather_league_records(rec)
+    if rank == 0:
+        q.put((stats.numpy(), allrec.numpy(), replay_league_elo(allrec, LK, LN)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_league_gather_equals_single_process():
+    """world_size 2 over gloo: the league's per-agent sums (all_reduce) and the
+    gathered records + Elo replay (all_gather, rank order = global slot order)
+    equal one process holding every slot."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_league_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    stats, allrec, elos = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from rl_6_nimmt.league import league_agent_stats, replay_league_elo
+
+    ref = _league_records(0, 2 * B)
+    assert np.array_equal(allrec, ref.numpy())
+    assert np.allclose(stats, league_agent_stats(ref, LK, LN).numpy())
+    assert np.array_equal(elos, replay_league_elo(ref, LK, LN))

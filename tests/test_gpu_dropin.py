@@ -110,3 +110,40 @@ def test_tournament_dropin_plays_games():
         assert all(0.0 <= p <= 1.0 for p in t.tournament_positions[name])
         assert len(t.elos[name]) == 1 + t.played_games[name]
     assert "Tournament after 6 games:" in str(t)
+
+
+def test_tournament_dropin_replays_reference_leagues():
+    """Golden F11 (a): seeded reference Tournament.play_game() sequences over
+    DrunkHamster and MCSAgent seats -- seat draws (tournament.py:166-177),
+    results, relative positions, winners and the per-agent tallies -- replayed
+    through the drop-in Tournament on the GPU.  _compute_elos is a no-op on
+    both sides (multi_elo is absent: Elo unpinned)."""
+    from rl_6_nimmt import GameSession, Tournament
+    from rl_6_nimmt.agents import DrunkHamster, MCSAgent
+
+    d = load("tournament_games.json")["dropin"]
+    assert len(d) == 3
+    for lg in d:
+        np.random.seed(lg["seed"])
+        specs = [(n, MCSAgent(mc_max=lg["mc_max"], mc_per_card=lg["mc_per_card"]) if k == "M" else DrunkHamster())
+                 for n, k in zip(lg["agents"], lg["kinds"])]
+        t = Tournament(min_players=lg["min_players"], max_players=lg["max_players"])
+        for n, a in specs:
+            t.add_player(n, a)
+        t._compute_elos = lambda names, scores, t=t: [t.elos[n][-1] for n in names]
+        for g in lg["games"]:
+            names, agents = t._choose_players(None)
+            assert list(names) == g["names"], lg["seed"]
+            sess = GameSession(*agents)
+            sess.play_game(render=False)
+            scores = sess.results[0]
+            t.score_game(names, scores)
+            assert [int(x) for x in scores] == g["results"], lg["seed"]
+            assert np.allclose(t._compute_relative_positions(scores), g["relative"])
+            assert names[int(np.argmax(scores))] == g["winner"]
+        assert t.total_games == lg["total_games"]
+        for n, tl in lg["tallies"].items():
+            assert t.played_games[n] == tl["played_games"]
+            assert [int(x) for x in t.tournament_scores[n]] == tl["scores"]
+            assert np.allclose(t.tournament_positions[n], tl["positions"])
+            assert [float(x) for x in t.tournament_wins[n]] == tl["wins"]

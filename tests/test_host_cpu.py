@@ -203,3 +203,65 @@ def test_discounted_returns_formula():
         acc = r[t] + 0.9 * acc
         want[t] = acc
     assert np.allclose(g, want, rtol=0, atol=1e-6)
+
+
+def _random_league_records(rng, G, K, N):
+    rec = np.zeros((G, 1 + N), dtype=np.int32)
+    for i in range(G):
+        k = int(rng.randint(2, N + 1))
+        ids = rng.permutation(K)[:k]
+        w = k
+        for p, a in enumerate(ids):
+            w |= int(a) << (4 + 4 * p)
+        rec[i, 0] = w
+        # few distinct values: many ties
+        rec[i, 1: 1 + k] = -rng.randint(0, 6 if i % 2 else 40, size=k)
+    return rec
+
+
+def test_native_elo_replay_equals_python_replay():
+    """sn_elo_replay (host C++ in libsechs.so, no GPU call) == the sequential
+    Python replay of Tournament._compute_elos with elo.py, bit for bit."""
+    from rl_6_nimmt import _native as nat  # noqa: F401  (loads libsechs.so)
+    from rl_6_nimmt.elo import EloPlayer, calc_elo
+    from rl_6_nimmt.league import replay_league_elo
+    from rl_6_nimmt.tournament import Tournament
+    import torch
+
+    rng = np.random.RandomState(5)
+    for K, N in ((5, 4), (6, 6), (3, 2)):
+        rec = _random_league_records(rng, 3000, K, N)
+        elos = np.full(K, 1600.0)
+        for row in rec:
+            k = row[0] & 15
+            ids = [(int(row[0]) >> (4 + 4 * p)) & 15 for p in range(k)]
+            places = Tournament._compute_absolute_positions(row[1: 1 + k])
+            new = calc_elo([EloPlayer(pl, elos[a]) for pl, a in zip(places, ids)], 32)
+            for a, e in zip(ids, new):
+                elos[a] = e
+        got = replay_league_elo(torch.from_numpy(rec), K, N, 1600.0, 32.0)
+        assert np.array_equal(got, elos), (K, N)
+
+
+def test_league_scoring_matches_reference_formulas():
+    """league.relative_positions / winners (vectorised) == Tournament's
+    per-game formulas on the golden F7 cases and random tied games."""
+    import torch
+
+    from rl_6_nimmt.league import relative_positions, winners
+    from rl_6_nimmt.tournament import Tournament
+
+    cases = [np.array(c["scores"], dtype=np.int64) for c in load("positions.json")["cases"]]
+    rng = np.random.RandomState(2)
+    cases += [-rng.randint(0, 4, size=rng.randint(2, 7)) for _ in range(300)]
+    P = 6
+    R = np.zeros((len(cases), P), dtype=np.int64)
+    k = np.array([len(c) for c in cases])
+    for i, c in enumerate(cases):
+        R[i, : len(c)] = c
+    rel = relative_positions(torch.from_numpy(R), torch.from_numpy(k)).numpy()
+    win = winners(torch.from_numpy(R), torch.from_numpy(k)).numpy()
+    for i, c in enumerate(cases):
+        ref = Tournament._compute_relative_positions(c)
+        assert np.allclose(rel[i, : len(c)], ref, atol=1e-6), c
+        assert win[i] == int(np.argmax(c))
