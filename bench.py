@@ -20,7 +20,13 @@ starts; the timed region includes both kernels.
 Multi-GPU: game shards are independent (rank r owns global games
 [r*B, (r+1)*B), streams keyed by the global id), so there is no collective
 on the data path; one RCCL all_reduce of the per-rank score sums after the
-timed loop is the "tournament score gather" (SURVEY.md §8(e)).
+timed loop is the score gather.
+
+Extra legs (reported beside the headline, never in `value`): config 3
+(MCS), config 4 (PUCT, PUCTCustomed), and config 5 on every rank: the
+batched tournament (league.py) -- 65 536 concurrent tournament slots per GPU
+with per-game seat draws, then the RCCL gather of the per-agent sums and
+every game's record and the rank-0 Elo replay.
 """
 import argparse
 import json
@@ -69,6 +75,8 @@ def parse():
     ap.add_argument("--mcs-games", type=int, default=8192)
     ap.add_argument("--mcs-rollouts", type=int, default=256)
     ap.add_argument("--no-puct", action="store_true", help="skip the config-4 PUCT leg")
+    ap.add_argument("--no-league", action="store_true", help="skip the config-5 batched tournament leg")
+    ap.add_argument("--league-rounds", type=int, default=10, help="timed tournament games per slot (config 5)")
     ap.add_argument("--puct-games", type=int, default=8192)
     return ap.parse_args()
 
@@ -294,6 +302,75 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
     }
 
 
+def bench_league(world, rank, slots, rounds, warmup=2, K=5, lo=2, hi=4):
+    """BASELINE config 5: tournament.py self-play sharded over the ranks.
+    Rank r plays global slots [r*slots, (r+1)*slots); slot g is the
+    reference's np.random.seed(g) + Tournament(2, 4) over 5 DrunkHamster
+    agents + play_game() repeatedly (seat draw, deal, moves in-kernel; golden
+    F11 pins it).  Timed: `rounds` games per slot (10 env-steps each) on every
+    rank.  Then the RCCL score gather: all_reduce of the per-agent sums and
+    all_gather of every game's record, Elo replayed on rank 0 (host C++) in
+    canonical order -- timed separately."""
+    import torch.distributed as dist
+
+    from rl_6_nimmt.distributed import gather_league_records, reduce_agent_stats
+    from rl_6_nimmt.league import BatchedTournament, replay_league_elo
+
+    t = BatchedTournament(slots, lo, hi, seed=0, game_offset=rank * slots, rng="numpy")
+    for i in range(K):
+        t.add_player(f"DrunkHamster_{i}")
+    t.play_games(warmup)
+    t.agent_stats()  # first use of the scoring kernels, outside the timing
+    t.records.clear()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(rounds):
+        t.play_games(1)
+    torch.cuda.synchronize()
+    barrier(world)
+    wall = time.perf_counter() - t0
+    if t.env.pipe_errors():
+        raise SystemExit("bench: tournament draws ran past the twisted words")
+    tg = time.perf_counter()
+    stats = reduce_agent_stats(t.agent_stats())
+    allrec = gather_league_records(t.all_records())
+    torch.cuda.synchronize()
+    gather_ms = (time.perf_counter() - tg) * 1e3
+    if world > 1:
+        w = torch.tensor([wall, gather_ms], dtype=torch.float64, device=t.env.device)
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        wall, gather_ms = float(w[0].item()), float(w[1].item())
+    out = None
+    if rank == 0:
+        te = time.perf_counter()
+        elos = replay_league_elo(allrec, K, hi)
+        elo_ms = (time.perf_counter() - te) * 1e3
+        s = stats.cpu().numpy()
+        games = world * slots * rounds
+        out = {
+            "workload": f"config5: tournament.py self-play, {world} x {slots} concurrent game slots ({world * slots} "
+                        f"games at once), {K} DrunkHamster agents, {lo}..{hi} players per game drawn per game, "
+                        f"{rounds} games per slot; numpy-MT (slot g = np.random.seed(g) reference tournament)",
+            "value": games * STEPS_PER_LAUNCH / wall,
+            "unit": "env-steps/s",
+            "games_per_s": games / wall,
+            "concurrent_games": world * slots,
+            "wall_s": wall,
+            "ms_per_round": wall / rounds * 1e3,
+            "score_gather_ms": gather_ms,
+            "score_gather": f"RCCL all_reduce of [{K}, 4] per-agent sums + all_gather of {games} game records "
+                            f"({allrec.numel() * 4 / 1e6:.1f} MB)" if world > 1 else "single rank (no collective)",
+            "elo_replay_ms": elo_ms,
+            "agents": {f"DrunkHamster_{i}": {"games": int(s[i, 0]), "mean_score": s[i, 1] / s[i, 0],
+                                              "mean_position": s[i, 2] / s[i, 0], "win_fraction": s[i, 3] / s[i, 0],
+                                              "elo": float(elos[i])} for i in range(K)},
+        }
+    t.close()
+    return out
+
+
 def bench_customed(games, episodes=5):
     """BASELINE config 4, policy/value-net variant: PUCTCustomedAgent
     (mcts.py:325-451) in every seat of `games` 4-player games -- per
@@ -437,6 +514,10 @@ def main():
     if world == 1 and not args.no_puct:
         result["extra_config4_puct"] = bench_puct(args.puct_games)
         result["extra_config4_customed"] = bench_customed(args.puct_games)
+    if not args.no_league:
+        league = bench_league(world, rank, B, args.league_rounds)
+        if rank == 0:
+            result["extra_config5_tournament"] = league
     if args.extras and world == 1:
         env2 = VecSechsNimmtEnv(B, N_PLAYERS, seed=0, rng="philox")
         env2.reset()

@@ -181,15 +181,12 @@ def league_agent_stats(records, num_agents, max_players):
     rel = relative_positions(res, k)
     win = winners(res, k)
     valid = ids >= 0
-    idx = torch.where(valid, ids, torch.zeros_like(ids)).reshape(-1)
-    vf = valid.reshape(-1).to(torch.float64)
-    stats = torch.zeros((K, 4), dtype=torch.float64, device=rec.device)
-    stats[:, STAT_GAMES].index_add_(0, idx, vf)
-    stats[:, STAT_SCORE].index_add_(0, idx, res.reshape(-1).to(torch.float64) * vf)
-    stats[:, STAT_POSITION].index_add_(0, idx, rel.reshape(-1) * vf)
-    is_win = (torch.arange(N, device=rec.device)[None, :] == win[:, None]).reshape(-1).to(torch.float64)
-    stats[:, STAT_WINS].index_add_(0, idx, is_win * vf)
-    return stats
+    is_win = torch.arange(N, device=rec.device)[None, :] == win[:, None]
+    vals = torch.stack((valid.to(torch.float64), res.to(torch.float64), rel, is_win.to(torch.float64)), dim=-1)
+    # one-hot [seatings, K] x [seatings, 4]: a GEMM instead of float64
+    # atomics on K addresses (index_add_ serialises millions of them)
+    onehot = ((ids.reshape(-1, 1) == torch.arange(K, device=rec.device)[None, :]) & valid.reshape(-1, 1)).to(torch.float64)
+    return onehot.T @ vals.reshape(-1, 4)
 
 
 def replay_league_elo(records, num_agents, max_players, elo_initial=1600.0, elo_k=32.0):
