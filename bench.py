@@ -76,6 +76,7 @@ def parse():
     ap.add_argument("--mcs-rollouts", type=int, default=256)
     ap.add_argument("--no-puct", action="store_true", help="skip the config-4 PUCT leg")
     ap.add_argument("--no-league", action="store_true", help="skip the config-5 batched tournament leg")
+    ap.add_argument("--no-scalar", action="store_true", help="skip the config-1 scalar drop-in leg")
     ap.add_argument("--league-rounds", type=int, default=10, help="timed tournament games per slot (config 5)")
     ap.add_argument("--puct-games", type=int, default=8192)
     return ap.parse_args()
@@ -371,6 +372,50 @@ def bench_league(world, rank, slots, rounds, warmup=2, K=5, lo=2, hi=4):
     return out
 
 
+def bench_scalar(games=200, step_games=200):
+    """BASELINE config 1 through the scalar drop-in (rl_6_nimmt.GameSession /
+    SechsNimmtEnv on a one-game device handle, sn_step1 / sn_reset1): ms per
+    GameSession(DrunkHamster(), DrunkHamster()) game (np.random.seed(g) per
+    game, results bit-exact vs the reference's sessions, golden F2), and
+    us per 4-player env.step with the actions drawn outside the timer -- the
+    two reference numbers of BASELINE.md §2 (1.39 ms/game, 67.9 us/step on
+    this image's CPU)."""
+    from rl_6_nimmt import GameSession, SechsNimmtEnv
+    from rl_6_nimmt.agents import DrunkHamster
+
+    sess = GameSession(DrunkHamster(), DrunkHamster())
+    np.random.seed(0)
+    sess.play_game()  # warm-up (kernels, pinned buffers)
+    t0 = time.perf_counter()
+    for g in range(games):
+        np.random.seed(g)
+        sess.play_game()
+    per_game = (time.perf_counter() - t0) / games
+    env = SechsNimmtEnv(4, verbose=False)
+    rng = np.random.RandomState(1)
+    env.reset()
+    step_s, steps = 0.0, 0
+    for g in range(step_games):
+        states, legal = env.reset()
+        done = False
+        while not done:
+            acts = [int(rng.choice(h)) for h in legal]
+            t = time.perf_counter()
+            (states, legal), rew, done, _ = env.step(acts)
+            step_s += time.perf_counter() - t
+            steps += 1
+    return {
+        "workload": "config1: GameSession(DrunkHamster(), DrunkHamster()).play_game() through the scalar drop-in "
+                    "(one-game device handle); 4-player env.step with actions drawn outside the timer",
+        "ms_per_game": per_game * 1e3,
+        "reference_ms_per_game": 1.39,
+        "us_per_env_step_4p": step_s / steps * 1e6,
+        "reference_us_per_env_step_4p": 67.9,
+        "games": games,
+        "steps_timed": steps,
+    }
+
+
 def bench_customed(games, episodes=5):
     """BASELINE config 4, policy/value-net variant: PUCTCustomedAgent
     (mcts.py:325-451) in every seat of `games` 4-player games -- per
@@ -514,6 +559,8 @@ def main():
     if world == 1 and not args.no_puct:
         result["extra_config4_puct"] = bench_puct(args.puct_games)
         result["extra_config4_customed"] = bench_customed(args.puct_games)
+    if world == 1 and not args.no_scalar:
+        result["extra_config1_scalar"] = bench_scalar()
     if not args.no_league:
         league = bench_league(world, rank, B, args.league_rounds)
         if rank == 0:

@@ -172,6 +172,21 @@ sn_status sn_kernel_times(sn_env* env, float* play_ms, float* ahead_ms, int32_t*
    SN_EUNSUPPORTED [sync]. */
 sn_status sn_debug_phases(uint64_t* out, int n);
 
+/* ---- One-game fast path (the scalar drop-in SechsNimmtEnv) ------------
+   For a handle of B == 1: one kernel launch and one stream sync per call
+   (host-memory arguments and results; pinned, device-mapped buffer inside
+   the handle).  out_host: int32 [2 + 2N + 12N] = first illegal seat or -1
+   (env.py:114-118; nothing changes then), done, rewards [N] (env.py:64-77),
+   scores [N] (penalties so far), then the N observation rows as int8 bytes,
+   48 per seat (47 used, env.py:174-212). [sync] */
+sn_status sn_step1(sn_env* env, const int32_t* actions_host, int32_t* out_host, int flags);
+/* env.py:43-51 reset() drawing from the numpy legacy state (key, pos) given
+   -- np.random.get_state() -- and returning the advanced state for
+   np.random.set_state(); out_host as sn_step1 (invalid -1, rewards 0).
+   numpy-compat handles only. [sync] */
+sn_status sn_reset1(sn_env* env, const uint32_t* key_host, int32_t pos, uint32_t* key_out_host, int32_t* pos_out,
+                    int32_t* out_host, int flags);
+
 /* ---- Batched tournament (tournament.py:132-177) ------------------------
    A tournament handle plays one league game per game slot at a time: slot
    g is the reference's `np.random.seed(seed + game_offset + g); t =

@@ -665,6 +665,101 @@ __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
     play_body<N, MODE, GPW, LG>(s, a, lds_dyn, (int)threadIdx.x);
 }
 
+// ---- one-game fast path (the scalar drop-in SechsNimmtEnv, B == 1) -------
+// One launch per env.step / env.reset: the actions arrive as kernel
+// arguments, the results (invalid seat, done, rewards, scores, int8 obs rows)
+// -- and for a reset the numpy MT19937 state in and out -- go through pinned,
+// device-mapped host words, so a call is one launch + one stream sync
+// instead of a chain of blocking copies.  Words of hbuf:
+constexpr int kH1In = 0;      // [624] key, [624] numpy pos        (sn_reset1 in)
+constexpr int kH1Out = 1024;  // [0] invalid, [1] done, [2, 2+N) rewards, [2+N, 2+2N) scores, obs bytes N x 48
+constexpr int kH1Mt = 2048;   // [624] key, [624] code, [625] mt0  (sn_reset1 out)
+constexpr int kH1Words = 4096;
+
+struct Acts1 {
+    int32_t a[kMaxPlayers];
+};
+
+template <int N>
+__device__ __forceinline__ void out1_game(const DevState& s, const Game<N>& G, uint32_t* out, int summ) {
+#pragma unroll
+    for (int p = 0; p < N; p++) out[2 + N + p] = (uint32_t)G.score[p];
+    uint32_t w2hi;
+    const GameWords gw = summ ? game_words<true>(N, G.b, w2hi) : game_words<false>(N, G.b, w2hi);
+    uint32_t* ob = out + 2 + 2 * N;
+#pragma unroll
+    for (int p = 0; p < N; p++) {
+        const Hand& h = G.hand[p];
+        const uint32_t row[12] = {(uint32_t)h.lo, (uint32_t)(h.lo >> 32), (h.hi & 0xFFFFu) | w2hi, gw.w0, gw.a.x, gw.a.y,
+                                  gw.a.z, gw.a.w, gw.b.x, gw.b.y, gw.b.z, gw.b.w};
+#pragma unroll
+        for (int i = 0; i < 12; i++) ob[12 * p + i] = row[i];
+    }
+}
+
+template <int N>
+__global__ void k_step1(DevState s, Acts1 acts, uint32_t* hb, int summ) {
+    if (threadIdx.x != 0) return;
+    uint32_t* out = hb + kH1Out;
+    Game<N> G;
+    load_game<N>(s, 0, G);
+    uint32_t card[N], pen[N], idx[N];
+    int bad = -1;
+#pragma unroll
+    for (int p = N - 1; p >= 0; p--) {  // env.py:114-118 in seat order: the first illegal seat
+        const int32_t c = acts.a[p];
+        const int k = (G.n > 0u && c >= 0 && c < s.C) ? hand_find(G.hand[p], (uint32_t)c) : -1;
+        card[p] = (uint32_t)c;
+        idx[p] = (uint32_t)k;
+        bad = (k >= 0) ? bad : p;
+    }
+#pragma unroll
+    for (int p = 0; p < N; p++) pen[p] = 0u;
+    if (bad < 0) {
+#pragma unroll
+        for (int p = 0; p < N; p++) hand_del(G.hand[p], idx[p]);
+        resolve<N>(G.b, card, pen);
+#pragma unroll
+        for (int p = 0; p < N; p++) G.score[p] += (int32_t)pen[p];
+        G.n -= 1u;
+        store_game<N>(s, 0, G);
+    }
+    out[0] = (uint32_t)bad;
+    out[1] = (G.n == 0u) ? 1u : 0u;
+#pragma unroll
+    for (int p = 0; p < N; p++) out[2 + p] = (uint32_t)(-(int32_t)pen[p]);
+    out1_game<N>(s, G, out, summ);
+}
+
+template <int N>
+__global__ __launch_bounds__(64) void k_reset1(DevState s, uint32_t* hb, int summ) {
+    __shared__ __attribute__((aligned(16))) uint8_t slot[kDealStride];
+    const int t = threadIdx.x;
+    for (int i = t; i < kMtN; i += 64) s.mt[i] = hb[kH1In + i];
+    __syncthreads();
+    if (t == 0) {
+        s.mt_pos[0] = mt_code_from_numpy((int)hb[kH1In + kMtN]);
+        Game<N> G;
+        typename RngOf<RNG_NUMPY_MT>::T rng;
+        ByteBuf buf;
+        RngOf<RNG_NUMPY_MT>::load(s, 0, rng, buf);
+        deck_shuffle2(rng, buf, slot, s.C);
+        deal_from_deck<N>(slot, s.C, G);
+        RngOf<RNG_NUMPY_MT>::store(s, 0, rng, buf);
+        store_game<N>(s, 0, G);
+        uint32_t* out = hb + kH1Out;
+        out[0] = 0xFFFFFFFFu;
+        out[1] = 0u;
+#pragma unroll
+        for (int p = 0; p < N; p++) out[2 + p] = 0u;
+        out1_game<N>(s, G, out, summ);
+        hb[kH1Mt + kMtN] = s.mt_pos[0];
+        hb[kH1Mt + kMtN + 1] = s.mt0[0];
+    }
+    __syncthreads();
+    for (int i = t; i < kMtN; i += 64) hb[kH1Mt + i] = s.mt[i];
+}
+
 // obs in any dtype, one thread per (game, seat)
 template <typename T>
 __global__ void k_obs(DevState s, T* out, int stride, int summ) {
@@ -849,6 +944,7 @@ sn_status sn_destroy(sn_env* e) {
     if (e->ev_main) (void)hipEventDestroy(e->ev_main);
     if (e->ev_play) (void)hipEventDestroy(e->ev_play);
     if (e->perr_host) (void)hipHostFree(e->perr_host);
+    if (e->hbuf) (void)hipHostFree(e->hbuf);
     if (e->side) (void)hipStreamDestroy(e->side);
     free_timing(e);
     void* ps[] = {s.hand, s.row_lo, s.row_hi, s.score, s.sum_res, s.episodes, s.mt_pos, s.ctr, s.mt, s.mt0, s.ring,
@@ -1432,6 +1528,62 @@ sn_status sn_mt_set(sn_env* e, int64_t game, const uint32_t* key, int32_t pos) {
     const uint32_t code = mt_code_from_numpy(pos);
     HIP_TRY(hipMemcpy(e->s.mt + game * kMtN, key, sizeof(uint32_t) * kMtN, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(e->s.mt_pos + game, &code, sizeof(uint32_t), hipMemcpyHostToDevice));
+    return SN_OK;
+}
+
+static sn_status h1_ready(sn_env* e) {
+    if (e->s.B != 1) return fail(SN_EINVAL, "the one-game fast path needs a one-game handle");
+    if (!e->hbuf) {
+        if (hipHostMalloc((void**)&e->hbuf, sizeof(uint32_t) * kH1Words, hipHostMallocMapped) != hipSuccess ||
+            hipHostGetDevicePointer((void**)&e->hbuf_dev, e->hbuf, 0) != hipSuccess)
+            return fail(SN_ENOMEM, "pinned exchange buffer");
+    }
+    return SN_OK;
+}
+
+static void h1_copy_out(const sn_env* e, int32_t* out) {
+    const int N = e->s.N;
+    std::memcpy(out, e->hbuf + kH1Out, sizeof(uint32_t) * (2 + 2 * N + 12 * N));
+}
+
+sn_status sn_step1(sn_env* e, const int32_t* actions_host, int32_t* out_host, int flags) {
+    if (!e || !actions_host || !out_host) return fail(SN_EINVAL, "NULL argument");
+    HIP_TRY(hipSetDevice(e->device));
+    if (h1_ready(e) != SN_OK) return SN_ENOMEM;
+    if (e->s.lg_K) return fail(SN_EUNSUPPORTED, "a tournament handle plays whole games with sn_league_rollout");
+    Acts1 a{};
+    for (int p = 0; p < e->s.N; p++) a.a[p] = actions_host[p];
+    const int summ = !(flags & SN_NO_SUMMARIES);
+    SN_DISPATCH_N(e->s.N, hipLaunchKernelGGL((k_step1<NN>), dim3(1), dim3(64), 0, 0, e->s, a, e->hbuf_dev, summ));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(0));
+    h1_copy_out(e, out_host);
+    return SN_OK;
+}
+
+sn_status sn_reset1(sn_env* e, const uint32_t* key_host, int32_t pos, uint32_t* key_out_host, int32_t* pos_out,
+                    int32_t* out_host, int flags) {
+    if (!e || !key_host || !key_out_host || !pos_out || !out_host) return fail(SN_EINVAL, "NULL argument");
+    if (e->s.rng_mode != SN_RNG_NUMPY_MT) return fail(SN_EINVAL, "env is not in numpy-compat RNG mode");
+    if (pos < 0 || pos > kMtN) return fail(SN_EINVAL, "pos must be in 0..624");
+    HIP_TRY(hipSetDevice(e->device));
+    if (h1_ready(e) != SN_OK) return SN_ENOMEM;
+    if (e->s.lg_K) return fail(SN_EUNSUPPORTED, "a tournament handle deals with sn_reset");
+    if (sn_pipe_sync(e, 0) != SN_OK) return SN_EHIP;
+    std::memcpy(e->hbuf + kH1In, key_host, sizeof(uint32_t) * kMtN);
+    e->hbuf[kH1In + kMtN] = (uint32_t)pos;
+    const int summ = !(flags & SN_NO_SUMMARIES);
+    SN_DISPATCH_N(e->s.N, hipLaunchKernelGGL((k_reset1<NN>), dim3(1), dim3(64), 0, 0, e->s, e->hbuf_dev, summ));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(0));
+    h1_copy_out(e, out_host);
+    // the advanced state in numpy's (key, pos) form, as sn_mt_get
+    std::memcpy(key_out_host, e->hbuf + kH1Mt, sizeof(uint32_t) * kMtN);
+    const uint32_t code = e->hbuf[kH1Mt + kMtN];
+    const int p = (int)(code & 0x7FFu), cnt = (int)((code >> 16) & kMtCntMask);
+    if (cnt > p && p > 0) mt_unstraddle(key_out_host, p, e->hbuf[kH1Mt + kMtN + 1]);
+    else if (p > 0 && p < kMtN) mt_finish_round(key_out_host, p);
+    *pos_out = (int32_t)mt_numpy_pos(code);
     return SN_OK;
 }
 

@@ -826,6 +826,8 @@ struct sn_env {
     hipEvent_t ev_prep, ev_main, ev_play;  // ev_play: after the last pipelined k_play (caller's stream)
     uint32_t* perr_host;                    // pinned, device-mapped mirror of s.perr (PlayArgs::perr_mirror)
     uint32_t* perr_host_dev;
+    uint32_t* hbuf;      // one-game fast path (sn_step1 / sn_reset1): pinned, device-mapped exchange words
+    uint32_t* hbuf_dev;
     // SN_OPT_TIMING: per-launch event pairs (k_play start/end on the launch
     // stream, k_mt_ahead start/end on `side`), tcap pairs, tn recorded
     hipEvent_t* tev;

@@ -69,6 +69,8 @@ SIGNATURES = {
     "sn_pipe_errors": ([_P, _P], _I),
     "sn_kernel_times": ([_P, _P, _P, _P], _I),
     "sn_debug_phases": ([_P, _I], _I),
+    "sn_step1": ([_P, _P, _P, _I], _I),
+    "sn_reset1": ([_P, _P, ctypes.c_int32, _P, _P, _P, _I], _I),
     "sn_league_config": ([_P, _I, _I, _I], _I),
     "sn_league_rollout": ([_P, _I, _P, _P, _P, _P, _I, _P, _P], _I),
     "sn_league_seats": ([_P, _P, _P], _I),

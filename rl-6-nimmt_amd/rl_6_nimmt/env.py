@@ -16,6 +16,7 @@ Known deviation: hands are card sets on the device, so `reset_to` with an
 unsorted hand list yields sorted legal lists (the reference's own callers
 always pass sorted hands: env.py:108, agents/mcts.py:118-125).
 """
+import ctypes
 import logging
 
 import numpy as np
@@ -75,6 +76,13 @@ class SechsNimmtEnv:
         self.spec = None
 
         self._vec = VecSechsNimmtEnv(1, num_players, num_cards, seed=0, rng="numpy", include_summaries=include_summaries)
+        # one-game fast path (sn_step1 / sn_reset1): host-side argument and
+        # result buffers, one kernel launch + one sync per call
+        self._out = np.zeros(2 + 2 * num_players + 12 * num_players, dtype=np.int32)
+        self._acts = np.zeros(num_players, dtype=np.int32)
+        self._key = np.zeros(624, dtype=np.uint32)
+        self._pos = ctypes.c_int32()
+        self._flags = 0 if include_summaries else nat.SN_NO_SUMMARIES
         self._board = [[] for _ in range(num_rows)]
         self._hands = [[] for _ in range(num_players)]
         self._scores = np.zeros(num_players, dtype=np.int32)
@@ -86,11 +94,12 @@ class SechsNimmtEnv:
         if self.verbose:
             logger.debug("Dealing cards")
         st = np.random.get_state()
-        self._vec.set_mt_state(st[1], st[2])
-        self._vec.reset()
-        key, pos = self._vec.get_mt_state()
-        np.random.set_state((st[0], key, pos, st[3], st[4]))
-        self._pull()
+        key = np.ascontiguousarray(st[1], dtype=np.uint32)
+        nat.check(nat.lib().sn_reset1(self._vec._h, key.ctypes.data_as(ctypes.c_void_p), int(st[2]),
+                                      self._key.ctypes.data_as(ctypes.c_void_p), ctypes.byref(self._pos),
+                                      self._out.ctypes.data_as(ctypes.c_void_p), self._flags), "sn_reset1")
+        np.random.set_state((st[0], self._key.copy(), int(self._pos.value), st[3], st[4]))
+        self._unpack()
         return self._create_states()
 
     def reset_to(self, board, hands):
@@ -120,16 +129,20 @@ class SechsNimmtEnv:
         for p, card in enumerate(acts):  # out-of-range cards can never be in a hand
             if not 0 <= card < self._num_cards:
                 self._invalid(p, card)
-        rew, done, inv = self._vec.step(torch.from_numpy(acts.astype(np.int32)).view(1, -1))
-        bad = int(inv[0].item())
+        self._acts[:] = acts
+        nat.check(nat.lib().sn_step1(self._vec._h, self._acts.ctypes.data_as(ctypes.c_void_p),
+                                     self._out.ctypes.data_as(ctypes.c_void_p), self._flags), "sn_step1")
+        bad = int(self._out[0])
         if bad >= 0:
             self._invalid(bad, acts[bad])
-        rewards = rew[0].cpu().numpy().astype(np.int32)
-        self._pull()
+        N = self._num_players
+        rewards = self._out[2: 2 + N].copy()
+        done = bool(self._out[1])
+        self._unpack()
         if self.verbose:
             for card, p in sorted((int(c), p) for p, c in enumerate(acts)):
                 logger.debug(f"{self._player_name(p)} plays card {card + 1}")
-        return self._create_states(), rewards, bool(done[0].item()), dict()
+        return self._create_states(), rewards, done, dict()
 
     def render(self, mode="human"):
         """Log the board and the hands (env.py:79-97)."""
@@ -187,6 +200,17 @@ class SechsNimmtEnv:
 
     def _invalid(self, p, card):
         raise InvalidMoveException(f"Player {p + 1} tried to play card {int(card) + 1}, but their hand is {self._hands[p]}")
+
+    def _unpack(self):
+        """Python mirrors from the packed fast-path result (scores, obs rows)."""
+        N = self._num_players
+        self._scores = self._out[2 + N: 2 + 2 * N].copy()
+        rows = self._out[2 + 2 * N:].view(np.int8).reshape(N, 48)
+        obs = rows[:, : obs_length(self._include_summaries)].astype(np.int64)
+        self._obs = obs
+        self._hands = [[int(c) for c in obs[p, :HAND] if c >= 0] for p in range(N)]
+        board = obs[0, -ROWS * THRESHOLD:].reshape(ROWS, THRESHOLD)
+        self._board = [[int(c) for c in row if c >= 0] for row in board]
 
     def _pull(self):
         """Copy the device state into the Python mirrors (one obs + one score read)."""

@@ -15,7 +15,7 @@ LIB = os.path.join(PKG_ROOT, "libsechs.so")
 def declared_symbols():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(sn_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(sn_[a-z_0-9]+)\s*\(", text)))
 
 
 def test_header_declares_the_boundary():
