@@ -233,6 +233,24 @@ def host_cpu_info():
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
+# VALU issue peak of MI355X: 256 CUs x 4 SIMD-32, one wave64 VALU
+# instruction per 2 cycles each (MI355X_MICROARCH.md "Wave scheduling"), at
+# the 2.4 GHz peak engine clock
+VALU_PEAK_GINSTR = 256 * 4 * 2.4 / 2  # 1228.8 G wave-instructions/s
+SQ_EXTRAS = os.path.join(ROOT, "profiles", "r02_sq_extras.json")
+
+
+def sq_extras(kernel):
+    """SQ counters of the config-3/4 kernels, summed over one run of the legs
+    (tools/sq_extras.sh -> profiles/r02_sq_extras.json)"""
+    if not os.path.exists(SQ_EXTRAS):
+        return None
+    for name, c in json.load(open(SQ_EXTRAS)).items():
+        if kernel in name:
+            return c
+    return None
+
+
 def bench_mcs(games, rollouts, episodes=1):
     """BASELINE config 3: every seat of `games` 4-player games is an MCS
     agent with `rollouts` playouts per legal move (stratified), one whole
@@ -256,6 +274,18 @@ def bench_mcs(games, rollouts, episodes=1):
     wall = time.perf_counter() - t0
     steps = rollout_env_steps_per_seat_game(rollouts) * N_PLAYERS * games * episodes
     decisions = 9 * N_PLAYERS * games * episodes
+    gpu_ms = ev0.elapsed_time(ev1)
+    sq = sq_extras("k_mcs_rollouts")
+    roof = None
+    if sq and episodes == 1 and games == 8192 and rollouts == 256:
+        # the search is integer VALU work (no HBM traffic to speak of: 189 B
+        # per playout env-step by the SURVEY model, ~0 real); bound = VALU issue
+        achieved = sq["SQ_INSTS_VALU"] / (gpu_ms * 1e-3) / 1e9
+        roof = {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_GINSTR, "unit": "G wave-instr/s",
+                "frac": achieved / VALU_PEAK_GINSTR, "traffic": None,
+                "valu_instructions": sq["SQ_INSTS_VALU"], "valu_source": os.path.relpath(SQ_EXTRAS, ROOT),
+                "wave_cycles": {k: sq.get(k + "_frac") for k in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY")},
+                "kernel": "k_mcs_rollouts<4> (+ memorize/choose), over the episode's GPU time (HIP events)"}
     return {
         "workload": f"config3: {games} x 4-player games, all seats MCS, {rollouts} playouts per legal move, "
                     f"{episodes} game(s); philox RNG",
@@ -263,7 +293,8 @@ def bench_mcs(games, rollouts, episodes=1):
         "unit": "playout env-steps/s",
         "decisions_per_s": decisions / wall,
         "wall_s": wall,
-        "gpu_ms": ev0.elapsed_time(ev1),
+        "gpu_ms": gpu_ms,
+        "roofline": roof,
         "mean_score_per_seat": (total.double().mean(dim=0)).tolist(),
     }
 
@@ -290,14 +321,26 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     steps = sum(eng.n_mc(n) * n for n in range(2, 11)) * N_PLAYERS * games
+    rows_s = eng.rows_evaluated / wall
+    # the MLP dominates: three hipBLASLt GEMMs per candidate-row batch
+    # (48->100 +ReLU, 100->100 +ReLU, 100->16-padded head).  Skinny K: HBM
+    # bound on its bf16 intermediates -- per row 96 B in, 2 x (200 B out +
+    # 200 B back in), 32 B head out = 928 B; 29 800 FLOP
+    row_bytes = 96 + 2 * (200 + 200) + 32
     return {
         "workload": f"config4: {games} x 4-player games, all seats PUCT (mc_max={mc_max}, mc_per_card={mc_per_card}, "
                     f"c_puct=2), bf16 policy MLP 48-100-100-1 via PyTorch-ROCm, 1 game",
         "value": steps / wall,
         "unit": "playout env-steps/s",
         "decisions_per_s": 9 * N_PLAYERS * games / wall,
-        "policy_rows_per_s": eng.rows_evaluated / wall,
+        "policy_rows_per_s": rows_s,
         "policy_tflops": eng.rows_evaluated * 29800 / wall / 1e12,
+        "roofline": {"bound": "hbm", "achieved": rows_s * row_bytes / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": rows_s * row_bytes / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                     "algo_bytes_per_row": row_bytes,
+                     "mfma_frac": eng.rows_evaluated * 29800 / wall / 1e12 / 2500.0,
+                     "kernel": "policy MLP (PyTorch-ROCm hipBLASLt bf16, ReLU fused in the GEMM epilogue), whole "
+                               "game wall time incl. the k_puct_* kernels"},
         "wall_s": wall,
         "mean_score_per_seat": total.double().mean(dim=0).tolist(),
     }

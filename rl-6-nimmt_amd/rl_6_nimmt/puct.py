@@ -30,6 +30,52 @@ def make_actor(hidden_sizes=(100, 100), activation=None):
                           head_activations=(None,))
 
 
+class FusedMLP:
+    """Inference form of MultiHeadedMLP(48, hidden, heads, ReLU, (None,)) on
+    PyTorch-ROCm (north_star: the net runs through PyTorch): every hidden
+    layer one hipBLASLt GEMM with the bias + ReLU fused into its epilogue
+    (torch._addmm_activation: no separate clamp pass over the [rows, 100]
+    activations), the heads one GEMM over the head rows zero-padded to 16
+    outputs (a [rows,100]x[100,1] GEMV runs 2x slower than the padded GEMM on
+    gfx950).  Measured on 1.31 M bf16 rows: 1091 -> 839 us (tools/mlp_bench.py).
+    Other layouts fall back to the module."""
+
+    def __init__(self, module, layers, head_w, head_b, head_sizes):
+        self.module, self.layers = module, layers
+        self.head_w, self.head_b, self.head_sizes = head_w, head_b, head_sizes
+
+    @classmethod
+    def of(cls, net):
+        lat = list(net.latent_net)
+        heads = list(net.head_nets)
+        ok = len(lat) % 2 == 0 and all(isinstance(m, nn.Linear) for m in lat[0::2]) and \
+            all(isinstance(m, nn.ReLU) for m in lat[1::2]) and \
+            all(len(h) == 1 and isinstance(h[0], nn.Linear) for h in heads)
+        if not ok:
+            return cls(net, None, None, None, None)
+        layers = [(m.weight.detach(), m.bias.detach()) for m in lat[0::2]]
+        w = torch.cat([h[0].weight.detach() for h in heads], dim=0)
+        b = torch.cat([h[0].bias.detach() for h in heads], dim=0)
+        pad = max(16, -(-w.shape[0] // 16) * 16)
+        wp = torch.zeros((pad, w.shape[1]), dtype=w.dtype, device=w.device)
+        bp = torch.zeros((pad,), dtype=b.dtype, device=b.device)
+        wp[: w.shape[0]], bp[: b.shape[0]] = w, b
+        return cls(net, layers, wp.t().contiguous(), bp, [h[0].out_features for h in heads])
+
+    def __call__(self, rows):
+        if self.layers is None:
+            return self.module(rows)
+        h = rows
+        for w, b in self.layers:
+            h = torch._addmm_activation(b, h, w.t())
+        out = torch.addmm(self.head_b, h, self.head_w)
+        res, c = [], 0
+        for n in self.head_sizes:
+            res.append(out[:, c: c + n])
+            c += n
+        return res
+
+
 class BatchedPUCT:
     def __init__(self, env, actor, mc_per_card=10, mc_max=100, c_puct=2.0, seed=0, seats_mask=None, puct_root=True,
                  net_dtype=torch.bfloat16, mcs_num_cards=104):
@@ -69,7 +115,7 @@ class BatchedPUCT:
 
             net = copy.deepcopy(self.actor).to(self.env.device, self.net_dtype)
             net.eval()
-            self._net, self._net_version = net, version
+            self._net, self._net_version = FusedMLP.of(net), version
         return self._net
 
     def actor_device(self):
