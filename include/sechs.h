@@ -297,6 +297,8 @@ typedef struct {
     int32_t* stats;
     int32_t* hist;
     float* root_probs;
+    const uint32_t* step_dev; /* NULL, or the decision counter in device memory (overrides `step`):
+                                 lets one captured hipGraph of a decision's launches serve every decision */
 } sn_puct;
 
 sn_status sn_puct_root_rows(sn_env* env, const sn_puct* q, void* rows, int bf16, void* stream);

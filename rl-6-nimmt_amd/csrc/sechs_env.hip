@@ -1187,7 +1187,10 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         e->pvalid = 1;
     }
     const int64_t B = s.B, N = s.N;
-    const int chunk = min(e->chunk_steps, pipe_max_chunk(s.N));
+    // a tournament game adds its seat draw (<= K - 1 + 1 draws): 10-step
+    // launches keep the pair tail < 1e-26 up to K = 8 agents at N <= 4
+    // (tools/pipe_tail.py), beyond that 5-step launches
+    const int chunk = min(e->chunk_steps, (s.lg_K > 8) ? 5 : pipe_max_chunk(s.N));
     for (int t0 = 0; t0 < a.steps; t0 += chunk) {
         PlayArgs c = a;
         c.steps = min(chunk, a.steps - t0);

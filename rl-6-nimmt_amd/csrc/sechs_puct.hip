@@ -39,7 +39,13 @@ struct PuctArgs {
     int32_t* stats;           // [D][24]
     int32_t* hist;            // [D][172]
     float* root_probs;        // [D][10]
+    const uint32_t* step_dev; // decision counter in device memory (graph replays), else `step`
 };
+
+// the decision counter mixed into every Philox key of a decision: from
+// device memory when the launches were captured into a graph (one capture
+// replayed for every decision), else the launch argument
+__device__ __forceinline__ uint32_t puct_step_of(const PuctArgs& a) { return a.step_dev ? *a.step_dev : a.step; }
 
 __device__ __forceinline__ void dec_to_gp(const PuctArgs& a, int64_t d, int64_t& g, int& p) {
     g = d / a.M;
@@ -151,7 +157,7 @@ __global__ void k_puct_deal(DevState s, PuctArgs a) {
     const uint64_t gid = s.game_offset + (uint64_t)g;
     PhiloxGen gen;
     ByteBuf buf;
-    gen.load(a.seed_lo ^ a.step, a.seed_hi, ((uint64_t)(uint32_t)gid << 32) | ((uint64_t)p << 28) | ((uint64_t)a.rollout << 8),
+    gen.load(a.seed_lo ^ puct_step_of(a), a.seed_hi, ((uint64_t)(uint32_t)gid << 32) | ((uint64_t)p << 28) | ((uint64_t)a.rollout << 8),
              0ull, buf);
     int32_t* ro = a.ro + d * kRoWords;
     const Board b = load_board(s, g);
@@ -281,7 +287,7 @@ __global__ void k_puct_step(DevState s, PuctArgs a, const float* logits, int t, 
             idx = puct_choose(a.stats + d * kStatWords, a.hist + d * kHistBins, a.root_probs + d * kHand, n_cur,
                               a.c_puct, nullptr);
         } else {
-            idx = sample_softmax(x, n_cur, philox_uniform(a.seed_lo ^ a.step, a.seed_hi, stream, (uint32_t)q));
+            idx = sample_softmax(x, n_cur, philox_uniform(a.seed_lo ^ puct_step_of(a), a.seed_hi, stream, (uint32_t)q));
         }
         if (t == 0 && q == 0) first = idx;
         card[q] = hand_get(G.hand[q], (uint32_t)idx);
@@ -381,7 +387,7 @@ __global__ void k_policy_sample(DevState s, PuctArgs a, const float* logits, int
     const float* x = logits + d * a.n;
     const uint64_t gid = s.game_offset + (uint64_t)g;
     const uint64_t stream = ((uint64_t)(uint32_t)gid << 32) | ((uint64_t)p << 28) | (0xFFFFFull << 8);
-    const int k = sample_softmax(x, a.n, philox_uniform(a.seed_lo ^ a.step, a.seed_hi, stream, 0u));
+    const int k = sample_softmax(x, a.n, philox_uniform(a.seed_lo ^ puct_step_of(a), a.seed_hi, stream, 0u));
     float m = x[0];
     for (int j = 1; j < a.n; j++) m = fmaxf(m, x[j]);
     float sum = 0.f, sx = 0.f;
@@ -423,6 +429,7 @@ static sn_status puct_args(sn_env* e, const sn_puct* q, PuctArgs& a) {
     a.c_puct = q->c_puct;
     a.seed_lo = (uint32_t)q->seed, a.seed_hi = (uint32_t)(q->seed >> 32), a.step = q->step;
     a.rollout = q->rollout;
+    a.step_dev = q->step_dev;
     a.avail = q->avail;
     a.ro = q->rollouts;
     a.stats = q->stats;

@@ -38,6 +38,7 @@ class SnPuct(ctypes.Structure):
         ("stats", ctypes.c_void_p),
         ("hist", ctypes.c_void_p),
         ("root_probs", ctypes.c_void_p),
+        ("step_dev", ctypes.c_void_p),
     ]
 
 

@@ -78,7 +78,7 @@ class FusedMLP:
 
 class BatchedPUCT:
     def __init__(self, env, actor, mc_per_card=10, mc_max=100, c_puct=2.0, seed=0, seats_mask=None, puct_root=True,
-                 net_dtype=torch.bfloat16, mcs_num_cards=104):
+                 net_dtype=torch.bfloat16, mcs_num_cards=104, graph=False):
         # `actor` stays where the caller keeps it (the drop-in agents run it
         # on the host): inference uses a device copy in net_dtype (sync_net),
         # the training losses run on the actor's own device (actor_device).
@@ -105,6 +105,13 @@ class BatchedPUCT:
         self._net = None
         self._net_version = None
         self.rows_evaluated = 0
+        # graph=True: a decision's rollout chain (n_mc x [deal, n x (rows,
+        # MLP, step)] launches) is captured once per (hand size, net version)
+        # as a hipGraph (torch.cuda.CUDAGraph) and replayed for every
+        # decision; the kernels read the decision counter from step_dev
+        self.graph = bool(graph)
+        self._graphs = {}
+        self._step_dev = torch.zeros((1,), dtype=torch.int32, device=dev)
 
     # ------------------------------------------------------------ policy net on the device
     def sync_net(self):
@@ -130,8 +137,9 @@ class BatchedPUCT:
     def n_mc(self, n):
         return min(self.mc_max, self.mc_per_card * math.factorial(n))
 
-    def _params(self, n, rollout=0):
+    def _params(self, n, rollout=0, step_dev=False):
         q = nat.SnPuct()
+        q.step_dev = self._step_dev.data_ptr() if step_dev else None
         q.seats_mask, q.n, q.puct_root, q.c_puct = self.seats_mask, n, int(self.puct_root), self.c_puct
         q.seed, q.step, q.rollout = self.seed & (2**64 - 1), self.step_id & 0xFFFFFFFF, rollout
         q.avail, q.rollouts, q.stats = self.avail.data_ptr(), self.ro.data_ptr(), self.stats.data_ptr()
@@ -156,16 +164,17 @@ class BatchedPUCT:
             rows = torch.empty((self.D * n, ROW), dtype=self.net_dtype, device=self.env.device)
             nat.check(L.sn_puct_root_rows(h, ctypes_ref(q), nat.ptr(rows), bf16, st), "sn_puct_root_rows")
             nat.check(L.sn_puct_init(h, ctypes_ref(q), nat.ptr(self._logits(rows)), st), "sn_puct_init")
-            N = self.env.num_players
-            bufs = {m: torch.empty((self.D * N * m, ROW), dtype=self.net_dtype, device=self.env.device)
-                    for m in range(1, n + 1)}
-            for r in range(self.n_mc(n)):
-                q.rollout = r
-                nat.check(L.sn_puct_deal(h, ctypes_ref(q), st), "sn_puct_deal")
-                for t in range(n):
-                    m = n - t
-                    nat.check(L.sn_puct_rows(h, ctypes_ref(q), m, nat.ptr(bufs[m]), bf16, st), "sn_puct_rows")
-                    nat.check(L.sn_puct_step(h, ctypes_ref(q), nat.ptr(self._logits(bufs[m])), t, m, st), "sn_puct_step")
+            if self.graph:
+                self._step_dev.fill_(self.step_id & 0x7FFFFFFF)
+                g = self._graphs.get((n, self._net_version))
+                if g is None:
+                    g = self._capture(n)
+                    self._graphs = {k: v for k, v in self._graphs.items() if k[1] == self._net_version}
+                    self._graphs[(n, self._net_version)] = g
+                g[0].replay()
+                self.rows_evaluated += g[1]
+            else:
+                self._rollouts(n, q)
         nat.check(L.sn_puct_choose(h, ctypes_ref(q), nat.ptr(self.actions), nat.ptr(self.best_index), st),
                   "sn_puct_choose")
         if record and n > 1:
@@ -182,6 +191,42 @@ class BatchedPUCT:
         nat.check(nat.lib().sn_puct_root_rows(self.env._h, ctypes_ref(q), nat.ptr(r32), 0, self.env._stream()),
                   "sn_puct_root_rows")
         return r32
+
+    def _rollouts(self, n, q):
+        """the decision's rollout chain: n_mc x [deal, n x (rows, MLP, step)]"""
+        L, h, st = nat.lib(), self.env._h, self.env._stream()
+        bf16 = int(self.net_dtype == torch.bfloat16)
+        N = self.env.num_players
+        bufs = self._bufs(n)
+        for r in range(self.n_mc(n)):
+            q.rollout = r
+            nat.check(L.sn_puct_deal(h, ctypes_ref(q), st), "sn_puct_deal")
+            for t in range(n):
+                m = n - t
+                nat.check(L.sn_puct_rows(h, ctypes_ref(q), m, nat.ptr(bufs[m]), bf16, st), "sn_puct_rows")
+                nat.check(L.sn_puct_step(h, ctypes_ref(q), nat.ptr(self._logits(bufs[m])), t, m, st), "sn_puct_step")
+
+    def _bufs(self, n):
+        N = self.env.num_players
+        if not hasattr(self, "_rowbufs"):
+            self._rowbufs = {}
+        for m in range(1, n + 1):
+            if m not in self._rowbufs:
+                self._rowbufs[m] = torch.empty((self.D * N * m, ROW), dtype=self.net_dtype, device=self.env.device)
+        return self._rowbufs
+
+    def _capture(self, n):
+        """capture _rollouts(n) with the decision counter read from step_dev"""
+        q = self._params(n, step_dev=True)
+        self._bufs(n)
+        before = self.rows_evaluated
+        torch.cuda.synchronize(self.env.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._rollouts(n, q)
+        rows = self.rows_evaluated - before
+        self.rows_evaluated = before
+        return g, rows
 
     def play_episode(self, others=None, record=False):
         """One whole game of every env game; deciding seats search, the other

@@ -217,6 +217,31 @@ def test_policy_loss_matches_reference_training_loss():
         assert torch.allclose(a.cpu(), r, rtol=1e-4, atol=1e-4), (a, r)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_graph_replay_equals_eager_search(dtype):
+    """graph=True (one captured hipGraph of a decision's rollout chain per
+    hand size, the decision counter read from device memory) gives the same
+    statistics, actions and root probabilities as launching eagerly, over a
+    whole game (every hand size, each graph replayed 4 x 1 decisions, and
+    captured once)."""
+    res = []
+    for graph in (False, True):
+        env, eng = _engine(B=96, dtype=dtype, mc_max=12, mc_per_card=2, seed=17)
+        eng.graph = graph
+        out = []
+        for t in range(10):
+            n = 10 - t
+            acts = eng.decide(n).clone()
+            out.append((acts.cpu(), eng.stats.cpu().clone(), eng.hist.cpu().clone(), eng.root_probs.cpu().clone()))
+            env.step(acts)
+        res.append((out, eng.rows_evaluated))
+    (a, ra), (b, rb) = res
+    assert ra == rb
+    for x, y in zip(a, b):
+        for u, v in zip(x, y):
+            assert torch.equal(u, v)
+
+
 def test_search_statistics_consistent():
     env, eng = _engine(B=32, mc_max=12, mc_per_card=2)
     for t in range(10):

@@ -46,6 +46,16 @@ def episode_pmf(N):
     return d
 
 
+def league_pmf(N, K, lo, hi):
+    """one tournament game (league.py): the seat draw -- choice of the player
+    count, permutation of the K agents -- then the episode"""
+    d = episode_pmf(N)
+    d = conv(d, geo(hi - lo))
+    for i in range(K - 1, 0, -1):
+        d = conv(d, geo(i))
+    return d
+
+
 def main(limit=592):
     print("N  words/episode  P(pair > %d): 10-step launches   5-step launches" % limit)
     for N in range(1, 11):
@@ -53,6 +63,11 @@ def main(limit=592):
         two = conv(ep, ep)
         mean = (np.arange(L) * ep).sum()
         print(f"{N:2d}  {mean:13.1f}  {two[limit + 1:].sum():28.2e}  {ep[limit + 1:].sum():16.2e}")
+    print("tournament handles (N = max_players, min_players 2): P(pair > %d)" % limit)
+    for N, K in ((4, 5), (4, 8), (4, 16), (6, 16)):
+        ep = league_pmf(N, K, 2, N)
+        two = conv(ep, ep)
+        print(f"  N={N} K={K:2d}: 10-step {two[limit + 1:].sum():.2e}   5-step {ep[limit + 1:].sum():.2e}")
 
 
 if __name__ == "__main__":
