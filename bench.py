@@ -68,9 +68,11 @@ def parse():
     ap.add_argument("--rng", default="numpy", choices=["numpy", "philox"])
     ap.add_argument("--no-obs", action="store_true", help="do not emit observations (not the headline)")
     ap.add_argument("--pipe-gpw", type=int, default=64, choices=[32, 64], help="games per k_play wave (pipelined path)")
+    ap.add_argument("--play-split", type=int, default=None, choices=[0, 1, 2, 3],
+                    help="SN_OPT_PLAY_SPLIT (default: the library's)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--extras", action="store_true", help="also time the philox mode and the per-step API")
+    ap.add_argument("--no-philox", action="store_true", help="skip the philox-mode leg of config 2")
     ap.add_argument("--no-mcs", action="store_true", help="skip the config-3 MCS leg")
     ap.add_argument("--mcs-games", type=int, default=8192)
     ap.add_argument("--mcs-rollouts", type=int, default=256)
@@ -514,7 +516,7 @@ def main():
     B = args.games
     env = VecSechsNimmtEnv(B, N_PLAYERS, seed=0, game_offset=rank * B, rng=args.rng)
     if args.rng == "numpy":
-        env.set_option(pipe_gpw=args.pipe_gpw)
+        env.set_option(pipe_gpw=args.pipe_gpw, play_split=args.play_split)
     env.reset()
     out = make_out(env, B, not args.no_obs)
     wall, kern_ms, kt = time_rollouts(env, out, args.steps, args.warmup, world)
@@ -614,11 +616,23 @@ def main():
         league = bench_league(world, rank, B, args.league_rounds)
         if rank == 0:
             result["extra_config5_tournament"] = league
-    if args.extras and world == 1:
+    if world == 1 and not args.no_philox and args.rng == "numpy":
+        # config 2 in the counter-based mode ("philox ... used for
+        # throughput"): same games-per-launch, role-split k_play (SN_OPT_PLAY_SPLIT 1)
         env2 = VecSechsNimmtEnv(B, N_PLAYERS, seed=0, rng="philox")
         env2.reset()
         w2, k2, _ = time_rollouts(env2, out, args.steps, args.warmup, world)
-        result["extra_philox"] = {"value": B * STEPS_PER_LAUNCH * args.steps / w2, "kernel_ms": k2}
+        env2.close()
+        ach2 = launch_steps * ALGO_BYTES_PER_STEP / (k2 * 1e-3) / 1e9
+        result["extra_config2_philox"] = {
+            "metric": "env-steps/sec at 65536 concurrent 4-player games (philox RNG mode)",
+            "value": B * STEPS_PER_LAUNCH * args.steps / w2, "unit": "env-steps/s",
+            "ms_per_step": w2 / args.steps * 1e3,
+            "roofline": {"bound": "hbm", "achieved": ach2, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": ach2 / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "k_play_split<4, RNG_PHILOX>: producer waves decode the draws into LDS",
+                         "kernel_ms": k2, "kernel_ms_source": "HIP events around each timed launch on the launch stream"},
+        }
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -150,9 +150,19 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
      SN_OPT_PIPE_LEAD    words k_mt_ahead keeps twisted past the consumer
                          (64..600, default 600).  TEST KNOB: below 600 the
                          overrun bound of sn_pipe_errors no longer holds;
-                         it exists to exercise the SN_ERNG path. */
+                         it exists to exercise the SN_ERNG path.
+     SN_OPT_PLAY_SPLIT   role-split k_play (producer waves decode every random
+                         decision into LDS beside the play waves) for in-kernel
+                         DrunkHamster rollouts of a handle whose games are in
+                         lockstep (after sn_reset; N <= 4, auto-reset):
+                         1 (default): philox handles; 2: also numpy-compat over
+                         the pipelined ring; 3: numpy-compat with each game's
+                         MT19937 twisted in the producer waves (no ring, no
+                         side stream); 0: never.  Measured (65 536 x 4p): philox
+                         74 -> 59 us per 10 env-steps; numpy 2 / 3 slower than
+                         the pipelined one-wave kernel. */
 enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3, SN_OPT_TIMING = 4, SN_OPT_PIPE_GPW = 5,
-       SN_OPT_PIPE_LEAD = 6 };
+       SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7 };
 sn_status sn_set_option(sn_env* env, int option, int value);
 /* pipelined rollouts whose draws ran past the twisted words (must be 0; a
    nonzero count means those games' draws are wrong) [sync].  The count is
@@ -165,9 +175,12 @@ sn_status sn_pipe_errors(sn_env* env, uint32_t* count);
 sn_status sn_kernel_times(sn_env* env, float* play_ms, float* ahead_ms, int32_t* n);
 /* Diagnostics (no reference counterpart): shader-clock cycles every k_play
    wave spent per phase of its step loop since the last call, summed over
-   waves -- out[0..8] = prologue, obs, draws, resolve, output stores, deck
-   shuffle targets, epilogue, hand sorting, deck shuffle swaps; out[9] =
-   waves.  Only the libsechs_prof.so build
+   waves -- out[0..10] = prologue, obs, draws, resolve, output stores, deck
+   shuffle targets, epilogue, hand sorting, deck shuffle swaps, and (role-
+   split play waves) the waits at the two barriers; out[11..18] = the split
+   kernel's producer waves: draws, barrier 1, shuffle targets, swaps, hands,
+   later draws, barrier 2, state store; out[19] = play waves, out[20] =
+   producer waves.  Only the libsechs_prof.so build
    (-DSECHS_PHASE_PROF) records them; the product build returns
    SN_EUNSUPPORTED [sync]. */
 sn_status sn_debug_phases(uint64_t* out, int n);

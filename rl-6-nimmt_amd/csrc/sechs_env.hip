@@ -12,6 +12,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <type_traits>
 
 #include "sechs_state.h"
 
@@ -376,9 +377,14 @@ __global__ void k_pipe_code(DevState s, int cin, int tin) {
 // the libsechs_prof.so variant).  Each wave accumulates shader-clock cycles
 // per phase of its step loop and adds them to g_phase at exit; the clock
 // reads add lgkmcnt waits at the phase marks, so the split is indicative.
-enum { PH_PROLOGUE = 0, PH_OBS, PH_DRAW, PH_RESOLVE, PH_STORE, PH_DEAL, PH_EPILOGUE, PH_HANDS, PH_APPLY, PH_N };
+// PH_B1 / PH_B2: a k_play_split play wave waiting at its barriers; PR_*: the
+// producer waves' phases.  g_phase[PH_N] counts play waves, [PH_N + 1] producers.
+enum {
+    PH_PROLOGUE = 0, PH_OBS, PH_DRAW, PH_RESOLVE, PH_STORE, PH_DEAL, PH_EPILOGUE, PH_HANDS, PH_APPLY, PH_B1, PH_B2,
+    PR_DRAWS, PR_B1, PR_TARGETS, PR_APPLY, PR_HANDS, PR_DRAWS2, PR_B2, PR_STORE, PH_N
+};
 #ifdef SECHS_PHASE_PROF
-__device__ unsigned long long g_phase[PH_N + 1];
+__device__ unsigned long long g_phase[PH_N + 2];
 struct PhaseProf {
     uint64_t t, acc[PH_N];
     __device__ __forceinline__ void start() {
@@ -391,11 +397,12 @@ struct PhaseProf {
         acc[k] += n - t;
         t = n;
     }
-    __device__ __forceinline__ void flush(int lane) {
+    __device__ __forceinline__ void flush(int lane, int role = 0) {
         if (lane == 0) {
 #pragma unroll
-            for (int k = 0; k < PH_N; k++) atomicAdd(&g_phase[k], (unsigned long long)acc[k]);
-            atomicAdd(&g_phase[PH_N], 1ull);
+            for (int k = 0; k < PH_N; k++)
+                if (acc[k]) atomicAdd(&g_phase[k], (unsigned long long)acc[k]);
+            atomicAdd(&g_phase[PH_N + role], 1ull);
         }
     }
 };
@@ -403,7 +410,7 @@ struct PhaseProf {
 struct PhaseProf {
     __device__ __forceinline__ void start() {}
     __device__ __forceinline__ void mark(int) {}
-    __device__ __forceinline__ void flush(int) {}
+    __device__ __forceinline__ void flush(int, int = 0) {}
 };
 #endif
 
@@ -424,6 +431,7 @@ struct PlayArgs {
     int32_t* invalid;        // [B]
     int32_t* league_rec;     // league: [episodes][B][1 + N] per finished game: seats word, results
     int step0;               // league: env-steps of this rollout before this launch (episode index of a record)
+    int n0;                  // k_play_split: every game's hand size at the launch's start (aligned handle)
 };
 
 // The env-step loop of one lane (game g).  R supplies the random words
@@ -433,22 +441,52 @@ struct PlayArgs {
 // are assembled so that they leave as 1-KB contiguous stores instead of 64
 // scattered 16-B pieces per instruction.  (Both uses never overlap in time
 // within a step: observations first, the deal at the very end.)
-template <int N, class R, int GPW = 64, bool LG = false>
+// Where a step's random decisions come from.  StreamSrc: the game's own
+// word stream, in the play loop (DrunkHamster draws, tournament seat draws,
+// the deal).  SplitSrc: decisions a producer wave decoded into LDS
+// (k_play_split): the indices of every step, the next deal's hands/rows.
+template <int N, class R>
+struct StreamSrc {
+    R& rng;
+    ByteBuf& buf;
+    uint8_t* deck;  // kDealStride bytes of LDS: deck + swap targets
+    __device__ __forceinline__ void draws(const Game<N>& G, int, uint32_t kp, bool lg, uint32_t (&idx)[N]) {
+        // DrunkHamster for every seat in seat order (play.py:38-41):
+        // legal[random_interval(n-1)], agents/random.py:9
+        if (lg && !__all(kp == (uint32_t)N)) {  // a tournament game with fewer players
+#pragma unroll
+            for (int p = 0; p < N; p++) idx[p] = ((uint32_t)p < kp) ? rng_interval(rng, buf, G.n - 1u) : 0u;
+        } else {
+            rng_draws<N>(rng, buf, G.n - 1u, idx);
+        }
+    }
+    __device__ __forceinline__ uint32_t league(const DevState& s) { return league_draw(rng, buf, s.lg_K, s.lg_lo, s.lg_hi); }
+    __device__ __forceinline__ void deal(const DevState& s, Game<N>& G, PhaseProf& pp) {
+        // deck_shuffle2 in its two phases (marked apart for the profiler)
+        shuffle_targets(rng, buf, deck + kDeckStride, s.C);
+        pp.mark(PH_DEAL);
+        for (int i = 0; i < s.C; i += 4) *(uint32_t*)(deck + i) = (uint32_t)i * 0x01010101u + 0x03020100u;
+        shuffle_apply(deck, deck + kDeckStride, s.C);
+        pp.mark(PH_APPLY);
+        deal_from_deck<N>(deck, s.C, G);
+    }
+};
+
+template <int N, class Src, int GPW = 64, bool LG = false>
 __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a, int64_t g, int lane, uint8_t* wave_lds,
-                                           Game<N>& G, R& rng, ByteBuf& buf, int32_t (&sum_res)[N], int32_t& episodes,
-                                           PhaseProf& pp, uint32_t& lg) {
+                                           Game<N>& G, Src& src, int32_t (&sum_res)[N], int32_t& episodes,
+                                           PhaseProf& pp, uint32_t& lg, int t_begin, int t_end) {
     const int64_t B = s.B;
-    uint8_t* my_deck = wave_lds + lane * kDealStride;
     const bool staged = a.obs && a.obs_stride == 48;
     const int64_t g0 = g - lane;                           // first game of this wave
     const int wave_games = (int)min((int64_t)GPW, B - g0);  // = active lanes (lanes past B left)
     const bool auto_reset = (a.flags & SN_AUTO_RESET) != 0;
     const bool summ = !(a.flags & SN_NO_SUMMARIES);
-    int32_t* rew = a.rewards ? a.rewards + g * N : nullptr;
-    uint8_t* act = a.actions_out ? a.actions_out + g * N : nullptr;
-    uint8_t* dn = a.done ? a.done + g : nullptr;
-    int8_t* ob = a.obs ? a.obs + g * N * a.obs_stride : nullptr;
-    for (int t = 0; t < a.steps; t++) {
+    int32_t* rew = a.rewards ? a.rewards + ((int64_t)t_begin * B + g) * N : nullptr;
+    uint8_t* act = a.actions_out ? a.actions_out + ((int64_t)t_begin * B + g) * N : nullptr;
+    uint8_t* dn = a.done ? a.done + (int64_t)t_begin * B + g : nullptr;
+    int8_t* ob = a.obs ? a.obs + ((int64_t)t_begin * B + g) * N * a.obs_stride : nullptr;
+    for (int t = t_begin; t < t_end; t++) {
         const uint32_t kp = LG ? (lg & 15u) : (uint32_t)N;  // players of this game
         if (ob) {
             uint32_t w2hi;
@@ -501,14 +539,7 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
                 bad = (k >= 0) ? bad : p;
             }
         } else {
-            // DrunkHamster for every seat in seat order (play.py:38-41):
-            // legal[random_interval(n-1)], agents/random.py:9
-            if (LG && !__all(kp == (uint32_t)N)) {  // a tournament game with fewer players
-#pragma unroll
-                for (int p = 0; p < N; p++) idx[p] = ((uint32_t)p < kp) ? rng_interval(rng, buf, G.n - 1u) : 0u;
-            } else {
-                rng_draws<N>(rng, buf, G.n - 1u, idx);
-            }
+            src.draws(G, t, kp, LG, idx);
 #pragma unroll
             for (int p = 0; p < N; p++) card[p] = hand_get(G.hand[p], idx[p]);
         }
@@ -570,14 +601,8 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
 #pragma unroll
             for (int p = 0; p < N; p++) sum_res[p] -= G.score[p];
             episodes += 1;
-            if (LG) lg = league_draw(rng, buf, s.lg_K, s.lg_lo, s.lg_hi);  // Tournament.play_game: seats first
-            // deck_shuffle2 in its two phases (marked apart for the profiler)
-            shuffle_targets(rng, buf, my_deck + kDeckStride, s.C);
-            pp.mark(PH_DEAL);
-            for (int i = 0; i < s.C; i += 4) *(uint32_t*)(my_deck + i) = (uint32_t)i * 0x01010101u + 0x03020100u;
-            shuffle_apply(my_deck, my_deck + kDeckStride, s.C);
-            pp.mark(PH_APPLY);
-            deal_from_deck<N>(my_deck, s.C, G);
+            if (LG) lg = src.league(s);  // Tournament.play_game: seats first
+            src.deal(s, G, pp);
             if (LG) {  // a k-player env deals k hands (env.py:108)
                 const uint32_t k2 = lg & 15u;
 #pragma unroll
@@ -637,7 +662,9 @@ __device__ __forceinline__ void play_body(const DevState& s, const PlayArgs& a, 
         RingPipe rng;
         rng.load(s, g, buf, wave_lds + a.wave_lds - GPW * a.ring_lds + lane * a.ring_lds, a.pipe_cin, a.pipe_t);
         pp.mark(PH_PROLOGUE);
-        play_steps<N, RingPipe, GPW, LG>(s, a, g, lane, wave_lds, G, rng, buf, sum_res, episodes, pp, lg);
+        StreamSrc<N, RingPipe> src{rng, buf, wave_lds + lane * kDealStride};
+        play_steps<N, StreamSrc<N, RingPipe>, GPW, LG>(s, a, g, lane, wave_lds, G, src, sum_res, episodes, pp, lg, 0,
+                                                       a.steps);
         s.pabsc[(int64_t)a.pipe_cout * s.B + g] = rng.consumed(buf);
     } else {
         typename RngOf<MODE, kPlayPrefetch>::T rng;
@@ -648,8 +675,9 @@ __device__ __forceinline__ void play_body(const DevState& s, const PlayArgs& a, 
             RngOf<MODE, kPlayPrefetch>::load(s, g, rng, buf);
         }
         pp.mark(PH_PROLOGUE);
-        play_steps<N, typename RngOf<MODE, kPlayPrefetch>::T, 64, LG>(s, a, g, lane, wave_lds, G, rng, buf, sum_res,
-                                                                      episodes, pp, lg);
+        using Gen = typename RngOf<MODE, kPlayPrefetch>::T;
+        StreamSrc<N, Gen> src{rng, buf, wave_lds + lane * kDealStride};
+        play_steps<N, StreamSrc<N, Gen>, 64, LG>(s, a, g, lane, wave_lds, G, src, sum_res, episodes, pp, lg, 0, a.steps);
         RngOf<MODE, kPlayPrefetch>::store(s, g, rng, buf);
     }
     store_game<N>(s, g, G);
@@ -758,6 +786,223 @@ __global__ __launch_bounds__(64) void k_reset1(DevState s, uint32_t* hb, int sum
     }
     __syncthreads();
     for (int i = t; i < kMtN; i += 64) hb[kH1Mt + i] = s.mt[i];
+}
+
+
+// ============================================================================
+// Role-split k_play (SN_OPT_PLAY_SPLIT, the default for aligned rollouts).
+// Every random decision of the DrunkHamster self-play depends on the word
+// stream only, never on the cards: the hand size at each step is fixed (the
+// games of a handle stay in lockstep after a reset: `phase`), so the
+// policy draws' maxima are known, and the deal is a function of the words.
+// A block is 4 PLAY waves + 4 PRODUCER waves on the same 256 games (two
+// waves per SIMD, where one game per lane leaves one: a single wave issues
+// a VALU instruction at most every 4 cycles, two every 2).  Producers decode
+// the launch's policy indices into LDS (nibbles), barrier B1, then shuffle
+// and deal the next episode and decode the steps after it while the play
+// waves play up to the episode's end; barrier B2; play waves install the
+// dealt hands and go on.  The play waves issue no RNG work at all; the
+// producers read the pipelined ring straight from HBM (RingGlobal: no
+// stores of theirs in flight, so no vmcnt stall behind the obs stores).
+// Same words, same order, same results: every parity test runs this path.
+// ============================================================================
+struct RingGlobal {  // RingPipe's stream, 16-B ring chunks read from HBM (4 in registers, 3 ahead)
+    const uint8_t* ring;
+    uint32_t* err;
+    int64_t B, g;
+    uint32_t c0, take, avail, q0;
+    u32x4 ch0, ch1, ch2, ch3;  // chunks q0 .. q0+3: a chunk's load goes out ~48 bytes before it is read
+
+    __device__ __forceinline__ u32x4 chunk(uint32_t q) const {
+        return *(const u32x4*)(ring + ((int64_t)(q & (uint32_t)(kPipeRing / 16 - 1)) * B + g) * 16);
+    }
+    __device__ __forceinline__ void load(const DevState& s, int64_t gg, ByteBuf& buf, int cin, int tpar) {
+        g = gg, B = s.B;
+        ring = (const uint8_t*)s.pring;
+        err = s.perr;
+        c0 = s.pabsc[(int64_t)cin * B + g];
+        const int32_t av = (int32_t)(s.ptend[(int64_t)tpar * B + g] - c0);
+        if (av < 0) atomicAdd(s.perr, 1u);
+        avail = (av < 0) ? 0u : (uint32_t)av;
+        take = 0u;
+        q0 = c0 >> 4;
+        ch0 = chunk(q0);
+        ch1 = chunk(q0 + 1u);
+        ch2 = chunk(q0 + 2u);
+        ch3 = chunk(q0 + 3u);
+        buf.clear();
+    }
+    __device__ __forceinline__ uint32_t consumed(const ByteBuf& buf) const { return c0 + take - buf.cnt; }
+    __device__ __forceinline__ bool gen(ByteBuf& buf, bool forced) {
+        if (take + 8u <= avail) {
+            const uint32_t p = c0 + take;  // absolute stream position (wraps at 2^32 like the ring's)
+            if (((p >> 4) - q0) & 0x0FFFFFFFu) {  // 8 bytes per call: crosses at most one chunk boundary
+                q0 += 1u;
+                ch0 = ch1, ch1 = ch2, ch2 = ch3;
+                ch3 = chunk(q0 + 3u);
+            }
+            const uint32_t o = p & 15u;
+            const uint64_t w0 = (uint64_t)ch0.x | ((uint64_t)ch0.y << 32), w1 = (uint64_t)ch0.z | ((uint64_t)ch0.w << 32);
+            const uint64_t w2 = (uint64_t)ch1.x | ((uint64_t)ch1.y << 32);
+            const uint64_t lo = (o < 8u) ? w0 : w1, hi = (o < 8u) ? w1 : w2;
+            const uint32_t sh = 8u * (o & 7u);
+            buf.append(sh ? ((lo >> sh) | (hi << (64u - sh))) : lo, 8u);
+            take += 8u;
+            return true;
+        }
+        const uint32_t left = (avail > take) ? avail - take : 0u;
+        if (left == 0u && !forced) return false;
+        const PipeSlow r = pipe_slow(ring, B, g, c0 + take, left, err);
+        buf.append(r.bytes, r.k);
+        take += r.k;
+        return true;
+    }
+    __device__ __forceinline__ void topup(ByteBuf& buf) {
+        if (buf.cnt <= 24u) gen(buf, false);
+    }
+    __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf, true); }
+};
+
+template <int N>
+struct SplitSrc {
+    const uint16_t* idx;  // this lane's column of the producer's [t][64] index words
+    __device__ __forceinline__ void draws(const Game<N>&, int t, uint32_t, bool, uint32_t (&out)[N]) {
+        const uint32_t v = idx[t * 64];
+#pragma unroll
+        for (int p = 0; p < N; p++) out[p] = (v >> (4 * p)) & 15u;
+    }
+    __device__ __forceinline__ uint32_t league(const DevState&) { return 0u; }
+    __device__ __forceinline__ void deal(const DevState&, Game<N>&, PhaseProf&) {}  // installed after B2
+};
+
+// the policy indices of steps [t_from, t_to): hand size m_first at t_from,
+// one less each step (the game's n), N seats in seat order (play.py:38-41)
+template <int N, class R>
+__device__ __forceinline__ void produce_draws(R& rng, ByteBuf& buf, uint16_t* idx, int t_from, int t_to, int m_first) {
+    for (int t = t_from; t < t_to; t++) {
+        const int m = m_first - (t - t_from);
+        uint32_t v = 0u;
+        if (m >= 2) {
+            uint32_t d[N];
+            rng_draws<N>(rng, buf, (uint32_t)(m - 1), d);
+#pragma unroll
+            for (int p = 0; p < N; p++) v |= d[p] << (4 * p);
+        }
+        idx[t * 64] = (uint16_t)v;
+    }
+}
+
+// LDS of a k_play_split block: play staging | decks | index words | dealt games
+__host__ __device__ __forceinline__ int split_deal_words(int N) { return 3 * N + 1; }
+__host__ __device__ __forceinline__ size_t split_lds(int N, int steps) {
+    return (size_t)4 * 64 * N * 48 + (size_t)4 * 64 * kDealStride + (size_t)4 * steps * 64 * 2 +
+           (size_t)4 * split_deal_words(N) * 64 * 4;
+}
+
+template <int N, int MODE>
+__global__ __launch_bounds__(2 * kBlock) void k_play_split(DevState s, PlayArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
+    // the role is wave-uniform: readfirstlane makes it a scalar branch, so each
+    // wave runs only its role's code -- and exactly its role's two barriers
+    const int tid = (int)threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, w = wave & 3;
+    const int64_t g = ((int64_t)blockIdx.x * 4 + w) * 64 + lane;
+    const bool live = g < s.B;
+    uint8_t* staging = lds_dyn + (size_t)w * 64 * N * 48;
+    uint8_t* decks = lds_dyn + (size_t)4 * 64 * N * 48;
+    uint16_t* idx = (uint16_t*)(decks + (size_t)4 * 64 * kDealStride) + (size_t)w * a.steps * 64 + lane;
+    uint32_t* dealt = (uint32_t*)((uint8_t*)((uint16_t*)(decks + (size_t)4 * 64 * kDealStride) + (size_t)4 * a.steps * 64)) +
+                      (size_t)w * split_deal_words(N) * 64 + lane;
+    const int n0 = a.n0;
+    const bool deal_in = n0 >= 1 && n0 <= a.steps;  // the episode ends at step n0 - 1 of this launch
+    const int tA = deal_in ? n0 : a.steps;
+    if (wave >= 4) {  // ---------------- producer (the critical path: issue priority over the play waves)
+        __builtin_amdgcn_s_setprio(1);
+        // the word stream: the pipelined ring (k_mt_ahead twisted it), the
+        // game's own MT19937 state twisted here 16 words per refill (no
+        // store of this wave is in flight to stall its loads), or Philox
+        using R = typename std::conditional<MODE == RNG_NUMPY_PIPE, RingGlobal,
+                                            typename std::conditional<MODE == RNG_NUMPY_MT, MtGenT<2>, PhiloxGen>::type>::type;
+        R rng;
+        ByteBuf buf;
+        PhaseProf pq;
+        pq.start();
+        if (live) {
+            if constexpr (MODE == RNG_NUMPY_PIPE) rng.load(s, g, buf, a.pipe_cin, a.pipe_t);
+            else RngOf<MODE, 2>::load(s, g, rng, buf);
+            produce_draws<N>(rng, buf, idx, 0, tA, n0);
+        }
+        pq.mark(PR_DRAWS);
+        __syncthreads();  // B1: this launch's first indices are in LDS
+        pq.mark(PR_B1);
+        if (live && deal_in) {
+            uint8_t* deck = decks + (size_t)(w * 64 + lane) * kDealStride;
+            Game<N> D;
+            shuffle_targets(rng, buf, deck + kDeckStride, s.C);
+            pq.mark(PR_TARGETS);
+            for (int i = 0; i < s.C; i += 4) *(uint32_t*)(deck + i) = (uint32_t)i * 0x01010101u + 0x03020100u;
+            shuffle_apply(deck, deck + kDeckStride, s.C);
+            pq.mark(PR_APPLY);
+            deal_from_deck<N>(deck, s.C, D);
+#pragma unroll
+            for (int p = 0; p < N; p++) {
+                dealt[(3 * p + 0) * 64] = (uint32_t)D.hand[p].lo;
+                dealt[(3 * p + 1) * 64] = (uint32_t)(D.hand[p].lo >> 32);
+                dealt[(3 * p + 2) * 64] = D.hand[p].hi;
+            }
+            dealt[3 * N * 64] = (D.b.lo.x & 0xFFu) | ((D.b.lo.y & 0xFFu) << 8) | ((D.b.lo.z & 0xFFu) << 16) | (D.b.lo.w << 24);
+            pq.mark(PR_HANDS);
+            produce_draws<N>(rng, buf, idx, tA, a.steps, kHand);
+            pq.mark(PR_DRAWS2);
+        }
+        __syncthreads();  // B2: the deal and the later indices are in LDS
+        pq.mark(PR_B2);
+        if (live) {
+            if constexpr (MODE == RNG_NUMPY_PIPE) s.pabsc[(int64_t)a.pipe_cout * s.B + g] = rng.consumed(buf);
+            else RngOf<MODE, 2>::store(s, g, rng, buf);
+        }
+        pq.mark(PR_STORE);
+        pq.flush(lane, 1);
+        return;
+    }
+    // -------------------------------------------------------- play
+    PhaseProf pp;
+    pp.start();
+    Game<N> G;
+    int32_t sum_res[N], episodes = 0;
+    uint32_t lg = 0u;
+    if (live) {
+        load_game<N>(s, g, G);
+        load_results<N>(s, g, a.flags, sum_res, episodes);
+    }
+    pp.mark(PH_PROLOGUE);
+    SplitSrc<N> src{idx};
+    __syncthreads();  // B1
+    pp.mark(PH_B1);
+    if (live) play_steps<N, SplitSrc<N>, 64, false>(s, a, g, lane, staging, G, src, sum_res, episodes, pp, lg, 0, tA);
+    pp.mark(PH_EPILOGUE);
+    __syncthreads();  // B2
+    pp.mark(PH_B2);
+    if (live) {
+        if (deal_in) {  // the next episode's deal (env.py:99-112), decoded by the producer
+#pragma unroll
+            for (int p = 0; p < N; p++) {
+                G.hand[p].lo = (uint64_t)dealt[(3 * p + 0) * 64] | ((uint64_t)dealt[(3 * p + 1) * 64] << 32);
+                G.hand[p].hi = dealt[(3 * p + 2) * 64];
+                G.score[p] = 0;
+            }
+            const uint32_t rw = dealt[3 * N * 64];
+            const uint32_t r0 = rw & 0xFFu, r1 = (rw >> 8) & 0xFFu, r2 = (rw >> 16) & 0xFFu, r3 = rw >> 24;
+            G.b.lo = u32x4{r0, r1, r2, r3};
+            G.b.hi = u32x4{meta_row(r0), meta_row(r1), meta_row(r2), meta_row(r3)};
+            G.n = kHand;
+        }
+        pp.mark(PH_DEAL);
+        play_steps<N, SplitSrc<N>, 64, false>(s, a, g, lane, staging, G, src, sum_res, episodes, pp, lg, tA, a.steps);
+        store_game<N>(s, g, G);
+        store_results<N>(s, g, a.flags, sum_res, episodes);
+    }
+    pp.mark(PH_EPILOGUE);
+    pp.flush(lane);
 }
 
 // obs in any dtype, one thread per (game, seat)
@@ -885,6 +1130,8 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
     e->pipe = 1;
     e->pipe_gpw = 64;
     e->pipe_lead = kPipeLead;
+    e->phase = -1;
+    e->play_split = 1;
     e->pvalid = 0;
     e->pcount = 0;
     if (rng_mode == SN_RNG_NUMPY_MT) {
@@ -994,6 +1241,10 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
             if (value != 32 && value != 64) return fail(SN_EINVAL, "games per wave must be 32 or 64");
             e->pipe_gpw = value;
             return SN_OK;
+        case SN_OPT_PLAY_SPLIT:
+            if (value < 0 || value > 3) return fail(SN_EINVAL, "play split must be 0..3");
+            e->play_split = value;
+            return SN_OK;
         case SN_OPT_PIPE_LEAD:
             if (value < 64 || value > kPipeLead) return fail(SN_EINVAL, "pipe lead must be in 64..600");
             e->pipe_lead = value;
@@ -1041,17 +1292,20 @@ sn_status sn_reset(sn_env* e, const uint8_t* decks, void* stream) {
             });
         }
         e->lg_phase = 0;
+        e->phase = -1;
     } else if (s.rng_mode == SN_RNG_NUMPY_MT) {
         SN_DISPATCH_N(s.N, hipLaunchKernelGGL((k_reset<NN, RNG_NUMPY_MT>), dim3(grid_for(s.B)), dim3(kBlock), 0, st, s, decks));
     } else {
         SN_DISPATCH_N(s.N, hipLaunchKernelGGL((k_reset<NN, RNG_PHILOX>), dim3(grid_for(s.B)), dim3(kBlock), 0, st, s, decks));
     }
+    if (!s.lg_K) e->phase = 0;  // every game dealt: in lockstep
     HIP_TRY(hipGetLastError());
     return SN_OK;
 }
 
 sn_status sn_reset_to(sn_env* e, const int8_t* board, const int8_t* hands, void* stream) {
     if (!e || !board || !hands) return fail(SN_EINVAL, "NULL argument");
+    e->phase = -1;
     hipStream_t st = (hipStream_t)stream;
     const DevState& s = e->s;
     SN_DISPATCH_N(s.N, hipLaunchKernelGGL((k_reset_to<NN>), dim3(grid_for(s.B)), dim3(kBlock), 0, st, s, board, hands));
@@ -1061,6 +1315,13 @@ sn_status sn_reset_to(sn_env* e, const int8_t* board, const int8_t* hands, void*
 
 // LDS per CU (gfx950); a k_play block (4 waves) must fit in it
 constexpr int kLdsBytes = 160 * 1024;
+
+// k_play_split applies to in-kernel DrunkHamster rollouts of a handle whose
+// games are in lockstep (e->phase), with auto-reset, N <= kSplitMaxPlayers
+static bool split_ok(const sn_env* e, const PlayArgs& a) {
+    return e->play_split && e->phase >= 0 && (a.flags & SN_AUTO_RESET) && !a.actions && !a.invalid && !e->s.lg_K &&
+           e->s.N <= kSplitMaxPlayers && !(a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15));
+}
 
 static sn_status launch_play_one(sn_env* e, PlayArgs a, hipStream_t st) {
     const DevState& s = e->s;
@@ -1110,6 +1371,16 @@ static sn_status launch_play_one(sn_env* e, PlayArgs a, hipStream_t st) {
             HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_MT>,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
             hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_MT>), dim3(grid_for(s.B)), dim3(kBlock), shmem, st, s, a);
+        });
+    } else if (split_ok(e, a) && a.steps <= kHand) {  // at most one deal per launch
+        a.n0 = kHand - e->phase;
+        SN_DISPATCH_N(s.N, {
+            if constexpr (NN <= kSplitMaxPlayers) {
+                const size_t sl = split_lds(NN, a.steps);
+                HIP_TRY(hipFuncSetAttribute((const void*)k_play_split<NN, RNG_PHILOX>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)sl));
+                hipLaunchKernelGGL((k_play_split<NN, RNG_PHILOX>), dim3(grid_for(s.B)), dim3(2 * kBlock), sl, st, s, a);
+            }
         });
     } else {
         SN_DISPATCH_N(s.N, {
@@ -1191,10 +1462,12 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     // launches keep the pair tail < 1e-26 up to K = 8 agents at N <= 4
     // (tools/pipe_tail.py), beyond that 5-step launches
     const int chunk = min(e->chunk_steps, (s.lg_K > 8) ? 5 : pipe_max_chunk(s.N));
+    const bool split = e->play_split == 2 && split_ok(e, a) && gpw == 64;
     for (int t0 = 0; t0 < a.steps; t0 += chunk) {
         PlayArgs c = a;
         c.steps = min(chunk, a.steps - t0);
         c.step0 = a.step0 + t0;
+        c.n0 = split ? kHand - (e->phase + t0) % kHand : 0;
         if (a.rewards) c.rewards = a.rewards + (int64_t)t0 * B * N;
         if (a.done) c.done = a.done + (int64_t)t0 * B;
         if (a.actions_out) c.actions_out = a.actions_out + (int64_t)t0 * B * N;
@@ -1211,6 +1484,13 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
                 hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_PIPE, 32>), dim3((unsigned)((s.B + 32 * (kBlock / 64) - 1) / (32 * (kBlock / 64)))),
                                    dim3(kBlock), shmem, st, s, c);
+            } else if (split) {
+                if constexpr (NN <= kSplitMaxPlayers) {
+                    const size_t sl = split_lds(NN, c.steps);
+                    HIP_TRY(hipFuncSetAttribute((const void*)k_play_split<NN, RNG_NUMPY_PIPE>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sl));
+                    hipLaunchKernelGGL((k_play_split<NN, RNG_NUMPY_PIPE>), dim3(grid_for(s.B)), dim3(2 * kBlock), sl, st, s, c);
+                }
             } else if (s.lg_K) {
                 if constexpr (NN >= 2 && NN <= kLeagueMaxPlayers) {
                     HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_PIPE, 64, true>,
@@ -1251,6 +1531,39 @@ static sn_status launch_play(sn_env* e, PlayArgs a, hipStream_t st) {
         }
         return launch_play_one(e, a, st);
     }
+    if (s.rng_mode == SN_RNG_NUMPY_MT && e->play_split == 3 && split_ok(e, a)) {
+        // role-split k_play twisting each game's MT19937 in its producer
+        // waves: one kernel per <= 10 env-steps, no ring, no side stream
+        const sn_status r = sn_pipe_sync(e, st);
+        if (r != SN_OK) return r;
+        const int64_t B = s.B, N = s.N;
+        for (int t0 = 0; t0 < a.steps; t0 += kHand) {
+            PlayArgs c = a;
+            c.steps = min(kHand, a.steps - t0);
+            c.n0 = kHand - (e->phase + t0) % kHand;
+            if (a.rewards) c.rewards = a.rewards + (int64_t)t0 * B * N;
+            if (a.done) c.done = a.done + (int64_t)t0 * B;
+            if (a.actions_out) c.actions_out = a.actions_out + (int64_t)t0 * B * N;
+            if (a.obs) c.obs = a.obs + (int64_t)t0 * B * N * a.obs_stride;
+            hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
+            if (tv) HIP_TRY(hipEventRecord(tv[0], st));
+            SN_DISPATCH_N(s.N, {
+                if constexpr (NN <= kSplitMaxPlayers) {
+                    const size_t sl = split_lds(NN, c.steps);
+                    HIP_TRY(hipFuncSetAttribute((const void*)k_play_split<NN, RNG_NUMPY_MT>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sl));
+                    hipLaunchKernelGGL((k_play_split<NN, RNG_NUMPY_MT>), dim3(grid_for(s.B)), dim3(2 * kBlock), sl, st, s, c);
+                }
+            });
+            HIP_TRY(hipGetLastError());
+            if (tv) {
+                HIP_TRY(hipEventRecord(tv[1], st));
+                HIP_TRY(hipEventRecord(tv[2], st));
+                HIP_TRY(hipEventRecord(tv[3], st));
+            }
+        }
+        return SN_OK;
+    }
     if (s.rng_mode == SN_RNG_NUMPY_MT && !a.actions && e->pipe) {
         int wave;
         if (pipe_lds(s, a, e->pipe_gpw, &wave) <= (size_t)kLdsBytes) return launch_pipe(e, a, st);
@@ -1279,6 +1592,7 @@ sn_status sn_step(sn_env* e, const int32_t* actions, int32_t* rewards, uint8_t* 
                   void* stream) {
     if (!e) return fail(SN_EINVAL, "env is NULL");
     if (e->s.lg_K) return fail(SN_EUNSUPPORTED, "a tournament handle plays whole games with sn_league_rollout");
+    e->phase = -1;  // external actions may be refused per game
     PlayArgs a{};
     a.steps = 1;
     a.flags = flags;
@@ -1310,6 +1624,7 @@ sn_status sn_rollout(sn_env* e, int steps, int32_t* rewards, uint8_t* done, uint
     a.obs = obs;
     const sn_status r = launch_play(e, a, (hipStream_t)stream);
     if (r == SN_OK && e->s.lg_K) e->lg_phase = (e->lg_phase + steps) % kHand;
+    e->phase = (r == SN_OK && e->phase >= 0 && (flags & SN_AUTO_RESET)) ? (e->phase + steps) % kHand : -1;
     return r;
 }
 
@@ -1554,6 +1869,7 @@ sn_status sn_step1(sn_env* e, const int32_t* actions_host, int32_t* out_host, in
     HIP_TRY(hipSetDevice(e->device));
     if (h1_ready(e) != SN_OK) return SN_ENOMEM;
     if (e->s.lg_K) return fail(SN_EUNSUPPORTED, "a tournament handle plays whole games with sn_league_rollout");
+    e->phase = -1;
     Acts1 a{};
     for (int p = 0; p < e->s.N; p++) a.a[p] = actions_host[p];
     const int summ = !(flags & SN_NO_SUMMARIES);
@@ -1610,11 +1926,11 @@ sn_status sn_kernel_times(sn_env* e, float* play_ms, float* ahead_ms, int32_t* n
 sn_status sn_debug_phases(uint64_t* out, int n) {
     if (!out || n < 1) return fail(SN_EINVAL, "NULL argument");
 #ifdef SECHS_PHASE_PROF
-    unsigned long long h[PH_N + 1];
+    unsigned long long h[PH_N + 2];
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase), sizeof(h)));
-    for (int k = 0; k < n; k++) out[k] = (k <= PH_N) ? (uint64_t)h[k] : 0ull;
-    const unsigned long long z[PH_N + 1] = {};
+    for (int k = 0; k < n; k++) out[k] = (k <= PH_N + 1) ? (uint64_t)h[k] : 0ull;
+    const unsigned long long z[PH_N + 2] = {};
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)));
     return SN_OK;
 #else

@@ -414,6 +414,7 @@ sn_status sn_mcs_play_exact(sn_env* e, uint32_t mcs_seats, int mc_per_card, int 
     if (e->s.rng_mode != SN_RNG_NUMPY_MT) return set_error(SN_EINVAL, "reference-exact MCS needs the numpy-MT RNG mode");
     if (sn_pipe_sync(e, (hipStream_t)stream) != SN_OK) return SN_EHIP;
     if (mc_per_card < 0 || mc_max < 0) return set_error(SN_EINVAL, "mc_per_card and mc_max must be >= 0");
+    e->phase = -1;
     ExactArgs a{};
     a.mcs_seats = mcs_seats, a.mcs_cards = kMaxCards, a.mc_per_card = mc_per_card, a.mc_max = mc_max;
     a.actions = actions, a.rewards = rewards, a.status = status;

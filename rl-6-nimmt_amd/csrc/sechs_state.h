@@ -61,6 +61,7 @@ constexpr int kPipeWin = 304;    // of them, copied to LDS per lane at a k_play 
 constexpr int kBlock = 256;
 constexpr int kLeagueMaxPlayers = 6;  // tournament handles: 2..6 seats (agent ids packed 4 bits per seat)
 constexpr int kLeagueMaxAgents = 16;
+constexpr int kSplitMaxPlayers = 4;   // k_play_split: LDS for 4 staging + 4 producer waves
 constexpr int kDeckStride = 108;  // 27 dwords: odd dword stride -> conflict-free LDS lanes
 constexpr int kDealStride = 212;  // deck (108) + swap targets (104): 53 dwords, odd as well
 
@@ -817,6 +818,8 @@ struct sn_env {
     int pipe_gpw;     // SN_OPT_PIPE_GPW: games per k_play wave on the pipelined path (32 or 64)
     int pipe_lead;    // SN_OPT_PIPE_LEAD: words k_mt_ahead keeps twisted ahead (kPipeLead; tests lower it)
     int lg_phase;     // tournament handle: env-steps since the games were dealt, mod 10 (-1: not dealt yet)
+    int phase;        // every game's env-steps since its deal, mod 10, when they are in lockstep; -1 unknown
+    int play_split;   // SN_OPT_PLAY_SPLIT: role-split k_play for lockstep DrunkHamster rollouts
     sechs::DevState s;
     // pipelined twist-ahead (sechs_env.hip launch_pipe): a k_mt_ahead for the
     // next play launch may be in flight on `side` (ev_prep) after a rollout

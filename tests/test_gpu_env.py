@@ -349,6 +349,39 @@ def test_ring_options_do_not_change_results(ring_words, chunk_steps, pipeline, g
     assert env.pipe_errors() == 0
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("rng,split", [("numpy", 0), ("numpy", 2), ("numpy", 3), ("philox", 0), ("philox", 1)])
+@pytest.mark.parametrize("N", [2, 3, 4])
+def test_play_split_modes_match_oracle(rng, split, N):
+    """SN_OPT_PLAY_SPLIT (role-split k_play: producer waves decode every
+    random decision into LDS) changes nothing observable: ragged B, launches
+    that start mid-episode (3 then 10-step chunks: the deal falls inside a
+    launch), obs/actions/rewards/done and the final RNG states equal the
+    oracle's."""
+    B, T0, T, seed = 300, 3, 37, 5
+    env = venv(B, N, seed=seed, rng=rng)
+    env.set_option(play_split=split)
+    env.reset()
+    mode = O.RNG_NUMPY_MT if rng == "numpy" else O.RNG_PHILOX
+    ref = O.VecOracle(B, N, rng_mode=mode, seed=seed)
+    ref.reset()
+    for t in (T0, T):
+        out = env.rollout(t, want_actions=True, want_obs=True)
+        rr, rd, ra, ro = ref.rollout(t, want_obs=True)
+        torch.cuda.synchronize()
+        assert np.array_equal(out["actions"].cpu().numpy(), ra)
+        assert np.array_equal(out["rewards"].cpu().numpy(), rr)
+        assert np.array_equal(out["done"].cpu().numpy(), rd)
+        assert np.array_equal(out["obs"].cpu().numpy()[..., :47], ro)
+    if rng == "numpy":
+        rngs = ref.v.contents.rngs
+        for g in range(0, B, 13):
+            k, p = _np_form(*env.get_mt_state(g))
+            rk, rp = _np_form(np.frombuffer(bytes(rngs[g].mt), dtype=np.uint32), rngs[g].pos)
+            assert p == rp and np.array_equal(k, rk), g
+        assert env.pipe_errors() == 0
+
+
 def test_ring_option_validation():
     env = venv(4, 4, rng="numpy")
     for bad in (-64, 32, 576):

@@ -21,9 +21,11 @@ def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
     T = int(sys.argv[2]) if len(sys.argv) > 2 else 30
     N = 4
+    split = int(os.environ.get("SECHS_PLAY_SPLIT", "1"))  # 0..3 (SN_OPT_PLAY_SPLIT)
     for rng, mode in (("numpy", O.RNG_NUMPY_MT), ("philox", O.RNG_PHILOX)):
         for want_obs in (True, False):
             env = VecSechsNimmtEnv(B, N, seed=11, rng=rng, device="cuda:0")
+            env.set_option(play_split=split)
             env.reset()
             ref = O.VecOracle(B, N, rng_mode=mode, seed=11)
             ref.reset()
@@ -32,13 +34,18 @@ def main():
                 out = env.rollout(chunk, want_actions=True, want_obs=want_obs)
                 rr, rd, ra, ro = ref.rollout(chunk, want_obs=want_obs, nthreads=8)
                 torch.cuda.synchronize()
-                ok &= np.array_equal(out["rewards"].cpu().numpy(), rr)
-                ok &= np.array_equal(out["actions"].cpu().numpy(), ra)
-                ok &= np.array_equal(out["done"].cpu().numpy(), rd)
+                pairs = [("rewards", out["rewards"].cpu().numpy(), rr), ("actions", out["actions"].cpu().numpy(), ra),
+                         ("done", out["done"].cpu().numpy(), rd)]
                 if want_obs:
-                    ok &= np.array_equal(out["obs"].cpu().numpy()[..., :47], ro)
+                    pairs.append(("obs", out["obs"].cpu().numpy()[..., :47], ro))
+                for nm, got, want in pairs:
+                    if not np.array_equal(got, want):
+                        ok = False
+                        bad = np.argwhere(got != want)
+                        print(f"  chunk {chunk} {nm}: {len(bad)} mismatches, first at {bad[0].tolist()} got "
+                              f"{got[tuple(bad[0])]} ref {want[tuple(bad[0])]}", flush=True)
             perr = env.pipe_errors() if rng == "numpy" else 0
-            print(f"parity {rng} obs={want_obs} B={B} T={T}: {'OK' if ok and perr == 0 else 'FAIL'} perr={perr}",
+            print(f"parity split={split} {rng} obs={want_obs} B={B} T={T}: {'OK' if ok and perr == 0 else 'FAIL'} perr={perr}",
                   flush=True)
             if not ok or perr:
                 sys.exit(1)
