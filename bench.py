@@ -56,7 +56,7 @@ ALGO_BYTES_PER_STEP = (33 * N_PLAYERS + 57) + 47 * N_PLAYERS  # 377 B at N = 4
 # applied by tools/pmc_traffic.py.  PMC counters cannot be read inside a plain
 # run, so the committed summary of the current kernels is reported beside the
 # live timing.
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_v21_pmc_traffic_{rng}.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02_pmc_traffic_{rng}.json")
 
 
 def parse():
@@ -68,7 +68,7 @@ def parse():
     ap.add_argument("--rng", default="numpy", choices=["numpy", "philox"])
     ap.add_argument("--no-obs", action="store_true", help="do not emit observations (not the headline)")
     ap.add_argument("--pipe-gpw", type=int, default=64, choices=[32, 64], help="games per k_play wave (pipelined path)")
-    ap.add_argument("--play-split", type=int, default=None, choices=[0, 1, 2, 3],
+    ap.add_argument("--play-split", type=int, default=None, choices=[0, 1, 2, 3, 4],
                     help="SN_OPT_PLAY_SPLIT (default: the library's)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
@@ -554,6 +554,9 @@ def main():
     achieved = launch_steps * ALGO_BYTES_PER_STEP / (play_ms * 1e-3) / 1e9
     per_kernel, traffic_src = pmc_traffic(args.rng, B) if not args.no_obs else (None, None)
     traffic = per_kernel.get("k_play<4") if per_kernel else None
+    # bytes the counters saw per launch / its duration: below `frac` when the
+    # game state stays in VGPRs within a launch (SURVEY §8(d) counts it twice)
+    real_frac = traffic / (play_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None
     result = {
         "metric": "env-steps/sec at 65536 concurrent 4-player games, 1/2/4/8 MI355X",
         "value": value,
@@ -586,6 +589,7 @@ def main():
             "traffic": traffic,
             "traffic_unit": "HBM bytes per k_play launch (PMC FETCH_SIZE x2 + WRITE_SIZE, separate passes)",
             "traffic_source": traffic_src,
+            "real_frac": real_frac,
             "kernel": f"k_play<4, {'RNG_NUMPY_PIPE' if args.rng == 'numpy' else 'RNG_PHILOX'}>: 10 env-steps of 65536 games",
             "kernel_ms": play_ms,
             "kernel_ms_source": ("HIP events around each k_play launch on its stream (sn_kernel_times), over a second "
@@ -624,12 +628,15 @@ def main():
         w2, k2, _ = time_rollouts(env2, out, args.steps, args.warmup, world)
         env2.close()
         ach2 = launch_steps * ALGO_BYTES_PER_STEP / (k2 * 1e-3) / 1e9
+        pk2, src2 = pmc_traffic("philox", B)
+        tr2 = pk2.get("k_play_split<4") if pk2 else None
         result["extra_config2_philox"] = {
             "metric": "env-steps/sec at 65536 concurrent 4-player games (philox RNG mode)",
             "value": B * STEPS_PER_LAUNCH * args.steps / w2, "unit": "env-steps/s",
             "ms_per_step": w2 / args.steps * 1e3,
             "roofline": {"bound": "hbm", "achieved": ach2, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": ach2 / HBM_PEAK_GBS, "traffic": None,
+                         "frac": ach2 / HBM_PEAK_GBS, "traffic": tr2, "traffic_source": src2,
+                         "real_frac": tr2 / (k2 * 1e-3) / 1e9 / HBM_PEAK_GBS if tr2 else None,
                          "kernel": "k_play_split<4, RNG_PHILOX>: producer waves decode the draws into LDS",
                          "kernel_ms": k2, "kernel_ms_source": "HIP events around each timed launch on the launch stream"},
         }

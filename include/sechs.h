@@ -179,8 +179,8 @@ sn_status sn_kernel_times(sn_env* env, float* play_ms, float* ahead_ms, int32_t*
    shuffle targets, epilogue, hand sorting, deck shuffle swaps, and (role-
    split play waves) the waits at the two barriers; out[11..18] = the split
    kernel's producer waves: draws, barrier 1, shuffle targets, swaps, hands,
-   later draws, barrier 2, state store; out[19] = play waves, out[20] =
-   producer waves.  Only the libsechs_prof.so build
+   later draws, barrier 2, state store, twist-ahead; out[20] = play waves,
+   out[21] = producer waves.  Only the libsechs_prof.so build
    (-DSECHS_PHASE_PROF) records them; the product build returns
    SN_EUNSUPPORTED [sync]. */
 sn_status sn_debug_phases(uint64_t* out, int n);

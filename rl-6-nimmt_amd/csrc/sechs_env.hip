@@ -381,7 +381,7 @@ __global__ void k_pipe_code(DevState s, int cin, int tin) {
 // producer waves' phases.  g_phase[PH_N] counts play waves, [PH_N + 1] producers.
 enum {
     PH_PROLOGUE = 0, PH_OBS, PH_DRAW, PH_RESOLVE, PH_STORE, PH_DEAL, PH_EPILOGUE, PH_HANDS, PH_APPLY, PH_B1, PH_B2,
-    PR_DRAWS, PR_B1, PR_TARGETS, PR_APPLY, PR_HANDS, PR_DRAWS2, PR_B2, PR_STORE, PH_N
+    PR_DRAWS, PR_B1, PR_TARGETS, PR_APPLY, PR_HANDS, PR_DRAWS2, PR_B2, PR_STORE, PR_TWIST, PH_N
 };
 #ifdef SECHS_PHASE_PROF
 __device__ unsigned long long g_phase[PH_N + 2];
@@ -432,6 +432,8 @@ struct PlayArgs {
     int32_t* league_rec;     // league: [episodes][B][1 + N] per finished game: seats word, results
     int step0;               // league: env-steps of this rollout before this launch (episode index of a record)
     int n0;                  // k_play_split: every game's hand size at the launch's start (aligned handle)
+    int pipe_tout, pipe_lead;  // RNG_NUMPY_FUSED: ptend parity written by the in-kernel twist-ahead, words to lead
+    uint32_t* perr_mirror;     // RNG_NUMPY_FUSED: host-mapped copy of *perr (k_mt_ahead's job otherwise)
 };
 
 // The env-step loop of one lane (game g).  R supplies the random words
@@ -810,7 +812,7 @@ struct RingGlobal {  // RingPipe's stream, 16-B ring chunks read from HBM (4 in 
     const uint8_t* ring;
     uint32_t* err;
     int64_t B, g;
-    uint32_t c0, take, avail, q0;
+    uint32_t c0, take, avail, q0, tend;
     u32x4 ch0, ch1, ch2, ch3;  // chunks q0 .. q0+3: a chunk's load goes out ~48 bytes before it is read
 
     __device__ __forceinline__ u32x4 chunk(uint32_t q) const {
@@ -821,7 +823,8 @@ struct RingGlobal {  // RingPipe's stream, 16-B ring chunks read from HBM (4 in 
         ring = (const uint8_t*)s.pring;
         err = s.perr;
         c0 = s.pabsc[(int64_t)cin * B + g];
-        const int32_t av = (int32_t)(s.ptend[(int64_t)tpar * B + g] - c0);
+        tend = s.ptend[(int64_t)tpar * B + g];
+        const int32_t av = (int32_t)(tend - c0);
         if (av < 0) atomicAdd(s.perr, 1u);
         avail = (av < 0) ? 0u : (uint32_t)av;
         take = 0u;
@@ -862,6 +865,149 @@ struct RingGlobal {  // RingPipe's stream, 16-B ring chunks read from HBM (4 in 
     }
     __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf, true); }
 };
+
+// k_mt_ahead's work for the 64 games of one producer wave (RNG_NUMPY_FUSED),
+// after the wave has drawn this launch's words: each game's stream is
+// twisted until `lead` words lie past its consumer position `c` again, the
+// tempered low bytes into its ring.  Lane l owns game l's (c, twisted end
+// t0, twist pointer Tp); the twist itself runs 4 games per instruction, 16
+// consecutive words of one game per 16 lanes (one 64-B piece of its state),
+// so every load is coalesced.  Words j < 224 of a game have all inputs in
+// memory (their loads go out first, the next 4 games' loads before this
+// group's stores); later words read word j - 227 of the same call (rare:
+// only when a launch consumed > 224 - (lead slack) words).  Same words as
+// k_mt_ahead<false>: the ring and MT state a later entry point sees are
+// identical (every pipeline test).
+struct TwistGroup {
+    uint32_t A[14], Cv[14], Bx;  // Bx: word 224 (lane 15's B of the last chunk)
+};
+
+// within a 16-lane DPP row: lane k gets lane k + N (row_shl:N; 0 past the row)
+template <int N>
+__device__ __forceinline__ uint32_t row_next(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x100 + N, 0xF, 0xF, true);
+}
+// lane k gets lane (k + 1) mod 16 (row_ror:15)
+__device__ __forceinline__ uint32_t row_rot1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x12F, 0xF, 0xF, false);
+}
+
+__device__ __forceinline__ void twist_group_load(const DevState& s, TwistGroup& X, int64_t gq, uint32_t T0, uint32_t n, uint32_t k) {
+    constexpr uint32_t D = kMtN - kMtM;
+    const uint32_t* st = s.mt + gq * kMtN;
+    const uint32_t m1 = min(n, 224u);
+#pragma unroll
+    for (int m = 0; m < 14; m++) {
+        const uint32_t j = 16u * m + k;
+        if (j <= m1 && n) {  // one word past the group's last: its B
+            uint32_t idx = T0 + j;
+            if (idx >= (uint32_t)kMtN) idx -= kMtN;
+            X.A[m] = st[idx];
+            X.Cv[m] = st[(idx < D) ? idx + kMtM : idx - D];
+        }
+    }
+    if (k == 15u && m1 == 224u) {
+        uint32_t idx = T0 + 224u;
+        if (idx >= (uint32_t)kMtN) idx -= kMtN;
+        X.Bx = st[idx];
+    }
+}
+
+__device__ __forceinline__ void twist_ring_dword(const DevState& s, int64_t gq, uint32_t t0, uint32_t j, uint32_t n, uint32_t k, uint32_t v) {
+    const uint32_t y = mt_temper(v) & 0xFFu;
+    const uint32_t d = y | (row_next<1>(y) << 8) | (row_next<2>(y) << 16) | (row_next<3>(y) << 24);
+    const uint32_t ri = (t0 + j) & (uint32_t)(kPipeRing - 1);
+    if ((k & 3u) == 0u && j < n)
+        st_nt((uint32_t*)((uint8_t*)s.pring + ((int64_t)(ri >> 4) * s.B + gq) * 16 + (ri & 12u)), d, SECHS_NT_MORE);
+}
+
+__device__ __forceinline__ void twist_group_store(const DevState& s, const TwistGroup& X, int64_t gq, uint32_t T0, uint32_t t0,
+                                                  uint32_t n, uint32_t k) {
+    constexpr uint32_t D = kMtN - kMtM;
+    uint32_t* st = s.mt + gq * kMtN;
+    const uint32_t m1 = min(n, 224u);
+    uint32_t r = row_rot1(X.A[0]);
+#pragma unroll
+    for (int m = 0; m < 14; m++) {
+        const uint32_t j = 16u * m + k;
+        // B(j) = word j + 1 = A of the next lane (lane 15: lane 0 of the next chunk)
+        const uint32_t rn = (m < 13) ? row_rot1(X.A[m + 1 < 14 ? m + 1 : 13]) : X.Bx;
+        const uint32_t b = (k == 15u) ? rn : r;
+        uint32_t v = 0u;
+        if (j < m1) {
+            uint32_t idx = T0 + j;
+            if (idx >= (uint32_t)kMtN) idx -= kMtN;
+            v = mt_mix(X.A[m], b, X.Cv[m]);
+            st_nt(&st[idx], v, SECHS_NT_MORE);
+            if (idx == 0u) s.mt0[gq] = X.A[m];
+        }
+        twist_ring_dword(s, gq, t0, j, n, k, v);
+        r = rn;
+    }
+    if (__builtin_amdgcn_readfirstlane(__ballot(n > 224u) != 0ull ? 1 : 0)) {
+        // words 224 .. n in order: word j reads word j - 227, stored above by
+        // another lane of this wave -- let those stores land first
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        for (uint32_t j0 = 224u; j0 < 600u; j0 += 16u) {
+            if (!__ballot(j0 < n)) break;
+            const uint32_t j = j0 + k;
+            uint32_t v = 0u;
+            if (j < n) {
+                uint32_t idx = T0 + j;
+                if (idx >= (uint32_t)kMtN) idx -= kMtN;
+                const uint32_t aa = st[idx];
+                v = mt_mix(aa, st[(idx + 1u == (uint32_t)kMtN) ? 0u : idx + 1u], st[(idx < D) ? idx + kMtM : idx - D]);
+                st[idx] = v;
+                if (idx == 0u) s.mt0[gq] = aa;
+            }
+            twist_ring_dword(s, gq, t0, j, n, k, v);
+            __builtin_amdgcn_s_waitcnt(0x0F70);
+        }
+    }
+}
+
+// the whole wave calls this (shuffles); dead lanes pass live = false
+__device__ __forceinline__ void twist_ahead_wave(const DevState& s, const PlayArgs& a, int64_t g0, uint32_t lane, bool live,
+                                                 uint32_t c, uint32_t t0) {
+    uint32_t n = 0u, T0 = 0u, Tp = 0u;
+    if (live) {
+        Tp = s.ptp[g0 + lane];
+        const int32_t lead = (int32_t)(t0 - c);  // < 0: an overrun, already counted by the consumer
+        n = (lead >= 0 && lead < a.pipe_lead) ? (((uint32_t)(a.pipe_lead - lead)) & ~7u) : 0u;
+        T0 = (Tp == (uint32_t)kMtN) ? 0u : Tp;
+    }
+    const uint32_t k = lane & 15u, sub = lane >> 4;
+    TwistGroup X, Y;
+    // group q = games 4q .. 4q+3 of the wave; two groups in flight
+    auto args = [&](int q, int64_t& gq, uint32_t& Tq, uint32_t& tq, uint32_t& nq) {
+        const int gi = 4 * q + (int)sub;
+        gq = g0 + gi;
+        Tq = __shfl(T0, gi), tq = __shfl(t0, gi), nq = __shfl(n, gi);
+    };
+    int64_t gx, gy;
+    uint32_t Tx, tx, nx, Ty, ty, ny;
+    args(0, gx, Tx, tx, nx);
+    twist_group_load(s, X, gx, Tx, nx, k);
+    for (int q = 0; q < 16; q += 2) {
+        args(q + 1, gy, Ty, ty, ny);
+        twist_group_load(s, Y, gy, Ty, ny, k);
+        twist_group_store(s, X, gx, Tx, tx, nx, k);
+        if (q + 2 < 16) {
+            args(q + 2, gx, Tx, tx, nx);
+            twist_group_load(s, X, gx, Tx, nx, k);
+        }
+        twist_group_store(s, Y, gy, Ty, ty, ny, k);
+    }
+    if (live) {
+        uint32_t Tn = Tp;
+        if (n) {
+            Tn = T0 + n;
+            while (Tn > (uint32_t)kMtN) Tn -= kMtN;
+        }
+        s.ptp[g0 + lane] = Tn;
+        s.ptend[(int64_t)a.pipe_tout * s.B + g0 + lane] = t0 + n;
+    }
+}
 
 template <int N>
 struct SplitSrc {
@@ -915,24 +1061,37 @@ __global__ __launch_bounds__(2 * kBlock) void k_play_split(DevState s, PlayArgs 
     const int n0 = a.n0;
     const bool deal_in = n0 >= 1 && n0 <= a.steps;  // the episode ends at step n0 - 1 of this launch
     const int tA = deal_in ? n0 : a.steps;
+    // B0 hands the play waves the first kSplitEarly steps' indices at once, so
+    // they start playing while the producers decode the rest (B1)
+    const int tE = min(tA, kSplitEarly);
     if (wave >= 4) {  // ---------------- producer (the critical path: issue priority over the play waves)
         __builtin_amdgcn_s_setprio(1);
         // the word stream: the pipelined ring (k_mt_ahead twisted it), the
         // game's own MT19937 state twisted here 16 words per refill (no
         // store of this wave is in flight to stall its loads), or Philox
-        using R = typename std::conditional<MODE == RNG_NUMPY_PIPE, RingGlobal,
+        // (RNG_NUMPY_FUSED: the ring, twisted by the previous launch's producers)
+        constexpr bool kRing = MODE == RNG_NUMPY_PIPE || MODE == RNG_NUMPY_FUSED;
+        using R = typename std::conditional<kRing, RingGlobal,
                                             typename std::conditional<MODE == RNG_NUMPY_MT, MtGenT<2>, PhiloxGen>::type>::type;
         R rng;
         ByteBuf buf;
         PhaseProf pq;
         pq.start();
-        if (live) {
-            if constexpr (MODE == RNG_NUMPY_PIPE) rng.load(s, g, buf, a.pipe_cin, a.pipe_t);
-            else RngOf<MODE, 2>::load(s, g, rng, buf);
-            produce_draws<N>(rng, buf, idx, 0, tA, n0);
+        if constexpr (MODE == RNG_NUMPY_FUSED) {
+            // publish the overrun count of the launches before to the host (sn_rollout reads it at entry)
+            if (g == 0 && a.perr_mirror)
+                __hip_atomic_store(a.perr_mirror, __hip_atomic_load(s.perr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+        if (live) {
+            if constexpr (kRing) rng.load(s, g, buf, a.pipe_cin, a.pipe_t);
+            else RngOf<MODE, 2>::load(s, g, rng, buf);
+            produce_draws<N>(rng, buf, idx, 0, tE, n0);
+        }
+        __syncthreads();  // B0: the first steps' indices are in LDS
+        if (live) produce_draws<N>(rng, buf, idx, tE, tA, n0 - tE);
         pq.mark(PR_DRAWS);
-        __syncthreads();  // B1: this launch's first indices are in LDS
+        __syncthreads();  // B1: every index before the deal is in LDS
         pq.mark(PR_B1);
         if (live && deal_in) {
             uint8_t* deck = decks + (size_t)(w * 64 + lane) * kDealStride;
@@ -954,10 +1113,14 @@ __global__ __launch_bounds__(2 * kBlock) void k_play_split(DevState s, PlayArgs 
             produce_draws<N>(rng, buf, idx, tA, a.steps, kHand);
             pq.mark(PR_DRAWS2);
         }
+        if constexpr (MODE == RNG_NUMPY_FUSED) {  // the next launch's words, while the play waves play
+            twist_ahead_wave(s, a, g - lane, (uint32_t)lane, live, live ? rng.consumed(buf) : 0u, live ? rng.tend : 0u);
+            pq.mark(PR_TWIST);
+        }
         __syncthreads();  // B2: the deal and the later indices are in LDS
         pq.mark(PR_B2);
         if (live) {
-            if constexpr (MODE == RNG_NUMPY_PIPE) s.pabsc[(int64_t)a.pipe_cout * s.B + g] = rng.consumed(buf);
+            if constexpr (kRing) s.pabsc[(int64_t)a.pipe_cout * s.B + g] = rng.consumed(buf);
             else RngOf<MODE, 2>::store(s, g, rng, buf);
         }
         pq.mark(PR_STORE);
@@ -976,9 +1139,12 @@ __global__ __launch_bounds__(2 * kBlock) void k_play_split(DevState s, PlayArgs 
     }
     pp.mark(PH_PROLOGUE);
     SplitSrc<N> src{idx};
+    __syncthreads();  // B0
+    pp.mark(PH_B1);
+    if (live) play_steps<N, SplitSrc<N>, 64, false>(s, a, g, lane, staging, G, src, sum_res, episodes, pp, lg, 0, tE);
     __syncthreads();  // B1
     pp.mark(PH_B1);
-    if (live) play_steps<N, SplitSrc<N>, 64, false>(s, a, g, lane, staging, G, src, sum_res, episodes, pp, lg, 0, tA);
+    if (live) play_steps<N, SplitSrc<N>, 64, false>(s, a, g, lane, staging, G, src, sum_res, episodes, pp, lg, tE, tA);
     pp.mark(PH_EPILOGUE);
     __syncthreads();  // B2
     pp.mark(PH_B2);
@@ -1134,6 +1300,7 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
     e->play_split = 1;
     e->pvalid = 0;
     e->pcount = 0;
+    e->pside = 0;
     if (rng_mode == SN_RNG_NUMPY_MT) {
         struct {
             void** p;
@@ -1148,10 +1315,15 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
             }
             (void)hipMemset(*a.p, 0, a.bytes);
         }
+        // the pipeline's events order kernels on one device only: a device-scope
+        // release is enough (the default system-scope one writes L2 back at
+        // every record; SECHS_EV_SYSFENCE=1 restores it for A/B runs)
+        const char* sf = getenv("SECHS_EV_SYSFENCE");
+        const unsigned evf = hipEventDisableTiming | ((sf && sf[0] == '1') ? 0u : (unsigned)hipEventDisableSystemFence);
         if (hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&e->ev_prep, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&e->ev_main, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&e->ev_play, hipEventDisableTiming) != hipSuccess) {
+            hipEventCreateWithFlags(&e->ev_prep, evf) != hipSuccess ||
+            hipEventCreateWithFlags(&e->ev_main, evf) != hipSuccess ||
+            hipEventCreateWithFlags(&e->ev_play, evf) != hipSuccess) {
             sn_destroy(e);
             return fail(SN_EHIP, "stream/event creation failed");
         }
@@ -1242,7 +1414,7 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
             e->pipe_gpw = value;
             return SN_OK;
         case SN_OPT_PLAY_SPLIT:
-            if (value < 0 || value > 3) return fail(SN_EINVAL, "play split must be 0..3");
+            if (value < 0 || value > 4) return fail(SN_EINVAL, "play split must be 0..4");
             e->play_split = value;
             return SN_OK;
         case SN_OPT_PIPE_LEAD:
@@ -1462,7 +1634,11 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     // launches keep the pair tail < 1e-26 up to K = 8 agents at N <= 4
     // (tools/pipe_tail.py), beyond that 5-step launches
     const int chunk = min(e->chunk_steps, (s.lg_K > 8) ? 5 : pipe_max_chunk(s.N));
-    const bool split = e->play_split == 2 && split_ok(e, a) && gpw == 64;
+    // SN_OPT_PLAY_SPLIT 2: role-split k_play over the ring k_mt_ahead twists
+    // on the side stream; 4: its producer waves twist the next launch's words
+    // themselves (one kernel per launch, no side stream, no cross-stream event)
+    const bool fused = e->play_split == 4 && split_ok(e, a) && gpw == 64;
+    const bool split = (e->play_split == 2 || fused) && split_ok(e, a) && gpw == 64;
     for (int t0 = 0; t0 < a.steps; t0 += chunk) {
         PlayArgs c = a;
         c.steps = min(chunk, a.steps - t0);
@@ -1474,6 +1650,31 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         if (a.obs) c.obs = a.obs + (int64_t)t0 * B * N * a.obs_stride;
         const int p = (int)(e->pcount & 1u);
         c.pipe_cin = 1 - p, c.pipe_cout = p, c.pipe_t = p;
+        if (fused) {
+            {
+                c.pipe_tout = 1 - p, c.pipe_lead = e->pipe_lead, c.perr_mirror = e->perr_host_dev;
+                if (e->pside) HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));  // a side-stream twist still owns ptend[p]
+                e->pside = 0;
+                hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
+                if (tv) HIP_TRY(hipEventRecord(tv[0], st));
+                SN_DISPATCH_N(s.N, {
+                    if constexpr (NN <= kSplitMaxPlayers) {
+                        const size_t sl = split_lds(NN, c.steps);
+                        HIP_TRY(hipFuncSetAttribute((const void*)k_play_split<NN, RNG_NUMPY_FUSED>,
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)sl));
+                        hipLaunchKernelGGL((k_play_split<NN, RNG_NUMPY_FUSED>), dim3(grid_for(s.B)), dim3(2 * kBlock), sl, st, s, c);
+                    }
+                });
+                HIP_TRY(hipGetLastError());
+                if (tv) {
+                    HIP_TRY(hipEventRecord(tv[1], st));
+                    HIP_TRY(hipEventRecord(tv[2], st));
+                    HIP_TRY(hipEventRecord(tv[3], st));
+                }
+                e->pcount++;
+                continue;
+            }
+        }
         HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));  // this launch's words are twisted
         HIP_TRY(hipEventRecord(e->ev_main, st));         // the previous launch's consumption is final
         hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
@@ -1512,6 +1713,7 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         HIP_TRY(hipGetLastError());
         if (tv) HIP_TRY(hipEventRecord(tv[3], e->side));
         HIP_TRY(hipEventRecord(e->ev_prep, e->side));
+        e->pside = 1;
         e->pcount++;
     }
     HIP_TRY(hipEventRecord(e->ev_play, st));  // sn_pipe_sync orders behind the last k_play

@@ -62,6 +62,7 @@ constexpr int kBlock = 256;
 constexpr int kLeagueMaxPlayers = 6;  // tournament handles: 2..6 seats (agent ids packed 4 bits per seat)
 constexpr int kLeagueMaxAgents = 16;
 constexpr int kSplitMaxPlayers = 4;   // k_play_split: LDS for 4 staging + 4 producer waves
+constexpr int kSplitEarly = 2;  // k_play_split: steps handed to the play waves before the rest is decoded
 constexpr int kDeckStride = 108;  // 27 dwords: odd dword stride -> conflict-free LDS lanes
 constexpr int kDealStride = 212;  // deck (108) + swap targets (104): 53 dwords, odd as well
 
@@ -825,6 +826,7 @@ struct sn_env {
     // next play launch may be in flight on `side` (ev_prep) after a rollout
     int pvalid;         // ring + ptend/pabsc/ptp are the live RNG state (mt_pos is stale)
     uint64_t pcount;    // play launches so far (parity selects the pabsc / ptend buffers)
+    int pside;          // the last twist-ahead ran on `side` (ev_prep); 0 after an in-kernel one (RNG_NUMPY_FUSED)
     hipStream_t side;
     hipEvent_t ev_prep, ev_main, ev_play;  // ev_play: after the last pipelined k_play (caller's stream)
     uint32_t* perr_host;                    // pinned, device-mapped mirror of s.perr (PlayArgs::perr_mirror)

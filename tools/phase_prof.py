@@ -23,7 +23,7 @@ from rl_6_nimmt.vec_env import VecSechsNimmtEnv  # noqa: E402
 
 NAMES = ["prologue", "obs", "draw", "resolve", "store", "shuffle_targets", "epilogue", "hands", "shuffle_apply",
          "b1_wait", "b2_wait"]
-PRODUCER = ["draws", "b1_wait", "shuffle_targets", "shuffle_apply", "hands", "draws2", "b2_wait", "store"]
+PRODUCER = ["draws", "b1_wait", "shuffle_targets", "shuffle_apply", "hands", "draws2", "b2_wait", "store", "twist"]
 NP = len(NAMES) + len(PRODUCER)
 
 
