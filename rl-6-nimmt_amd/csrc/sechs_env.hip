@@ -1675,6 +1675,9 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
                 continue;
             }
         }
+#ifdef SECHS_DEBUG_NOWAIT  // measurement only: cost of the cross-stream wait (racy)
+        if (!getenv("SECHS_NOWAIT"))
+#endif
         HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));  // this launch's words are twisted
         HIP_TRY(hipEventRecord(e->ev_main, st));         // the previous launch's consumption is final
         hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
