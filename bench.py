@@ -499,6 +499,48 @@ def bench_customed(games, episodes=5):
     }
 
 
+def bench_acer(games, episodes=3):
+    """BatchedACERAgent (actor_critic.py:119-207) in every seat
+    of `games` 4-player games -- per decision one 2-head MLP forward (bf16,
+    PyTorch-ROCm) over the root candidates + the Philox sampler; after every
+    game the reference's update schedule (one on-policy + one off-policy Adam
+    step per flushed sequence; minibatch 2 sequences per decider) on the fp32
+    rows of the device replay.  Times self-play and updates separately."""
+    from rl_6_nimmt.acer import BatchedACER, make_actor_critic
+    from rl_6_nimmt.vec_env import VecSechsNimmtEnv
+
+    env = VecSechsNimmtEnv(games, N_PLAYERS, seed=3, rng="philox")
+    torch.manual_seed(0)
+    eng = BatchedACER(env, make_actor_critic().to(env.device), seed=4, net_dtype=torch.bfloat16, warmup=2,
+                      minibatch=2, capacity=4)
+    opt = torch.optim.Adam(eng.actor.parameters())
+    for _ in range(3):  # fill the replay past warmup
+        eng.play_episode()
+        eng.learn(opt)
+    play = learn = 0.0
+    updates = 0
+    for _ in range(episodes):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.play_episode()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        updates += len(eng.learn(opt))
+        torch.cuda.synchronize()
+        play, learn = play + t1 - t0, learn + time.perf_counter() - t1
+    return {
+        "workload": f"ACER: {games} x 4-player games, all seats BatchedACER (bf16 2-head MLP 48-100-100-(1,1) via "
+                    f"PyTorch-ROCm, Philox sampler), replay of 4 episodes, {episodes} timed games + updates",
+        "value": 10 * games * episodes / play,
+        "unit": "env-steps/s (self-play)",
+        "decisions_per_s": 10 * N_PLAYERS * games * episodes / play,
+        "updates": updates,
+        "update_ms": 1e3 * learn / max(1, updates),
+        "sequence_rows_per_s": (updates // 2) * 3 * N_PLAYERS * games * 10 / learn,
+        "last_losses": list(eng.last_losses[-1]),
+    }
+
+
 def pmc_traffic(rng, games):
     path = PMC_TRAFFIC.format(rng=rng)
     if games != 65536 or not os.path.exists(path):
@@ -614,6 +656,7 @@ def main():
     if world == 1 and not args.no_puct:
         result["extra_config4_puct"] = bench_puct(args.puct_games)
         result["extra_config4_customed"] = bench_customed(args.puct_games)
+        result["extra_acer"] = bench_acer(args.puct_games // 2)
     if world == 1 and not args.no_scalar:
         result["extra_config1_scalar"] = bench_scalar()
     if not args.no_league:

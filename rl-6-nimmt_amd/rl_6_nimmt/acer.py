@@ -1,0 +1,232 @@
+"""Batched ACER self-play and training on one MI355X.
+
+Reference: BatchedACERAgent (agents/actor_critic.py:119-207), AGENTS["acer"].
+Every deciding seat of every game acts together: per decision batch one
+sn_puct_root_rows launch (normalised `[card, obs]` candidate rows straight
+from the device state), one forward of the 2-head net (policy logit, q) on
+PyTorch-ROCm, one sn_policy_sample launch (Philox softmax sample over the
+legal cards, log pi).  The reference draws from exp(clamp(log pi, -20)) over
+10 padded slots and re-draws pad hits, i.e. from softmax over the legal cards
+except that a card below e^-20 keeps e^-20: the sampler here is the exact
+softmax (Philox: parity unpinned bitwise, frequency-tested).
+
+Replay on the device (the reference's SequentialHistory of Python lists):
+`capacity` episodes x 10 steps x D deciders of padded candidate rows (fp32,
+the rows the training forward sees), chosen slot, behaviour log pi (padded
+with log_epsilon = -20 like actor_critic.py:108-111) and reward x r_factor.
+A decider's episode splits into sequences of rollout_len steps (the last one
+ends at done), exactly where the reference flushes (actor_critic.py:146).
+
+Training (actor_critic.py:153-207), per decider d over a batch of its
+sequences, vectorised over deciders and sequences:
+    v      = sum_a q(a) pi(a)                 rho = pi_now / pi_then
+    q_ret  = Retrace target, walked backwards within each sequence
+    actor  = mean -min(rho_a, c) log pi(a) (q_ret - v)
+    corr   = mean sum_a -max(0, 1 - c/rho) pi_then log pi (q - v)
+    critic = critic_weight * mean SmoothL1(q(a), q_ret)
+and the batch loss is the sum over deciders of actor + corr + critic (the
+reference takes one Adam step per agent and sequence batch).  `learn()`
+follows the reference's schedule: after every flushed sequence, once more
+than max(warmup, minibatch) sequences are stored, one on-policy update (the
+newest sequence of every decider) and one off-policy update (`minibatch`
+stored sequences per decider, drawn without replacement on the device).
+"""
+import torch
+from torch import nn
+
+from . import _native as nat
+from .puct import ROW, BatchedPUCT, ctypes_ref
+from .utils.nets import MultiHeadedMLP
+
+T_STEPS = 10
+
+
+def make_actor_critic(hidden_sizes=(100, 100), activation=None):
+    """the reference's net (actor_critic.py:44-46): MultiHeadedMLP(48, (100, 100), (1, 1)) -- policy logit, q"""
+    return MultiHeadedMLP(ROW, hidden_sizes=hidden_sizes, head_sizes=(1, 1), activation=activation or nn.ReLU(),
+                          head_activations=(None, None))
+
+
+class BatchedACER(BatchedPUCT):
+    def __init__(self, env, actor=None, seats_mask=None, net_dtype=torch.bfloat16, seed=0, gamma=0.99, rollout_len=10,
+                 minibatch=5, truncate=1.0, warmup=100, r_factor=0.1, critic_weight=1.0, capacity=4,
+                 log_epsilon=-20.0):
+        super().__init__(env, actor if actor is not None else make_actor_critic(), seed=seed, seats_mask=seats_mask,
+                         puct_root=False, net_dtype=net_dtype)
+        self.gamma, self.truncate, self.r_factor = float(gamma), float(truncate), float(r_factor)
+        self.rollout_len, self.minibatch, self.warmup = int(rollout_len), int(minibatch), int(warmup)
+        self.critic_weight, self.log_epsilon = float(critic_weight), float(log_epsilon)
+        self.capacity = int(capacity)
+        D, dev = self.D, env.device
+        self.log_prob = torch.zeros((D,), dtype=torch.float32, device=dev)
+        self.entropy = torch.zeros((D,), dtype=torch.float32, device=dev)
+        C = self.capacity
+        self.rep_rows = torch.zeros((C, T_STEPS, D, 10, ROW), dtype=torch.float32, device=dev)
+        self.rep_act = torch.zeros((C, T_STEPS, D), dtype=torch.long, device=dev)
+        self.rep_logp = torch.full((C, T_STEPS, D, 10), self.log_epsilon, dtype=torch.float32, device=dev)
+        self.rep_rew = torch.zeros((C, T_STEPS, D), dtype=torch.float32, device=dev)
+        self.episodes = 0  # episodes written (slot = episodes % capacity)
+        self._t = 0
+        self._gen = torch.Generator(device=dev)
+        self._gen.manual_seed(self.seed ^ 0xACE5)
+        self.last_losses = []
+
+    # ------------------------------------------------------------ acting
+    def decide(self, n, memorize=False, record=False):
+        """sample every deciding seat's card at hand size n: actions [B, N] int32"""
+        L, h, st = nat.lib(), self.env._h, self.env._stream()
+        bf16 = int(self.net_dtype == torch.bfloat16)
+        q = self._params(n)
+        self.sync_net()
+        rows = torch.empty((self.D * n, ROW), dtype=self.net_dtype, device=self.env.device)
+        nat.check(L.sn_puct_root_rows(h, ctypes_ref(q), nat.ptr(rows), bf16, st), "sn_puct_root_rows")
+        with torch.no_grad():
+            logit, _ = self._net(rows)
+        self.rows_evaluated += rows.shape[0]
+        logits = logit.reshape(-1).float().contiguous()
+        nat.check(L.sn_policy_sample(h, ctypes_ref(q), nat.ptr(logits), nat.ptr(self.actions), nat.ptr(self.best_index),
+                                     nat.ptr(self.log_prob), nat.ptr(self.entropy), st), "sn_policy_sample")
+        if record:
+            s, t = self.episodes % self.capacity, T_STEPS - n
+            self.rep_rows[s, t, :, :n] = self._train_rows(q, n, rows).view(self.D, n, ROW)
+            self.rep_rows[s, t, :, n:] = 0.0
+            self.rep_act[s, t] = self.best_index.long()
+            self.rep_logp[s, t].fill_(self.log_epsilon)
+            self.rep_logp[s, t, :, :n] = torch.log_softmax(logits.view(self.D, n), dim=1)
+        self.step_id += 1
+        return self.actions
+
+    def play_episode(self, others=None, record=True):
+        """one whole game of every env game (non-deciding seats: uniform moves);
+        with record, the episode goes into replay slot episodes % capacity.
+        Returns (summed rewards [B, N] int32, per-step rewards [10, B, N])."""
+        env = self.env
+        env.reset()
+        per_step = torch.zeros((T_STEPS, env.num_games, env.num_players), dtype=torch.int32, device=env.device)
+        for t in range(T_STEPS):
+            acts = self.decide(T_STEPS - t, record=record)
+            if self.M < env.num_players:
+                keep = torch.tensor([(self.seats_mask >> p) & 1 for p in range(env.num_players)], device=env.device,
+                                    dtype=torch.bool)
+                acts = torch.where(keep[None, :], acts, self._random_moves())
+            rew, done, inv = env.step(acts)
+            per_step[t] = rew
+        if record:
+            seats = [p for p in range(env.num_players) if (self.seats_mask >> p) & 1]
+            # learn(next_reward=r_t) of the step's own reward, x r_factor in float64 (actor_critic.py:142)
+            r = per_step[:, :, seats].reshape(T_STEPS, -1).double() * self.r_factor
+            self.rep_rew[self.episodes % self.capacity] = r.float()
+            self.episodes += 1
+        self.episode_rewards = per_step
+        return per_step.sum(dim=0), per_step
+
+    # ------------------------------------------------------------ sequences in the replay
+    def chunks(self):
+        """step ranges of one episode's sequences (flush at rollout_len or done)"""
+        L = self.rollout_len
+        return [(c, min(T_STEPS, c + L)) for c in range(0, T_STEPS, L)]
+
+    def stored_sequences(self, upto_chunk=None):
+        """(slot, chunk index) of every stored sequence, oldest episode first;
+        the newest episode only up to `upto_chunk` (inclusive)"""
+        nch = len(self.chunks())
+        full = min(self.episodes, self.capacity)
+        newest = (self.episodes - 1) % self.capacity
+        out = []
+        for e in range(self.episodes - full, self.episodes):
+            s = e % self.capacity
+            last = nch - 1 if (upto_chunk is None or s != newest) else upto_chunk
+            out += [(s, c) for c in range(last + 1)]
+        return out
+
+    # ------------------------------------------------------------ the ACER loss
+    def loss(self, slots, chunk_ids):
+        """sum over deciders of the reference's ACER loss on a batch of each
+        decider's sequences: `slots`, `chunk_ids` [D, K] long (sequence k of
+        decider d = replay slot slots[d, k], chunk chunk_ids[d, k]).
+        Returns (total, actor, correction, critic) -- components summed over
+        deciders, total carrying the gradient."""
+        dev = self.actor_device()
+        D, K = slots.shape
+        L = self.rollout_len
+        ch = torch.tensor([c for c, _ in self.chunks()], device=self.env.device)
+        ln = torch.tensor([e - c for c, e in self.chunks()], device=self.env.device)
+        j = torch.arange(L, device=self.env.device)
+        t = ch[chunk_ids][:, :, None] + j  # [D, K, L]
+        valid = j < ln[chunk_ids][:, :, None]
+        t = torch.where(valid, t, torch.zeros_like(t))
+        d = torch.arange(D, device=self.env.device)[:, None, None].expand(D, K, L)
+        s = slots[:, :, None].expand(D, K, L)
+        rows = self.rep_rows[s, t, d]  # [D, K, L, 10, 48]
+        act = self.rep_act[s, t, d].to(dev)
+        logp_then = self.rep_logp[s, t, d].to(dev)
+        rew = self.rep_rew[s, t, d].to(dev)
+        done = (t == T_STEPS - 1).to(dev)
+        n = (T_STEPS - t).to(dev)
+        valid = valid.to(dev)
+        legal = torch.arange(10, device=dev) < n[..., None]
+        logit, q = self.actor(rows.to(dev).reshape(-1, ROW))
+        logit = logit.reshape(D, K, L, 10).masked_fill(~legal, float("-inf"))
+        q = q.reshape(D, K, L, 10).masked_fill(~legal, 0.0)
+        logp = torch.log_softmax(logit, dim=-1).masked_fill(~legal, self.log_epsilon)
+        a = act[..., None]
+        q_a = q.gather(-1, a)[..., 0]
+        logp_a = logp.gather(-1, a)[..., 0]
+        v = (q * logp.exp()).sum(-1).detach()
+        rho = (logp - logp_then).exp().detach()
+        rho_bar = rho.gather(-1, a)[..., 0].clamp(max=self.truncate)
+        coeff = (1.0 - self.truncate / rho).clamp(min=0.0)
+        # Retrace targets, backwards within each sequence (actor_critic.py:195-207)
+        last = (ln[chunk_ids] - 1).to(dev)  # [D, K]
+        q_ret = torch.zeros((D, K), dtype=torch.float32, device=dev)
+        qa_d = q_a.detach()
+        targets = torch.zeros((D, K, L), dtype=torch.float32, device=dev)
+        for i in range(L - 1, -1, -1):
+            start = last == i
+            q_ret = torch.where(start, v[:, :, i] * (1.0 - done[:, :, i].float()), q_ret)
+            tgt = rew[:, :, i] + self.gamma * q_ret
+            targets[:, :, i] = tgt
+            q_ret = torch.where(valid[:, :, i], rho_bar[:, :, i] * (tgt - qa_d[:, :, i]) + v[:, :, i], q_ret)
+        w = valid.float()
+        rows_per_d = w.sum(dim=(1, 2))  # [D]
+
+        def per_decider(x):
+            return ((x * w).sum(dim=(1, 2)) / rows_per_d).sum()
+
+        actor = per_decider(-rho_bar * logp_a * (targets - v))
+        corr = per_decider((-coeff * logp_then.exp() * logp * (q.detach() - v[..., None])).sum(-1))
+        err = (q_a - targets).abs()
+        critic = self.critic_weight * per_decider(torch.where(err < 1.0, 0.5 * err * err, err - 0.5))
+        return actor + corr + critic, actor.detach(), corr.detach(), critic.detach()
+
+    def on_policy_batch(self, chunk):
+        """every decider's newest sequence: [D, 1] slots / chunk ids"""
+        D, dev = self.D, self.env.device
+        s = (self.episodes - 1) % self.capacity
+        return (torch.full((D, 1), s, dtype=torch.long, device=dev),
+                torch.full((D, 1), chunk, dtype=torch.long, device=dev))
+
+    def off_policy_batch(self, upto_chunk):
+        """`minibatch` distinct stored sequences per decider, uniform"""
+        seqs = self.stored_sequences(upto_chunk)
+        S, dev = len(seqs), self.env.device
+        pick = torch.rand((self.D, S), generator=self._gen, device=dev).argsort(dim=1)[:, : self.minibatch]
+        tab = torch.tensor(seqs, dtype=torch.long, device=dev)  # [S, 2]
+        return tab[pick, 0], tab[pick, 1]
+
+    def learn(self, optimizer):
+        """the reference's update schedule for the episode just played: per
+        flushed sequence, if more than max(warmup, minibatch) are stored, one
+        on-policy and one off-policy Adam step (actor_critic.py:146-151)"""
+        done_updates = []
+        for c in range(len(self.chunks())):
+            if len(self.stored_sequences(c)) <= max(self.warmup, self.minibatch):
+                continue
+            for batch in (self.on_policy_batch(c), self.off_policy_batch(c)):
+                total, actor, corr, critic = self.loss(*batch)
+                optimizer.zero_grad()
+                total.backward()
+                optimizer.step()
+                done_updates.append((float(actor), float(corr), float(critic)))
+        self.last_losses += done_updates
+        return done_updates

@@ -33,6 +33,12 @@ Fixture families (SURVEY.md §4 "What the build must add"):
   F10 reinforce_games.json seeded GameSession(BatchedReinforceAgent, ...)
       reinforce_weights.npz  training games: actions, log-probs, entropies,
                            losses, final weights
+  F12 acer_games.json    seeded GameSession(BatchedACERAgent, ...) training
+      acer_weights.npz     sessions (torch + numpy + Python `random` seeded):
+                           per ACER seat and step the observation, legal
+                           cards, move, log-prob, value, reward and done; the
+                           (actor, correction, critic) losses of every update;
+                           initial and final weights
   F11 tournament_games.json seeded Tournament.play_game() sequences: seat
                            draws (agent names in seat order), results,
                            relative positions, wins, per-agent tallies --
@@ -666,6 +672,76 @@ def gen_reinforce(ref, out):
 
 
 # ----------------------------------------------------------------------------
+# F12: BatchedACERAgent (ACER) in training sessions
+# ----------------------------------------------------------------------------
+ACER_SPECS = [("ARRR", 0, 5, {"warmup": 2, "minibatch": 2}),
+              ("AR", 3, 4, {"rollout_len": 4, "warmup": 3, "minibatch": 2, "r_factor": 0.5}),
+              ("AA", 6, 3, {"warmup": 1, "minibatch": 1, "truncate": 0.5, "critic_weight": 0.5}),
+              ("ARR", 8, 6, {"history_length": 3, "warmup": 1, "minibatch": 2, "rollout_len": 3, "gamma": 0.9})]
+
+
+def gen_acer(ref, out):
+    import random
+
+    import torch
+    from rl_6_nimmt.agents import BatchedACERAgent, DrunkHamster
+    from rl_6_nimmt.play import GameSession
+
+    sessions, arrays = [], {}
+    for si, (seats, seed, n_games, kw) in enumerate(ACER_SPECS):
+        torch.manual_seed(seed)
+        agents = [BatchedACERAgent(**kw) if ch == "A" else DrunkHamster() for ch in seats]
+        trace = {}
+        for i, ch in enumerate(seats):
+            if ch != "A":
+                continue
+            ag = agents[i]
+            ag.train()
+            for k, v in ag.actor_critic.state_dict().items():
+                arrays[f"s{si}_a{i}_init_{k}"] = v.detach().numpy().astype(np.float32)
+            trace[i] = {"steps": [], "losses": []}
+            fwd, lrn, trn = ag.forward, ag.learn, ag._train
+
+            def fwd_rec(state, legal_actions, *a, _fwd=fwd, _i=i, **k):
+                act, info = _fwd(state, legal_actions, *a, **k)
+                trace[_i]["steps"].append({"obs": [int(x) for x in state.tolist()], "legal": [int(x) for x in legal_actions],
+                                           "action": int(act), "log_prob": float(info["log_prob"]),
+                                           "value": float(info["value"])})
+                return act, info
+
+            def lrn_rec(*a, _lrn=lrn, _i=i, **k):
+                st = trace[_i]["steps"][-1]
+                st["next_reward"], st["done"] = int(k["next_reward"]), bool(k["done"])
+                return _lrn(*a, **k)
+
+            def trn_rec(on_policy=True, _trn=trn, _i=i):
+                losses = _trn(on_policy)
+                trace[_i]["losses"].append([len(trace[_i]["steps"]), bool(on_policy)] + [float(x) for x in losses])
+                return losses
+
+            ag.forward, ag.learn, ag._train = fwd_rec, lrn_rec, trn_rec
+        np.random.seed(seed)
+        random.seed(seed)
+        sess = GameSession(*agents)
+        for _ in range(n_games):
+            sess.play_game()
+        for i in trace:
+            for k, v in agents[i].actor_critic.state_dict().items():
+                arrays[f"s{si}_a{i}_final_{k}"] = v.detach().numpy().astype(np.float32)
+        sessions.append({"seats": seats, "seed": seed, "games": n_games, "kwargs": kw,
+                         "results": [[int(x) for x in r] for r in sess.results],
+                         "trace": {str(i): t for i, t in trace.items()}})
+    np.savez_compressed(os.path.join(out, "acer_weights.npz"), **arrays)
+    with open(os.path.join(out, "acer_games.json"), "w") as f:
+        json.dump({"protocol": "torch.manual_seed(seed); agents (A = BatchedACERAgent(**kwargs) in train mode, "
+                               "R = DrunkHamster); np.random.seed(seed); random.seed(seed); "
+                               "GameSession(*agents).play_game() x games. trace[seat].steps = per forward the obs, legal "
+                               "cards, action, log_prob, value, and the next_reward/done learn() received; losses = "
+                               "per _train call [steps so far, on_policy, actor, correction, critic]",
+                   "sessions": sessions}, f)
+
+
+# ----------------------------------------------------------------------------
 # F7: tournament positions
 # ----------------------------------------------------------------------------
 def gen_positions(ref, out):
@@ -780,6 +856,7 @@ def main():
         ("mcs", gen_mcs),
         ("customed", gen_customed),
         ("reinforce", gen_reinforce),
+        ("acer", gen_acer),
         ("tournament", gen_tournament),
     ]
     for name, fn in steps:
