@@ -105,6 +105,9 @@ def barrier(world):
         dist.barrier()
 
 
+ENQUEUE_S = None
+
+
 def time_rollouts(env, out, steps, warmup, world):
     """Warm up, then time exactly `steps` launches between barrier+sync on
     both sides (nothing else enqueued in between: per-launch timing events
@@ -119,6 +122,8 @@ def time_rollouts(env, out, steps, warmup, world):
     t0 = time.perf_counter()
     for i in range(steps):
         env.rollout(STEPS_PER_LAUNCH, out=out)
+    global ENQUEUE_S
+    ENQUEUE_S = time.perf_counter() - t0  # host time to enqueue the timed launches (host-bound if ~ the wall)
     torch.cuda.synchronize()
     barrier(world)
     t1 = time.perf_counter()
@@ -607,6 +612,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": wall / args.steps * 1e3,
+        "host_enqueue_ms_per_step": ENQUEUE_S / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

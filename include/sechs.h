@@ -160,9 +160,15 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          MT19937 twisted in the producer waves (no ring, no
                          side stream); 0: never.  Measured (65 536 x 4p): philox
                          74 -> 59 us per 10 env-steps; numpy 2 / 3 slower than
-                         the pipelined one-wave kernel. */
+                         the pipelined one-wave kernel.
+     SN_OPT_AHEAD_DELAY  microseconds (0..50) the side stream idles (one
+                         sleeping wave) between the end of a k_play and the
+                         dispatch of the twist two launches ahead, so that the
+                         next k_play's waves reach the CUs before the twist's
+                         many small waves fill them.  Schedule only; results
+                         never depend on it. */
 enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3, SN_OPT_TIMING = 4, SN_OPT_PIPE_GPW = 5,
-       SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7 };
+       SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7, SN_OPT_AHEAD_DELAY = 8 };
 sn_status sn_set_option(sn_env* env, int option, int value);
 /* pipelined rollouts whose draws ran past the twisted words (must be 0; a
    nonzero count means those games' draws are wrong) [sync].  The count is

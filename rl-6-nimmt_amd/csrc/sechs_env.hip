@@ -265,6 +265,12 @@ struct AheadArgs {
     uint32_t* perr_mirror;  // host-mapped copy of *perr, refreshed at launch start (off the play stream)
 };
 
+// one wave that only sleeps: ~3.4 us per s_sleep(127) (127 x 64 cycles at
+// ~2.4 GHz); holds the side stream back while a k_play dispatches
+__global__ __launch_bounds__(64) void k_idle(int rounds) {
+    for (int i = 0; i < rounds; i++) __builtin_amdgcn_s_sleep(127);
+}
+
 template <bool INIT>
 __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
     constexpr uint32_t D = kMtN - kMtM;  // 227
@@ -1298,6 +1304,7 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
     e->pipe_lead = kPipeLead;
     e->phase = -1;
     e->play_split = 1;
+    e->ahead_delay = 0;
     e->pvalid = 0;
     e->pcount = 0;
     e->pside = 0;
@@ -1412,6 +1419,10 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
         case SN_OPT_PIPE_GPW:
             if (value != 32 && value != 64) return fail(SN_EINVAL, "games per wave must be 32 or 64");
             e->pipe_gpw = value;
+            return SN_OK;
+        case SN_OPT_AHEAD_DELAY:
+            if (value < 0 || value > 50) return fail(SN_EINVAL, "ahead delay must be in 0..50 us");
+            e->ahead_delay = value;
             return SN_OK;
         case SN_OPT_PLAY_SPLIT:
             if (value < 0 || value > 4) return fail(SN_EINVAL, "play split must be 0..4");
@@ -1711,6 +1722,10 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         if (tv) HIP_TRY(hipEventRecord(tv[1], st));
         // the next launch's twist, beside this one: leads the consumer of the launch before
         HIP_TRY(hipStreamWaitEvent(e->side, e->ev_main, 0));
+        if (e->ahead_delay > 0) {  // let this k_play's waves reach the CUs first (SN_OPT_AHEAD_DELAY)
+            hipLaunchKernelGGL(k_idle, dim3(1), dim3(64), 0, e->side, (e->ahead_delay * 10 + 33) / 34);
+            HIP_TRY(hipGetLastError());
+        }
         if (tv) HIP_TRY(hipEventRecord(tv[2], e->side));
         hipLaunchKernelGGL(k_mt_ahead<false>, pg, dim3(kBlock), 0, e->side, s, AheadArgs{1 - p, p, 1 - p, e->pipe_lead, e->perr_host_dev});
         HIP_TRY(hipGetLastError());

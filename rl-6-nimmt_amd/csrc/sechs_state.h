@@ -820,6 +820,7 @@ struct sn_env {
     int pipe_lead;    // SN_OPT_PIPE_LEAD: words k_mt_ahead keeps twisted ahead (kPipeLead; tests lower it)
     int lg_phase;     // tournament handle: env-steps since the games were dealt, mod 10 (-1: not dealt yet)
     int phase;        // every game's env-steps since its deal, mod 10, when they are in lockstep; -1 unknown
+    int ahead_delay;  // SN_OPT_AHEAD_DELAY: us the side stream idles before each k_mt_ahead
     int play_split;   // SN_OPT_PLAY_SPLIT: role-split k_play for lockstep DrunkHamster rollouts
     sechs::DevState s;
     // pipelined twist-ahead (sechs_env.hip launch_pipe): a k_mt_ahead for the

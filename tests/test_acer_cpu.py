@@ -44,6 +44,9 @@ def _check_weights(agent, W, si, i, games):
     for k, v in agent.actor_critic.state_dict().items():
         got, want = v.detach().numpy(), W[f"s{si}_a{i}_final_{k}"]
         d = np.abs(got - want)
+        if k == "head_nets.0.0.bias":  # softmax-invariant: exact gradient 0, Adam scales rounding noise to ~lr
+            assert d.max() <= 3e-3 * games, (si, i)
+            continue
         # bit-identical on the fixture host; a different CPU rounds the GEMMs
         # differently and Adam amplifies near-cancelling gradients to O(lr)
         assert np.mean(d <= 1e-4) >= 0.5 and d.max() <= 3e-3 * games, (si, i, k, d.max())

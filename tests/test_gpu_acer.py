@@ -65,6 +65,11 @@ def test_dropin_acer_agent_replays_reference_training_sessions():
             assert np.allclose(agents[i].last_losses, [w[2:] for w in tr["losses"]], rtol=1e-3, atol=1e-4), (si, i)
             for k, v in agents[i].actor_critic.state_dict().items():
                 d = np.abs(v.detach().numpy() - W[f"s{si}_a{i}_final_{k}"])
+                if k == "head_nets.0.0.bias":
+                    # the policy-logit bias shifts every candidate equally: softmax ignores it, its exact
+                    # gradient is 0 and Adam scales the host CPU's rounding noise up to ~lr per step
+                    assert d.max() <= 3e-3 * sess["games"], (si, i)
+                    continue
                 assert np.mean(d <= 1e-4) >= 0.5 and d.max() <= 3e-3 * sess["games"], (si, i, k, d.max())
 
 
