@@ -91,8 +91,16 @@ def dist_setup(args):
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # SECHS_BENCH_BACKEND=gloo: rehearsal of the N-rank path with several
+        # ranks sharing the visible GPUs (RCCL needs one GPU per rank); the
+        # driver's runs use the default, nccl (= RCCL), one GPU per rank
+        backend = os.environ.get("SECHS_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     return world, rank, local
