@@ -648,13 +648,16 @@ __device__ __forceinline__ void store_results(const DevState& s, int64_t g, int 
 // GPW = games per wave: 64 (one game per lane), or 32 for the pipelined
 // path (lanes 32..63 idle) -- half the LDS per wave, so two blocks fit a CU
 // and a SIMD holds two waves to hide each other's latency
+#ifndef SECHS_PLAY_PRIO
+#define SECHS_PLAY_PRIO 1  // play-wave issue priority (0..3)
+#endif
 template <int N, int MODE, int GPW, bool LG = false>
 __device__ __forceinline__ void play_body(const DevState& s, const PlayArgs& a, uint8_t* lds_dyn, int tid) {
     const int lane = tid & 63;
     if (GPW < 64 && lane >= GPW) return;
     // issue priority over the co-resident k_mt_ahead waves: the game loop
     // is one latency-bound wave per SIMD (measured +1.7 %)
-    __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(SECHS_PLAY_PRIO);
     const int64_t g = ((int64_t)blockIdx.x * (kBlock / 64) + (tid >> 6)) * GPW + lane;
     if (g >= s.B) return;
     uint8_t* wave_lds = lds_dyn + (tid >> 6) * a.wave_lds;
