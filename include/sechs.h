@@ -153,22 +153,13 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          it exists to exercise the SN_ERNG path.
      SN_OPT_PLAY_SPLIT   role-split k_play (producer waves decode every random
                          decision into LDS beside the play waves) for in-kernel
-                         DrunkHamster rollouts of a handle whose games are in
-                         lockstep (after sn_reset; N <= 4, auto-reset):
-                         1 (default): philox handles; 2: also numpy-compat over
-                         the pipelined ring; 3: numpy-compat with each game's
-                         MT19937 twisted in the producer waves (no ring, no
-                         side stream); 0: never.  Measured (65 536 x 4p): philox
-                         74 -> 59 us per 10 env-steps; numpy 2 / 3 slower than
-                         the pipelined one-wave kernel.
-     SN_OPT_AHEAD_DELAY  microseconds (0..50) the side stream idles (one
-                         sleeping wave) between the end of a k_play and the
-                         dispatch of the twist two launches ahead, so that the
-                         next k_play's waves reach the CUs before the twist's
-                         many small waves fill them.  Schedule only; results
-                         never depend on it. */
+                         DrunkHamster rollouts of a Philox handle whose games
+                         are in lockstep (after sn_reset; N <= 4, auto-reset):
+                         1 (default) or 0 (never).  Measured (65 536 x 4p):
+                         74 -> 59 us per 10 env-steps.  Numpy-compat handles
+                         always use the pipelined one-wave k_play. */
 enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3, SN_OPT_TIMING = 4, SN_OPT_PIPE_GPW = 5,
-       SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7, SN_OPT_AHEAD_DELAY = 8 };
+       SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7 };
 sn_status sn_set_option(sn_env* env, int option, int value);
 /* pipelined rollouts whose draws ran past the twisted words (must be 0; a
    nonzero count means those games' draws are wrong) [sync].  The count is

@@ -265,12 +265,6 @@ struct AheadArgs {
     uint32_t* perr_mirror;  // host-mapped copy of *perr, refreshed at launch start (off the play stream)
 };
 
-// one wave that only sleeps: ~3.4 us per s_sleep(127) (127 x 64 cycles at
-// ~2.4 GHz); holds the side stream back while a k_play dispatches
-__global__ __launch_bounds__(64) void k_idle(int rounds) {
-    for (int i = 0; i < rounds; i++) __builtin_amdgcn_s_sleep(127);
-}
-
 template <bool INIT>
 __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
     constexpr uint32_t D = kMtN - kMtM;  // 227
@@ -387,7 +381,7 @@ __global__ void k_pipe_code(DevState s, int cin, int tin) {
 // producer waves' phases.  g_phase[PH_N] counts play waves, [PH_N + 1] producers.
 enum {
     PH_PROLOGUE = 0, PH_OBS, PH_DRAW, PH_RESOLVE, PH_STORE, PH_DEAL, PH_EPILOGUE, PH_HANDS, PH_APPLY, PH_B1, PH_B2,
-    PR_DRAWS, PR_B1, PR_TARGETS, PR_APPLY, PR_HANDS, PR_DRAWS2, PR_B2, PR_STORE, PR_TWIST, PH_N
+    PR_DRAWS, PR_B1, PR_TARGETS, PR_APPLY, PR_HANDS, PR_DRAWS2, PR_B2, PR_STORE, PR_SPARE, PH_N
 };
 #ifdef SECHS_PHASE_PROF
 __device__ unsigned long long g_phase[PH_N + 2];
@@ -438,8 +432,6 @@ struct PlayArgs {
     int32_t* league_rec;     // league: [episodes][B][1 + N] per finished game: seats word, results
     int step0;               // league: env-steps of this rollout before this launch (episode index of a record)
     int n0;                  // k_play_split: every game's hand size at the launch's start (aligned handle)
-    int pipe_tout, pipe_lead;  // RNG_NUMPY_FUSED: ptend parity written by the in-kernel twist-ahead, words to lead
-    uint32_t* perr_mirror;     // RNG_NUMPY_FUSED: host-mapped copy of *perr (k_mt_ahead's job otherwise)
 };
 
 // The env-step loop of one lane (game g).  R supplies the random words
@@ -648,16 +640,13 @@ __device__ __forceinline__ void store_results(const DevState& s, int64_t g, int 
 // GPW = games per wave: 64 (one game per lane), or 32 for the pipelined
 // path (lanes 32..63 idle) -- half the LDS per wave, so two blocks fit a CU
 // and a SIMD holds two waves to hide each other's latency
-#ifndef SECHS_PLAY_PRIO
-#define SECHS_PLAY_PRIO 1  // play-wave issue priority (0..3)
-#endif
 template <int N, int MODE, int GPW, bool LG = false>
 __device__ __forceinline__ void play_body(const DevState& s, const PlayArgs& a, uint8_t* lds_dyn, int tid) {
     const int lane = tid & 63;
     if (GPW < 64 && lane >= GPW) return;
     // issue priority over the co-resident k_mt_ahead waves: the game loop
     // is one latency-bound wave per SIMD (measured +1.7 %)
-    __builtin_amdgcn_s_setprio(SECHS_PLAY_PRIO);
+    __builtin_amdgcn_s_setprio(1);
     const int64_t g = ((int64_t)blockIdx.x * (kBlock / 64) + (tid >> 6)) * GPW + lane;
     if (g >= s.B) return;
     uint8_t* wave_lds = lds_dyn + (tid >> 6) * a.wave_lds;
@@ -812,212 +801,11 @@ __global__ __launch_bounds__(64) void k_reset1(DevState s, uint32_t* hb, int sum
 // the launch's policy indices into LDS (nibbles), barrier B1, then shuffle
 // and deal the next episode and decode the steps after it while the play
 // waves play up to the episode's end; barrier B2; play waves install the
-// dealt hands and go on.  The play waves issue no RNG work at all; the
-// producers read the pipelined ring straight from HBM (RingGlobal: no
-// stores of theirs in flight, so no vmcnt stall behind the obs stores).
+// dealt hands and go on.  The play waves issue no RNG work at all.  Philox
+// handles only (numpy-compat variants over the pipelined ring were measured
+// slower than k_play + k_mt_ahead and removed).
 // Same words, same order, same results: every parity test runs this path.
 // ============================================================================
-struct RingGlobal {  // RingPipe's stream, 16-B ring chunks read from HBM (4 in registers, 3 ahead)
-    const uint8_t* ring;
-    uint32_t* err;
-    int64_t B, g;
-    uint32_t c0, take, avail, q0, tend;
-    u32x4 ch0, ch1, ch2, ch3;  // chunks q0 .. q0+3: a chunk's load goes out ~48 bytes before it is read
-
-    __device__ __forceinline__ u32x4 chunk(uint32_t q) const {
-        return *(const u32x4*)(ring + ((int64_t)(q & (uint32_t)(kPipeRing / 16 - 1)) * B + g) * 16);
-    }
-    __device__ __forceinline__ void load(const DevState& s, int64_t gg, ByteBuf& buf, int cin, int tpar) {
-        g = gg, B = s.B;
-        ring = (const uint8_t*)s.pring;
-        err = s.perr;
-        c0 = s.pabsc[(int64_t)cin * B + g];
-        tend = s.ptend[(int64_t)tpar * B + g];
-        const int32_t av = (int32_t)(tend - c0);
-        if (av < 0) atomicAdd(s.perr, 1u);
-        avail = (av < 0) ? 0u : (uint32_t)av;
-        take = 0u;
-        q0 = c0 >> 4;
-        ch0 = chunk(q0);
-        ch1 = chunk(q0 + 1u);
-        ch2 = chunk(q0 + 2u);
-        ch3 = chunk(q0 + 3u);
-        buf.clear();
-    }
-    __device__ __forceinline__ uint32_t consumed(const ByteBuf& buf) const { return c0 + take - buf.cnt; }
-    __device__ __forceinline__ bool gen(ByteBuf& buf, bool forced) {
-        if (take + 8u <= avail) {
-            const uint32_t p = c0 + take;  // absolute stream position (wraps at 2^32 like the ring's)
-            if (((p >> 4) - q0) & 0x0FFFFFFFu) {  // 8 bytes per call: crosses at most one chunk boundary
-                q0 += 1u;
-                ch0 = ch1, ch1 = ch2, ch2 = ch3;
-                ch3 = chunk(q0 + 3u);
-            }
-            const uint32_t o = p & 15u;
-            const uint64_t w0 = (uint64_t)ch0.x | ((uint64_t)ch0.y << 32), w1 = (uint64_t)ch0.z | ((uint64_t)ch0.w << 32);
-            const uint64_t w2 = (uint64_t)ch1.x | ((uint64_t)ch1.y << 32);
-            const uint64_t lo = (o < 8u) ? w0 : w1, hi = (o < 8u) ? w1 : w2;
-            const uint32_t sh = 8u * (o & 7u);
-            buf.append(sh ? ((lo >> sh) | (hi << (64u - sh))) : lo, 8u);
-            take += 8u;
-            return true;
-        }
-        const uint32_t left = (avail > take) ? avail - take : 0u;
-        if (left == 0u && !forced) return false;
-        const PipeSlow r = pipe_slow(ring, B, g, c0 + take, left, err);
-        buf.append(r.bytes, r.k);
-        take += r.k;
-        return true;
-    }
-    __device__ __forceinline__ void topup(ByteBuf& buf) {
-        if (buf.cnt <= 24u) gen(buf, false);
-    }
-    __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf, true); }
-};
-
-// k_mt_ahead's work for the 64 games of one producer wave (RNG_NUMPY_FUSED),
-// after the wave has drawn this launch's words: each game's stream is
-// twisted until `lead` words lie past its consumer position `c` again, the
-// tempered low bytes into its ring.  Lane l owns game l's (c, twisted end
-// t0, twist pointer Tp); the twist itself runs 4 games per instruction, 16
-// consecutive words of one game per 16 lanes (one 64-B piece of its state),
-// so every load is coalesced.  Words j < 224 of a game have all inputs in
-// memory (their loads go out first, the next 4 games' loads before this
-// group's stores); later words read word j - 227 of the same call (rare:
-// only when a launch consumed > 224 - (lead slack) words).  Same words as
-// k_mt_ahead<false>: the ring and MT state a later entry point sees are
-// identical (every pipeline test).
-struct TwistGroup {
-    uint32_t A[14], Cv[14], Bx;  // Bx: word 224 (lane 15's B of the last chunk)
-};
-
-// within a 16-lane DPP row: lane k gets lane k + N (row_shl:N; 0 past the row)
-template <int N>
-__device__ __forceinline__ uint32_t row_next(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x100 + N, 0xF, 0xF, true);
-}
-// lane k gets lane (k + 1) mod 16 (row_ror:15)
-__device__ __forceinline__ uint32_t row_rot1(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x12F, 0xF, 0xF, false);
-}
-
-__device__ __forceinline__ void twist_group_load(const DevState& s, TwistGroup& X, int64_t gq, uint32_t T0, uint32_t n, uint32_t k) {
-    constexpr uint32_t D = kMtN - kMtM;
-    const uint32_t* st = s.mt + gq * kMtN;
-    const uint32_t m1 = min(n, 224u);
-#pragma unroll
-    for (int m = 0; m < 14; m++) {
-        const uint32_t j = 16u * m + k;
-        if (j <= m1 && n) {  // one word past the group's last: its B
-            uint32_t idx = T0 + j;
-            if (idx >= (uint32_t)kMtN) idx -= kMtN;
-            X.A[m] = st[idx];
-            X.Cv[m] = st[(idx < D) ? idx + kMtM : idx - D];
-        }
-    }
-    if (k == 15u && m1 == 224u) {
-        uint32_t idx = T0 + 224u;
-        if (idx >= (uint32_t)kMtN) idx -= kMtN;
-        X.Bx = st[idx];
-    }
-}
-
-__device__ __forceinline__ void twist_ring_dword(const DevState& s, int64_t gq, uint32_t t0, uint32_t j, uint32_t n, uint32_t k, uint32_t v) {
-    const uint32_t y = mt_temper(v) & 0xFFu;
-    const uint32_t d = y | (row_next<1>(y) << 8) | (row_next<2>(y) << 16) | (row_next<3>(y) << 24);
-    const uint32_t ri = (t0 + j) & (uint32_t)(kPipeRing - 1);
-    if ((k & 3u) == 0u && j < n)
-        st_nt((uint32_t*)((uint8_t*)s.pring + ((int64_t)(ri >> 4) * s.B + gq) * 16 + (ri & 12u)), d, SECHS_NT_MORE);
-}
-
-__device__ __forceinline__ void twist_group_store(const DevState& s, const TwistGroup& X, int64_t gq, uint32_t T0, uint32_t t0,
-                                                  uint32_t n, uint32_t k) {
-    constexpr uint32_t D = kMtN - kMtM;
-    uint32_t* st = s.mt + gq * kMtN;
-    const uint32_t m1 = min(n, 224u);
-    uint32_t r = row_rot1(X.A[0]);
-#pragma unroll
-    for (int m = 0; m < 14; m++) {
-        const uint32_t j = 16u * m + k;
-        // B(j) = word j + 1 = A of the next lane (lane 15: lane 0 of the next chunk)
-        const uint32_t rn = (m < 13) ? row_rot1(X.A[m + 1 < 14 ? m + 1 : 13]) : X.Bx;
-        const uint32_t b = (k == 15u) ? rn : r;
-        uint32_t v = 0u;
-        if (j < m1) {
-            uint32_t idx = T0 + j;
-            if (idx >= (uint32_t)kMtN) idx -= kMtN;
-            v = mt_mix(X.A[m], b, X.Cv[m]);
-            st_nt(&st[idx], v, SECHS_NT_MORE);
-            if (idx == 0u) s.mt0[gq] = X.A[m];
-        }
-        twist_ring_dword(s, gq, t0, j, n, k, v);
-        r = rn;
-    }
-    if (__builtin_amdgcn_readfirstlane(__ballot(n > 224u) != 0ull ? 1 : 0)) {
-        // words 224 .. n in order: word j reads word j - 227, stored above by
-        // another lane of this wave -- let those stores land first
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-        for (uint32_t j0 = 224u; j0 < 600u; j0 += 16u) {
-            if (!__ballot(j0 < n)) break;
-            const uint32_t j = j0 + k;
-            uint32_t v = 0u;
-            if (j < n) {
-                uint32_t idx = T0 + j;
-                if (idx >= (uint32_t)kMtN) idx -= kMtN;
-                const uint32_t aa = st[idx];
-                v = mt_mix(aa, st[(idx + 1u == (uint32_t)kMtN) ? 0u : idx + 1u], st[(idx < D) ? idx + kMtM : idx - D]);
-                st[idx] = v;
-                if (idx == 0u) s.mt0[gq] = aa;
-            }
-            twist_ring_dword(s, gq, t0, j, n, k, v);
-            __builtin_amdgcn_s_waitcnt(0x0F70);
-        }
-    }
-}
-
-// the whole wave calls this (shuffles); dead lanes pass live = false
-__device__ __forceinline__ void twist_ahead_wave(const DevState& s, const PlayArgs& a, int64_t g0, uint32_t lane, bool live,
-                                                 uint32_t c, uint32_t t0) {
-    uint32_t n = 0u, T0 = 0u, Tp = 0u;
-    if (live) {
-        Tp = s.ptp[g0 + lane];
-        const int32_t lead = (int32_t)(t0 - c);  // < 0: an overrun, already counted by the consumer
-        n = (lead >= 0 && lead < a.pipe_lead) ? (((uint32_t)(a.pipe_lead - lead)) & ~7u) : 0u;
-        T0 = (Tp == (uint32_t)kMtN) ? 0u : Tp;
-    }
-    const uint32_t k = lane & 15u, sub = lane >> 4;
-    TwistGroup X, Y;
-    // group q = games 4q .. 4q+3 of the wave; two groups in flight
-    auto args = [&](int q, int64_t& gq, uint32_t& Tq, uint32_t& tq, uint32_t& nq) {
-        const int gi = 4 * q + (int)sub;
-        gq = g0 + gi;
-        Tq = __shfl(T0, gi), tq = __shfl(t0, gi), nq = __shfl(n, gi);
-    };
-    int64_t gx, gy;
-    uint32_t Tx, tx, nx, Ty, ty, ny;
-    args(0, gx, Tx, tx, nx);
-    twist_group_load(s, X, gx, Tx, nx, k);
-    for (int q = 0; q < 16; q += 2) {
-        args(q + 1, gy, Ty, ty, ny);
-        twist_group_load(s, Y, gy, Ty, ny, k);
-        twist_group_store(s, X, gx, Tx, tx, nx, k);
-        if (q + 2 < 16) {
-            args(q + 2, gx, Tx, tx, nx);
-            twist_group_load(s, X, gx, Tx, nx, k);
-        }
-        twist_group_store(s, Y, gy, Ty, ty, ny, k);
-    }
-    if (live) {
-        uint32_t Tn = Tp;
-        if (n) {
-            Tn = T0 + n;
-            while (Tn > (uint32_t)kMtN) Tn -= kMtN;
-        }
-        s.ptp[g0 + lane] = Tn;
-        s.ptend[(int64_t)a.pipe_tout * s.B + g0 + lane] = t0 + n;
-    }
-}
-
 template <int N>
 struct SplitSrc {
     const uint16_t* idx;  // this lane's column of the producer's [t][64] index words
@@ -1075,26 +863,13 @@ __global__ __launch_bounds__(2 * kBlock) void k_play_split(DevState s, PlayArgs 
     const int tE = min(tA, kSplitEarly);
     if (wave >= 4) {  // ---------------- producer (the critical path: issue priority over the play waves)
         __builtin_amdgcn_s_setprio(1);
-        // the word stream: the pipelined ring (k_mt_ahead twisted it), the
-        // game's own MT19937 state twisted here 16 words per refill (no
-        // store of this wave is in flight to stall its loads), or Philox
-        // (RNG_NUMPY_FUSED: the ring, twisted by the previous launch's producers)
-        constexpr bool kRing = MODE == RNG_NUMPY_PIPE || MODE == RNG_NUMPY_FUSED;
-        using R = typename std::conditional<kRing, RingGlobal,
-                                            typename std::conditional<MODE == RNG_NUMPY_MT, MtGenT<2>, PhiloxGen>::type>::type;
-        R rng;
+        static_assert(MODE == RNG_PHILOX, "k_play_split decodes Philox streams only");
+        PhiloxGen rng;
         ByteBuf buf;
         PhaseProf pq;
         pq.start();
-        if constexpr (MODE == RNG_NUMPY_FUSED) {
-            // publish the overrun count of the launches before to the host (sn_rollout reads it at entry)
-            if (g == 0 && a.perr_mirror)
-                __hip_atomic_store(a.perr_mirror, __hip_atomic_load(s.perr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
         if (live) {
-            if constexpr (kRing) rng.load(s, g, buf, a.pipe_cin, a.pipe_t);
-            else RngOf<MODE, 2>::load(s, g, rng, buf);
+            RngOf<MODE, 2>::load(s, g, rng, buf);
             produce_draws<N>(rng, buf, idx, 0, tE, n0);
         }
         __syncthreads();  // B0: the first steps' indices are in LDS
@@ -1122,16 +897,9 @@ __global__ __launch_bounds__(2 * kBlock) void k_play_split(DevState s, PlayArgs 
             produce_draws<N>(rng, buf, idx, tA, a.steps, kHand);
             pq.mark(PR_DRAWS2);
         }
-        if constexpr (MODE == RNG_NUMPY_FUSED) {  // the next launch's words, while the play waves play
-            twist_ahead_wave(s, a, g - lane, (uint32_t)lane, live, live ? rng.consumed(buf) : 0u, live ? rng.tend : 0u);
-            pq.mark(PR_TWIST);
-        }
         __syncthreads();  // B2: the deal and the later indices are in LDS
         pq.mark(PR_B2);
-        if (live) {
-            if constexpr (kRing) s.pabsc[(int64_t)a.pipe_cout * s.B + g] = rng.consumed(buf);
-            else RngOf<MODE, 2>::store(s, g, rng, buf);
-        }
+        if (live) RngOf<MODE, 2>::store(s, g, rng, buf);
         pq.mark(PR_STORE);
         pq.flush(lane, 1);
         return;
@@ -1307,10 +1075,8 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
     e->pipe_lead = kPipeLead;
     e->phase = -1;
     e->play_split = 1;
-    e->ahead_delay = 0;
     e->pvalid = 0;
     e->pcount = 0;
-    e->pside = 0;
     if (rng_mode == SN_RNG_NUMPY_MT) {
         struct {
             void** p;
@@ -1423,12 +1189,8 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
             if (value != 32 && value != 64) return fail(SN_EINVAL, "games per wave must be 32 or 64");
             e->pipe_gpw = value;
             return SN_OK;
-        case SN_OPT_AHEAD_DELAY:
-            if (value < 0 || value > 50) return fail(SN_EINVAL, "ahead delay must be in 0..50 us");
-            e->ahead_delay = value;
-            return SN_OK;
         case SN_OPT_PLAY_SPLIT:
-            if (value < 0 || value > 4) return fail(SN_EINVAL, "play split must be 0..4");
+            if (value < 0 || value > 1) return fail(SN_EINVAL, "play split must be 0 or 1");
             e->play_split = value;
             return SN_OK;
         case SN_OPT_PIPE_LEAD:
@@ -1648,50 +1410,16 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     // launches keep the pair tail < 1e-26 up to K = 8 agents at N <= 4
     // (tools/pipe_tail.py), beyond that 5-step launches
     const int chunk = min(e->chunk_steps, (s.lg_K > 8) ? 5 : pipe_max_chunk(s.N));
-    // SN_OPT_PLAY_SPLIT 2: role-split k_play over the ring k_mt_ahead twists
-    // on the side stream; 4: its producer waves twist the next launch's words
-    // themselves (one kernel per launch, no side stream, no cross-stream event)
-    const bool fused = e->play_split == 4 && split_ok(e, a) && gpw == 64;
-    const bool split = (e->play_split == 2 || fused) && split_ok(e, a) && gpw == 64;
     for (int t0 = 0; t0 < a.steps; t0 += chunk) {
         PlayArgs c = a;
         c.steps = min(chunk, a.steps - t0);
         c.step0 = a.step0 + t0;
-        c.n0 = split ? kHand - (e->phase + t0) % kHand : 0;
         if (a.rewards) c.rewards = a.rewards + (int64_t)t0 * B * N;
         if (a.done) c.done = a.done + (int64_t)t0 * B;
         if (a.actions_out) c.actions_out = a.actions_out + (int64_t)t0 * B * N;
         if (a.obs) c.obs = a.obs + (int64_t)t0 * B * N * a.obs_stride;
         const int p = (int)(e->pcount & 1u);
         c.pipe_cin = 1 - p, c.pipe_cout = p, c.pipe_t = p;
-        if (fused) {
-            {
-                c.pipe_tout = 1 - p, c.pipe_lead = e->pipe_lead, c.perr_mirror = e->perr_host_dev;
-                if (e->pside) HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));  // a side-stream twist still owns ptend[p]
-                e->pside = 0;
-                hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
-                if (tv) HIP_TRY(hipEventRecord(tv[0], st));
-                SN_DISPATCH_N(s.N, {
-                    if constexpr (NN <= kSplitMaxPlayers) {
-                        const size_t sl = split_lds(NN, c.steps);
-                        HIP_TRY(hipFuncSetAttribute((const void*)k_play_split<NN, RNG_NUMPY_FUSED>,
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)sl));
-                        hipLaunchKernelGGL((k_play_split<NN, RNG_NUMPY_FUSED>), dim3(grid_for(s.B)), dim3(2 * kBlock), sl, st, s, c);
-                    }
-                });
-                HIP_TRY(hipGetLastError());
-                if (tv) {
-                    HIP_TRY(hipEventRecord(tv[1], st));
-                    HIP_TRY(hipEventRecord(tv[2], st));
-                    HIP_TRY(hipEventRecord(tv[3], st));
-                }
-                e->pcount++;
-                continue;
-            }
-        }
-#ifdef SECHS_DEBUG_NOWAIT  // measurement only: cost of the cross-stream wait (racy)
-        if (!getenv("SECHS_NOWAIT"))
-#endif
         HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));  // this launch's words are twisted
         HIP_TRY(hipEventRecord(e->ev_main, st));         // the previous launch's consumption is final
         hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
@@ -1702,13 +1430,6 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
                 hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_PIPE, 32>), dim3((unsigned)((s.B + 32 * (kBlock / 64) - 1) / (32 * (kBlock / 64)))),
                                    dim3(kBlock), shmem, st, s, c);
-            } else if (split) {
-                if constexpr (NN <= kSplitMaxPlayers) {
-                    const size_t sl = split_lds(NN, c.steps);
-                    HIP_TRY(hipFuncSetAttribute((const void*)k_play_split<NN, RNG_NUMPY_PIPE>,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sl));
-                    hipLaunchKernelGGL((k_play_split<NN, RNG_NUMPY_PIPE>), dim3(grid_for(s.B)), dim3(2 * kBlock), sl, st, s, c);
-                }
             } else if (s.lg_K) {
                 if constexpr (NN >= 2 && NN <= kLeagueMaxPlayers) {
                     HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_PIPE, 64, true>,
@@ -1725,16 +1446,11 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         if (tv) HIP_TRY(hipEventRecord(tv[1], st));
         // the next launch's twist, beside this one: leads the consumer of the launch before
         HIP_TRY(hipStreamWaitEvent(e->side, e->ev_main, 0));
-        if (e->ahead_delay > 0) {  // let this k_play's waves reach the CUs first (SN_OPT_AHEAD_DELAY)
-            hipLaunchKernelGGL(k_idle, dim3(1), dim3(64), 0, e->side, (e->ahead_delay * 10 + 33) / 34);
-            HIP_TRY(hipGetLastError());
-        }
         if (tv) HIP_TRY(hipEventRecord(tv[2], e->side));
         hipLaunchKernelGGL(k_mt_ahead<false>, pg, dim3(kBlock), 0, e->side, s, AheadArgs{1 - p, p, 1 - p, e->pipe_lead, e->perr_host_dev});
         HIP_TRY(hipGetLastError());
         if (tv) HIP_TRY(hipEventRecord(tv[3], e->side));
         HIP_TRY(hipEventRecord(e->ev_prep, e->side));
-        e->pside = 1;
         e->pcount++;
     }
     HIP_TRY(hipEventRecord(e->ev_play, st));  // sn_pipe_sync orders behind the last k_play
@@ -1753,39 +1469,6 @@ static sn_status launch_play(sn_env* e, PlayArgs a, hipStream_t st) {
             return launch_pipe(e, a, st);
         }
         return launch_play_one(e, a, st);
-    }
-    if (s.rng_mode == SN_RNG_NUMPY_MT && e->play_split == 3 && split_ok(e, a)) {
-        // role-split k_play twisting each game's MT19937 in its producer
-        // waves: one kernel per <= 10 env-steps, no ring, no side stream
-        const sn_status r = sn_pipe_sync(e, st);
-        if (r != SN_OK) return r;
-        const int64_t B = s.B, N = s.N;
-        for (int t0 = 0; t0 < a.steps; t0 += kHand) {
-            PlayArgs c = a;
-            c.steps = min(kHand, a.steps - t0);
-            c.n0 = kHand - (e->phase + t0) % kHand;
-            if (a.rewards) c.rewards = a.rewards + (int64_t)t0 * B * N;
-            if (a.done) c.done = a.done + (int64_t)t0 * B;
-            if (a.actions_out) c.actions_out = a.actions_out + (int64_t)t0 * B * N;
-            if (a.obs) c.obs = a.obs + (int64_t)t0 * B * N * a.obs_stride;
-            hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
-            if (tv) HIP_TRY(hipEventRecord(tv[0], st));
-            SN_DISPATCH_N(s.N, {
-                if constexpr (NN <= kSplitMaxPlayers) {
-                    const size_t sl = split_lds(NN, c.steps);
-                    HIP_TRY(hipFuncSetAttribute((const void*)k_play_split<NN, RNG_NUMPY_MT>,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sl));
-                    hipLaunchKernelGGL((k_play_split<NN, RNG_NUMPY_MT>), dim3(grid_for(s.B)), dim3(2 * kBlock), sl, st, s, c);
-                }
-            });
-            HIP_TRY(hipGetLastError());
-            if (tv) {
-                HIP_TRY(hipEventRecord(tv[1], st));
-                HIP_TRY(hipEventRecord(tv[2], st));
-                HIP_TRY(hipEventRecord(tv[3], st));
-            }
-        }
-        return SN_OK;
     }
     if (s.rng_mode == SN_RNG_NUMPY_MT && !a.actions && e->pipe) {
         int wave;
@@ -2118,6 +1801,7 @@ sn_status sn_reset1(sn_env* e, const uint32_t* key_host, int32_t pos, uint32_t* 
     SN_DISPATCH_N(e->s.N, hipLaunchKernelGGL((k_reset1<NN>), dim3(1), dim3(64), 0, 0, e->s, e->hbuf_dev, summ));
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(0));
+    e->phase = 0;  // one game, just dealt
     h1_copy_out(e, out_host);
     // the advanced state in numpy's (key, pos) form, as sn_mt_get
     std::memcpy(key_out_host, e->hbuf + kH1Mt, sizeof(uint32_t) * kMtN);

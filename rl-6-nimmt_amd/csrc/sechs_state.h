@@ -820,14 +820,12 @@ struct sn_env {
     int pipe_lead;    // SN_OPT_PIPE_LEAD: words k_mt_ahead keeps twisted ahead (kPipeLead; tests lower it)
     int lg_phase;     // tournament handle: env-steps since the games were dealt, mod 10 (-1: not dealt yet)
     int phase;        // every game's env-steps since its deal, mod 10, when they are in lockstep; -1 unknown
-    int ahead_delay;  // SN_OPT_AHEAD_DELAY: us the side stream idles before each k_mt_ahead
     int play_split;   // SN_OPT_PLAY_SPLIT: role-split k_play for lockstep DrunkHamster rollouts
     sechs::DevState s;
     // pipelined twist-ahead (sechs_env.hip launch_pipe): a k_mt_ahead for the
     // next play launch may be in flight on `side` (ev_prep) after a rollout
     int pvalid;         // ring + ptend/pabsc/ptp are the live RNG state (mt_pos is stale)
     uint64_t pcount;    // play launches so far (parity selects the pabsc / ptend buffers)
-    int pside;          // the last twist-ahead ran on `side` (ev_prep); 0 after an in-kernel one (RNG_NUMPY_FUSED)
     hipStream_t side;
     hipEvent_t ev_prep, ev_main, ev_play;  // ev_play: after the last pipelined k_play (caller's stream)
     uint32_t* perr_host;                    // pinned, device-mapped mirror of s.perr (PlayArgs::perr_mirror)

@@ -31,6 +31,8 @@ than max(warmup, minibatch) sequences are stored, one on-policy update (the
 newest sequence of every decider) and one off-policy update (`minibatch`
 stored sequences per decider, drawn without replacement on the device).
 """
+import warnings
+
 import torch
 from torch import nn
 
@@ -41,6 +43,16 @@ from .utils.nets import MultiHeadedMLP
 T_STEPS = 10
 
 
+def default_capacity(rollout_len=10, minibatch=5, warmup=100):
+    """replay episodes that let learn() start: the reference's SequentialHistory
+    is unbounded (agents/base.py history_length=None), so its warmup of
+    `warmup` sequences is always reached; a ring of C episodes stores
+    C * ceil(10 / rollout_len) sequences, which must exceed max(warmup, minibatch)"""
+    chunks = -(-T_STEPS // int(rollout_len))
+    need = max(int(warmup), int(minibatch)) + 1
+    return max(4, -(-need // chunks) + 1)
+
+
 def make_actor_critic(hidden_sizes=(100, 100), activation=None):
     """the reference's net (actor_critic.py:44-46): MultiHeadedMLP(48, (100, 100), (1, 1)) -- policy logit, q"""
     return MultiHeadedMLP(ROW, hidden_sizes=hidden_sizes, head_sizes=(1, 1), activation=activation or nn.ReLU(),
@@ -49,14 +61,18 @@ def make_actor_critic(hidden_sizes=(100, 100), activation=None):
 
 class BatchedACER(BatchedPUCT):
     def __init__(self, env, actor=None, seats_mask=None, net_dtype=torch.bfloat16, seed=0, gamma=0.99, rollout_len=10,
-                 minibatch=5, truncate=1.0, warmup=100, r_factor=0.1, critic_weight=1.0, capacity=4,
+                 minibatch=5, truncate=1.0, warmup=100, r_factor=0.1, critic_weight=1.0, capacity=None,
                  log_epsilon=-20.0):
         super().__init__(env, actor if actor is not None else make_actor_critic(), seed=seed, seats_mask=seats_mask,
                          puct_root=False, net_dtype=net_dtype)
         self.gamma, self.truncate, self.r_factor = float(gamma), float(truncate), float(r_factor)
         self.rollout_len, self.minibatch, self.warmup = int(rollout_len), int(minibatch), int(warmup)
         self.critic_weight, self.log_epsilon = float(critic_weight), float(log_epsilon)
-        self.capacity = int(capacity)
+        self.capacity = default_capacity(rollout_len, minibatch, warmup) if capacity is None else int(capacity)
+        if self.capacity * len(self.chunks()) <= max(self.warmup, self.minibatch):
+            warnings.warn(f"BatchedACER: capacity {self.capacity} episodes hold {self.capacity * len(self.chunks())} "
+                          f"sequences per decider, so learn() never passes warmup {max(self.warmup, self.minibatch)} "
+                          f"(capacity >= {default_capacity(rollout_len, minibatch, warmup)} learns)")
         D, dev = self.D, env.device
         self.log_prob = torch.zeros((D,), dtype=torch.float32, device=dev)
         self.entropy = torch.zeros((D,), dtype=torch.float32, device=dev)
@@ -88,11 +104,21 @@ class BatchedACER(BatchedPUCT):
                                      nat.ptr(self.log_prob), nat.ptr(self.entropy), st), "sn_policy_sample")
         if record:
             s, t = self.episodes % self.capacity, T_STEPS - n
-            self.rep_rows[s, t, :, :n] = self._train_rows(q, n, rows).view(self.D, n, ROW)
+            r32 = self._train_rows(q, n, rows)
+            self.rep_rows[s, t, :, :n] = r32.view(self.D, n, ROW)
             self.rep_rows[s, t, :, n:] = 0.0
             self.rep_act[s, t] = self.best_index.long()
             self.rep_logp[s, t].fill_(self.log_epsilon)
-            self.rep_logp[s, t, :, :n] = torch.log_softmax(logits.view(self.D, n), dim=1)
+            # behaviour log pi in the training forward's precision (fp32), so that
+            # rho = pi_now / pi_then is exactly 1 on-policy as in the reference
+            # (the bf16 inference logits differ from it by rounding)
+            if self.net_dtype == torch.float32:
+                lt = logits.view(self.D, n)
+            else:
+                with torch.no_grad():
+                    lt, _ = self.actor(r32.to(self.actor_device()))
+                lt = lt.reshape(self.D, n).to(self.env.device)
+            self.rep_logp[s, t, :, :n] = torch.log_softmax(lt.float(), dim=1)
         self.step_id += 1
         return self.actions
 

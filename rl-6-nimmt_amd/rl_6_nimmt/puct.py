@@ -165,7 +165,9 @@ class BatchedPUCT:
             nat.check(L.sn_puct_root_rows(h, ctypes_ref(q), nat.ptr(rows), bf16, st), "sn_puct_root_rows")
             nat.check(L.sn_puct_init(h, ctypes_ref(q), nat.ptr(self._logits(rows)), st), "sn_puct_init")
             if self.graph:
-                self._step_dev.fill_(self.step_id & 0x7FFFFFFF)
+                # the same 32-bit counter as the eager path's q.step, as int32 bits
+                sid = self.step_id & 0xFFFFFFFF
+                self._step_dev.fill_(sid - (1 << 32) if sid >= (1 << 31) else sid)
                 g = self._graphs.get((n, self._net_version))
                 if g is None:
                     g = self._capture(n)

@@ -230,3 +230,26 @@ def test_batched_acer_replay_bookkeeping():
     for d in range(eng.D):
         pairs = list(zip(s[d].tolist(), c[d].tolist()))
         assert len(set(pairs)) == 2 and all(p in eng.stored_sequences(1) for p in pairs)
+
+
+def test_batched_acer_default_capacity_reaches_warmup():
+    """with the reference's defaults (rollout_len 10, warmup 100,
+    minibatch 5) the device replay must hold more than max(warmup, minibatch)
+    sequences per decider, or learn() never updates (the reference's
+    SequentialHistory is unbounded)"""
+    from rl_6_nimmt.acer import BatchedACER, default_capacity
+
+    for rl, mb, wu in ((10, 5, 100), (10, 10, 100), (4, 5, 100), (3, 2, 7), (10, 200, 50)):
+        cap = default_capacity(rl, mb, wu)
+        assert cap * (-(-10 // rl)) > max(wu, mb), (rl, mb, wu, cap)
+    eng = BatchedACER(_HostEnv(2, 2), net_dtype=torch.float32)
+    assert eng.capacity * len(eng.chunks()) > max(eng.warmup, eng.minibatch)
+    # fill past the warmup: the schedule now asks for updates
+    _fill_replay(eng, eng.capacity, np.random.default_rng(3))
+    assert len(eng.stored_sequences(0)) > max(eng.warmup, eng.minibatch)
+    before = [p.detach().clone() for p in eng.actor.parameters()]
+    updates = eng.learn(torch.optim.Adam(eng.actor.parameters()))
+    assert len(updates) == 2  # one on-policy + one off-policy step, actor_critic.py:146-151
+    assert any(not torch.equal(a, b) for a, b in zip(eng.actor.parameters(), before))
+    with pytest.warns(UserWarning):
+        BatchedACER(_HostEnv(2, 2), net_dtype=torch.float32, capacity=4)

@@ -350,11 +350,11 @@ def test_ring_options_do_not_change_results(ring_words, chunk_steps, pipeline, g
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rng,split", [("numpy", 0), ("numpy", 2), ("numpy", 3), ("numpy", 4), ("philox", 0), ("philox", 1)])
-@pytest.mark.parametrize("N", [2, 3, 4])
+@pytest.mark.parametrize("rng,split", [("numpy", 0), ("philox", 0), ("philox", 1)])
+@pytest.mark.parametrize("N", [2, 4])
 def test_play_split_modes_match_oracle(rng, split, N):
-    """SN_OPT_PLAY_SPLIT (role-split k_play: producer waves decode every
-    random decision into LDS) changes nothing observable: ragged B, launches
+    """SN_OPT_PLAY_SPLIT (role-split k_play of philox handles: producer waves
+    decode every random decision into LDS) changes nothing observable: ragged B, launches
     that start mid-episode (3 then 10-step chunks: the deal falls inside a
     launch), obs/actions/rewards/done and the final RNG states equal the
     oracle's."""
@@ -380,40 +380,6 @@ def test_play_split_modes_match_oracle(rng, split, N):
             rk, rp = _np_form(np.frombuffer(bytes(rngs[g].mt), dtype=np.uint32), rngs[g].pos)
             assert p == rp and np.array_equal(k, rk), g
         assert env.pipe_errors() == 0
-
-
-@pytest.mark.gpu
-def test_fused_twist_interleaves_with_side_stream_twist():
-    """SN_OPT_PLAY_SPLIT 4 twists the next launch's words inside the play
-    kernel; a launch the split kernel cannot take (obs buffer not 16-B
-    aligned) falls back to k_play + k_mt_ahead on the side stream.  Both
-    keep the same ring / MT19937 bookkeeping: alternating them stays bit-exact."""
-    B, N, T, seed = 300, 4, 10, 9
-    env = venv(B, N, seed=seed, rng="numpy")
-    env.set_option(play_split=4)
-    env.reset()
-    ref = O.VecOracle(B, N, rng_mode=O.RNG_NUMPY_MT, seed=seed)
-    ref.reset()
-    dev = env.device
-    for steps, misaligned in ((T, False), (T, True), (7, False), (T, True), (T, False), (13, False)):
-        flat = torch.empty(steps * B * N * 48 + 4, dtype=torch.int8, device=dev)
-        obs = (flat[4:] if misaligned else flat[:-4]).view(steps, B, N, 48)
-        out = {"rewards": torch.empty((steps, B, N), dtype=torch.int32, device=dev),
-               "done": torch.empty((steps, B), dtype=torch.uint8, device=dev),
-               "actions": torch.empty((steps, B, N), dtype=torch.uint8, device=dev), "obs": obs}
-        env.rollout(steps, out=out)
-        rr, rd, ra, ro = ref.rollout(steps, want_obs=True)
-        torch.cuda.synchronize()
-        assert np.array_equal(out["actions"].cpu().numpy(), ra)
-        assert np.array_equal(out["rewards"].cpu().numpy(), rr)
-        assert np.array_equal(out["done"].cpu().numpy(), rd)
-        assert np.array_equal(out["obs"].cpu().numpy()[..., :47], ro)
-    rngs = ref.v.contents.rngs
-    for g in range(0, B, 11):
-        k, p = _np_form(*env.get_mt_state(g))
-        rk, rp = _np_form(np.frombuffer(bytes(rngs[g].mt), dtype=np.uint32), rngs[g].pos)
-        assert p == rp and np.array_equal(k, rk), g
-    assert env.pipe_errors() == 0
 
 
 def test_ring_option_validation():
