@@ -222,6 +222,38 @@ sn_status sn_league_rollout(sn_env* env, int steps, int32_t* rewards, uint8_t* d
                             int obs_stride, int32_t* records, void* stream);
 /* the seats word of every slot's current game, [B] uint32 */
 sn_status sn_league_seats(sn_env* env, uint32_t* out, void* stream);
+
+/* Mixed leagues (run.py:20-40: DrunkHamster, MCSAgent, PUCTAgent,
+   PUCTCustomedAgent, BatchedACERAgent seats).  sn_league_agents gives every
+   agent of a tournament handle its kind (kinds[num_agents]; all
+   SN_AGENT_RANDOM after sn_league_config):
+     SN_AGENT_RANDOM    DrunkHamster, drawn in-kernel from the slot's stream
+     SN_AGENT_MCS       MCSAgent(mc_per_card[a], mc_max[a]) (agents/mcts.py:17-188):
+                        card memory and the reference-exact search on the
+                        slot's numpy stream (numpy handles only)
+     SN_AGENT_EXTERNAL  the caller plays the seat (the net agents: their
+                        batched engines pick the card, sn_puct over the
+                        handle's decision list, sn_puct.dec_list)
+   mc_per_card / mc_max may be NULL (10 / 100, mcts.py:24-25).  Leagues with
+   any non-RANDOM agent play with sn_league_step; all-RANDOM ones also with
+   sn_league_rollout. [sync] */
+enum { SN_AGENT_RANDOM = 0, SN_AGENT_MCS = 1, SN_AGENT_EXTERNAL = 2 };
+sn_status sn_league_agents(sn_env* env, const int32_t* kinds_host, const int32_t* mc_per_card_host,
+                           const int32_t* mc_max_host);
+/* One env-step of every slot's current game (numpy handles; sn_reset then
+   10 steps per game): seats in seat order as GameSession calls
+   them (play.py:38-41) -- RANDOM and MCS seats draw from the slot's stream in
+   the reference's exact order, EXTERNAL seats play actions [B][N] (checked
+   against the hand, env.py:114-118).  A game that ends (every 10th step)
+   writes records [B][1 + N] (seats word, GameSession.results[0]); the
+   slots' next games start with sn_reset (seat draw, then deal:
+   tournament.py:132-138), after any roster change.  Outputs (each may
+   be NULL): rewards [B][N], played [B][N] (cards, -1 past k), invalid [B]
+   (first seat whose external card is illegal -- that slot is left untouched --
+   or -1), status [B] |= 1 where an MCSAgent move got no playout (the
+   reference raises IndexError there, quirk Q6). */
+sn_status sn_league_step(sn_env* env, const int32_t* actions, int32_t* rewards, int32_t* played, int32_t* records,
+                         int32_t* invalid, int32_t* status, void* stream);
 /* Sequential multiplayer Elo over game records in the given order (host
    memory, no GPU): records [G][1 + max_players] int32 as sn_league_rollout
    writes them; elos [num_agents] float64 in/out (initial ratings in).
@@ -309,6 +341,11 @@ typedef struct {
     float* root_probs;
     const uint32_t* step_dev; /* NULL, or the decision counter in device memory (overrides `step`):
                                  lets one captured hipGraph of a decision's launches serve every decision */
+    const int32_t* dec_list;  /* NULL (seats_mask), or num_dec decisions g * N + p in device memory: one
+                                 agent's seats of a tournament handle (required there); a game of k < N
+                                 players then rolls out k seats (obs N field k, mcts.py:62-64) and writes
+                                 dummy rows for the absent seats */
+    int64_t num_dec;
 } sn_puct;
 
 sn_status sn_puct_root_rows(sn_env* env, const sn_puct* q, void* rows, int bf16, void* stream);

@@ -292,3 +292,32 @@ def mcs_stratified(game, seat, avail, rollouts, seed, step, gid):
                                     ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p]
     L.or_mcs_stratified(ctypes.byref(game.g), seat, _p(a), len(a), rollouts, seed, step, gid, _p(s))
     return s
+
+
+# ---------------------------------------------------------------- tournament
+def league_records(num_agents, min_players, max_players, seed=0, game_offset=0, slots=1, games=1):
+    """DrunkHamster tournament streams (tournament.py:132-177 over K
+    DrunkHamster agents, play.py:23-75): slot g replays np.random.seed(seed +
+    game_offset + g); Tournament(min, max); play_game() x games -- per game
+    _choose_players (num_players = lo + random_interval(hi - lo), agents =
+    permutation(K)[:k]), env.reset() and 10 DrunkHamster steps.  Returns
+    int32 [games, slots, 1 + max_players] in the device's record format
+    (seats word k | agent(seat p) << (4 + 4p), then -penalties, 0 past k)."""
+    K, N = int(num_agents), int(max_players)
+    out = np.zeros((games, slots, 1 + N), dtype=np.int32)
+    for j in range(slots):
+        rng = Rng(RNG_NUMPY_MT, seed + game_offset + j)
+        for e in range(games):
+            k = min_players + rng.interval(max_players - min_players)
+            seats = rng.shuffle(np.arange(K))[:k]
+            g = Game(k)
+            g.reset(rng)
+            while not g.done():
+                acts = [g.random_action(rng, p) for p in range(k)]
+                g.step(acts)
+            w = k
+            for p, a in enumerate(seats):
+                w |= int(a) << (4 + 4 * p)
+            out[e, j, 0] = w  # < 2^28: K <= 16 agents, k <= 6 seats
+            out[e, j, 1: 1 + k] = [-s for s in g.scores]
+    return out

@@ -1143,7 +1143,7 @@ sn_status sn_destroy(sn_env* e) {
     if (e->side) (void)hipStreamDestroy(e->side);
     free_timing(e);
     void* ps[] = {s.hand, s.row_lo, s.row_hi, s.score, s.sum_res, s.episodes, s.mt_pos, s.ctr, s.mt, s.mt0, s.ring,
-                  s.pring, s.pabsc, s.ptend, s.ptp, s.perr, s.lgs};
+                  s.pring, s.pabsc, s.ptend, s.ptp, s.perr, s.lgs, s.lmem};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     delete e;
@@ -1553,6 +1553,7 @@ sn_status sn_league_config(sn_env* e, int num_agents, int min_players, int max_p
     if (!s.lgs && hipMalloc((void**)&s.lgs, sizeof(uint32_t) * s.B) != hipSuccess) return fail(SN_ENOMEM, "league state");
     HIP_TRY(hipMemset(s.lgs, 0, sizeof(uint32_t) * s.B));
     s.lg_K = num_agents, s.lg_lo = min_players, s.lg_hi = max_players;
+    for (int i = 0; i < kLeagueMaxAgents; i++) e->lg_kind[i] = SN_AGENT_RANDOM, e->lg_mpc[i] = 10, e->lg_mmax[i] = 100;
     e->lg_phase = -1;  // sn_reset deals the first games
     return SN_OK;
 }
@@ -1561,6 +1562,9 @@ sn_status sn_league_rollout(sn_env* e, int steps, int32_t* rewards, uint8_t* don
                             int obs_stride, int32_t* records, void* stream) {
     if (!e) return fail(SN_EINVAL, "env is NULL");
     if (!e->s.lg_K) return fail(SN_EINVAL, "not a tournament handle (sn_league_config)");
+    for (int i = 0; i < e->s.lg_K; i++)
+        if (e->lg_kind[i] != SN_AGENT_RANDOM)
+            return fail(SN_EUNSUPPORTED, "sn_league_rollout plays DrunkHamster agents in-kernel; mixed leagues use sn_league_step");
     if (e->lg_phase != 0) return fail(SN_EINVAL, "tournament rollouts start right after sn_reset or a whole number of games");
     if (steps % kHand) return fail(SN_EINVAL, "tournament rollouts play whole games (steps a multiple of 10)");
     if (steps < 0) return fail(SN_EINVAL, "steps must be >= 0");

@@ -28,8 +28,11 @@ constexpr int kHistBins = 172;   // outcomes of seat 0: -171..0
 constexpr int kRowLen = 48;      // 1 (action) + 47 (observation)
 
 struct PuctArgs {
-    int64_t D;                // decisions = B * popcount(seats_mask)
+    int64_t D;                // decisions = B * popcount(seats_mask), or num_dec of a decision list
     uint32_t seats_mask, M;   // deciding seats, M = popcount
+    const int32_t* dec;       // decision list (g * N + p per decision) or NULL (seats_mask)
+    const uint32_t* lgs;      // tournament handle: per game k | agents..., the rollouts seat k players; NULL: N
+    int N;                    // the handle's seats
     int n;                    // root hand size (all decisions in lockstep)
     int flags;                // 1: PUCT at the root (PUCTAgent), 0: sample it (PolicyMCSAgent)
     double c_puct;
@@ -48,11 +51,21 @@ struct PuctArgs {
 __device__ __forceinline__ uint32_t puct_step_of(const PuctArgs& a) { return a.step_dev ? *a.step_dev : a.step; }
 
 __device__ __forceinline__ void dec_to_gp(const PuctArgs& a, int64_t d, int64_t& g, int& p) {
+    if (a.dec) {  // a tournament agent's seats (sn_puct.dec_list)
+        const int32_t gp = a.dec[d];
+        g = gp / a.N;
+        p = gp - (int)g * a.N;
+        return;
+    }
     g = d / a.M;
     uint32_t k = (uint32_t)(d - g * a.M), m = a.seats_mask;
     for (uint32_t i = 0; i < k; i++) m &= m - 1u;  // drop the k lowest deciding seats
     p = __builtin_ctz(m);
 }
+
+// players of game g: the agent's num_players = state[10] (mcts.py:62-64); a
+// tournament game seats k <= N of the handle's N seats
+__device__ __forceinline__ int players_of(const PuctArgs& a, int64_t g) { return a.lgs ? (int)(a.lgs[g] & 15u) : a.N; }
 
 // utils/preprocessing.py:55-57 in float32, same operation order as torch
 __device__ __forceinline__ float nrm(float x, float lo, float hi) {
@@ -118,7 +131,7 @@ __global__ void k_puct_root_rows(DevState s, PuctArgs a, T* rows) {
     int p;
     dec_to_gp(a, d, g, p);
     const Hand h = load_hand(s, p, g);
-    write_row<T>(rows + i * kRowLen, hand_get(h, k), h, s.N, load_board(s, g));
+    write_row<T>(rows + i * kRowLen, hand_get(h, k), h, players_of(a, g), load_board(s, g));
 }
 
 // softmax(dim=0) of the root logits (mcts.py:227) and empty statistics
@@ -167,17 +180,18 @@ __global__ void k_puct_deal(DevState s, PuctArgs a) {
     ro[4] = b.hi.x, ro[5] = b.hi.y, ro[6] = b.hi.z, ro[7] = b.hi.w;
     ro[8] = (int32_t)(uint32_t)me.lo, ro[9] = (int32_t)(uint32_t)(me.lo >> 32), ro[10] = (int32_t)me.hi;
     uint32_t left = set_count(av);
+    const int kp = players_of(a, g);
 #pragma unroll
     for (int q = 1; q < N; q++) {
         u32x4 set = {0u, 0u, 0u, 0u};
-        for (uint32_t i = 0; i < n && left > 0u; i++) {
+        for (uint32_t i = 0; i < n && left > 0u && q < kp; i++) {
             const uint32_t k = rng_interval(gen, buf, left - 1u);
             const uint32_t c = set_select(av, k);
             av = clear_bit(av, c);
             set = set_bit(set, c);
             left--;
         }
-        const Hand h = hand_from_set(set);
+        const Hand h = hand_from_set(set);  // seats past k: empty (0xFF), they play nothing
         ro[8 + 3 * q] = (int32_t)(uint32_t)h.lo, ro[9 + 3 * q] = (int32_t)(uint32_t)(h.lo >> 32), ro[10 + 3 * q] = (int32_t)h.hi;
     }
     ro[40] = 0;   // outcome
@@ -194,8 +208,20 @@ __global__ void k_puct_rows(PuctArgs a, int N, int n_cur, T* rows) {
     const int rem = (int)(i - d * per_d);
     const int q = rem / n_cur, k = rem - q * n_cur;
     const int32_t* ro = a.ro + d * kRoWords;
+    int kp = N;
+    if (a.lgs) {
+        int64_t g;
+        int p;
+        dec_to_gp(a, d, g, p);
+        kp = players_of(a, g);
+    }
+    if (q >= kp) {  // an absent seat of a smaller tournament game: a dummy row (its logits are never read)
+#pragma unroll
+        for (int j = 0; j < kRowLen; j++) rows[i * kRowLen + j] = to_out<T>(0.f);
+        return;
+    }
     const Hand h = ro_hand(ro, q);
-    write_row<T>(rows + i * kRowLen, hand_get(h, (uint32_t)k), h, N, ro_board(ro));
+    write_row<T>(rows + i * kRowLen, hand_get(h, (uint32_t)k), h, kp, ro_board(ro));
 }
 
 // np.median of all outcomes so far, from the histogram (kth smallest)
@@ -279,8 +305,13 @@ __global__ void k_puct_step(DevState s, PuctArgs a, const float* logits, int t, 
     const uint64_t stream = ((uint64_t)(uint32_t)gid << 32) | ((uint64_t)p << 28) | ((uint64_t)a.rollout << 8) | (uint64_t)(1 + t);
     uint32_t card[N], pen[N];
     int first = ro[41];
+    const int kp = players_of(a, g);
 #pragma unroll
     for (int q = 0; q < N; q++) {
+        if (q >= kp) {  // absent seat of a smaller tournament game
+            card[q] = 0xFFu;
+            continue;
+        }
         int idx;
         const float* x = logits + (d * N + q) * n_cur;
         if (t == 0 && q == 0 && (a.flags & 1)) {
@@ -293,7 +324,7 @@ __global__ void k_puct_step(DevState s, PuctArgs a, const float* logits, int t, 
         card[q] = hand_get(G.hand[q], (uint32_t)idx);
         hand_del(G.hand[q], (uint32_t)idx);
     }
-    resolve<N>(G.b, card, pen);
+    resolve<N, true>(G.b, card, pen);
     const int32_t outcome = ro[40] - (int32_t)pen[0];
     if (n_cur == 1) {
         // backup: outcomes[first].append(outcome) (mcts.py:100)
@@ -418,12 +449,23 @@ __global__ void k_puct_score(int64_t D, int n_max, const int32_t* n, const int32
 // ============================================================================
 static sn_status puct_args(sn_env* e, const sn_puct* q, PuctArgs& a) {
     if (!e || !q) return set_error(SN_EINVAL, "NULL argument");
-    const uint32_t mask = q->seats_mask & ((1u << e->s.N) - 1u);
-    if (!mask) return set_error(SN_EINVAL, "seats_mask selects no seat");
     if (q->n < 1 || q->n > kHand) return set_error(SN_EINVAL, "hand size out of range");
-    a.M = (uint32_t)__builtin_popcount(mask);
-    a.seats_mask = mask;
-    a.D = e->s.B * a.M;
+    a.N = e->s.N;
+    a.lgs = e->s.lg_K ? e->s.lgs : nullptr;
+    if (q->dec_list) {
+        if (q->num_dec < 1 || q->num_dec > e->s.B * e->s.N) return set_error(SN_EINVAL, "num_dec out of range");
+        a.dec = q->dec_list;
+        a.D = q->num_dec;
+        a.M = 1u;
+        a.seats_mask = 0u;
+    } else {
+        if (a.lgs) return set_error(SN_EINVAL, "a tournament handle's engines take decision lists (dec_list)");
+        const uint32_t mask = q->seats_mask & ((1u << e->s.N) - 1u);
+        if (!mask) return set_error(SN_EINVAL, "seats_mask selects no seat");
+        a.M = (uint32_t)__builtin_popcount(mask);
+        a.seats_mask = mask;
+        a.D = e->s.B * a.M;
+    }
     a.n = q->n;
     a.flags = q->puct_root ? 1 : 0;
     a.c_puct = q->c_puct;

@@ -52,6 +52,7 @@ struct DevState {
     // player count k and seat agents, k | agent(seat p) << (4 + 4p)
     uint32_t* lgs;   // [B]
     int lg_K, lg_lo, lg_hi, lg_pad;
+    uint32_t* lmem;  // [4][B*N] card memory of MCSAgent seats (sn_league_step), word-major
 };
 
 constexpr int kPipeRing = 1024;  // ring bytes per game (>= lead + one launch)
@@ -819,6 +820,8 @@ struct sn_env {
     int pipe_gpw;     // SN_OPT_PIPE_GPW: games per k_play wave on the pipelined path (32 or 64)
     int pipe_lead;    // SN_OPT_PIPE_LEAD: words k_mt_ahead keeps twisted ahead (kPipeLead; tests lower it)
     int lg_phase;     // tournament handle: env-steps since the games were dealt, mod 10 (-1: not dealt yet)
+    int lg_kind[16];  // tournament handle: per agent SN_AGENT_* (sn_league_agents; all RANDOM by default)
+    int lg_mpc[16], lg_mmax[16];  // MCSAgent agents: mc_per_card, mc_max
     int phase;        // every game's env-steps since its deal, mod 10, when they are in lockstep; -1 unknown
     int play_split;   // SN_OPT_PLAY_SPLIT: role-split k_play for lockstep DrunkHamster rollouts
     sechs::DevState s;

@@ -22,6 +22,7 @@ SN_I8, SN_I16, SN_I32, SN_I64, SN_F32 = 1, 2, 3, 4, 5
 SN_AUTO_RESET, SN_NO_SUMMARIES = 1, 2
 SN_OPT_RING_WORDS, SN_OPT_CHUNK_STEPS, SN_OPT_PIPELINE, SN_OPT_TIMING, SN_OPT_PIPE_GPW, SN_OPT_PIPE_LEAD = 1, 2, 3, 4, 5, 6
 SN_OPT_PLAY_SPLIT = 7
+SN_AGENT_RANDOM, SN_AGENT_MCS, SN_AGENT_EXTERNAL = 0, 1, 2
 
 class SnPuct(ctypes.Structure):
     """sn_puct (include/sechs.h)"""
@@ -40,6 +41,8 @@ class SnPuct(ctypes.Structure):
         ("hist", ctypes.c_void_p),
         ("root_probs", ctypes.c_void_p),
         ("step_dev", ctypes.c_void_p),
+        ("dec_list", ctypes.c_void_p),
+        ("num_dec", ctypes.c_int64),
     ]
 
 
@@ -76,6 +79,8 @@ SIGNATURES = {
     "sn_league_config": ([_P, _I, _I, _I], _I),
     "sn_league_rollout": ([_P, _I, _P, _P, _P, _P, _I, _P, _P], _I),
     "sn_league_seats": ([_P, _P, _P], _I),
+    "sn_league_agents": ([_P, _P, _P, _P], _I),
+    "sn_league_step": ([_P, _P, _P, _P, _P, _P, _P, _P], _I),
     "sn_elo_replay": ([_P, _I64, _I, _I, ctypes.c_double, _P], _I),
     "sn_mcs_memorize": ([_P, _P, _I, _P], _I),
     "sn_mcs_rollouts": ([_P, _P, _I, _U64, ctypes.c_uint32, _P, _P], _I),

@@ -62,18 +62,19 @@ def make_actor_critic(hidden_sizes=(100, 100), activation=None):
 class BatchedACER(BatchedPUCT):
     def __init__(self, env, actor=None, seats_mask=None, net_dtype=torch.bfloat16, seed=0, gamma=0.99, rollout_len=10,
                  minibatch=5, truncate=1.0, warmup=100, r_factor=0.1, critic_weight=1.0, capacity=None,
-                 log_epsilon=-20.0):
+                 log_epsilon=-20.0, max_decisions=None):
         super().__init__(env, actor if actor is not None else make_actor_critic(), seed=seed, seats_mask=seats_mask,
-                         puct_root=False, net_dtype=net_dtype)
+                         puct_root=False, net_dtype=net_dtype, max_decisions=max_decisions)
         self.gamma, self.truncate, self.r_factor = float(gamma), float(truncate), float(r_factor)
         self.rollout_len, self.minibatch, self.warmup = int(rollout_len), int(minibatch), int(warmup)
         self.critic_weight, self.log_epsilon = float(critic_weight), float(log_epsilon)
         self.capacity = default_capacity(rollout_len, minibatch, warmup) if capacity is None else int(capacity)
-        if self.capacity * len(self.chunks()) <= max(self.warmup, self.minibatch):
+        # (tournament mode stores every seat of a round: one round passes the warmup)
+        if max_decisions is None and self.capacity * len(self.chunks()) <= max(self.warmup, self.minibatch):
             warnings.warn(f"BatchedACER: capacity {self.capacity} episodes hold {self.capacity * len(self.chunks())} "
                           f"sequences per decider, so learn() never passes warmup {max(self.warmup, self.minibatch)} "
                           f"(capacity >= {default_capacity(rollout_len, minibatch, warmup)} learns)")
-        D, dev = self.D, env.device
+        D, dev = self.D_max, env.device
         self.log_prob = torch.zeros((D,), dtype=torch.float32, device=dev)
         self.entropy = torch.zeros((D,), dtype=torch.float32, device=dev)
         C = self.capacity
@@ -82,6 +83,7 @@ class BatchedACER(BatchedPUCT):
         self.rep_logp = torch.full((C, T_STEPS, D, 10), self.log_epsilon, dtype=torch.float32, device=dev)
         self.rep_rew = torch.zeros((C, T_STEPS, D), dtype=torch.float32, device=dev)
         self.episodes = 0  # episodes written (slot = episodes % capacity)
+        self.rep_nd = [0] * C  # deciders stored in each slot (tournament mode: the round's seats of this agent)
         self._t = 0
         self._gen = torch.Generator(device=dev)
         self._gen.manual_seed(self.seed ^ 0xACE5)
@@ -91,6 +93,9 @@ class BatchedACER(BatchedPUCT):
     def decide(self, n, memorize=False, record=False):
         """sample every deciding seat's card at hand size n: actions [B, N] int32"""
         L, h, st = nat.lib(), self.env._h, self.env._stream()
+        if self.D == 0:
+            self.step_id += 1
+            return self.actions
         bf16 = int(self.net_dtype == torch.bfloat16)
         q = self._params(n)
         self.sync_net()
@@ -103,12 +108,12 @@ class BatchedACER(BatchedPUCT):
         nat.check(L.sn_policy_sample(h, ctypes_ref(q), nat.ptr(logits), nat.ptr(self.actions), nat.ptr(self.best_index),
                                      nat.ptr(self.log_prob), nat.ptr(self.entropy), st), "sn_policy_sample")
         if record:
-            s, t = self.episodes % self.capacity, T_STEPS - n
+            s, t, D = self.episodes % self.capacity, T_STEPS - n, self.D
             r32 = self._train_rows(q, n, rows)
-            self.rep_rows[s, t, :, :n] = r32.view(self.D, n, ROW)
-            self.rep_rows[s, t, :, n:] = 0.0
-            self.rep_act[s, t] = self.best_index.long()
-            self.rep_logp[s, t].fill_(self.log_epsilon)
+            self.rep_rows[s, t, :D, :n] = r32.view(D, n, ROW)
+            self.rep_rows[s, t, :D, n:] = 0.0
+            self.rep_act[s, t, :D] = self.best_index[:D].long()
+            self.rep_logp[s, t, :D].fill_(self.log_epsilon)
             # behaviour log pi in the training forward's precision (fp32), so that
             # rho = pi_now / pi_then is exactly 1 on-policy as in the reference
             # (the bf16 inference logits differ from it by rounding)
@@ -118,7 +123,7 @@ class BatchedACER(BatchedPUCT):
                 with torch.no_grad():
                     lt, _ = self.actor(r32.to(self.actor_device()))
                 lt = lt.reshape(self.D, n).to(self.env.device)
-            self.rep_logp[s, t, :, :n] = torch.log_softmax(lt.float(), dim=1)
+            self.rep_logp[s, t, :D, :n] = torch.log_softmax(lt.float(), dim=1)
         self.step_id += 1
         return self.actions
 
@@ -142,9 +147,20 @@ class BatchedACER(BatchedPUCT):
             # learn(next_reward=r_t) of the step's own reward, x r_factor in float64 (actor_critic.py:142)
             r = per_step[:, :, seats].reshape(T_STEPS, -1).double() * self.r_factor
             self.rep_rew[self.episodes % self.capacity] = r.float()
+            self.rep_nd[self.episodes % self.capacity] = self.D
             self.episodes += 1
         self.episode_rewards = per_step
         return per_step.sum(dim=0), per_step
+
+    def record_rewards(self, per_step):
+        """tournament mode: close the round's episode -- the rewards of this
+        agent's seats (per_step [10, B, N] int32, learn(next_reward=r_t) of
+        the step's own reward x r_factor, actor_critic.py:142)"""
+        s = self.episodes % self.capacity
+        r = per_step.reshape(T_STEPS, -1)[:, self.dec.long()].double() * self.r_factor
+        self.rep_rew[s, :, : self.D] = r.float()
+        self.rep_nd[s] = self.D
+        self.episodes += 1
 
     # ------------------------------------------------------------ sequences in the replay
     def chunks(self):
@@ -166,10 +182,11 @@ class BatchedACER(BatchedPUCT):
         return out
 
     # ------------------------------------------------------------ the ACER loss
-    def loss(self, slots, chunk_ids):
+    def loss(self, slots, chunk_ids, decs=None):
         """sum over deciders of the reference's ACER loss on a batch of each
         decider's sequences: `slots`, `chunk_ids` [D, K] long (sequence k of
-        decider d = replay slot slots[d, k], chunk chunk_ids[d, k]).
+        decider d = replay slot slots[d, k], chunk chunk_ids[d, k], decider
+        index decs[d, k] within the slot -- default d).
         Returns (total, actor, correction, critic) -- components summed over
         deciders, total carrying the gradient."""
         dev = self.actor_device()
@@ -181,7 +198,10 @@ class BatchedACER(BatchedPUCT):
         t = ch[chunk_ids][:, :, None] + j  # [D, K, L]
         valid = j < ln[chunk_ids][:, :, None]
         t = torch.where(valid, t, torch.zeros_like(t))
-        d = torch.arange(D, device=self.env.device)[:, None, None].expand(D, K, L)
+        if decs is None:
+            d = torch.arange(D, device=self.env.device)[:, None, None].expand(D, K, L)
+        else:
+            d = decs[:, :, None].expand(D, K, L)
         s = slots[:, :, None].expand(D, K, L)
         rows = self.rep_rows[s, t, d]  # [D, K, L, 10, 48]
         act = self.rep_act[s, t, d].to(dev)
@@ -240,15 +260,43 @@ class BatchedACER(BatchedPUCT):
         tab = torch.tensor(seqs, dtype=torch.long, device=dev)  # [S, 2]
         return tab[pick, 0], tab[pick, 1]
 
+    # ------------------------------------------------------------ tournament mode (decision lists)
+    def league_batches(self, chunk):
+        """(slots, chunk ids, decider indices) of the on-policy batch (every
+        seat of the newest episode: its sequence `chunk`) and the off-policy
+        batch (`minibatch` stored sequences per seat, uniform over every
+        stored (slot, chunk, seat) of this agent)"""
+        dev = self.env.device
+        s_new = (self.episodes - 1) % self.capacity
+        Dn = self.rep_nd[s_new]
+        on = (torch.full((Dn, 1), s_new, dtype=torch.long, device=dev),
+              torch.full((Dn, 1), chunk, dtype=torch.long, device=dev),
+              torch.arange(Dn, device=dev)[:, None])
+        tab = []
+        for sl, c in self.stored_sequences(chunk):
+            nd = self.rep_nd[sl]
+            tab.append(torch.stack((torch.full((nd,), sl), torch.full((nd,), c), torch.arange(nd)), dim=1))
+        tab = torch.cat(tab, dim=0).to(dev)
+        pick = torch.randint(0, tab.shape[0], (Dn, self.minibatch), generator=self._gen, device=dev)
+        off = (tab[pick, 0], tab[pick, 1], tab[pick, 2])
+        return on, off
+
+    def stored_count(self, upto_chunk):
+        """sequences stored (tournament mode: over every seat of every stored episode)"""
+        if self.dec is None:
+            return len(self.stored_sequences(upto_chunk))
+        return sum(self.rep_nd[sl] for sl, _ in self.stored_sequences(upto_chunk))
+
     def learn(self, optimizer):
         """the reference's update schedule for the episode just played: per
         flushed sequence, if more than max(warmup, minibatch) are stored, one
         on-policy and one off-policy Adam step (actor_critic.py:146-151)"""
         done_updates = []
         for c in range(len(self.chunks())):
-            if len(self.stored_sequences(c)) <= max(self.warmup, self.minibatch):
+            if self.stored_count(c) <= max(self.warmup, self.minibatch):
                 continue
-            for batch in (self.on_policy_batch(c), self.off_policy_batch(c)):
+            batches = self.league_batches(c) if self.dec is not None else (self.on_policy_batch(c), self.off_policy_batch(c))
+            for batch in batches:
                 total, actor, corr, critic = self.loss(*batch)
                 optimizer.zero_grad()
                 total.backward()

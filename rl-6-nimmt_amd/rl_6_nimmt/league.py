@@ -3,38 +3,77 @@
 Reference: Tournament (rl_6_nimmt/tournament.py:12-262) -- `play_game()`
 draws the seats (`_choose_players`, :166-177), plays one GameSession game
 (:132-138) and scores it (`score_game`, :140-164: relative positions, first-
-argmax winner, order-dependent multiplayer Elo).
+argmax winner, order-dependent multiplayer Elo); `evolve` / `copy_player`
+(:54-130) clone and prune the roster between games.
 
 Here every slot g of a tournament handle (`sn_league_config`) is one
 reference tournament stream: slot g replays
 
     np.random.seed(seed + game_offset + g)
-    t = Tournament(min_players, max_players); t.add_player(name, DrunkHamster()) ...
+    t = Tournament(min_players, max_players); t.add_player(name, agent) ...
     t.play_game()  # x games
 
-bit for bit -- seat draw, deal and every move come from the slot's own
-numpy MT19937 stream inside the k_play kernel (tests/golden/
-tournament_games.json pins it).  All slots play at once; the games of all
-slots (and, over RCCL, of all ranks) form one tournament whose scoring is
-per game (vectorised here on the device) and whose Elo -- the only
-order-dependent part -- is replayed on the host in a canonical order: game
-round major, then global slot id (`sn_elo_replay`, C++; multi_elo parity
-unpinned, elo.py).
+All slots play at once; the games of all slots (and, over RCCL, of all
+ranks) form one tournament whose scoring is per game (vectorised on the
+device) and whose Elo -- the only order-dependent part -- is replayed on the
+host in a canonical order: game round major, then global slot id
+(`sn_elo_replay`, C++; multi_elo parity unpinned, elo.py).
 
-Agents are the reference's DrunkHamster (played in-kernel); a search agent
-(MCSAgent, PUCTAgent, ...) in a league plays through the drop-in
-`Tournament` instead (host loop over the device env).
+Agents (the pool of run.py:20-40):
+  * DrunkHamster -- drawn in-kernel from the slot's numpy stream;
+  * MCSAgent -- card memory + the reference-exact search on the slot's
+    stream (sn_league_step), so a league of DrunkHamster and MCSAgent seats
+    replays the reference's seeded Tournament bit for bit (golden F11);
+  * PUCTAgent / PolicyMCSAgent, PUCTCustomedAgent, BatchedACERAgent -- one
+    batched engine per agent (puct.BatchedPUCT / BatchedPUCTCustomed,
+    acer.BatchedACER) over the decision list of its seats in the slots'
+    current games (sn_puct.dec_list); the policy net runs on PyTorch-ROCm.
+    Their random draws are Philox, not torch's CPU generator (parity
+    unpinned, like the engines themselves), and they consume no numpy words
+    (the reference's _draw_env shuffles do), so a league with net agents is
+    the reference's in law, not draw for draw.
+All-DrunkHamster leagues play whole games per launch (sn_league_rollout,
+`fused`); every other league plays sn_reset (seat draw + deal) then 10
+sn_league_step launches per game round.
+
+Training (train=True, like run.py's agent.train()): after each round every
+net agent takes one Adam step on its loss summed over the round's games
+(the reference steps once per game: puct.py / acer.py document the batched
+losses).  Nets move to the tournament's device.
 """
+import copy
 import ctypes
+import io
+import logging
 
 import numpy as np
 import torch
 
 from . import _native as nat
-from .agents.random import DrunkHamster
 from .vec_env import VecSechsNimmtEnv
 
+logger = logging.getLogger(__name__)
+
 STAT_GAMES, STAT_SCORE, STAT_POSITION, STAT_WINS = range(4)
+KIND_RANDOM, KIND_MCS, KIND_PUCT, KIND_CUSTOMED, KIND_ACER = "random", "mcs", "puct", "customed", "acer"
+T_STEPS = 10
+
+
+def agent_kind(agent):
+    """the batched engine that plays `agent` (tournament.py seats any Agent)"""
+    from .agents import BatchedACERAgent, DrunkHamster, MCSAgent, PolicyMCSAgent, PUCTCustomedAgent
+
+    if isinstance(agent, PUCTCustomedAgent):
+        return KIND_CUSTOMED
+    if isinstance(agent, PolicyMCSAgent):  # PUCTAgent included
+        return KIND_PUCT
+    if isinstance(agent, MCSAgent):
+        return KIND_MCS
+    if isinstance(agent, BatchedACERAgent):
+        return KIND_ACER
+    if isinstance(agent, DrunkHamster):
+        return KIND_RANDOM
+    raise NotImplementedError(f"the batched tournament has no engine for {type(agent).__name__}")
 
 
 def decode_seats(words, max_players):
@@ -71,98 +110,341 @@ def winners(results, k):
 
 
 class BatchedTournament:
-    """A tournament of DrunkHamster agents played by `num_slots` concurrent
-    game slots on one GPU (one rank's shard: global slot ids game_offset ..
-    game_offset + num_slots - 1)."""
+    """A tournament played by `num_slots` concurrent game slots on one GPU
+    (one rank's shard: global slot ids game_offset .. game_offset + num_slots - 1)."""
 
     def __init__(self, num_slots, min_players=2, max_players=4, seed=0, game_offset=0, rng="numpy", device=None,
-                 elo_initial=1600, elo_k=32):
+                 elo_initial=1600, elo_k=32, net_dtype=torch.bfloat16, train=False, fused=True):
         assert 0 < min_players <= max_players
         self.num_slots, self.min_players, self.max_players = int(num_slots), int(min_players), int(max_players)
         self.seed, self.game_offset, self.rng, self.device = int(seed), int(game_offset), rng, device
         self.elo_initial, self.elo_k = float(elo_initial), float(elo_k)
-        self.names, self.agents = [], {}
+        self.net_dtype, self.train, self.fused = net_dtype, bool(train), bool(fused)
+        # the roster, in the reference's dict order (tournament.py:25-35)
+        self.names, self.agents, self.active, self.descendants, self.kinds = [], {}, {}, {}, {}
         self.env = None
-        self.records = []  # per play_games call: int32 [games, num_slots, 1 + max_players] on the device
+        self.mode = None  # "fused" (all DrunkHamster, sn_league_rollout) or "step" (sn_league_step)
+        self.engines = {}  # net agent name -> batched engine
+        self.records = []  # (int32 [games, slots, 1 + N] on the device, roster index of each active agent)
+        self.stats = np.zeros((0, 4), dtype=np.float64)  # per roster agent: games, score, position, wins
+        self.elos = np.zeros((0,), dtype=np.float64)     # current Elo per roster agent
+        self.total_games = 0
+        self._seen = 0  # records already folded into stats / elos
 
-    # ------------------------------------------------------------ roster (tournament.py:36-52)
+    # ------------------------------------------------------------ roster (tournament.py:36-76)
     def add_player(self, name, agent=None):
-        assert name not in self.agents and self.env is None, "add every player before the first game"
+        from .agents.random import DrunkHamster
+
+        assert name not in self.agents
+        if self.mode == "fused":
+            raise NotImplementedError("the fused all-DrunkHamster league has drawn its next seats already; add every "
+                                      "player before the first game (or use fused=False)")
         agent = DrunkHamster() if agent is None else agent
-        if type(agent) is not DrunkHamster:
-            raise NotImplementedError("the batched tournament plays DrunkHamster agents in-kernel; leagues with "
-                                      "search agents play through rl_6_nimmt.Tournament")
-        agent.__name__ = name
+        kind = agent_kind(agent)
+        agent.__name__ = name  # tournament.py:40
         self.names.append(name)
-        self.agents[name] = agent
+        self.agents[name], self.kinds[name] = agent, kind
+        self.active[name], self.descendants[name] = True, name
+        self.stats = np.concatenate((self.stats, np.zeros((1, 4))), axis=0)
+        self.elos = np.concatenate((self.elos, [self.elo_initial]))
+        if self.env is not None:
+            self._configure()
+
+    def copy_player(self, old_name, new_name):
+        """tournament.py:54-60: the clone inherits the tallies, Elo and family
+        (the reference round-trips the module through temp_model.pt)"""
+        self._fold()
+        try:
+            clone = copy.deepcopy(self.agents[old_name])
+        except Exception:
+            buf = io.BytesIO()
+            torch.save(self.agents[old_name], buf)
+            buf.seek(0)
+            clone = torch.load(buf, weights_only=False)  # our own object, serialised just above
+        i = self.names.index(old_name)
+        clone.__name__ = new_name
+        self.names.append(new_name)
+        self.agents[new_name], self.kinds[new_name] = clone, self.kinds[old_name]
+        self.active[new_name], self.descendants[new_name] = self.active[old_name], self.descendants[old_name]
+        self.stats = np.concatenate((self.stats, self.stats[i: i + 1]), axis=0)
+        self.elos = np.concatenate((self.elos, self.elos[i: i + 1]))
+
+    def remove_player(self, name, full_delete=False):
+        """tournament.py:62-76"""
+        self._fold()
+        if full_delete:
+            i = self.names.index(name)
+            self.names.pop(i)
+            for d in (self.agents, self.kinds, self.active, self.descendants):
+                del d[name]
+            self.stats = np.delete(self.stats, i, axis=0)
+            self.elos = np.delete(self.elos, i)
+            self.engines.pop(name, None)
+        else:
+            self.active[name] = False
+
+    def active_agents(self):
+        return [n for n in self.names if self.active[n]]
 
     def __len__(self):
-        return len(self.names)
+        return len(self.active_agents())
 
+    def evolve(self, copies=(2,), max_players=None, max_per_descendant=2, metric="elo"):
+        """tournament.py:78-130 on the batched tallies: rank the active agents
+        by `metric`, clone the top ones, prune past max_players / per family.
+        The next round's seats are drawn over the new active list."""
+        if self.mode == "fused":
+            raise NotImplementedError("evolve needs the per-game round (BatchedTournament(..., fused=False)): the fused "
+                                      "rollout draws each slot's next seats at the end of the game before")
+        self._fold()
+        s = self.stats
+        table = {"tournament_scores": (STAT_SCORE, True, True), "tournament_positions": (STAT_POSITION, False, True),
+                 "tournament_wins": (STAT_WINS, False, True), "elo": (None, True, False)}
+        if metric not in table:
+            raise NotImplementedError(metric)
+        col, reverse, use_mean = table[metric]
+
+        def key(name):
+            i = self.names.index(name)
+            if not use_mean:
+                return float(self.elos[i])  # the latest Elo (never empty)
+            g = s[i, STAT_GAMES]
+            return float(s[i, col] / g) if g > 0 else 0.0
+
+        ranking = sorted(self.active_agents(), key=key, reverse=reverse)
+        kept, per_family = 0, {}
+        for pos, name in enumerate(ranking):
+            fam = self.descendants[name]
+            per_family.setdefault(fam, 0)
+            if pos < len(copies):
+                n_copies = copies[pos]
+                logger.info(f"Copying player {name} into {n_copies} instances!")
+            elif max_players is not None and kept >= max_players:
+                n_copies = 0
+                logger.info(f"Removing player {name}")
+            elif max_per_descendant is not None and per_family[fam] >= max_per_descendant:
+                n_copies = 0
+                logger.info(f"Removing player {name}")
+            else:
+                n_copies = 1
+            for c in range(n_copies):
+                self.copy_player(name, f"{name}_{c}")
+            self.remove_player(name, full_delete=n_copies > 0)
+            kept += n_copies
+            per_family[fam] += n_copies
+        if self.env is not None:
+            self._configure()
+
+    # ------------------------------------------------------------ the handle
     def _start(self):
-        K = len(self.names)
+        K = len(self)
         assert K >= self.max_players, "tournament.py:170: len(self) >= num_players"
+        all_random = all(self.kinds[n] == KIND_RANDOM for n in self.active_agents())
+        self.mode = "fused" if (self.fused and all_random) else "step"
+        if self.mode == "step" and self.rng != "numpy":
+            raise NotImplementedError("mixed leagues play numpy-MT tournament streams (rng='numpy')")
         self.env = VecSechsNimmtEnv(self.num_slots, self.max_players, seed=self.seed, game_offset=self.game_offset,
                                     rng=self.rng, device=self.device)
-        nat.check(nat.lib().sn_league_config(self.env._h, K, self.min_players, self.max_players), "sn_league_config")
-        self.env.reset()  # every slot draws its first seats, then deals
+        self._configure()
+        if self.mode == "fused":
+            self.env.reset()  # every slot draws its first seats, then deals
+
+    def _configure(self):
+        """(re)configure the handle for the current active roster"""
+        act = self.active_agents()
+        K = len(act)
+        if K > 16:
+            raise NotImplementedError("a tournament handle seats at most 16 active agents")
+        L = nat.lib()
+        nat.check(L.sn_league_config(self.env._h, K, self.min_players, self.max_players), "sn_league_config")
+        kind_code = {KIND_RANDOM: nat.SN_AGENT_RANDOM, KIND_MCS: nat.SN_AGENT_MCS}
+        kinds = np.array([kind_code.get(self.kinds[n], nat.SN_AGENT_EXTERNAL) for n in act], dtype=np.int32)
+        mpc = np.array([getattr(self.agents[n], "mc_per_card", 10) for n in act], dtype=np.int32)
+        mmax = np.array([getattr(self.agents[n], "mc_max", 100) for n in act], dtype=np.int32)
+        P = ctypes.c_void_p
+        nat.check(L.sn_league_agents(self.env._h, P(kinds.ctypes.data), P(mpc.ctypes.data), P(mmax.ctypes.data)),
+                  "sn_league_agents")
+        self._ids = torch.tensor([self.names.index(n) for n in act], dtype=torch.long)
+        keep = {}
+        for n in act:
+            if self.kinds[n] in (KIND_PUCT, KIND_CUSTOMED, KIND_ACER):
+                keep[n] = self.engines.get(n) or self._engine(n)
+        self.engines = keep
+
+    def _engine(self, name):
+        """the batched engine of one net agent over this handle (decision-list mode)"""
+        from .acer import BatchedACER
+        from .puct import BatchedPUCT, BatchedPUCTCustomed
+
+        agent, kind, env = self.agents[name], self.kinds[name], self.env
+        agent.to(env.device)
+        agent.device = env.device
+        seed = (self.seed * 1000003 + self.names.index(name) * 7919 + self.game_offset) & (2**62 - 1)
+        B = self.num_slots
+        if kind == KIND_PUCT:
+            return BatchedPUCT(env, agent.actor, mc_per_card=agent.mc_per_card, mc_max=agent.mc_max,
+                               c_puct=getattr(agent, "c_puct", 2.0), seed=seed, puct_root=agent._puct_root,
+                               net_dtype=self.net_dtype, mcs_num_cards=agent.num_cards, max_decisions=B)
+        if kind == KIND_CUSTOMED:
+            return BatchedPUCTCustomed(env, agent.actor, net_dtype=self.net_dtype, seed=seed, max_decisions=B)
+        return BatchedACER(env, agent.actor_critic, net_dtype=self.net_dtype, seed=seed, gamma=agent.gamma,
+                           rollout_len=agent.rollout_len, minibatch=agent.batchsize, truncate=agent.truncate,
+                           warmup=agent.warmup, r_factor=agent.r_factor, critic_weight=agent.critic_weight,
+                           capacity=2, log_epsilon=agent.log_epsilon, max_decisions=B)
 
     # ------------------------------------------------------------ games (tournament.py:132-138)
     def play_games(self, games=1, rewards=False):
         """`games` tournament games per slot.  Returns the records int32
-        [games, num_slots, 1 + max_players]: seats word (k | agent(seat p)
-        << (4 + 4p)), then the results (GameSession.results[0], 0 past k);
-        with rewards=True also the per-step rewards [10 games, slots, N]."""
+        [games, num_slots, 1 + max_players]: seats word (k | active agent
+        index of seat p << (4 + 4p)), then the results (GameSession.results[0],
+        0 past k); with rewards=True also the per-step rewards [10 games, slots, N]."""
         if self.env is None:
             self._start()
         env = self.env
-        T = 10 * int(games)
-        rec = torch.empty((games, self.num_slots, 1 + self.max_players), dtype=torch.int32, device=env.device)
-        rew = torch.empty((T, self.num_slots, self.max_players), dtype=torch.int32, device=env.device) if rewards else None
-        nat.check(nat.lib().sn_league_rollout(env._h, T, nat.ptr(rew), None, None, None, 0, nat.ptr(rec), env._stream()),
-                  "sn_league_rollout")
-        self.records.append(rec)
+        if self.mode == "fused":
+            T = T_STEPS * int(games)
+            rec = torch.empty((games, self.num_slots, 1 + self.max_players), dtype=torch.int32, device=env.device)
+            rew = torch.empty((T, self.num_slots, self.max_players), dtype=torch.int32, device=env.device) if rewards else None
+            nat.check(nat.lib().sn_league_rollout(env._h, T, nat.ptr(rew), None, None, None, 0, nat.ptr(rec), env._stream()),
+                      "sn_league_rollout")
+        else:
+            recs, rews = [], []
+            for _ in range(int(games)):
+                r, w = self._round()
+                recs.append(r)
+                rews.append(w)
+            rec = torch.stack(recs, dim=0)
+            rew = torch.cat(rews, dim=0) if rewards else None
+        self.records.append((rec, self._ids.clone()))
+        self.total_games += int(games) * self.num_slots
         return (rec, rew) if rewards else rec
 
+    def _round(self):
+        """one game per slot: sn_reset (seat draw + deal), then 10 x [net
+        agents' engines on their seats -> sn_league_step]"""
+        env, L, st = self.env, nat.lib(), self.env._stream()
+        B, N, dev = self.num_slots, self.max_players, env.device
+        nat.check(L.sn_reset(env._h, None, st), "sn_reset")  # Tournament.play_game: seats, then the deal
+        if self.engines:
+            k, ids = self.seats()
+            flat = ids.reshape(-1)
+            act = self.active_agents()
+            for name, eng in self.engines.items():
+                eng.use_decisions(torch.nonzero(flat == act.index(name)).flatten())
+                eng.decisions = []
+        acts = torch.zeros((B, N), dtype=torch.int32, device=dev)
+        per_step = torch.zeros((T_STEPS, B, N), dtype=torch.int32, device=dev)
+        rec = torch.zeros((B, 1 + N), dtype=torch.int32, device=dev)
+        invalid = torch.empty((T_STEPS, B), dtype=torch.int32, device=dev)
+        status = torch.zeros((B,), dtype=torch.int32, device=dev)
+        flat_acts = acts.view(-1)
+        for t in range(T_STEPS):
+            n = T_STEPS - t
+            for name, eng in self.engines.items():
+                if eng.D == 0:
+                    continue
+                a = eng.decide(n, record=self.train)
+                idx = eng.dec.long()
+                flat_acts[idx] = a.reshape(-1)[idx]
+            nat.check(L.sn_league_step(env._h, nat.ptr(acts), nat.ptr(per_step[t]), None,
+                                       nat.ptr(rec) if t == T_STEPS - 1 else None, nat.ptr(invalid[t]),
+                                       nat.ptr(status), st), "sn_league_step")
+        bad = int((invalid >= 0).sum())
+        if bad:
+            raise RuntimeError(f"sn_league_step: {bad} illegal moves of the net agents' engines")
+        if int(status.sum()):
+            logger.warning("MCS: a legal move got no playout (the reference raises IndexError here, quirk Q6)")
+        if self.train:
+            self._learn(per_step)
+        return rec, per_step
+
+    def _learn(self, per_step):
+        """one Adam step per net agent on its loss over the round's games"""
+        from .acer import BatchedACER
+        from .puct import BatchedPUCTCustomed
+
+        for name, eng in self.engines.items():
+            agent = self.agents[name]
+            if agent.optimizer is None:
+                agent.train()
+            if isinstance(eng, BatchedACER):
+                if eng.D:
+                    eng.record_rewards(per_step)
+                    eng.learn(agent.optimizer)
+                continue
+            if eng.D == 0 or not eng.decisions:
+                continue
+            loss = eng.loss(per_step) if isinstance(eng, BatchedPUCTCustomed) else eng.policy_loss()
+            agent.optimizer.zero_grad()
+            loss.backward()
+            agent.optimizer.step()
+            eng.decisions = []
+
     def seats(self):
-        """(k [slots], agent ids [slots, max_players]) of every slot's next game"""
+        """(k [slots], active agent index [slots, max_players]) of every slot's current game"""
         out = torch.empty((self.num_slots,), dtype=torch.int32, device=self.env.device)
         nat.check(nat.lib().sn_league_seats(self.env._h, nat.ptr(out), self.env._stream()), "sn_league_seats")
         return decode_seats(out, self.max_players)
 
     # ------------------------------------------------------------ scoring (tournament.py:140-164)
+    def _fold(self):
+        """fold records not yet seen into the per-agent tallies and Elo (in
+        play order: the Elo is sequential, tournament.py:157-164)"""
+        while self._seen < len(self.records):
+            rec, ids = self.records[self._seen]
+            K = int(ids.numel())
+            s = league_agent_stats(rec, K, self.max_players).cpu().numpy()
+            np.add.at(self.stats, ids.numpy(), s)
+            sub = replay_league_elo(rec, K, self.max_players, 0.0, self.elo_k, initial=self.elos[ids.numpy()])
+            self.elos[ids.numpy()] = sub
+            self._seen += 1
+
     def all_records(self):
-        """every game played so far, [games, slots, 1 + N] (round major)"""
-        return torch.cat(self.records, dim=0) if self.records else torch.zeros(
+        """every game played so far, [games, slots, 1 + N] (round major;
+        seat ids index the active list of their round -- see records)"""
+        return torch.cat([r for r, _ in self.records], dim=0) if self.records else torch.zeros(
             (0, self.num_slots, 1 + self.max_players), dtype=torch.int32)
 
     def agent_stats(self, records=None):
-        """per-agent sums float64 [K, 4]: games played, score, relative position, wins"""
-        rec = self.all_records() if records is None else records
-        return league_agent_stats(rec, len(self.names), self.max_players)
+        """per-agent sums float64 [roster, 4]: games played, score, relative position, wins"""
+        if records is not None:
+            return league_agent_stats(records, len(self.names), self.max_players)
+        self._fold()
+        return torch.from_numpy(self.stats.copy())
 
     def replay_elo(self, records=None):
-        """Elo of every agent after replaying the games in canonical order
-        (round major, then global slot id) -- sn_elo_replay, host C++"""
-        rec = self.all_records() if records is None else records
-        return replay_league_elo(rec, len(self.names), self.max_players, self.elo_initial, self.elo_k)
+        """Elo of every roster agent after the games so far (round major, then
+        global slot id -- sn_elo_replay, host C++)"""
+        if records is not None:
+            return replay_league_elo(records, len(self.names), self.max_players, self.elo_initial, self.elo_k)
+        self._fold()
+        return self.elos.copy()
 
     def table(self, stats=None, elos=None):
         """the reference's tournament table (tournament.py:208-238) from the sums"""
         stats = self.agent_stats() if stats is None else stats
         elos = self.replay_elo() if elos is None else elos
-        s = stats.cpu().numpy()
+        s = stats.cpu().numpy() if hasattr(stats, "cpu") else np.asarray(stats)
         total = int(s[:, STAT_WINS].sum())  # one winner per game
         bar = "-----------------------------------------------------------------"
         out = [f"Tournament after {total} games:", bar,
                " Agent                | Games | Mean score | Win fraction |  ELO ", bar]
-        for i, name in enumerate(self.names):
+
+        def row(i, name):
             g = s[i, STAT_GAMES]
             score = f"{s[i, STAT_SCORE] / g:>5.2f}" if g else "-"
             wins = f"{s[i, STAT_WINS] / g:>5.2f}" if g else "-"
-            out.append(f" {name:>20s} | {int(g):>5} | {score:>10} | {wins:>12} | {elos[i]:>4.0f} ")
+            return f" {name:>20s} | {int(g):>5} | {score:>10} | {wins:>12} | {elos[i]:>4.0f} "
+
+        out += [row(i, n) for i, n in enumerate(self.names) if self.active[n]]
         out.append(bar)
+        out += [row(i, n) for i, n in enumerate(self.names) if not self.active[n]]
+        if out[-1] != bar:
+            out.append(bar)
         return "\n".join(out)
+
+    def __str__(self):
+        return self.table()
 
     def close(self):
         if self.env is not None:
@@ -189,10 +471,14 @@ def league_agent_stats(records, num_agents, max_players):
     return onehot.T @ vals.reshape(-1, 4)
 
 
-def replay_league_elo(records, num_agents, max_players, elo_initial=1600.0, elo_k=32.0):
-    """sn_elo_replay over records [..., 1 + max_players] in row order"""
+def replay_league_elo(records, num_agents, max_players, elo_initial=1600.0, elo_k=32.0, initial=None):
+    """sn_elo_replay over records [..., 1 + max_players] in row order
+    (starting from `initial` [num_agents] if given)"""
     rec = np.ascontiguousarray(records.reshape(-1, 1 + max_players).cpu().numpy(), dtype=np.int32)
-    elos = np.full(num_agents, float(elo_initial), dtype=np.float64)
+    if initial is None:
+        elos = np.full(num_agents, float(elo_initial), dtype=np.float64)
+    else:
+        elos = np.ascontiguousarray(initial, dtype=np.float64).copy()
     nat.check(nat.lib().sn_elo_replay(rec.ctypes.data_as(ctypes.c_void_p), rec.shape[0], max_players, num_agents,
                                       float(elo_k), elos.ctypes.data_as(ctypes.c_void_p)), "sn_elo_replay")
     return elos

@@ -78,7 +78,7 @@ class FusedMLP:
 
 class BatchedPUCT:
     def __init__(self, env, actor, mc_per_card=10, mc_max=100, c_puct=2.0, seed=0, seats_mask=None, puct_root=True,
-                 net_dtype=torch.bfloat16, mcs_num_cards=104, graph=False):
+                 net_dtype=torch.bfloat16, mcs_num_cards=104, graph=False, max_decisions=None):
         # `actor` stays where the caller keeps it (the drop-in agents run it
         # on the host): inference uses a device copy in net_dtype (sync_net),
         # the training losses run on the actor's own device (actor_device).
@@ -92,7 +92,14 @@ class BatchedPUCT:
         self.seats_mask = ((1 << N) - 1) if seats_mask is None else int(seats_mask)
         self.M = bin(self.seats_mask & ((1 << N) - 1)).count("1")
         self.D = B * self.M
-        D = self.D
+        # tournament mode (max_decisions given): the deciding seats are a
+        # decision list (use_decisions: g * N + p of this agent's seats in the
+        # slots' current games), at most max_decisions of them
+        self.dec = None
+        if max_decisions is not None:
+            self.D = 0
+        self.D_max = B * self.M if max_decisions is None else int(max_decisions)
+        D = self.D_max
         self.avail = torch.zeros((4, B * N), dtype=torch.int32, device=dev)
         self.ro = torch.zeros((D, 48), dtype=torch.int32, device=dev)
         self.stats = torch.zeros((D, 24), dtype=torch.int32, device=dev)
@@ -109,7 +116,7 @@ class BatchedPUCT:
         # MLP, step)] launches) is captured once per (hand size, net version)
         # as a hipGraph (torch.cuda.CUDAGraph) and replayed for every
         # decision; the kernels read the decision counter from step_dev
-        self.graph = bool(graph)
+        self.graph = bool(graph) and max_decisions is None
         self._graphs = {}
         self._step_dev = torch.zeros((1,), dtype=torch.int32, device=dev)
 
@@ -137,8 +144,17 @@ class BatchedPUCT:
     def n_mc(self, n):
         return min(self.mc_max, self.mc_per_card * math.factorial(n))
 
+    def use_decisions(self, dec):
+        """tournament mode: the seats to decide for, int32 [D] = g * N + p on
+        the device (sn_puct.dec_list); a game of k players rolls out k seats"""
+        dec = torch.as_tensor(dec, device=self.env.device).to(torch.int32).contiguous()
+        assert dec.numel() <= self.D_max, "more decisions than max_decisions"
+        self.dec, self.D = dec, int(dec.numel())
+
     def _params(self, n, rollout=0, step_dev=False):
         q = nat.SnPuct()
+        if self.dec is not None:
+            q.dec_list, q.num_dec = self.dec.data_ptr(), self.D
         q.step_dev = self._step_dev.data_ptr() if step_dev else None
         q.seats_mask, q.n, q.puct_root, q.c_puct = self.seats_mask, n, int(self.puct_root), self.c_puct
         q.seed, q.step, q.rollout = self.seed & (2**64 - 1), self.step_id & 0xFFFFFFFF, rollout
@@ -157,6 +173,9 @@ class BatchedPUCT:
         L, h, st = nat.lib(), self.env._h, self.env._stream()
         if memorize:
             self.memorize()
+        if self.D == 0:  # tournament mode: this agent has no seat in any current game
+            self.step_id += 1
+            return self.actions
         bf16 = int(self.net_dtype == torch.bfloat16)
         q = self._params(n)
         if n > 1:
@@ -180,7 +199,7 @@ class BatchedPUCT:
         nat.check(L.sn_puct_choose(h, ctypes_ref(q), nat.ptr(self.actions), nat.ptr(self.best_index), st),
                   "sn_puct_choose")
         if record and n > 1:
-            self.decisions.append((self._train_rows(q, n, rows), n, self.best_index.clone()))
+            self.decisions.append((self._train_rows(q, n, rows), n, self.best_index[: self.D].clone()))
         self.step_id += 1
         return self.actions
 
@@ -200,13 +219,14 @@ class BatchedPUCT:
         bf16 = int(self.net_dtype == torch.bfloat16)
         N = self.env.num_players
         bufs = self._bufs(n)
+        views = {m: bufs[m][: self.D * N * m] for m in range(1, n + 1)}  # this batch's decisions
         for r in range(self.n_mc(n)):
             q.rollout = r
             nat.check(L.sn_puct_deal(h, ctypes_ref(q), st), "sn_puct_deal")
             for t in range(n):
                 m = n - t
-                nat.check(L.sn_puct_rows(h, ctypes_ref(q), m, nat.ptr(bufs[m]), bf16, st), "sn_puct_rows")
-                nat.check(L.sn_puct_step(h, ctypes_ref(q), nat.ptr(self._logits(bufs[m])), t, m, st), "sn_puct_step")
+                nat.check(L.sn_puct_rows(h, ctypes_ref(q), m, nat.ptr(views[m]), bf16, st), "sn_puct_rows")
+                nat.check(L.sn_puct_step(h, ctypes_ref(q), nat.ptr(self._logits(views[m])), t, m, st), "sn_puct_step")
 
     def _bufs(self, n):
         N = self.env.num_players
@@ -214,7 +234,7 @@ class BatchedPUCT:
             self._rowbufs = {}
         for m in range(1, n + 1):
             if m not in self._rowbufs:
-                self._rowbufs[m] = torch.empty((self.D * N * m, ROW), dtype=self.net_dtype, device=self.env.device)
+                self._rowbufs[m] = torch.empty((self.D_max * N * m, ROW), dtype=self.net_dtype, device=self.env.device)
         return self._rowbufs
 
     def _capture(self, n):
@@ -295,15 +315,19 @@ class BatchedPUCTCustomed(BatchedPUCT):
     play.py:29,57,72, so the last step's never reaches the agent); the batch
     loss is the sum over games (the reference steps Adam after every game)."""
 
-    def __init__(self, env, actor, seats_mask=None, net_dtype=torch.bfloat16, seed=0):
-        super().__init__(env, actor, seed=seed, seats_mask=seats_mask, puct_root=False, net_dtype=net_dtype)
-        D = self.D
+    def __init__(self, env, actor, seats_mask=None, net_dtype=torch.bfloat16, seed=0, max_decisions=None):
+        super().__init__(env, actor, seed=seed, seats_mask=seats_mask, puct_root=False, net_dtype=net_dtype,
+                         max_decisions=max_decisions)
+        D = self.D_max
         self.log_prob = torch.zeros((D,), dtype=torch.float32, device=env.device)
         self.value = torch.zeros((D,), dtype=torch.float32, device=env.device)
 
     def decide(self, n, memorize=False, record=False):
         """every deciding seat at hand size n; returns actions [B, N] int32"""
         L, h, st = nat.lib(), self.env._h, self.env._stream()
+        if self.D == 0:
+            self.step_id += 1
+            return self.actions
         bf16 = int(self.net_dtype == torch.bfloat16)
         q = self._params(n)
         self.sync_net()
@@ -316,7 +340,7 @@ class BatchedPUCTCustomed(BatchedPUCT):
         nat.check(L.sn_pcv_choose(h, ctypes_ref(q), nat.ptr(heads), nat.ptr(self.actions), nat.ptr(self.best_index),
                                   nat.ptr(self.log_prob), nat.ptr(self.value), st), "sn_pcv_choose")
         if record:
-            self.decisions.append((self._train_rows(q, n, rows), n, self.best_index.clone()))
+            self.decisions.append((self._train_rows(q, n, rows), n, self.best_index[: self.D].clone()))
         self.step_id += 1
         return self.actions
 
@@ -338,6 +362,8 @@ class BatchedPUCTCustomed(BatchedPUCT):
         return per_step.sum(dim=0), per_step
 
     def _decider_rewards(self, per_step):
+        if self.dec is not None:  # tournament mode: the decision list's seats
+            return per_step.reshape(per_step.shape[0], -1)[:, self.dec.long()]
         seats = [p for p in range(self.env.num_players) if (self.seats_mask >> p) & 1]
         return per_step[:, :, seats].reshape(per_step.shape[0], -1)  # [10, D] in decision order
 

@@ -92,20 +92,15 @@ LK, LN, LG = 5, 4, 3
 
 
 def _league_records(offset, count):
-    """synthetic league records [games, count, 1 + N] for global slots
-    offset.., a pure function of (round, global slot id) like the device's"""
-    rec = np.zeros((LG, count, 1 + LN), dtype=np.int32)
-    for e in range(LG):
-        for j in range(count):
-            rng = np.random.RandomState(1000 * e + offset + j)
-            k = int(rng.randint(2, LN + 1))
-            ids = rng.permutation(LK)[:k]
-            w = k
-            for p, a in enumerate(ids):
-                w |= int(a) << (4 + 4 * p)
-            rec[e, j, 0] = w
-            rec[e, j, 1: 1 + k] = -rng.randint(0, 12, size=k)
-    return torch.from_numpy(rec)
+    """this rank's league records, int32 [games, count, 1 + N] for global
+    slots offset.., in the device's format: the oracle's restatement of the
+    DrunkHamster tournament (oracle.league_records, pinned to the reference's
+    seeded tournaments by golden F11 in test_oracle_golden.py; the GPU
+    kernel equals it slot for slot, test_gpu_league.py) stands in for the
+    rank's device shard"""
+    from oracle import oracle as O
+
+    return torch.from_numpy(O.league_records(LK, 2, LN, seed=0, game_offset=offset, slots=count, games=LG))
 
 
 def _league_worker(rank, world, port, q):

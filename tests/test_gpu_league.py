@@ -95,3 +95,143 @@ def test_league_full_size_sharding_and_scoring_invariants(rng):
         assert t.env.pipe_errors() == 0 and t2.env.pipe_errors() == 0
     t.close()
     t2.close()
+
+
+def _mixed(B, specs, lo, hi, seed, game_offset=0, fused=False, train=False):
+    """a tournament over (name, agent) specs"""
+    from rl_6_nimmt.league import BatchedTournament
+
+    t = BatchedTournament(B, lo, hi, seed=seed, game_offset=game_offset, fused=fused, train=train)
+    for name, agent in specs:
+        t.add_player(name, agent)
+    return t
+
+
+def test_dropin_leagues_replay_reference_tournaments_batched():
+    """golden F11 "dropin" leagues (DrunkHamster + MCSAgent seats, seeded
+    reference Tournament.play_game x games): the batched tournament's slot 0
+    (sn_reset seat draw + deal, 10 sn_league_step launches per game, the MCS
+    seats' reference-exact search on the slot's stream) replays every seat
+    draw, result, relative position and winner, and the tallies"""
+    from rl_6_nimmt.agents import DrunkHamster, MCSAgent
+    from rl_6_nimmt.league import decode_seats, relative_positions, winners
+
+    for lg in load("tournament_games.json")["dropin"]:
+        specs = [(n, MCSAgent(mc_max=lg["mc_max"], mc_per_card=lg["mc_per_card"]) if c == "M" else DrunkHamster())
+                 for n, c in zip(lg["agents"], lg["kinds"])]
+        G, hi = len(lg["games"]), lg["max_players"]
+        t = _mixed(3, specs, lg["min_players"], hi, seed=lg["seed"])
+        assert t.mode == "step"
+        rec = t.play_games(G).cpu()
+        k, ids = decode_seats(rec[..., 0], hi)
+        res = rec[..., 1:]
+        rel, win = relative_positions(res, k), winners(res, k)
+        for e, g in enumerate(lg["games"]):
+            kk = len(g["names"])
+            assert int(k[e, 0]) == kk, (lg["kinds"], e)
+            assert [lg["agents"][i] for i in ids[e, 0, :kk].tolist()] == g["names"], (lg["kinds"], e)
+            assert res[e, 0, :kk].tolist() == g["results"], (lg["kinds"], e)
+            assert np.allclose(rel[e, 0, :kk].numpy(), g["relative"]), (lg["kinds"], e)
+            assert g["names"][int(win[e, 0])] == g["winner"]
+        # tallies of the slot-0 tournament (tournament.py:147-152)
+        st = t.agent_stats(rec[:, :1])
+        for i, n in enumerate(lg["agents"]):
+            ref = lg["tallies"][n]
+            assert int(st[i, 0]) == ref["played_games"], n
+            assert int(st[i, 1]) == sum(ref["scores"]), n
+            assert abs(float(st[i, 2]) - sum(ref["positions"])) < 1e-9, n
+            assert int(st[i, 3]) == int(sum(ref["wins"])), n
+        t.close()
+
+
+def test_league_step_mode_equals_fused_rollout():
+    """an all-DrunkHamster league played round by round (sn_reset +
+    sn_league_step) draws the same words in the same order as the fused
+    sn_league_rollout: identical records"""
+    B, K, lo, hi, G = 4096, 5, 2, 4, 3
+    t1 = _league(B, K, lo, hi, seed=11)
+    r1 = t1.play_games(G)
+    from rl_6_nimmt.agents import DrunkHamster
+
+    t2 = _mixed(B, [(f"a{i}", DrunkHamster()) for i in range(K)], lo, hi, seed=11, fused=False)
+    r2 = t2.play_games(1)
+    r2 = torch.cat((r2, t2.play_games(G - 1)), dim=0)
+    assert t1.mode == "fused" and t2.mode == "step"
+    assert torch.equal(r1, r2)
+    assert np.allclose(t1.replay_elo(), t2.replay_elo())
+    t1.close()
+    t2.close()
+
+
+def _run_py_pool(mc_max=200):
+    """run.py:24-27's league plus the random agent of its notebook stage"""
+    from rl_6_nimmt.agents import BatchedACERAgent, DrunkHamster, MCSAgent, PUCTAgent, PUCTCustomedAgent
+
+    torch.manual_seed(0)
+    return [("ACER", BatchedACERAgent(minibatch=10)), ("MCS", MCSAgent(mc_max=mc_max)),
+            ("Alpha0.5", PUCTAgent(mc_max=mc_max)), ("Alpha0.5_customed", PUCTCustomedAgent(mc_max=mc_max)),
+            ("Random", DrunkHamster())]
+
+
+def test_mixed_league_with_net_agents_plays_and_trains():
+    """a run.py-seated league (ACER, MCS, Alpha0.5, Alpha0.5_customed at
+    mc_max=200, plus Random) on 256 slots, training on: every move legal
+    (sn_league_step checks the engines' cards), records well formed, tallies
+    and Elo consistent, and every net agent's weights move"""
+    from rl_6_nimmt.league import decode_seats, relative_positions
+
+    specs = _run_py_pool(mc_max=20)
+    before = {n: [p.detach().clone() for p in a.parameters()] for n, a in specs if n not in ("MCS", "Random")}
+    for _, a in specs:
+        a.train()
+    B, lo, hi, G = 256, 2, 4, 2
+    t = _mixed(B, specs, lo, hi, seed=3, train=True)
+    rec = t.play_games(G)
+    k, ids = decode_seats(rec[..., 0], hi)
+    assert int(k.min()) >= lo and int(k.max()) <= hi and int(ids.max()) < len(specs)
+    valid = ids >= 0
+    res = rec[..., 1:]
+    assert int(res.max()) <= 0 and int((-res.sum(-1)).max()) <= 171 and not res[~valid].any()
+    assert torch.allclose(relative_positions(res, k).sum(-1), k.double() / 2)
+    st = t.agent_stats()
+    assert int(st[:, 0].sum()) == int(k.sum()) and int(st[:, 3].sum()) == G * B
+    assert all(st[i, 0] > 0 for i in range(len(specs)))
+    assert abs(t.replay_elo().sum() - len(specs) * 1600.0) < 1e-6
+    for n, ps in before.items():
+        now = list(t.agents[n].parameters())
+        assert any(not torch.equal(a.cpu(), b.cpu()) for a, b in zip(now, ps)), n
+    t.close()
+
+
+def test_mixed_league_evolve_reseats_the_new_roster():
+    """Tournament.evolve between rounds (tournament.py:78-130): clones join,
+    pruned agents leave, and the next round's seats come from the new active
+    list (seat ids index it)"""
+    from rl_6_nimmt.agents import DrunkHamster, MCSAgent
+    from rl_6_nimmt.league import decode_seats
+
+    specs = [("R0", DrunkHamster()), ("M", MCSAgent(mc_max=20)), ("R1", DrunkHamster()), ("R2", DrunkHamster())]
+    t = _mixed(512, specs, 2, 4, seed=5)
+    t.play_games(1)
+    t.evolve(copies=(2,), max_players=4, max_per_descendant=2, metric="tournament_scores")
+    act = t.active_agents()
+    assert len(act) == 4 and len(t.names) == 5  # best x2, two more x1, the worst deactivated (max_players)
+    rec = t.play_games(1)
+    k, ids = decode_seats(rec[..., 0], 4)
+    assert int(ids.max()) == len(act) - 1  # 512 slots: every active agent is seated somewhere
+    st = t.agent_stats()
+    assert int(st[:, 0].sum()) >= int(k.sum())
+    t.close()
+
+
+def test_league_records_equal_oracle_shards():
+    """the device's records of a rank's shard (game_offset) equal the
+    oracle's tournament restatement -- what the 2-rank gloo test
+    (test_distributed_cpu.py) gathers in place of device records"""
+    from oracle import oracle as O
+
+    for off in (0, 96):
+        t = _league(96, 5, 2, 4, seed=0, game_offset=off)
+        rec = t.play_games(3).cpu().numpy()
+        assert np.array_equal(rec, O.league_records(5, 2, 4, seed=0, game_offset=off, slots=96, games=3))
+        t.close()

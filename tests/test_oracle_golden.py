@@ -178,3 +178,22 @@ def test_mcs_games_reference_exact():
         assert a.tolist() == g["actions"], (g["seats"], g["seed"])
         assert r.tolist() == g["rewards"]
         assert r.sum(axis=0).tolist() == g["results"]
+
+
+def test_league_records_replay_reference_tournaments():
+    """golden F11 "league": seeded reference Tournament(lo, hi) over K
+    DrunkHamster agents -- oracle.league_records (the device's record format)
+    reproduces every seat draw and result"""
+    groups = {}
+    for r in load("tournament_games.json")["league"]:
+        groups.setdefault((r["num_agents"], r["min_players"], r["max_players"]), []).append(r)
+    for (K, lo, hi), recs in groups.items():
+        base, G = recs[0]["seed"], len(recs[0]["results"])
+        out = O.league_records(K, lo, hi, seed=base, slots=len(recs), games=G)
+        for j, r in enumerate(recs):
+            for e in range(G):
+                seats, res = r["seats"][e], r["results"][e]
+                w = int(out[e, j, 0])
+                assert w & 15 == len(seats)
+                assert [(w >> (4 + 4 * p)) & 15 for p in range(len(seats))] == seats
+                assert out[e, j, 1: 1 + len(seats)].tolist() == res
