@@ -68,7 +68,9 @@ def parse():
     ap.add_argument("--rng", default="numpy", choices=["numpy", "philox"])
     ap.add_argument("--no-obs", action="store_true", help="do not emit observations (not the headline)")
     ap.add_argument("--pipe-gpw", type=int, default=64, choices=[32, 64], help="games per k_play wave (pipelined path)")
-    ap.add_argument("--play-split", type=int, default=None, choices=[0, 1, 2, 3, 4],
+    ap.add_argument("--pipe-decode", type=int, default=None, choices=[0, 1],
+                    help="SN_OPT_PIPE_DECODE: draws decoded in the twist-ahead (default: the library's)")
+    ap.add_argument("--play-split", type=int, default=None, choices=[0, 1],
                     help="SN_OPT_PLAY_SPLIT (default: the library's)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
@@ -80,6 +82,12 @@ def parse():
     ap.add_argument("--no-league", action="store_true", help="skip the config-5 batched tournament leg")
     ap.add_argument("--no-scalar", action="store_true", help="skip the config-1 scalar drop-in leg")
     ap.add_argument("--league-rounds", type=int, default=10, help="timed tournament games per slot (config 5)")
+    ap.add_argument("--no-mixed-league", action="store_true", help="skip the run.py-seated config-5 league leg")
+    ap.add_argument("--mixed-slots", type=int, default=65536, help="tournament slots per GPU of the run.py league")
+    ap.add_argument("--mixed-mc-max", type=int, default=200, help="mc_max of the run.py league's search agents")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in GameSession / Tournament search legs")
+    ap.add_argument("--only", default="", help="comma list of legs to run (headline,cpu,mcs,puct,scalar,league,"
+                                             "mixed,dropin,philox); empty = all")
     ap.add_argument("--puct-games", type=int, default=8192)
     return ap.parse_args()
 
@@ -436,6 +444,163 @@ def bench_league(world, rank, slots, rounds, warmup=2, K=5, lo=2, hi=4):
     return out
 
 
+def run_py_league(mc_max=200, with_random=True):
+    """the agents of run.py:24-27 (ACER minibatch 10, MCS / Alpha0.5 /
+    Alpha0.5_customed at mc_max), all .train() as run.py:29-33 does, plus the
+    DrunkHamster of the notebook's league (simple_tournament.ipynb)"""
+    from rl_6_nimmt.agents import BatchedACERAgent, DrunkHamster, MCSAgent, PUCTAgent, PUCTCustomedAgent
+
+    torch.manual_seed(0)
+    agents = [("ACER", BatchedACERAgent(minibatch=10)), ("MCS", MCSAgent(mc_max=mc_max)),
+              ("Alpha0.5", PUCTAgent(mc_max=mc_max)), ("Alpha0.5_customed", PUCTCustomedAgent(mc_max=mc_max))]
+    if with_random:
+        agents.append(("Random", DrunkHamster()))
+    for _, a in agents:
+        try:  # run.py:29-33: agents without parameters have no optimizer
+            a.train()
+        except ValueError:
+            pass
+    return agents
+
+
+def bench_league_mixed(world, rank, slots, mc_max=200, rounds=1, warmup=1):
+    """BASELINE config 5 with the reference's real league (run.py:20-40):
+    ACER, MCS, Alpha0.5 (PUCT) and Alpha0.5_customed at mc_max=200 plus
+    Random, Tournament(2, 4), training on, `slots` concurrent tournament games
+    per GPU (slot g = np.random.seed(g) stream: seat draws, deals, Random and
+    MCS seats in-kernel; the net agents' batched engines over their seats).
+    Timed: `rounds` game rounds on every rank (each: every slot plays one
+    whole game, then every net agent's batched update), then the RCCL
+    gather of the per-agent sums and every game record + the rank-0 Elo
+    replay."""
+    import torch.distributed as dist
+
+    from rl_6_nimmt.distributed import gather_league_records, reduce_agent_stats
+    from rl_6_nimmt.league import BatchedTournament, replay_league_elo
+
+    # warm-up on a small league of the same agents (kernels, GEMM heuristics,
+    # optimizer state): a round at full size costs as much as the timed one
+    specs = run_py_league(mc_max)
+    w = BatchedTournament(min(slots, 1024), 2, 4, seed=0, game_offset=(1 << 30) + rank * slots, rng="numpy", train=True)
+    for name, agent in specs:
+        w.add_player(name, agent)
+    for _ in range(warmup):
+        w.play_games(1)
+    w.agent_stats()
+    w.close()
+    specs = run_py_league(mc_max)
+    t = BatchedTournament(slots, 2, 4, seed=0, game_offset=rank * slots, rng="numpy", train=True)
+    for name, agent in specs:
+        t.add_player(name, agent)
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    rec0 = len(t.records)
+    t0 = time.perf_counter()
+    for _ in range(rounds):
+        t.play_games(1)
+    torch.cuda.synchronize()
+    barrier(world)
+    wall = time.perf_counter() - t0
+    rows = {n: e.rows_evaluated for n, e in t.engines.items()}  # the timed rounds only: a fresh league
+    tg = time.perf_counter()
+    recs = torch.cat([r for r, _ in t.records[rec0:]], dim=0)
+    K = len(specs)
+    from rl_6_nimmt.league import league_agent_stats
+
+    stats = reduce_agent_stats(league_agent_stats(recs, K, 4))
+    allrec = gather_league_records(recs)
+    torch.cuda.synchronize()
+    gather_ms = (time.perf_counter() - tg) * 1e3
+    if world > 1:
+        w = torch.tensor([wall, gather_ms], dtype=torch.float64, device=t.env.device)
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        wall, gather_ms = float(w[0].item()), float(w[1].item())
+    out = None
+    if rank == 0:
+        te = time.perf_counter()
+        elos = replay_league_elo(allrec, K, 4)
+        elo_ms = (time.perf_counter() - te) * 1e3
+        s = stats.cpu().numpy()
+        games = world * slots * rounds
+        out = {
+            "workload": f"config5 (run.py league): tournament.py self-play, {world} x {slots} concurrent game slots, "
+                        f"agents ACER(minibatch=10), MCS, Alpha0.5 (PUCT), Alpha0.5_customed at mc_max={mc_max} + "
+                        f"Random, 2..4 players drawn per game, training on (one batched Adam step per net agent per "
+                        f"round); numpy-MT slot streams (slot g = np.random.seed(g)); {rounds} timed round(s)",
+            "value": games * STEPS_PER_LAUNCH / wall,
+            "unit": "env-steps/s",
+            "games_per_s": games / wall,
+            "s_per_round": wall / rounds,
+            "concurrent_games": world * slots,
+            "reference_s_per_game": [21.47, 46.95],
+            "reference_source": "experiments/simple_tournament.ipynb:158-410 tqdm logs (CPU, one game at a time)",
+            "policy_rows_per_round": {n: r / rounds for n, r in rows.items()},
+            "score_gather_ms": gather_ms,
+            "score_gather": f"RCCL all_reduce of [{K}, 4] per-agent sums + all_gather of {games} game records"
+                            if world > 1 else "single rank (no collective)",
+            "elo_replay_ms": elo_ms,
+            "agents": {n: {"games": int(s[i, 0]), "mean_score": s[i, 1] / max(1, s[i, 0]),
+                           "win_fraction": s[i, 3] / max(1, s[i, 0]), "elo": float(elos[i])}
+                       for i, (n, _) in enumerate(specs)},
+        }
+    t.close()
+    return out
+
+
+def bench_dropin(mcs_games=3, puct_games=2, tour_games=3, mc_max_tour=200):
+    """The drop-in search path a reference user runs: s per
+    game of GameSession(MCSAgent(), DrunkHamster() x 3) and GameSession(
+    PUCTAgent() [training], DrunkHamster() x 3) -- SURVEY §6's cProfile setups,
+    1.06-1.89 s and 11.6-14.7 s per game on this image's CPU -- and of a
+    Tournament(2, 4) seated like run.py (the notebook's 21-47 s per game).
+    One game at a time, the search on the GPU (reference-exact MCS lane,
+    batched PUCT over one decision)."""
+    from rl_6_nimmt import GameSession, Tournament
+    from rl_6_nimmt.agents import DrunkHamster, MCSAgent, PUCTAgent
+
+    def per_game(sess, n):
+        np.random.seed(0)
+        sess.play_game()  # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for g in range(n):
+            np.random.seed(g + 1)
+            sess.play_game()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / n
+
+    out = {}
+    out["mcs_3random_s_per_game"] = per_game(GameSession(MCSAgent(), DrunkHamster(), DrunkHamster(), DrunkHamster()),
+                                             mcs_games)
+    out["mcs_reference_s_per_game"] = [1.06, 1.89]
+    torch.manual_seed(0)
+    puct = PUCTAgent()
+    puct.train()
+    out["puct_train_3random_s_per_game"] = per_game(GameSession(puct, DrunkHamster(), DrunkHamster(), DrunkHamster()),
+                                                    puct_games)
+    out["puct_reference_s_per_game"] = [11.6, 14.7]
+    tour = Tournament(min_players=2, max_players=4)
+    for name, agent in run_py_league(mc_max_tour, with_random=False):
+        tour.add_player(name, agent)
+    np.random.seed(0)
+    tour.play_game()  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(tour_games):
+        tour.play_game()
+    torch.cuda.synchronize()
+    out["run_py_tournament_s_per_game"] = (time.perf_counter() - t0) / tour_games
+    out["tournament_reference_s_per_game"] = [21.47, 46.95]
+    out["workload"] = (f"drop-in (one game at a time, host loop over the one-game device env): GameSession(MCSAgent() "
+                       f"[mc_max 100], DrunkHamster x3) x {mcs_games}, GameSession(PUCTAgent() [mc_max 100, training], "
+                       f"DrunkHamster x3) x {puct_games}, Tournament(2, 4) of run.py's agents at mc_max={mc_max_tour} "
+                       f"(training) x {tour_games} games")
+    out["reference_source"] = ("SURVEY.md §6 cProfile runs of the reference on this image's CPU (MCS, PUCT) and "
+                               "experiments/simple_tournament.ipynb:158-410 (tournament)")
+    return out
+
+
 def bench_scalar(games=200, step_games=200):
     """BASELINE config 1 through the scalar drop-in (rl_6_nimmt.GameSession /
     SechsNimmtEnv on a one-game device handle, sn_step1 / sn_reset1): ms per
@@ -566,12 +731,30 @@ def pmc_traffic(rng, games):
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
+    legs = set(x for x in args.only.split(",") if x)
+
+    def want(leg):
+        return not legs or leg in legs
+
+    if legs and "headline" not in legs:  # profiling runs of single legs (tools/), not the driver's line
+        result = {"legs": sorted(legs)}
+        if want("mixed"):
+            result["extra_config5_run_py_league"] = bench_league_mixed(world, rank, args.mixed_slots, args.mixed_mc_max)
+        if want("dropin"):
+            result["extra_dropin_search"] = bench_dropin()
+        if want("puct"):
+            result["extra_config4_puct"] = bench_puct(args.puct_games)
+        if want("mcs"):
+            result["extra_config3_mcs"] = bench_mcs(args.mcs_games, args.mcs_rollouts)
+        if rank == 0:
+            print(json.dumps(result), flush=True)
+        return
     from rl_6_nimmt.vec_env import VecSechsNimmtEnv
 
     B = args.games
     env = VecSechsNimmtEnv(B, N_PLAYERS, seed=0, game_offset=rank * B, rng=args.rng)
     if args.rng == "numpy":
-        env.set_option(pipe_gpw=args.pipe_gpw, play_split=args.play_split)
+        env.set_option(pipe_gpw=args.pipe_gpw, play_split=args.play_split, pipe_decode=args.pipe_decode)
     env.reset()
     out = make_out(env, B, not args.no_obs)
     wall, kern_ms, kt = time_rollouts(env, out, args.steps, args.warmup, world)
@@ -677,6 +860,12 @@ def main():
         league = bench_league(world, rank, B, args.league_rounds)
         if rank == 0:
             result["extra_config5_tournament"] = league
+    if not args.no_mixed_league:
+        mixed = bench_league_mixed(world, rank, args.mixed_slots, args.mixed_mc_max)
+        if rank == 0:
+            result["extra_config5_run_py_league"] = mixed
+    if world == 1 and not args.no_dropin:
+        result["extra_dropin_search"] = bench_dropin()
     if world == 1 and not args.no_philox and args.rng == "numpy":
         # config 2 in the counter-based mode ("philox ... used for
         # throughput"): same games-per-launch, role-split k_play (SN_OPT_PLAY_SPLIT 1)

@@ -121,8 +121,8 @@ def test_dropin_leagues_replay_reference_tournaments_batched():
                  for n, c in zip(lg["agents"], lg["kinds"])]
         G, hi = len(lg["games"]), lg["max_players"]
         t = _mixed(3, specs, lg["min_players"], hi, seed=lg["seed"])
-        assert t.mode == "step"
         rec = t.play_games(G).cpu()
+        assert t.mode == "step"
         k, ids = decode_seats(rec[..., 0], hi)
         res = rec[..., 1:]
         rel, win = relative_positions(res, k), winners(res, k)
@@ -139,7 +139,7 @@ def test_dropin_leagues_replay_reference_tournaments_batched():
             ref = lg["tallies"][n]
             assert int(st[i, 0]) == ref["played_games"], n
             assert int(st[i, 1]) == sum(ref["scores"]), n
-            assert abs(float(st[i, 2]) - sum(ref["positions"])) < 1e-9, n
+            assert abs(float(st[i, 2]) - sum(ref["positions"])) < 1e-6, n  # the reference's positions are float32
             assert int(st[i, 3]) == int(sum(ref["wins"])), n
         t.close()
 
@@ -182,8 +182,9 @@ def test_mixed_league_with_net_agents_plays_and_trains():
 
     specs = _run_py_pool(mc_max=20)
     before = {n: [p.detach().clone() for p in a.parameters()] for n, a in specs if n not in ("MCS", "Random")}
-    for _, a in specs:
-        a.train()
+    for n, a in specs:
+        if n not in ("MCS", "Random"):  # run.py:29-33 (its try/except skips the parameter-free agents)
+            a.train()
     B, lo, hi, G = 256, 2, 4, 2
     t = _mixed(B, specs, lo, hi, seed=3, train=True)
     rec = t.play_games(G)
