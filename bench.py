@@ -746,6 +746,8 @@ def main():
             result["extra_config4_puct"] = bench_puct(args.puct_games)
         if want("mcs"):
             result["extra_config3_mcs"] = bench_mcs(args.mcs_games, args.mcs_rollouts)
+        if want("scalar"):
+            result["extra_config1_scalar"] = bench_scalar()
         if rank == 0:
             print(json.dumps(result), flush=True)
         return

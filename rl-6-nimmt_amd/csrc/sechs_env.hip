@@ -987,33 +987,134 @@ __global__ void k_step1(DevState s, Acts1 acts, uint32_t* hb, int summ) {
     out1_game<N>(s, G, out, summ);
 }
 
+// sn_reset1, one wave: numpy's (key, pos) arrives in pinned words and is
+// imported by all 64 lanes at once into LDS; the 103 Fisher-Yates targets of
+// env.py:99-112 (np.random.shuffle: j = random_interval(i), i = C-1 .. 1,
+// masked rejection) are decoded 64 stream words per instruction -- a word's
+// draw index is its prefix count of accepted words, iterated acceptance ->
+// ballot -> v_mbcnt to the fixed point -- with whole 624-word blocks twisted
+// in LDS when the stream crosses one (as numpy does); one lane then applies
+// the swaps and deals.  The state goes back in numpy's own form (the block
+// holding the consumer + pos), so the host converts nothing.
 template <int N>
 __global__ __launch_bounds__(64) void k_reset1(DevState s, uint32_t* hb, int summ) {
+    constexpr uint32_t D = kMtN - kMtM;  // 227
+    __shared__ uint32_t blk[2 * kMtN];   // the consumer's block, then the next one
     __shared__ __attribute__((aligned(16))) uint8_t slot[kDealStride];
-    const int t = threadIdx.x;
-    for (int i = t; i < kMtN; i += 64) s.mt[i] = hb[kH1In + i];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t C = (uint32_t)s.C, C1 = C - 1u;
+    PhaseProf prof;  // libsechs_prof.so only: import / twist / decode / shuffle / deal / out (tools/reset1_prof.py)
+    prof.start();
+    uint32_t kv[(kMtN + 63) / 64];
+#pragma unroll
+    for (int q = 0; q < (kMtN + 63) / 64; q++) {  // every lane's host loads in flight at once
+        const uint32_t i = 64u * q + lane;
+        kv[q] = (i < (uint32_t)kMtN) ? hb[kH1In + i] : 0u;
+    }
+    const uint32_t pos = __builtin_amdgcn_readfirstlane(hb[kH1In + kMtN]);
+#pragma unroll
+    for (int q = 0; q < (kMtN + 63) / 64; q++) {
+        const uint32_t i = 64u * q + lane;
+        if (i < (uint32_t)kMtN) blk[i] = kv[q];
+    }
+    for (uint32_t i = lane; i < C; i += 64u) slot[i] = (uint8_t)i;  // the ordered deck (np.arange)
     __syncthreads();
-    if (t == 0) {
-        s.mt_pos[0] = mt_code_from_numpy((int)hb[kH1In + kMtN]);
+    prof.mark(PR_DRAWS);
+    // numpy's twist of blk[0, 624) into blk[624, 1248), in its own order:
+    // word j reads old j, j + 1 and j + 397 (j < 227) or new j - 227
+    auto twist_next = [&]() {
+        for (uint32_t j = lane; j < D; j += 64u) blk[kMtN + j] = mt_mix(blk[j], blk[j + 1u], blk[j + kMtM]);
+        __syncthreads();
+        for (uint32_t j = D + lane; j < 2u * D; j += 64u) blk[kMtN + j] = mt_mix(blk[j], blk[j + 1u], blk[kMtN + j - D]);
+        __syncthreads();
+        for (uint32_t j = 2u * D + lane; j < (uint32_t)kMtN - 1u; j += 64u)
+            blk[kMtN + j] = mt_mix(blk[j], blk[j + 1u], blk[kMtN + j - D]);
+        __syncthreads();
+        if (lane == 0u) blk[2 * kMtN - 1] = mt_mix(blk[kMtN - 1], blk[kMtN], blk[kMtN + kMtN - 1 - D]);
+        __syncthreads();
+    };
+    uint32_t dw = pos, o0 = 0u, avail = (uint32_t)kMtN;  // word cursor (from blk[0]), draws done, words in blk
+    uint8_t* jslot = slot + kDeckStride;
+    while (o0 < C1) {
+        while (dw + 64u > avail) {  // the next 64 words: twist (a third block: slide the window first)
+            if (avail == 2u * kMtN) {
+                uint32_t t[(kMtN + 63) / 64];
+#pragma unroll
+                for (int q = 0; q < (kMtN + 63) / 64; q++) {
+                    const uint32_t i = 64u * q + lane;
+                    t[q] = (i < (uint32_t)kMtN) ? blk[kMtN + i] : 0u;
+                }
+                __syncthreads();
+#pragma unroll
+                for (int q = 0; q < (kMtN + 63) / 64; q++) {
+                    const uint32_t i = 64u * q + lane;
+                    if (i < (uint32_t)kMtN) blk[i] = t[q];
+                }
+                __syncthreads();
+                dw -= kMtN;
+            }
+            prof.mark(PR_TARGETS);
+            twist_next();
+            prof.mark(PR_SPARE);
+            avail = 2u * kMtN;
+        }
+        const uint32_t x = mt_temper(blk[dw + lane]) & 0xFFu;
+        auto eval = [&](uint32_t pre, uint32_t& m) -> bool {
+            const uint32_t o = o0 + pre;
+            m = (o < C1) ? C1 - o : 1u;  // step o shuffles position i = C-1-o: random_interval(i)
+            return o < C1 && (x & (0xFFFFFFFFu >> __builtin_clz(m))) <= m;
+        };
+        uint32_t m;
+        uint64_t Acc = __ballot(eval((lane * 3u) >> 2, m));
+        while (true) {
+            const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(Acc >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)Acc, 0u));
+            const uint64_t A2 = __ballot(eval(pre, m));
+            if (A2 == Acc) break;
+            Acc = A2;
+        }
+        const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(Acc >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)Acc, 0u));
+        if ((Acc >> lane) & 1ull) {
+            (void)eval(pre, m);
+            jslot[o0 + pre] = (uint8_t)(x & (0xFFFFFFFFu >> __builtin_clz(m)));
+        }
+        const uint32_t na = (uint32_t)__popcll(Acc);
+        if (o0 + na >= C1) {  // the last draw is in this batch: the consumer stops past its word
+            dw += 64u - (uint32_t)__builtin_clzll(Acc);
+            break;
+        }
+        o0 += na;
+        dw += 64u;
+    }
+    __syncthreads();
+    prof.mark(PR_TARGETS);
+    // numpy's state after the deal: the block holding the consumer, pos in 1..624
+    const uint32_t b0 = (dw > (uint32_t)kMtN) ? (uint32_t)kMtN : 0u, npos = dw - b0;
+    for (uint32_t i = lane; i < (uint32_t)kMtN; i += 64u) {
+        const uint32_t v = blk[b0 + i];
+        s.mt[i] = v;
+        hb[kH1Mt + i] = v;
+    }
+    if (lane == 0u) {
+        prof.mark(PR_STORE);
+        shuffle_apply(slot, jslot, (int)C);
+        prof.mark(PR_APPLY);
         Game<N> G;
-        typename RngOf<RNG_NUMPY_MT>::T rng;
-        ByteBuf buf;
-        RngOf<RNG_NUMPY_MT>::load(s, 0, rng, buf);
-        deck_shuffle2(rng, buf, slot, s.C);
-        deal_from_deck<N>(slot, s.C, G);
-        RngOf<RNG_NUMPY_MT>::store(s, 0, rng, buf);
+        deal_from_deck<N>(slot, (int)C, G);
+        prof.mark(PR_HANDS);
         store_game<N>(s, 0, G);
+        const uint32_t code = mt_code_from_numpy((int)npos);
+        s.mt_pos[0] = code;
         uint32_t* out = hb + kH1Out;
         out[0] = 0xFFFFFFFFu;
         out[1] = 0u;
 #pragma unroll
         for (int p = 0; p < N; p++) out[2 + p] = 0u;
         out1_game<N>(s, G, out, summ);
-        hb[kH1Mt + kMtN] = s.mt_pos[0];
-        hb[kH1Mt + kMtN + 1] = s.mt0[0];
+        hb[kH1Mt + kMtN] = code;
+        hb[kH1Mt + kMtN + 1] = 0u;
+        prof.mark(PR_B2);
+        prof.flush(0, 1);
     }
-    __syncthreads();
-    for (int i = t; i < kMtN; i += 64) hb[kH1Mt + i] = s.mt[i];
 }
 
 

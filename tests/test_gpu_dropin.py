@@ -48,6 +48,33 @@ def test_game_session_multi_episode_stream():
         assert [x.tolist() for x in sess.results] == r["results"]
 
 
+@pytest.mark.parametrize("n", [2, 4, 10])
+def test_scalar_reset_matches_numpy_shuffle(n):
+    """sn_reset1 (the wave-parallel one-game deal) against numpy itself:
+    env.py:99-112's np.random.shuffle of arange(104) from numpy states at
+    every position class -- fresh, mid-block, a deal that crosses into the
+    next 624-word block (numpy twists there), pos = 624 (twist first) -- the
+    hands, rows and numpy's state afterwards."""
+    from rl_6_nimmt import SechsNimmtEnv
+
+    env = SechsNimmtEnv(n, verbose=False)
+    for seed, skip in [(0, 0), (1, 1), (2, 300), (3, 480), (4, 560), (5, 600), (6, 623), (7, 624), (8, 1000)]:
+        rs = np.random.RandomState(seed)
+        rs.randint(0, 2**32, size=skip, dtype=np.uint64)
+        st = rs.get_state()
+        np.random.set_state(st)
+        env.reset()
+        deck = np.arange(104, dtype=np.int32)
+        rs.shuffle(deck)
+        cards = list(deck)
+        hands = [sorted(int(c) for c in cards[10 * p:10 * p + 10]) for p in range(n)]
+        rows = [int(cards[103 - r]) for r in range(4)]
+        assert [[int(c) for c in h] for h in env._hands] == hands, (n, seed, skip)
+        assert [[int(c) for c in r] for r in env._board] == [[c] for c in rows], (n, seed, skip)
+        got, want = np.random.get_state(), rs.get_state()
+        assert np.array_equal(got[1], want[1]) and got[2] == want[2], (n, seed, skip, got[2], want[2])
+
+
 def test_env_dropin_trace_and_errors():
     from rl_6_nimmt import InvalidMoveException, SechsNimmtEnv
 
