@@ -993,9 +993,10 @@ __global__ void k_step1(DevState s, Acts1 acts, uint32_t* hb, int summ) {
 // masked rejection) are decoded 64 stream words per instruction -- a word's
 // draw index is its prefix count of accepted words, iterated acceptance ->
 // ballot -> v_mbcnt to the fixed point -- with whole 624-word blocks twisted
-// in LDS when the stream crosses one (as numpy does); one lane then applies
-// the swaps and deals.  The state goes back in numpy's own form (the block
-// holding the consumer + pos), so the host converts nothing.
+// in LDS when the stream crosses one (as numpy does); the swaps run on the
+// deck held in the wave's registers, one lane deals.  The state goes back in
+// numpy's own form (the block holding the consumer + pos): the host
+// converts nothing.
 template <int N>
 __global__ __launch_bounds__(64) void k_reset1(DevState s, uint32_t* hb, int summ) {
     constexpr uint32_t D = kMtN - kMtM;  // 227
@@ -1017,7 +1018,6 @@ __global__ __launch_bounds__(64) void k_reset1(DevState s, uint32_t* hb, int sum
         const uint32_t i = 64u * q + lane;
         if (i < (uint32_t)kMtN) blk[i] = kv[q];
     }
-    for (uint32_t i = lane; i < C; i += 64u) slot[i] = (uint8_t)i;  // the ordered deck (np.arange)
     __syncthreads();
     prof.mark(PR_DRAWS);
     // numpy's twist of blk[0, 624) into blk[624, 1248), in its own order:
@@ -1087,6 +1087,74 @@ __global__ __launch_bounds__(64) void k_reset1(DevState s, uint32_t* hb, int sum
     }
     __syncthreads();
     prof.mark(PR_TARGETS);
+    // the swaps, in numpy's order (step o swaps position i_o = C-1-o with
+    // its target j_o), resolved in parallel: v(o), the card step o moves from
+    // i_o to j_o, is what an earlier step last moved onto i_o (the latest
+    // o' < o with j_o' = i_o), else the card i_o itself -- a chain over
+    // earlier steps, resolved by pointer jumping; the final card at i_o is
+    // what sat on j_o before step o (the same rule), at position 0 v of the
+    // last step targeting 0.  Lane l holds steps l and 64 + l.
+    {
+        __shared__ int32_t val[128], ptr[128], tail[128];
+        __shared__ unsigned long long msk[128];
+        const uint32_t oa = lane, ob = 64u + lane;
+        const bool va = oa < C1, vb = ob < C1;
+        const int32_t ia = (int32_t)(C1 - oa), ib = (int32_t)C1 - (int32_t)ob;
+        const int32_t ja = va ? jslot[oa] : -1, jb = vb ? jslot[ob] : -1;
+        // the latest earlier step with a given target: per 64-step chunk a
+        // mask of the lanes targeting each position (LDS atomic or), the
+        // highest lane below mine, else the last one of the chunk before
+        tail[lane] = -1, tail[64u + lane] = -1;
+        msk[lane] = 0ull, msk[64u + lane] = 0ull;
+        __syncthreads();
+        const uint64_t below = (1ull << lane) - 1ull;
+        if (va) atomicOr(&msk[ja], 1ull << lane);
+        __syncthreads();
+        uint64_t mj = va ? msk[ja] & below : 0ull, mi = va ? msk[ia] & below : 0ull;
+        const int32_t pja = mj ? 63 - (int32_t)__builtin_clzll(mj) : -1;
+        const int32_t pia = mi ? 63 - (int32_t)__builtin_clzll(mi) : -1;
+        if (va && (msk[ja] >> lane) == 1ull) tail[ja] = (int32_t)lane;  // the chunk's last step onto ja
+        __syncthreads();
+        if (va) msk[ja] = 0ull;
+        __syncthreads();
+        if (vb) atomicOr(&msk[jb], 1ull << lane);
+        __syncthreads();
+        mj = vb ? msk[jb] & below : 0ull, mi = vb ? msk[ib] & below : 0ull;
+        const int32_t pjb = mj ? 127 - (int32_t)__builtin_clzll(mj) : (vb ? tail[jb] : -1);
+        const int32_t pib = mi ? 127 - (int32_t)__builtin_clzll(mi) : (vb ? tail[ib] : -1);
+        const uint64_t z1 = __ballot(vb && jb == 0), z0 = __ballot(va && ja == 0);
+        const int32_t last0 = z1 ? 127 - (int32_t)__builtin_clzll(z1) : (z0 ? 63 - (int32_t)__builtin_clzll(z0) : -1);
+        // v: resolved values (>= 0) or pointers to earlier steps
+        int32_t pa = pia, pb = pib;
+        int32_t xa = (pa < 0) ? ia : -1, xb = (pb < 0) ? ib : -1;
+        val[oa] = xa, ptr[oa] = pa, val[ob] = xb, ptr[ob] = pb;
+        __syncthreads();
+        while (__ballot((va && xa < 0) || (vb && xb < 0))) {
+            int32_t na = xa, nb = xb, qa = pa, qb = pb;
+            if (va && xa < 0) {
+                const int32_t w = val[pa];
+                if (w >= 0) na = w;
+                else qa = ptr[pa];
+            }
+            if (vb && xb < 0) {
+                const int32_t w = val[pb];
+                if (w >= 0) nb = w;
+                else qb = ptr[pb];
+            }
+            __syncthreads();
+            xa = na, xb = nb, pa = qa, pb = qb;
+            val[oa] = xa, ptr[oa] = pa, val[ob] = xb, ptr[ob] = pb;
+            __syncthreads();
+        }
+        const int32_t fa = (pja < 0) ? ja : val[max(pja, 0)], fb = (pjb < 0) ? jb : val[max(pjb, 0)];
+        const int32_t f0 = (last0 < 0) ? 0 : val[last0];
+        __syncthreads();
+        if (va) slot[ia] = (uint8_t)fa;
+        if (vb) slot[ib] = (uint8_t)fb;
+        if (lane == 0u) slot[0] = (uint8_t)f0;
+    }
+    __syncthreads();
+    prof.mark(PR_APPLY);
     // numpy's state after the deal: the block holding the consumer, pos in 1..624
     const uint32_t b0 = (dw > (uint32_t)kMtN) ? (uint32_t)kMtN : 0u, npos = dw - b0;
     for (uint32_t i = lane; i < (uint32_t)kMtN; i += 64u) {
@@ -1096,8 +1164,6 @@ __global__ __launch_bounds__(64) void k_reset1(DevState s, uint32_t* hb, int sum
     }
     if (lane == 0u) {
         prof.mark(PR_STORE);
-        shuffle_apply(slot, jslot, (int)C);
-        prof.mark(PR_APPLY);
         Game<N> G;
         deal_from_deck<N>(slot, (int)C, G);
         prof.mark(PR_HANDS);

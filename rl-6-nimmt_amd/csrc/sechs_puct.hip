@@ -224,6 +224,80 @@ __global__ void k_puct_rows(PuctArgs a, int N, int n_cur, T* rows) {
     write_row<T>(rows + i * kRowLen, hand_get(h, (uint32_t)k), h, kp, ro_board(ro));
 }
 
+// Layer-1 split of the rollout rows.  A candidate row is [card, obs]: the
+// observation part is the same for every candidate of a seat, so layer 1
+// (MultiHeadedMLP's first Linear, 48 -> H) is W1[:, 1:] obs + b1 once per
+// seat (a PyTorch GEMM over the D*N seat rows [0, obs]) plus the card column
+// W1[:, 0] * card per candidate (k_puct_h1, with the ReLU): no GEMM over the
+// D*N*n_cur candidate rows, and those rows are never written.
+template <typename T>
+__device__ __forceinline__ float round_to(float v) { return v; }
+template <>
+__device__ __forceinline__ float round_to<__hip_bfloat16>(float v) { return __bfloat162float(__float2bfloat16(v)); }
+
+template <typename T>
+__global__ void k_puct_seat_rows(PuctArgs a, int N, int n_cur, T* rows, float* cards) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.D * N) return;
+    const int64_t d = i / N;
+    const int q = (int)(i - d * N);
+    const int32_t* ro = a.ro + d * kRoWords;
+    int kp = N;
+    if (a.lgs) {
+        int64_t g;
+        int p;
+        dec_to_gp(a, d, g, p);
+        kp = players_of(a, g);
+    }
+    if (q >= kp) {  // an absent seat of a smaller tournament game (its logits are never read)
+#pragma unroll
+        for (int j = 0; j < kRowLen; j++) rows[i * kRowLen + j] = to_out<T>(0.f);
+        for (int k = 0; k < n_cur; k++) cards[i * n_cur + k] = 0.f;
+        return;
+    }
+    const Hand h = ro_hand(ro, q);
+    write_row<T>(rows + i * kRowLen, 0u, h, kp, ro_board(ro));
+    rows[i * kRowLen] = to_out<T>(0.f);  // the card column: k_puct_h1
+    for (int k = 0; k < n_cur; k++)      // the card feature as the row would hold it (T-rounded)
+        cards[i * n_cur + k] = round_to<T>(nrm((float)hand_get(h, (uint32_t)k), 0.f, 103.f));
+}
+
+// h1[r][j] = relu(base[r / n_cur][j] + cards[r] * w1c[j]): a block of
+// (32, 8) threads covers 8 rows, lane x the 4 columns 4x .. 4x+3 (H <= 128),
+// so a row's stores are one contiguous run
+template <typename T>
+__global__ __launch_bounds__(256) void k_puct_h1(uint32_t R, int H, int n_cur, const T* base, const float* cards,
+                                                 const float* w1c, T* h1) {
+    const uint32_t r = blockIdx.x * 8u + threadIdx.y;
+    const int c = 4 * (int)threadIdx.x;
+    if (r >= R || c >= H) return;
+    const float x = cards[r];
+    const T* bs = base + (size_t)(r / (uint32_t)n_cur) * H;
+    T* out = h1 + (size_t)r * H;
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const int j = min(c + u, H - 1);
+        v[u] = fmaxf((float)bs[j] + x * w1c[j], 0.f);
+    }
+    if ((H & 3) == 0) {
+        if constexpr (sizeof(T) == 2) {
+            const __hip_bfloat16 b0 = __float2bfloat16(v[0]), b1 = __float2bfloat16(v[1]), b2 = __float2bfloat16(v[2]),
+                                 b3 = __float2bfloat16(v[3]);
+            uint2 w;
+            w.x = (uint32_t)*(const uint16_t*)&b0 | ((uint32_t)*(const uint16_t*)&b1 << 16);
+            w.y = (uint32_t)*(const uint16_t*)&b2 | ((uint32_t)*(const uint16_t*)&b3 << 16);
+            *(uint2*)(out + c) = w;
+        } else {
+            *(float4*)(out + c) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (c + u < H) out[c + u] = to_out<T>(v[u]);
+    }
+}
+
 // np.median of all outcomes so far, from the histogram (kth smallest)
 __device__ double hist_median(const int32_t* hist, int32_t total) {
     const int32_t k0 = (total - 1) / 2, k1 = total / 2;
@@ -289,8 +363,41 @@ __device__ __forceinline__ int sample_softmax(const float* x, int n, float u) {
     return n - 1;
 }
 
-template <int N>
-__global__ void k_puct_step(DevState s, PuctArgs a, const float* logits, int t, int n_cur) {
+// one candidate's logit: f32, or bf16 (the padded head GEMM's output), `ls` apart
+template <bool LB>
+__device__ __forceinline__ float logit_at(const void* lg, int64_t i, int ls) {
+    if constexpr (LB) {
+        const uint32_t u = (uint32_t)((const uint16_t*)lg)[i * ls] << 16;
+        return __uint_as_float(u);
+    } else {
+        return ((const float*)lg)[i * ls];
+    }
+}
+
+// Categorical(softmax(x[0..n))).sample() over a register row (unrolled to 10)
+__device__ __forceinline__ int sample_row(const float (&x)[kHand], int n, float u) {
+    float m = x[0];
+#pragma unroll
+    for (int k = 1; k < kHand; k++) m = (k < n) ? fmaxf(m, x[k]) : m;
+    float e[kHand], sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < kHand; k++) {
+        e[k] = (k < n) ? __expf(x[k] - m) : 0.f;
+        sum += e[k];
+    }
+    const float target = u * sum;
+    float acc = 0.f;
+    int pick = n - 1;
+#pragma unroll
+    for (int k = 0; k < kHand - 1; k++) {
+        acc += e[k];
+        pick = (k < n - 1 && acc > target && pick == n - 1 && k < pick) ? k : pick;
+    }
+    return pick;
+}
+
+template <int N, bool LB>
+__global__ void k_puct_step(DevState s, PuctArgs a, const void* logits, int ls, int t, int n_cur) {
     const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (d >= a.D) return;
     int64_t g;
@@ -306,6 +413,13 @@ __global__ void k_puct_step(DevState s, PuctArgs a, const float* logits, int t, 
     uint32_t card[N], pen[N];
     int first = ro[41];
     const int kp = players_of(a, g);
+    // every seat's logits first: N x n_cur independent loads in flight
+    float lg[N][kHand];
+#pragma unroll
+    for (int q = 0; q < N; q++)
+#pragma unroll
+        for (int k = 0; k < kHand; k++)
+            lg[q][k] = (q < kp && k < n_cur) ? logit_at<LB>(logits, (d * N + q) * n_cur + k, ls) : 0.f;
 #pragma unroll
     for (int q = 0; q < N; q++) {
         if (q >= kp) {  // absent seat of a smaller tournament game
@@ -313,12 +427,11 @@ __global__ void k_puct_step(DevState s, PuctArgs a, const float* logits, int t, 
             continue;
         }
         int idx;
-        const float* x = logits + (d * N + q) * n_cur;
         if (t == 0 && q == 0 && (a.flags & 1)) {
             idx = puct_choose(a.stats + d * kStatWords, a.hist + d * kHistBins, a.root_probs + d * kHand, n_cur,
                               a.c_puct, nullptr);
         } else {
-            idx = sample_softmax(x, n_cur, philox_uniform(a.seed_lo ^ puct_step_of(a), a.seed_hi, stream, (uint32_t)q));
+            idx = sample_row(lg[q], n_cur, philox_uniform(a.seed_lo ^ puct_step_of(a), a.seed_hi, stream, (uint32_t)q));
         }
         if (t == 0 && q == 0) first = idx;
         card[q] = hand_get(G.hand[q], (uint32_t)idx);
@@ -537,8 +650,54 @@ sn_status sn_puct_step(sn_env* e, const sn_puct* q, const float* logits, int t, 
     if (st != SN_OK) return st;
     if (n_cur < 1 || n_cur > a.n || t < 0 || t + n_cur != a.n) return set_error(SN_EINVAL, "t / n_cur inconsistent");
     hipStream_t s = (hipStream_t)stream;
-    SN_DISPATCH_N(e->s.N, hipLaunchKernelGGL((k_puct_step<NN>), dim3(grid_for(a.D)), dim3(kBlock), 0, s, e->s, a, logits,
-                                             t, n_cur));
+    const int ls = q->logit_stride > 1 ? q->logit_stride : 1;
+    if (q->logit_bf16) {
+        SN_DISPATCH_N(e->s.N, hipLaunchKernelGGL((k_puct_step<NN, true>), dim3(grid_for(a.D)), dim3(kBlock), 0, s, e->s, a,
+                                                 (const void*)logits, ls, t, n_cur));
+    } else {
+        SN_DISPATCH_N(e->s.N, hipLaunchKernelGGL((k_puct_step<NN, false>), dim3(grid_for(a.D)), dim3(kBlock), 0, s, e->s, a,
+                                                 (const void*)logits, ls, t, n_cur));
+    }
+    HIP_TRY(hipGetLastError());
+    return SN_OK;
+}
+
+sn_status sn_puct_seat_rows(sn_env* e, const sn_puct* q, int n_cur, void* rows, float* cards, int bf16, void* stream) {
+    PuctArgs a{};
+    sn_status st = puct_args(e, q, a);
+    if (st != SN_OK) return st;
+    if (n_cur < 1 || n_cur > a.n) return set_error(SN_EINVAL, "n_cur out of range");
+    if (!rows || !cards) return set_error(SN_EINVAL, "NULL argument");
+    const int64_t total = a.D * e->s.N;
+    hipStream_t s = (hipStream_t)stream;
+    if (bf16)
+        hipLaunchKernelGGL(k_puct_seat_rows<__hip_bfloat16>, dim3(grid_for(total)), dim3(kBlock), 0, s, a, e->s.N, n_cur,
+                           (__hip_bfloat16*)rows, cards);
+    else
+        hipLaunchKernelGGL(k_puct_seat_rows<float>, dim3(grid_for(total)), dim3(kBlock), 0, s, a, e->s.N, n_cur,
+                           (float*)rows, cards);
+    HIP_TRY(hipGetLastError());
+    return SN_OK;
+}
+
+sn_status sn_puct_h1(sn_env* e, const sn_puct* q, int n_cur, const void* base, int hidden, const float* w1c,
+                     const float* cards, void* h1, int bf16, void* stream) {
+    PuctArgs a{};
+    sn_status st = puct_args(e, q, a);
+    if (st != SN_OK) return st;
+    if (n_cur < 1 || n_cur > a.n) return set_error(SN_EINVAL, "n_cur out of range");
+    if (hidden < 1 || hidden > 128) return set_error(SN_EINVAL, "hidden size out of range (1..128)");
+    if (!base || !w1c || !cards || !h1) return set_error(SN_EINVAL, "NULL argument");
+    const int64_t R = a.D * e->s.N * n_cur;
+    if (R >= (1ll << 31)) return set_error(SN_EINVAL, "too many rows");
+    const dim3 grid((unsigned)((R + 7) / 8)), blk(32, 8);
+    hipStream_t s = (hipStream_t)stream;
+    if (bf16)
+        hipLaunchKernelGGL(k_puct_h1<__hip_bfloat16>, grid, blk, 0, s, (uint32_t)R, hidden, n_cur,
+                           (const __hip_bfloat16*)base, cards, w1c, (__hip_bfloat16*)h1);
+    else
+        hipLaunchKernelGGL(k_puct_h1<float>, grid, blk, 0, s, (uint32_t)R, hidden, n_cur, (const float*)base, cards, w1c,
+                           (float*)h1);
     HIP_TRY(hipGetLastError());
     return SN_OK;
 }

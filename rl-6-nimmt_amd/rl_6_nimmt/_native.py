@@ -44,6 +44,8 @@ class SnPuct(ctypes.Structure):
         ("step_dev", ctypes.c_void_p),
         ("dec_list", ctypes.c_void_p),
         ("num_dec", ctypes.c_int64),
+        ("logit_stride", ctypes.c_int32),
+        ("logit_bf16", ctypes.c_int32),
     ]
 
 
@@ -94,6 +96,8 @@ SIGNATURES = {
     "sn_puct_deal": ([_P, _P, _P], _I),
     "sn_puct_rows": ([_P, _P, _I, _P, _I, _P], _I),
     "sn_puct_step": ([_P, _P, _P, _I, _I, _P], _I),
+    "sn_puct_seat_rows": ([_P, _P, _I, _P, _P, _I, _P], _I),
+    "sn_puct_h1": ([_P, _P, _I, _P, _I, _P, _P, _P, _I, _P], _I),
     "sn_puct_choose": ([_P, _P, _P, _P, _P], _I),
     "sn_pcv_choose": ([_P, _P, _P, _P, _P, _P, _P, _P], _I),
     "sn_policy_sample": ([_P, _P, _P, _P, _P, _P, _P, _P], _I),

@@ -62,6 +62,24 @@ class FusedMLP:
         wp[: w.shape[0]], bp[: b.shape[0]] = w, b
         return cls(net, layers, wp.t().contiguous(), bp, [h[0].out_features for h in heads])
 
+    def split(self):
+        """layer 1 split for the rollout rows (sn_puct_seat_rows / sn_puct_h1):
+        (W1^T [48, H], b1, W1[:, 0] as f32 [H]) or None for other layouts"""
+        if self.layers is None or self.layers[0][0].shape[1] != ROW or self.layers[0][0].shape[0] > 128:
+            return None
+        if not hasattr(self, "_split"):
+            w, b = self.layers[0]
+            self._split = (w.t().contiguous(), b, w[:, 0].float().contiguous())
+        return self._split
+
+    def tail(self, h1):
+        """the layers after the first on layer-1 activations: the padded head
+        output [rows, 16] (column 0 = the policy logit)"""
+        h = h1
+        for w, b in self.layers[1:]:
+            h = torch._addmm_activation(b, h, w.t())
+        return torch.addmm(self.head_b, h, self.head_w)
+
     def __call__(self, rows):
         if self.layers is None:
             return self.module(rows)
@@ -118,6 +136,8 @@ class BatchedPUCT:
         # decision; the kernels read the decision counter from step_dev
         self.graph = bool(graph) and max_decisions is None
         self._graphs = {}
+        # the rollout rows' layer 1 split (FusedMLP.split): once per seat + the card column
+        self.split_l1 = True
         self._step_dev = torch.zeros((1,), dtype=torch.int32, device=dev)
 
     # ------------------------------------------------------------ policy net on the device
@@ -218,6 +238,32 @@ class BatchedPUCT:
         L, h, st = nat.lib(), self.env._h, self.env._stream()
         bf16 = int(self.net_dtype == torch.bfloat16)
         N = self.env.num_players
+        sp = self._net.split() if self.split_l1 else None
+        if sp is not None:
+            # layer 1 once per rollout seat + the card column per candidate
+            # (sn_puct_h1); the padded head's bf16/f32 output feeds
+            # sn_puct_step in place (column 0, stride 16)
+            w1t, b1, w1c = sp
+            seat_rows, cards, h1 = self._split_bufs(n, w1t.shape[1])
+            S = self.D * N
+            for r in range(self.n_mc(n)):
+                q.rollout = r
+                nat.check(L.sn_puct_deal(h, ctypes_ref(q), st), "sn_puct_deal")
+                for t in range(n):
+                    m = n - t
+                    nat.check(L.sn_puct_seat_rows(h, ctypes_ref(q), m, nat.ptr(seat_rows[:S]), nat.ptr(cards), bf16, st),
+                              "sn_puct_seat_rows")
+                    base = torch.addmm(b1, seat_rows[:S], w1t)
+                    hv = h1[: S * m]
+                    nat.check(L.sn_puct_h1(h, ctypes_ref(q), m, nat.ptr(base), base.shape[1], nat.ptr(w1c), nat.ptr(cards),
+                                           nat.ptr(hv), bf16, st), "sn_puct_h1")
+                    with torch.no_grad():
+                        out = self._net.tail(hv)
+                    self.rows_evaluated += S * m
+                    q.logit_stride, q.logit_bf16 = out.stride(0), int(out.dtype == torch.bfloat16)
+                    nat.check(L.sn_puct_step(h, ctypes_ref(q), nat.ptr(out), t, m, st), "sn_puct_step")
+                    q.logit_stride, q.logit_bf16 = 0, 0
+            return
         bufs = self._bufs(n)
         views = {m: bufs[m][: self.D * N * m] for m in range(1, n + 1)}  # this batch's decisions
         for r in range(self.n_mc(n)):
@@ -227,6 +273,18 @@ class BatchedPUCT:
                 m = n - t
                 nat.check(L.sn_puct_rows(h, ctypes_ref(q), m, nat.ptr(views[m]), bf16, st), "sn_puct_rows")
                 nat.check(L.sn_puct_step(h, ctypes_ref(q), nat.ptr(self._logits(views[m])), t, m, st), "sn_puct_step")
+
+    def _split_bufs(self, n, H):
+        """seat rows [D_max*N][48], candidate cards [D_max*N*10] f32 and the
+        layer-1 activations [D_max*N*10][H] (views of these serve every hand size)"""
+        N = self.env.num_players
+        if getattr(self, "_sbufs", None) is None or self._sbufs[2].shape[1] != H:
+            dev = self.env.device
+            S = self.D_max * N
+            self._sbufs = (torch.empty((S, ROW), dtype=self.net_dtype, device=dev),
+                           torch.empty((S * 10,), dtype=torch.float32, device=dev),
+                           torch.empty((S * 10, H), dtype=self.net_dtype, device=dev))
+        return self._sbufs
 
     def _bufs(self, n):
         N = self.env.num_players

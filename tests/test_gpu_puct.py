@@ -242,6 +242,72 @@ def test_graph_replay_equals_eager_search(dtype):
             assert torch.equal(u, v)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_layer1_split_equals_full_rows(dtype):
+    """sn_puct_seat_rows + the per-seat GEMM + sn_puct_h1 give the first
+    layer's activations of every candidate row: relu(rows @ W1^T + b1) over
+    sn_puct_rows' full [card, obs] rows (f32: to 1e-5; bf16: the base is
+    rounded once more, to 2 bf16 ulps)."""
+    import ctypes
+
+    from rl_6_nimmt import _native as nat
+
+    env, eng = _engine(B=64, dtype=dtype, mc_max=4, mc_per_card=2, seed=23)
+    N, n = env.num_players, 7
+    for t in range(10 - n):
+        env.step(eng.decide(10 - t))
+    net = eng.sync_net()
+    w1t, b1, w1c = net.split()
+    q = eng._params(n)
+    L, h, st = nat.lib(), env._h, env._stream()
+    eng.memorize()
+    nat.check(L.sn_puct_deal(h, ctypes.byref(q), st), "deal")
+    bf = int(dtype == torch.bfloat16)
+    for m in (n, 3, 1):
+        S, R = eng.D * N, eng.D * N * m
+        rows = torch.empty((R, 48), dtype=dtype, device=env.device)
+        nat.check(L.sn_puct_rows(h, ctypes.byref(q), m, nat.ptr(rows), bf, st), "rows")
+        ref = torch.relu(rows.float() @ w1t.float() + b1.float())
+        seat = torch.empty((S, 48), dtype=dtype, device=env.device)
+        cards = torch.empty((R,), dtype=torch.float32, device=env.device)
+        nat.check(L.sn_puct_seat_rows(h, ctypes.byref(q), m, nat.ptr(seat), nat.ptr(cards), bf, st), "seat_rows")
+        assert torch.equal(seat[:, 1:], rows.view(S, m, 48)[:, 0, 1:]) and (seat[:, 0] == 0).all()
+        assert torch.equal(cards, rows[:, 0].float())
+        base = torch.addmm(b1, seat, w1t)
+        h1 = torch.empty((R, w1t.shape[1]), dtype=dtype, device=env.device)
+        nat.check(L.sn_puct_h1(h, ctypes.byref(q), m, nat.ptr(base), base.shape[1], nat.ptr(w1c), nat.ptr(cards),
+                               nat.ptr(h1), bf, st), "h1")
+        if dtype == torch.float32:
+            assert torch.allclose(h1, ref, rtol=1e-5, atol=1e-5)
+        else:
+            assert torch.allclose(h1.float(), ref, rtol=2 ** -6, atol=2 ** -6), (h1.float() - ref).abs().max()
+
+
+def test_search_statistics_consistent_bf16_full_size():
+    """Config 4's shape: 8192 games, every seat searching, bf16 net through
+    the layer-1 split and the padded head's strided bf16 logits; one
+    decision at n = 10 and n = 4 -- the playout counts, the outcome
+    histogram and the chosen moves agree with each other."""
+    env, eng = _engine(B=8192, dtype=torch.bfloat16, mc_max=12, mc_per_card=2, seed=31)
+    eng.graph = True
+    for t in range(10):
+        n = 10 - t
+        acts = eng.decide(n)
+        if n in (10, 4):
+            st, hist = eng.stats.cpu().numpy(), eng.hist.cpu().numpy()
+            n_mc = eng.n_mc(n)
+            assert (st[:, 10:10 + n].sum(axis=1) == n_mc).all()
+            assert (st[:, 20] == n_mc).all() and (hist.sum(axis=1) == n_mc).all()
+            vals = np.arange(172) - 171
+            assert ((hist * vals).sum(axis=1) == st[:, :10].sum(axis=1)).all()
+            cnt = st[:, 10:10 + n]
+            means = np.where(cnt > 0, st[:, :n] / np.maximum(cnt, 1), -np.inf)
+            assert (eng.best_index.cpu().numpy()[: eng.D] == np.argmax(means, axis=1)).all()
+        rew, done, inv = env.step(acts)
+        assert (inv.cpu().numpy() == -1).all()
+    assert bool(done.all())
+
+
 def test_search_statistics_consistent():
     env, eng = _engine(B=32, mc_max=12, mc_per_card=2)
     for t in range(10):
