@@ -364,18 +364,23 @@ sn_status sn_puct_init(sn_env* env, const sn_puct* q, const float* root_logits, 
 sn_status sn_puct_deal(sn_env* env, const sn_puct* q, void* stream);
 sn_status sn_puct_rows(sn_env* env, const sn_puct* q, int n_cur, void* rows, int bf16, void* stream);
 sn_status sn_puct_step(sn_env* env, const sn_puct* q, const float* logits, int t, int n_cur, void* stream);
-/* Layer-1 split of the rollout MLP (MultiHeadedMLP 48 -> H -> ...): a candidate
-   row is [card, obs] with obs shared by the seat's n_cur candidates, so
-     sn_puct_seat_rows  rows [D*N][48] (bf16 or f32) = [0, obs] per rollout seat,
+/* Layer-1 split of the rollout MLP (MultiHeadedMLP 48 -> H -> ...), in
+   feature-major activations ([features][columns], so the caller's GEMMs run
+   as W . h^T): a candidate row is [card, obs] with obs shared by the seat's
+   n_cur candidates, so
+     sn_puct_seat_cols  cols [ks][D*N] (bf16 or f32) = [0 (card slot), obs (47),
+                        1 (bias feature), 0 ...] per rollout seat (ks >= 49), and
                         cards [D*N*n_cur] f32 = the candidates' normalised cards
-                        (rounded to the row dtype, as the row would hold them)
-     (caller, PyTorch)  base [D*N][H] = rows @ W1^T + b1
-     sn_puct_h1         h1 [D*N*n_cur][H] = relu(base[seat] + card * w1c) (H <= 128), w1c =
-                        W1[:, 0] f32; then the caller's remaining layers -> logits
+                        (rounded to the column dtype, as a row would hold them)
+     (caller, PyTorch)  baseT [H][D*N] = [W1 | b1 | 0] @ cols
+     sn_puct_h1_cols    h1T [kp][D*N*n_cur]: relu(baseT[j][seat] + card * w1c[j])
+                        for j < H (w1c = W1[:, 0] f32), 1 at j = H (the next
+                        layer's bias feature), 0 up to kp
    replaces sn_puct_rows + the first GEMM over the D*N*n_cur candidate rows. */
-sn_status sn_puct_seat_rows(sn_env* env, const sn_puct* q, int n_cur, void* rows, float* cards, int bf16, void* stream);
-sn_status sn_puct_h1(sn_env* env, const sn_puct* q, int n_cur, const void* base, int hidden, const float* w1c,
-                     const float* cards, void* h1, int bf16, void* stream);
+sn_status sn_puct_seat_cols(sn_env* env, const sn_puct* q, int n_cur, void* cols, int ks, float* cards, int bf16,
+                            void* stream);
+sn_status sn_puct_h1_cols(sn_env* env, const sn_puct* q, int n_cur, const void* baseT, int hidden, const float* w1c,
+                          const float* cards, void* h1T, int kp, int bf16, void* stream);
 /* best_index [D] (optional): index of the chosen card in the root legal list */
 sn_status sn_puct_choose(sn_env* env, const sn_puct* q, int32_t* actions, int32_t* best_index, void* stream);
 /* PUCTCustomedAgent (agents/mcts.py:325-451, replaces _mcts /

@@ -84,25 +84,25 @@ __device__ __forceinline__ __hip_bfloat16 to_out<__hip_bfloat16>(float v) { retu
 
 // one candidate row: [card, observation of a seat holding `h` on board `b`]
 template <typename T>
-__device__ __forceinline__ void write_row(T* dst, uint32_t card, const Hand& h, int N, const Board& b) {
+__device__ __forceinline__ void write_row(T* dst, uint32_t card, const Hand& h, int N, const Board& b, int64_t st = 1) {
     dst[0] = to_out<T>(nrm((float)card, 0.f, 103.f));
 #pragma unroll
     for (int k = 0; k < kHand; k++) {
         const uint32_t c = hand_get(h, (uint32_t)k);
-        dst[1 + k] = to_out<T>(nrm(c == 0xFFu ? -1.f : (float)c, 0.f, 103.f));
+        dst[(1 + k) * st] = to_out<T>(nrm(c == 0xFFu ? -1.f : (float)c, 0.f, 103.f));
     }
-    dst[11] = to_out<T>(nrm((float)N, 0.f, 6.f));
+    dst[11 * st] = to_out<T>(nrm((float)N, 0.f, 6.f));
     const uint32_t lo[4] = {b.lo.x, b.lo.y, b.lo.z, b.lo.w};
     const uint32_t hi[4] = {b.hi.x, b.hi.y, b.hi.z, b.hi.w};
 #pragma unroll
     for (int r = 0; r < kRows; r++) {
-        dst[12 + r] = to_out<T>(nrm((float)len_of(hi[r]), 1.f, 5.f));
-        dst[16 + r] = to_out<T>(nrm((float)end_of(hi[r]), 0.f, 103.f));
-        dst[20 + r] = to_out<T>(nrm((float)heads_in(hi[r]), 1.f, 10.f));
+        dst[(12 + r) * st] = to_out<T>(nrm((float)len_of(hi[r]), 1.f, 5.f));
+        dst[(16 + r) * st] = to_out<T>(nrm((float)end_of(hi[r]), 0.f, 103.f));
+        dst[(20 + r) * st] = to_out<T>(nrm((float)heads_in(hi[r]), 1.f, 10.f));
 #pragma unroll
         for (int i = 0; i < kThreshold; i++) {
             const float v = (i < 5 && (uint32_t)i < len_of(hi[r])) ? (float)card_at(lo[r], hi[r], i < 5 ? i : 0) : -1.f;
-            dst[24 + r * kThreshold + i] = to_out<T>(nrm(v, 0.f, 103.f));
+            dst[(24 + r * kThreshold + i) * st] = to_out<T>(nrm(v, 0.f, 103.f));
         }
     }
 }
@@ -224,21 +224,28 @@ __global__ void k_puct_rows(PuctArgs a, int N, int n_cur, T* rows) {
     write_row<T>(rows + i * kRowLen, hand_get(h, (uint32_t)k), h, kp, ro_board(ro));
 }
 
-// Layer-1 split of the rollout rows.  A candidate row is [card, obs]: the
-// observation part is the same for every candidate of a seat, so layer 1
-// (MultiHeadedMLP's first Linear, 48 -> H) is W1[:, 1:] obs + b1 once per
-// seat (a PyTorch GEMM over the D*N seat rows [0, obs]) plus the card column
-// W1[:, 0] * card per candidate (k_puct_h1, with the ReLU): no GEMM over the
-// D*N*n_cur candidate rows, and those rows are never written.
+// Layer-1 split of the rollout rows, feature-major.  A candidate row is
+// [card, obs]: the observation part is the same for every candidate of a
+// seat, so layer 1 (MultiHeadedMLP's first Linear, 48 -> H) is W1[:, 1:] obs
+// + b1 once per seat (the caller's GEMM over the D*N seat columns) plus the
+// card column W1[:, 0] * card per candidate (k_puct_h1_cols, with the ReLU):
+// no GEMM over the D*N*n_cur candidate rows, and those rows are never
+// written.  Activations are feature-major ([features][rows]: the GEMMs run as
+// W . h^T, which hipBLASLt handles ~1.6x faster than h . W^T at these skinny
+// shapes) with a ones feature after the last real one, so every bias rides
+// in its layer's GEMM as a weight column and the ReLU in its epilogue.
 template <typename T>
 __device__ __forceinline__ float round_to(float v) { return v; }
 template <>
 __device__ __forceinline__ float round_to<__hip_bfloat16>(float v) { return __bfloat162float(__float2bfloat16(v)); }
 
+// seat column i = [0 (the card slot), obs (47)] normalised, 1 (bias), 0 pad
+// to ks features; cards[(i * n_cur) + k] = candidate k's normalised card
 template <typename T>
-__global__ void k_puct_seat_rows(PuctArgs a, int N, int n_cur, T* rows, float* cards) {
+__global__ void k_puct_seat_cols(PuctArgs a, int N, int n_cur, T* cols, int ks, float* cards) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.D * N) return;
+    const int64_t S = a.D * N;
+    if (i >= S) return;
     const int64_t d = i / N;
     const int q = (int)(i - d * N);
     const int32_t* ro = a.ro + d * kRoWords;
@@ -249,52 +256,50 @@ __global__ void k_puct_seat_rows(PuctArgs a, int N, int n_cur, T* rows, float* c
         dec_to_gp(a, d, g, p);
         kp = players_of(a, g);
     }
+    T* c = cols + i;
     if (q >= kp) {  // an absent seat of a smaller tournament game (its logits are never read)
-#pragma unroll
-        for (int j = 0; j < kRowLen; j++) rows[i * kRowLen + j] = to_out<T>(0.f);
+        for (int f = 0; f < ks; f++) c[f * S] = to_out<T>(f == kRowLen ? 1.f : 0.f);
         for (int k = 0; k < n_cur; k++) cards[i * n_cur + k] = 0.f;
         return;
     }
     const Hand h = ro_hand(ro, q);
-    write_row<T>(rows + i * kRowLen, 0u, h, kp, ro_board(ro));
-    rows[i * kRowLen] = to_out<T>(0.f);  // the card column: k_puct_h1
-    for (int k = 0; k < n_cur; k++)      // the card feature as the row would hold it (T-rounded)
+    write_row<T>(c, 0u, h, kp, ro_board(ro), S);
+    c[0] = to_out<T>(0.f);  // the card slot: k_puct_h1_cols
+    c[kRowLen * S] = to_out<T>(1.f);
+    for (int f = kRowLen + 1; f < ks; f++) c[f * S] = to_out<T>(0.f);
+    for (int k = 0; k < n_cur; k++)  // the card feature as the row would hold it (T-rounded)
         cards[i * n_cur + k] = round_to<T>(nrm((float)hand_get(h, (uint32_t)k), 0.f, 103.f));
 }
 
-// h1[r][j] = relu(base[r / n_cur][j] + cards[r] * w1c[j]): a block of
-// (32, 8) threads covers 8 rows, lane x the 4 columns 4x .. 4x+3 (H <= 128),
-// so a row's stores are one contiguous run
+// h1T[j][r] = relu(baseT[j][r / n_cur] + cards[r] * w1c[j]) for j < H, 1 at
+// j = H (the next layer's bias feature), 0 up to kp; two rows per thread
 template <typename T>
-__global__ __launch_bounds__(256) void k_puct_h1(uint32_t R, int H, int n_cur, const T* base, const float* cards,
-                                                 const float* w1c, T* h1) {
-    const uint32_t r = blockIdx.x * 8u + threadIdx.y;
-    const int c = 4 * (int)threadIdx.x;
-    if (r >= R || c >= H) return;
-    const float x = cards[r];
-    const T* bs = base + (size_t)(r / (uint32_t)n_cur) * H;
-    T* out = h1 + (size_t)r * H;
-    float v[4];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-        const int j = min(c + u, H - 1);
-        v[u] = fmaxf((float)bs[j] + x * w1c[j], 0.f);
-    }
-    if ((H & 3) == 0) {
-        if constexpr (sizeof(T) == 2) {
-            const __hip_bfloat16 b0 = __float2bfloat16(v[0]), b1 = __float2bfloat16(v[1]), b2 = __float2bfloat16(v[2]),
-                                 b3 = __float2bfloat16(v[3]);
-            uint2 w;
-            w.x = (uint32_t)*(const uint16_t*)&b0 | ((uint32_t)*(const uint16_t*)&b1 << 16);
-            w.y = (uint32_t)*(const uint16_t*)&b2 | ((uint32_t)*(const uint16_t*)&b3 << 16);
-            *(uint2*)(out + c) = w;
+__global__ __launch_bounds__(256) void k_puct_h1_cols(uint32_t R, uint32_t S, int H, int kp, int n_cur, const T* baseT,
+                                                      const float* cards, const float* w1c, T* h1T) {
+    const uint32_t r = 2u * (blockIdx.x * blockDim.x + threadIdx.x);
+    if (r >= R) return;
+    const bool two = r + 1u < R;
+    const uint32_t s0 = r / (uint32_t)n_cur, s1 = (r + 1u) / (uint32_t)n_cur;
+    const float x0 = cards[r], x1 = two ? cards[r + 1u] : 0.f;
+    const bool pack = (sizeof(T) == 2) && ((R & 1u) == 0u);  // 4-B aligned row pairs
+#pragma unroll 4
+    for (int j = 0; j < kp; j++) {
+        float v0, v1;
+        if (j < H) {
+            const float w = w1c[j];
+            v0 = fmaxf((float)baseT[(size_t)j * S + s0] + x0 * w, 0.f);
+            v1 = fmaxf((float)baseT[(size_t)j * S + s1] + x1 * w, 0.f);
         } else {
-            *(float4*)(out + c) = make_float4(v[0], v[1], v[2], v[3]);
+            v0 = v1 = (j == H) ? 1.f : 0.f;
         }
-    } else {
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-            if (c + u < H) out[c + u] = to_out<T>(v[u]);
+        T* o = h1T + (size_t)j * R + r;
+        if (pack) {
+            const __hip_bfloat16 b0 = __float2bfloat16(v0), b1 = __float2bfloat16(v1);
+            *(uint32_t*)o = (uint32_t)*(const uint16_t*)&b0 | ((uint32_t)*(const uint16_t*)&b1 << 16);
+        } else {
+            o[0] = to_out<T>(v0);
+            if (two) o[1] = to_out<T>(v1);
+        }
     }
 }
 
@@ -662,42 +667,45 @@ sn_status sn_puct_step(sn_env* e, const sn_puct* q, const float* logits, int t, 
     return SN_OK;
 }
 
-sn_status sn_puct_seat_rows(sn_env* e, const sn_puct* q, int n_cur, void* rows, float* cards, int bf16, void* stream) {
+sn_status sn_puct_seat_cols(sn_env* e, const sn_puct* q, int n_cur, void* cols, int ks, float* cards, int bf16,
+                            void* stream) {
     PuctArgs a{};
     sn_status st = puct_args(e, q, a);
     if (st != SN_OK) return st;
     if (n_cur < 1 || n_cur > a.n) return set_error(SN_EINVAL, "n_cur out of range");
-    if (!rows || !cards) return set_error(SN_EINVAL, "NULL argument");
+    if (!cols || !cards) return set_error(SN_EINVAL, "NULL argument");
+    if (ks <= kRowLen || ks > 256) return set_error(SN_EINVAL, "ks must be in 49..256 (48 features + the bias feature)");
     const int64_t total = a.D * e->s.N;
     hipStream_t s = (hipStream_t)stream;
     if (bf16)
-        hipLaunchKernelGGL(k_puct_seat_rows<__hip_bfloat16>, dim3(grid_for(total)), dim3(kBlock), 0, s, a, e->s.N, n_cur,
-                           (__hip_bfloat16*)rows, cards);
+        hipLaunchKernelGGL(k_puct_seat_cols<__hip_bfloat16>, dim3(grid_for(total)), dim3(kBlock), 0, s, a, e->s.N, n_cur,
+                           (__hip_bfloat16*)cols, ks, cards);
     else
-        hipLaunchKernelGGL(k_puct_seat_rows<float>, dim3(grid_for(total)), dim3(kBlock), 0, s, a, e->s.N, n_cur,
-                           (float*)rows, cards);
+        hipLaunchKernelGGL(k_puct_seat_cols<float>, dim3(grid_for(total)), dim3(kBlock), 0, s, a, e->s.N, n_cur,
+                           (float*)cols, ks, cards);
     HIP_TRY(hipGetLastError());
     return SN_OK;
 }
 
-sn_status sn_puct_h1(sn_env* e, const sn_puct* q, int n_cur, const void* base, int hidden, const float* w1c,
-                     const float* cards, void* h1, int bf16, void* stream) {
+sn_status sn_puct_h1_cols(sn_env* e, const sn_puct* q, int n_cur, const void* baseT, int hidden, const float* w1c,
+                          const float* cards, void* h1T, int kp, int bf16, void* stream) {
     PuctArgs a{};
     sn_status st = puct_args(e, q, a);
     if (st != SN_OK) return st;
     if (n_cur < 1 || n_cur > a.n) return set_error(SN_EINVAL, "n_cur out of range");
-    if (hidden < 1 || hidden > 128) return set_error(SN_EINVAL, "hidden size out of range (1..128)");
-    if (!base || !w1c || !cards || !h1) return set_error(SN_EINVAL, "NULL argument");
-    const int64_t R = a.D * e->s.N * n_cur;
-    if (R >= (1ll << 31)) return set_error(SN_EINVAL, "too many rows");
-    const dim3 grid((unsigned)((R + 7) / 8)), blk(32, 8);
+    if (hidden < 1 || kp <= hidden || kp > 4096) return set_error(SN_EINVAL, "need 1 <= hidden < kp <= 4096");
+    if (!baseT || !w1c || !cards || !h1T) return set_error(SN_EINVAL, "NULL argument");
+    if (((uintptr_t)h1T) & 3) return set_error(SN_EINVAL, "h1T must be 4-B aligned");
+    const int64_t S = a.D * e->s.N, R = S * n_cur;
+    if (R * kp >= (1ll << 40) || R >= (1ll << 31)) return set_error(SN_EINVAL, "too many rows");
     hipStream_t s = (hipStream_t)stream;
+    const int64_t threads = (R + 1) / 2;
     if (bf16)
-        hipLaunchKernelGGL(k_puct_h1<__hip_bfloat16>, grid, blk, 0, s, (uint32_t)R, hidden, n_cur,
-                           (const __hip_bfloat16*)base, cards, w1c, (__hip_bfloat16*)h1);
+        hipLaunchKernelGGL(k_puct_h1_cols<__hip_bfloat16>, dim3(grid_for(threads)), dim3(kBlock), 0, s, (uint32_t)R,
+                           (uint32_t)S, hidden, kp, n_cur, (const __hip_bfloat16*)baseT, cards, w1c, (__hip_bfloat16*)h1T);
     else
-        hipLaunchKernelGGL(k_puct_h1<float>, grid, blk, 0, s, (uint32_t)R, hidden, n_cur, (const float*)base, cards, w1c,
-                           (float*)h1);
+        hipLaunchKernelGGL(k_puct_h1_cols<float>, dim3(grid_for(threads)), dim3(kBlock), 0, s, (uint32_t)R, (uint32_t)S,
+                           hidden, kp, n_cur, (const float*)baseT, cards, w1c, (float*)h1T);
     HIP_TRY(hipGetLastError());
     return SN_OK;
 }

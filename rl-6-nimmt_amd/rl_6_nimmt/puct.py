@@ -63,22 +63,32 @@ class FusedMLP:
         return cls(net, layers, wp.t().contiguous(), bp, [h[0].out_features for h in heads])
 
     def split(self):
-        """layer 1 split for the rollout rows (sn_puct_seat_rows / sn_puct_h1):
-        (W1^T [48, H], b1, W1[:, 0] as f32 [H]) or None for other layouts"""
-        if self.layers is None or self.layers[0][0].shape[1] != ROW or self.layers[0][0].shape[0] > 128:
+        """the feature-major rollout form (sn_puct_seat_cols / sn_puct_h1_cols):
+        augmented weights with each bias as the column against a ones feature
+        -- W1a [H, 56] = [W1 | b1 | 0] (column 0, the card, meets a zero),
+        per later hidden layer [Wa | ba | 0; 0 | 1 | 0] (the ones feature
+        passes through its ReLU), the head [Wh | bh | 0] (16 rows) -- plus
+        W1[:, 0] as f32; None for other layouts"""
+        if self.layers is None or self.layers[0][0].shape[1] != ROW:
             return None
         if not hasattr(self, "_split"):
-            w, b = self.layers[0]
-            self._split = (w.t().contiguous(), b, w[:, 0].float().contiguous())
+            w1, b1 = self.layers[0]
+            H = w1.shape[0]
+            pad = lambda n: -(-(n + 1) // 8) * 8  # noqa: E731  features + the ones feature, to 8
+            w1a = torch.zeros((H, 56), dtype=w1.dtype, device=w1.device)
+            w1a[:, :ROW], w1a[:, ROW] = w1, b1
+            hidden, kin = [], pad(H)
+            for w, b in self.layers[1:]:
+                ho = w.shape[0]
+                wa = torch.zeros((pad(ho), kin), dtype=w.dtype, device=w.device)
+                wa[:ho, : w.shape[1]], wa[:ho, w.shape[1]], wa[ho, w.shape[1]] = w, b, 1
+                hidden.append(wa)
+                kin = pad(ho)
+            hw, hb = self.head_w.t(), self.head_b  # [16, last]
+            ha = torch.zeros((hw.shape[0], kin), dtype=hw.dtype, device=hw.device)
+            ha[:, : hw.shape[1]], ha[:, hw.shape[1]] = hw, hb
+            self._split = (w1a, H, pad(H), hidden, ha, w1[:, 0].float().contiguous())
         return self._split
-
-    def tail(self, h1):
-        """the layers after the first on layer-1 activations: the padded head
-        output [rows, 16] (column 0 = the policy logit)"""
-        h = h1
-        for w, b in self.layers[1:]:
-            h = torch._addmm_activation(b, h, w.t())
-        return torch.addmm(self.head_b, h, self.head_w)
 
     def __call__(self, rows):
         if self.layers is None:
@@ -150,6 +160,9 @@ class BatchedPUCT:
             net = copy.deepcopy(self.actor).to(self.env.device, self.net_dtype)
             net.eval()
             self._net, self._net_version = FusedMLP.of(net), version
+            sp = self._net.split()  # built here: a graph capture may not allocate
+            if sp is not None:
+                self._split_bufs(sp[1], sp[2])
         return self._net
 
     def actor_device(self):
@@ -241,26 +254,31 @@ class BatchedPUCT:
         sp = self._net.split() if self.split_l1 else None
         if sp is not None:
             # layer 1 once per rollout seat + the card column per candidate
-            # (sn_puct_h1); the padded head's bf16/f32 output feeds
-            # sn_puct_step in place (column 0, stride 16)
-            w1t, b1, w1c = sp
-            seat_rows, cards, h1 = self._split_bufs(n, w1t.shape[1])
+            # (sn_puct_h1_cols), feature-major GEMMs with the biases inside,
+            # the head's first output row (bf16/f32) straight into sn_puct_step
+            w1a, H, kp, hidden, ha, w1c = sp
             S = self.D * N
+            cols, cards, h1, zb = self._split_bufs(H, kp)
+            ct = cols[: 56 * S].view(56, S)
             for r in range(self.n_mc(n)):
                 q.rollout = r
                 nat.check(L.sn_puct_deal(h, ctypes_ref(q), st), "sn_puct_deal")
                 for t in range(n):
                     m = n - t
-                    nat.check(L.sn_puct_seat_rows(h, ctypes_ref(q), m, nat.ptr(seat_rows[:S]), nat.ptr(cards), bf16, st),
-                              "sn_puct_seat_rows")
-                    base = torch.addmm(b1, seat_rows[:S], w1t)
-                    hv = h1[: S * m]
-                    nat.check(L.sn_puct_h1(h, ctypes_ref(q), m, nat.ptr(base), base.shape[1], nat.ptr(w1c), nat.ptr(cards),
-                                           nat.ptr(hv), bf16, st), "sn_puct_h1")
+                    R = S * m
+                    nat.check(L.sn_puct_seat_cols(h, ctypes_ref(q), m, nat.ptr(ct), 56, nat.ptr(cards), bf16, st),
+                              "sn_puct_seat_cols")
+                    base = torch.mm(w1a, ct)  # [H, S]
+                    hv = h1[: kp * R].view(kp, R)
+                    nat.check(L.sn_puct_h1_cols(h, ctypes_ref(q), m, nat.ptr(base), H, nat.ptr(w1c), nat.ptr(cards),
+                                                nat.ptr(hv), kp, bf16, st), "sn_puct_h1_cols")
                     with torch.no_grad():
-                        out = self._net.tail(hv)
-                    self.rows_evaluated += S * m
-                    q.logit_stride, q.logit_bf16 = out.stride(0), int(out.dtype == torch.bfloat16)
+                        x = hv
+                        for wa in hidden:
+                            x = torch._addmm_activation(zb[:R], wa, x)
+                        out = torch.mm(ha, x)  # [16, R]: row 0 = the policy logits
+                    self.rows_evaluated += R
+                    q.logit_stride, q.logit_bf16 = 1, int(out.dtype == torch.bfloat16)
                     nat.check(L.sn_puct_step(h, ctypes_ref(q), nat.ptr(out), t, m, st), "sn_puct_step")
                     q.logit_stride, q.logit_bf16 = 0, 0
             return
@@ -274,16 +292,18 @@ class BatchedPUCT:
                 nat.check(L.sn_puct_rows(h, ctypes_ref(q), m, nat.ptr(views[m]), bf16, st), "sn_puct_rows")
                 nat.check(L.sn_puct_step(h, ctypes_ref(q), nat.ptr(self._logits(views[m])), t, m, st), "sn_puct_step")
 
-    def _split_bufs(self, n, H):
-        """seat rows [D_max*N][48], candidate cards [D_max*N*10] f32 and the
-        layer-1 activations [D_max*N*10][H] (views of these serve every hand size)"""
+    def _split_bufs(self, H, kp):
+        """seat columns [56][D_max*N], candidate cards [D_max*N*10] f32, the
+        layer-1 activations [kp][rows] and a zero epilogue bias [rows] (flat:
+        views of these serve every hand size)"""
         N = self.env.num_players
-        if getattr(self, "_sbufs", None) is None or self._sbufs[2].shape[1] != H:
+        if getattr(self, "_sbufs", None) is None or self._sbufs[2].numel() != kp * self.D_max * N * 10:
             dev = self.env.device
             S = self.D_max * N
-            self._sbufs = (torch.empty((S, ROW), dtype=self.net_dtype, device=dev),
+            self._sbufs = (torch.empty((56 * S,), dtype=self.net_dtype, device=dev),
                            torch.empty((S * 10,), dtype=torch.float32, device=dev),
-                           torch.empty((S * 10, H), dtype=self.net_dtype, device=dev))
+                           torch.empty((kp * S * 10,), dtype=self.net_dtype, device=dev),
+                           torch.zeros((S * 10,), dtype=self.net_dtype, device=dev))
         return self._sbufs
 
     def _bufs(self, n):

@@ -244,10 +244,12 @@ def test_graph_replay_equals_eager_search(dtype):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_layer1_split_equals_full_rows(dtype):
-    """sn_puct_seat_rows + the per-seat GEMM + sn_puct_h1 give the first
-    layer's activations of every candidate row: relu(rows @ W1^T + b1) over
-    sn_puct_rows' full [card, obs] rows (f32: to 1e-5; bf16: the base is
-    rounded once more, to 2 bf16 ulps)."""
+    """sn_puct_seat_cols + the per-seat GEMM + sn_puct_h1_cols give the first
+    layer's activations of every candidate row, feature-major: relu(rows @
+    W1^T + b1) over sn_puct_rows' full [card, obs] rows (f32: to 1e-5; bf16:
+    the per-seat part is rounded once more, to 2 bf16 ulps), then the ones
+    feature and zero padding; and the augmented later layers + head equal the
+    module's own forward on those rows."""
     import ctypes
 
     from rl_6_nimmt import _native as nat
@@ -257,30 +259,38 @@ def test_layer1_split_equals_full_rows(dtype):
     for t in range(10 - n):
         env.step(eng.decide(10 - t))
     net = eng.sync_net()
-    w1t, b1, w1c = net.split()
+    w1a, H, kp, hidden, ha, w1c = net.split()
+    w1, b1 = net.layers[0]
     q = eng._params(n)
     L, h, st = nat.lib(), env._h, env._stream()
     eng.memorize()
     nat.check(L.sn_puct_deal(h, ctypes.byref(q), st), "deal")
     bf = int(dtype == torch.bfloat16)
+    tol = 1e-5 if dtype == torch.float32 else 2 ** -6
     for m in (n, 3, 1):
         S, R = eng.D * N, eng.D * N * m
         rows = torch.empty((R, 48), dtype=dtype, device=env.device)
         nat.check(L.sn_puct_rows(h, ctypes.byref(q), m, nat.ptr(rows), bf, st), "rows")
-        ref = torch.relu(rows.float() @ w1t.float() + b1.float())
-        seat = torch.empty((S, 48), dtype=dtype, device=env.device)
+        ref = torch.relu(rows.float() @ w1.float().t() + b1.float())
+        cols = torch.empty((56, S), dtype=dtype, device=env.device)
         cards = torch.empty((R,), dtype=torch.float32, device=env.device)
-        nat.check(L.sn_puct_seat_rows(h, ctypes.byref(q), m, nat.ptr(seat), nat.ptr(cards), bf, st), "seat_rows")
-        assert torch.equal(seat[:, 1:], rows.view(S, m, 48)[:, 0, 1:]) and (seat[:, 0] == 0).all()
+        nat.check(L.sn_puct_seat_cols(h, ctypes.byref(q), m, nat.ptr(cols), 56, nat.ptr(cards), bf, st), "seat_cols")
+        assert torch.equal(cols[1:48].t(), rows.view(S, m, 48)[:, 0, 1:]) and (cols[0] == 0).all()
+        assert (cols[48] == 1).all() and (cols[49:] == 0).all()
         assert torch.equal(cards, rows[:, 0].float())
-        base = torch.addmm(b1, seat, w1t)
-        h1 = torch.empty((R, w1t.shape[1]), dtype=dtype, device=env.device)
-        nat.check(L.sn_puct_h1(h, ctypes.byref(q), m, nat.ptr(base), base.shape[1], nat.ptr(w1c), nat.ptr(cards),
-                               nat.ptr(h1), bf, st), "h1")
-        if dtype == torch.float32:
-            assert torch.allclose(h1, ref, rtol=1e-5, atol=1e-5)
-        else:
-            assert torch.allclose(h1.float(), ref, rtol=2 ** -6, atol=2 ** -6), (h1.float() - ref).abs().max()
+        base = torch.mm(w1a, cols)
+        h1 = torch.empty((kp, R), dtype=dtype, device=env.device)
+        nat.check(L.sn_puct_h1_cols(h, ctypes.byref(q), m, nat.ptr(base), H, nat.ptr(w1c), nat.ptr(cards),
+                                    nat.ptr(h1), kp, bf, st), "h1_cols")
+        assert torch.allclose(h1[:H].t().float(), ref, rtol=tol, atol=tol), (h1[:H].t().float() - ref).abs().max()
+        assert (h1[H] == 1).all() and (h1[H + 1:] == 0).all()
+        x = h1
+        for wa in hidden:
+            x = torch._addmm_activation(torch.zeros(R, dtype=dtype, device=env.device), wa, x)
+        out = torch.mm(ha, x)[0].float()
+        with torch.no_grad():
+            (want,) = net.module(rows)
+        assert torch.allclose(out, want[:, 0].float(), rtol=4 * tol, atol=4 * tol), (out - want[:, 0].float()).abs().max()
 
 
 def test_search_statistics_consistent_bf16_full_size():
