@@ -325,22 +325,6 @@ def bench_mcs(games, rollouts, episodes=1):
     }
 
 
-# TunableOp selections for the config-4 GEMM shapes (tools/tune_puct.py on an
-# MI355X of this image): loaded, tuning off, when present
-PUCT_TUNED = os.environ.get("SECHS_PUCT_TUNED", os.path.join(ROOT, "profiles", "tunableop_puct_gfx950.csv"))
-
-
-def _tunableop(path):
-    if not os.path.exists(path):
-        return None
-    import torch.cuda.tunable as tun
-
-    tun.enable(True)
-    tun.tuning_enable(False)
-    tun.read_file(path)
-    return os.path.relpath(path, ROOT)
-
-
 def bench_puct(games, mc_max=100, mc_per_card=10):
     """BASELINE config 4: Alpha0.5 (PUCT) self-play, every seat of `games`
     4-player games searches with the reference's defaults (mc_max=100,
@@ -351,7 +335,6 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
     from rl_6_nimmt.puct import BatchedPUCT, make_actor
     from rl_6_nimmt.vec_env import VecSechsNimmtEnv
 
-    tuned = _tunableop(PUCT_TUNED)
     env = VecSechsNimmtEnv(games, N_PLAYERS, seed=3, rng="philox")
     torch.manual_seed(0)
     eng = BatchedPUCT(env, make_actor(), mc_per_card=mc_per_card, mc_max=mc_max, seed=4, net_dtype=torch.bfloat16,
@@ -388,7 +371,6 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
                      "kernel": "policy MLP (PyTorch-ROCm hipBLASLt bf16, ReLU fused in the GEMM epilogue), whole "
                                "game wall time incl. the k_puct_* kernels"},
         "wall_s": wall,
-        "gemm_selection": tuned or "hipBLASLt default heuristics",
         "mean_score_per_seat": total.double().mean(dim=0).tolist(),
     }
 
