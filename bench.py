@@ -748,6 +748,8 @@ def main():
             result["extra_config3_mcs"] = bench_mcs(args.mcs_games, args.mcs_rollouts)
         if want("scalar"):
             result["extra_config1_scalar"] = bench_scalar()
+        if want("acer"):
+            result["extra_acer"] = bench_acer(args.puct_games // 2)
         if rank == 0:
             print(json.dumps(result), flush=True)
         return

@@ -98,18 +98,30 @@ class BatchedACER(BatchedPUCT):
             return self.actions
         bf16 = int(self.net_dtype == torch.bfloat16)
         q = self._params(n)
-        self.sync_net()
-        rows = torch.empty((self.D * n, ROW), dtype=self.net_dtype, device=self.env.device)
-        nat.check(L.sn_puct_root_rows(h, ctypes_ref(q), nat.ptr(rows), bf16, st), "sn_puct_root_rows")
-        with torch.no_grad():
-            logit, _ = self._net(rows)
-        self.rows_evaluated += rows.shape[0]
-        logits = logit.reshape(-1).float().contiguous()
+        # recording with the actor on this device: the training-precision
+        # forward (fp32 rows) is the one sampled from, so the behaviour log pi
+        # is that forward's and no second, inference-dtype pass is needed
+        train_fwd = record and self.net_dtype != torch.float32 and self.actor_device() == self.env.device
+        if train_fwd:
+            r32 = self._train_rows(q, n, None)
+            with torch.no_grad():
+                lt, _ = self.actor(r32)
+            logits = lt.reshape(-1).float().contiguous()
+            self.rows_evaluated += r32.shape[0]
+        else:
+            self.sync_net()
+            rows = torch.empty((self.D * n, ROW), dtype=self.net_dtype, device=self.env.device)
+            nat.check(L.sn_puct_root_rows(h, ctypes_ref(q), nat.ptr(rows), bf16, st), "sn_puct_root_rows")
+            with torch.no_grad():
+                logit, _ = self._net(rows)
+            self.rows_evaluated += rows.shape[0]
+            logits = logit.reshape(-1).float().contiguous()
         nat.check(L.sn_policy_sample(h, ctypes_ref(q), nat.ptr(logits), nat.ptr(self.actions), nat.ptr(self.best_index),
                                      nat.ptr(self.log_prob), nat.ptr(self.entropy), st), "sn_policy_sample")
         if record:
             s, t, D = self.episodes % self.capacity, T_STEPS - n, self.D
-            r32 = self._train_rows(q, n, rows)
+            if not train_fwd:
+                r32 = self._train_rows(q, n, rows)
             self.rep_rows[s, t, :D, :n] = r32.view(D, n, ROW)
             self.rep_rows[s, t, :D, n:] = 0.0
             self.rep_act[s, t, :D] = self.best_index[:D].long()
@@ -117,7 +129,7 @@ class BatchedACER(BatchedPUCT):
             # behaviour log pi in the training forward's precision (fp32), so that
             # rho = pi_now / pi_then is exactly 1 on-policy as in the reference
             # (the bf16 inference logits differ from it by rounding)
-            if self.net_dtype == torch.float32:
+            if self.net_dtype == torch.float32 or train_fwd:
                 lt = logits.view(self.D, n)
             else:
                 with torch.no_grad():

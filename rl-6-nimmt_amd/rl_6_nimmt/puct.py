@@ -239,7 +239,7 @@ class BatchedPUCT:
     def _train_rows(self, q, n, rows):
         """the root rows of a recorded decision in fp32, as the reference's
         training forward sees them (inference may run on bf16 rows)"""
-        if rows.dtype == torch.float32:
+        if rows is not None and rows.dtype == torch.float32:
             return rows.clone()
         r32 = torch.empty((self.D * n, ROW), dtype=torch.float32, device=self.env.device)
         nat.check(nat.lib().sn_puct_root_rows(self.env._h, ctypes_ref(q), nat.ptr(r32), 0, self.env._stream()),
