@@ -707,8 +707,9 @@ def bench_acer(games, episodes=3):
         torch.cuda.synchronize()
         play, learn = play + t1 - t0, learn + time.perf_counter() - t1
     return {
-        "workload": f"ACER: {games} x 4-player games, all seats BatchedACER (bf16 2-head MLP 48-100-100-(1,1) via "
-                    f"PyTorch-ROCm, Philox sampler), replay of 4 episodes, {episodes} timed games + updates",
+        "workload": f"ACER: {games} x 4-player games, all seats BatchedACER (2-head MLP 48-100-100-(1,1) via "
+                    f"PyTorch-ROCm: recording self-play samples from the fp32 training forward, Philox sampler), "
+                    f"replay of 4 episodes, {episodes} timed games + updates",
         "value": 10 * games * episodes / play,
         "unit": "env-steps/s (self-play)",
         "decisions_per_s": 10 * N_PLAYERS * games * episodes / play,
