@@ -272,7 +272,45 @@ __global__ void k_puct_seat_cols(PuctArgs a, int N, int n_cur, T* cols, int ks, 
 }
 
 // h1T[j][r] = relu(baseT[j][r / n_cur] + cards[r] * w1c[j]) for j < H, 1 at
-// j = H (the next layer's bias feature), 0 up to kp; two rows per thread
+// j = H (the next layer's bias feature), 0 up to kp; four rows per thread
+// (one 8-B store per feature in bf16) when R % 4 == 0
+template <typename T>
+__global__ __launch_bounds__(256) void k_puct_h1_cols4(uint32_t R, uint32_t S, int H, int kp, int n_cur, const T* baseT,
+                                                       const float* cards, const float* w1c, T* h1T) {
+    const uint32_t r = 4u * (blockIdx.x * blockDim.x + threadIdx.x);
+    if (r >= R) return;
+    uint32_t sd[4];
+    float x[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) sd[u] = (r + u) / (uint32_t)n_cur, x[u] = cards[r + u];
+#pragma unroll 4
+    for (int j = 0; j < kp; j++) {
+        float v[4];
+        if (j < H) {
+            const float w = w1c[j];
+            const T* bj = baseT + (size_t)j * S;
+#pragma unroll
+            for (int u = 0; u < 4; u++) v[u] = fmaxf((float)bj[sd[u]] + x[u] * w, 0.f);
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; u++) v[u] = (j == H) ? 1.f : 0.f;
+        }
+        T* o = h1T + (size_t)j * R + r;
+        if constexpr (sizeof(T) == 2) {
+            uint16_t hb[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const __hip_bfloat16 b = __float2bfloat16(v[u]);
+                hb[u] = *(const uint16_t*)&b;
+            }
+            *(uint2*)o = make_uint2((uint32_t)hb[0] | ((uint32_t)hb[1] << 16), (uint32_t)hb[2] | ((uint32_t)hb[3] << 16));
+        } else {
+            *(float4*)o = make_float4(v[0], v[1], v[2], v[3]);
+        }
+    }
+}
+
+// the general form: two rows per thread
 template <typename T>
 __global__ __launch_bounds__(256) void k_puct_h1_cols(uint32_t R, uint32_t S, int H, int kp, int n_cur, const T* baseT,
                                                       const float* cards, const float* w1c, T* h1T) {
@@ -700,6 +738,17 @@ sn_status sn_puct_h1_cols(sn_env* e, const sn_puct* q, int n_cur, const void* ba
     if (R * kp >= (1ll << 40) || R >= (1ll << 31)) return set_error(SN_EINVAL, "too many rows");
     hipStream_t s = (hipStream_t)stream;
     const int64_t threads = (R + 1) / 2;
+    if ((R & 3) == 0 && (((uintptr_t)h1T) & 15) == 0) {  // 4-row groups: 8-B (bf16) / 16-B (f32) aligned stores
+        if (bf16)
+            hipLaunchKernelGGL(k_puct_h1_cols4<__hip_bfloat16>, dim3(grid_for(R / 4)), dim3(kBlock), 0, s, (uint32_t)R,
+                               (uint32_t)S, hidden, kp, n_cur, (const __hip_bfloat16*)baseT, cards, w1c,
+                               (__hip_bfloat16*)h1T);
+        else
+            hipLaunchKernelGGL(k_puct_h1_cols4<float>, dim3(grid_for(R / 4)), dim3(kBlock), 0, s, (uint32_t)R, (uint32_t)S,
+                               hidden, kp, n_cur, (const float*)baseT, cards, w1c, (float*)h1T);
+        HIP_TRY(hipGetLastError());
+        return SN_OK;
+    }
     if (bf16)
         hipLaunchKernelGGL(k_puct_h1_cols<__hip_bfloat16>, dim3(grid_for(threads)), dim3(kBlock), 0, s, (uint32_t)R,
                            (uint32_t)S, hidden, kp, n_cur, (const __hip_bfloat16*)baseT, cards, w1c, (__hip_bfloat16*)h1T);
