@@ -21,6 +21,7 @@
 // Tournament.play_game, tournament.py:132-138), so the roster may change
 // between games (Tournament.evolve).
 #include "sechs_mcs.h"
+#include "sechs_mcs_wave.h"
 
 using namespace sechs;
 
@@ -76,14 +77,29 @@ __global__ __launch_bounds__(kBlock) void k_league_step(DevState s, LeagueStepAr
     }
     if (G.n == 0u) bad = 0;
     if (a.invalid) a.invalid[g] = bad;
+    const int32_t pf = s.lpf ? s.lpf[g] : 0;
+    if (pf) s.lpf[g] = 0;
     if (bad >= 0) return;
+    if (pf) {  // k_league_mcs drew this slot's step: its non-external seats' cards
+#pragma unroll
+        for (int p = 0; p < N; p++) {
+            if ((uint32_t)p >= k) continue;
+            const uint32_t agent = (lg >> (4 + 4 * p)) & 15u;
+            if (((a.kinds >> (4 * agent)) & 15u) == (uint64_t)SN_AGENT_EXTERNAL) continue;
+            idx[p] = (uint32_t)max(hand_find(G.hand[p], (uint32_t)s.lpc[g * N + p]), 0);
+        }
+    }
     MtGen gen;
     ByteBuf buf;
-    RngOf<RNG_NUMPY_MT>::load(s, g, gen, buf);
-    int32_t status = 0;
+    if (!pf) RngOf<RNG_NUMPY_MT>::load(s, g, gen, buf);
+    int32_t status = (pf >> 1) & 1;
 #pragma unroll
     for (int p = 0; p < N; p++) {  // GameSession.play_game: agents in seat order (play.py:38-41)
         if ((uint32_t)p >= k) continue;
+        if (pf) {
+            card[p] = hand_get(G.hand[p], idx[p]);
+            continue;
+        }
         const uint32_t agent = (lg >> (4 + 4 * p)) & 15u;
         const uint32_t kind = (uint32_t)((a.kinds >> (4 * agent)) & 15u);
         if (kind == SN_AGENT_RANDOM) {
@@ -132,7 +148,58 @@ __global__ __launch_bounds__(kBlock) void k_league_step(DevState s, LeagueStepAr
     }
     if (a.status) a.status[g] |= status;
     store_game<N>(s, g, G);
-    RngOf<RNG_NUMPY_MT>::store(s, g, gen, buf);
+    if (!pf) RngOf<RNG_NUMPY_MT>::store(s, g, gen, buf);
+}
+
+// One wave per slot whose game seats an MCSAgent this step (n >= 2): the
+// slot's draws in seat order -- DrunkHamster seats' legal[random_interval(n-1)],
+// MCS seats' whole searches (sechs_mcs_wave.h) -- on its numpy stream, the
+// cards to lpc for k_league_step, which then resolves the step.
+template <int N>
+__global__ __launch_bounds__(64) void k_league_mcs(DevState s, LeagueStepArgs a) {
+    __shared__ WmcsLds L;
+    const int64_t g = blockIdx.x;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t lg = s.lgs[g], k = lg & 15u;
+    bool any = false;
+    for (uint32_t p = 0; p < k; p++)
+        any |= ((a.kinds >> (4 * ((lg >> (4 + 4 * p)) & 15u))) & 15u) == (uint64_t)SN_AGENT_MCS;
+    if (!any) return;
+    Game<N> G;
+    load_game<N>(s, g, G);
+    if (G.n < 2u) return;  // the last card: no search (mcts.py:52-53), k_league_step plays it
+    const int64_t DN = s.B * N;
+    WaveMt m{L.st, L.stage, 0u, 0u, 0u, 0u, false};
+    wmt_load(m, s.mt + g * kMtN, s.mt_pos[g], lane);
+    int32_t q6s = 0;
+    for (uint32_t p = 0; p < k; p++) {  // GameSession.play_game: agents in seat order (play.py:38-41)
+        const uint32_t agent = (lg >> (4 + 4 * p)) & 15u;
+        const uint32_t kind = (uint32_t)((a.kinds >> (4 * agent)) & 15u);
+        uint32_t card = 0xFFu;
+        if (kind == SN_AGENT_RANDOM) {
+            const uint32_t mx = G.n - 1u;
+            wmt_draws(m, 1u, [&](uint32_t) -> uint32_t { return mx; }, L.dr, lane);
+            card = hand_get(G.hand[p], L.dr[0]);
+        } else if (kind == SN_AGENT_MCS) {
+            const int64_t dn = g * N + p;
+            u32x4 mem = {s.lmem[dn], s.lmem[DN + dn], s.lmem[2 * DN + dn], s.lmem[3 * DN + dn]};
+            mem = memorize(mem, G.n, (uint32_t)kMaxCards, G.hand[p], G.b);  // mcts.py:47-49, 62-73
+            if (lane == 0u) s.lmem[dn] = mem.x, s.lmem[DN + dn] = mem.y, s.lmem[2 * DN + dn] = mem.z, s.lmem[3 * DN + dn] = mem.w;
+            bool q6 = false;
+            const int mpc = a.mpc[agent], mmax = a.mmax[agent];
+            switch (k) {  // the playouts seat the game's k players (mcts.py:62-64)
+                case 2: card = wmcs_decide<2>(m, L, G.b, G.hand[p], G.n, mem, mpc, mmax, &q6, lane); break;
+                case 3: card = wmcs_decide<3>(m, L, G.b, G.hand[p], G.n, mem, mpc, mmax, &q6, lane); break;
+                case 4: card = wmcs_decide<4>(m, L, G.b, G.hand[p], G.n, mem, mpc, mmax, &q6, lane); break;
+                case 5: card = wmcs_decide<5>(m, L, G.b, G.hand[p], G.n, mem, mpc, mmax, &q6, lane); break;
+                default: card = wmcs_decide<6>(m, L, G.b, G.hand[p], G.n, mem, mpc, mmax, &q6, lane); break;
+            }
+            q6s |= q6 ? 1 : 0;
+        }
+        if (lane == 0u) s.lpc[g * N + p] = (int32_t)card;
+    }
+    wmt_store(m, s.mt + g * kMtN, s.mt_pos + g, s.mt0 + g, lane);
+    if (lane == 0u) s.lpf[g] = 1 | (q6s << 1);
 }
 
 // ============================================================================
@@ -156,11 +223,13 @@ sn_status sn_league_agents(sn_env* e, const int32_t* kinds, const int32_t* mc_pe
     }
     if (mcs && s.rng_mode != SN_RNG_NUMPY_MT)
         return set_error(SN_EINVAL, "MCSAgent seats draw from numpy MT19937 streams (rng_mode numpy)");
-    if (mcs && !s.lmem) {
+    if (mcs && !s.lmem) {  // card memory [4][B*N], then k_league_mcs's cards [B*N] and flags [B]
         HIP_TRY(hipSetDevice(e->device));
-        const size_t bytes = sizeof(uint32_t) * 4 * (size_t)s.B * s.N;
+        const size_t BN = (size_t)s.B * s.N, bytes = sizeof(uint32_t) * (5 * BN + (size_t)s.B);
         if (hipMalloc((void**)&s.lmem, bytes) != hipSuccess) return set_error(SN_ENOMEM, "league card memory");
         HIP_TRY(hipMemset(s.lmem, 0, bytes));
+        s.lpc = (int32_t*)(s.lmem + 4 * BN);
+        s.lpf = s.lpc + BN;
     }
     return SN_OK;
 }
@@ -187,6 +256,16 @@ sn_status sn_league_step(sn_env* e, const int32_t* actions, int32_t* rewards, in
     if (sn_pipe_sync(e, st) != SN_OK) return SN_EHIP;  // the step draws from the plain MT state
     a.actions = actions, a.rewards = rewards, a.played = played, a.records = records, a.invalid = invalid;
     a.status = status;
+    if (mcs && kHand - e->lg_phase >= 2) {  // the MCS seats' searches, one wave per slot
+        switch (s.N) {
+            case 2: hipLaunchKernelGGL((k_league_mcs<2>), dim3((unsigned)s.B), dim3(64), 0, st, s, a); break;
+            case 3: hipLaunchKernelGGL((k_league_mcs<3>), dim3((unsigned)s.B), dim3(64), 0, st, s, a); break;
+            case 4: hipLaunchKernelGGL((k_league_mcs<4>), dim3((unsigned)s.B), dim3(64), 0, st, s, a); break;
+            case 5: hipLaunchKernelGGL((k_league_mcs<5>), dim3((unsigned)s.B), dim3(64), 0, st, s, a); break;
+            default: hipLaunchKernelGGL((k_league_mcs<6>), dim3((unsigned)s.B), dim3(64), 0, st, s, a); break;
+        }
+        HIP_TRY(hipGetLastError());
+    }
     switch (s.N) {
         case 2: hipLaunchKernelGGL((k_league_step<2>), dim3(grid_for(s.B)), dim3(kBlock), 0, st, s, a); break;
         case 3: hipLaunchKernelGGL((k_league_step<3>), dim3(grid_for(s.B)), dim3(kBlock), 0, st, s, a); break;

@@ -64,6 +64,8 @@ struct DevState {
     uint32_t* lgs;   // [B]
     int lg_K, lg_lo, lg_hi, lg_pad;
     uint32_t* lmem;  // [4][B*N] card memory of MCSAgent seats (sn_league_step), word-major
+    int32_t* lpc;    // [B*N] cards k_league_mcs chose for the step (in lmem's allocation)
+    int32_t* lpf;    // [B] 1 (| 2: quirk Q6): lpc holds this step's non-external cards
 };
 
 constexpr int kPipeRing = 1024;  // ring bytes per game (>= lead + one launch)

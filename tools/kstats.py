@@ -6,7 +6,10 @@ import sqlite3
 import sys
 
 tag = sys.argv[1]
-db = glob.glob(f"gpurun_out/{tag}/prof/**/*.db", recursive=True)[0]
+dbs = glob.glob(f"gpurun_out/{tag}/prof/**/*.db", recursive=True)
+if not dbs:  # summarised on the GPU box already
+    sys.exit(print(open(f"gpurun_out/{tag}/kernel_stats.csv").read()[:3000]))
+db = dbs[0]
 c = sqlite3.connect(db)
 rows = c.execute("select name, count(*), sum(end-start), avg(end-start), min(end-start), max(end-start) from kernels "
                  "group by name order by sum(end-start) desc").fetchall()

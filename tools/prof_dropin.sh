@@ -11,6 +11,5 @@ mkdir -p $OUT
 cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 $R/bench.py --only $LEG > $OUT/leg.json 2> $OUT/leg.err
 rc=$?; tail -3 $OUT/leg.err; cut -c1-3000 $OUT/leg.json; [ $rc -ne 0 ] && { echo "rc=$rc"; exit $rc; }
-f=$(find $OUT/prof -name '*kernel_stats.csv' | head -1)
-[ -n "$f" ] && cp "$f" $OUT/kernel_stats.csv && head -12 $OUT/kernel_stats.csv | cut -c1-220
+cd $R && python3 tools/kstats.py $TAG 20 && rm -rf $OUT/prof
 echo done
