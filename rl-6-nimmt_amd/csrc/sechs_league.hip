@@ -169,7 +169,7 @@ __global__ __launch_bounds__(64) void k_league_mcs(DevState s, LeagueStepArgs a)
     load_game<N>(s, g, G);
     if (G.n < 2u) return;  // the last card: no search (mcts.py:52-53), k_league_step plays it
     const int64_t DN = s.B * N;
-    WaveMt m{L.st, L.stage, 0u, 0u, 0u, 0u, false};
+    WaveMt m{L.st, L.stage, 0u, 0u, 0u, 0u, false, nullptr};
     wmt_load(m, s.mt + g * kMtN, s.mt_pos[g], lane);
     int32_t q6s = 0;
     for (uint32_t p = 0; p < k; p++) {  // GameSession.play_game: agents in seat order (play.py:38-41)

@@ -14,6 +14,7 @@
 //    MCSAgent (numpy global state bridged in and out) and by a whole-game
 //    kernel that replays GameSession(MCSAgent / DrunkHamster seats).
 #include "sechs_mcs.h"
+#include "sechs_mcs_wave.h"
 
 using namespace sechs;
 
@@ -201,14 +202,6 @@ __global__ __launch_bounds__(kBlock) void k_mcs_play_exact(DevState s, ExactArgs
     RngOf<RNG_NUMPY_MT>::store(s, g, gen, buf);
 }
 
-// numpy form of a lane's MT state, in place (the device twin of sn_mt_get)
-__device__ int32_t mt_export(uint32_t* st, uint32_t code) {
-    const uint32_t p = code & 0x7FFu;
-    if (p > 0u && p < (uint32_t)kMtN)
-        for (uint32_t i = p; i < (uint32_t)kMtN; i++) st[i] = mt_mix(st[i], st[(i + 1u) % kMtN], st[(i + kMtM) % kMtN]);
-    return mt_numpy_pos(code);
-}
-
 struct DecideArgs {
     int64_t D;
     const int8_t* board;    // [D][4][6]
@@ -222,17 +215,18 @@ struct DecideArgs {
     int32_t* counts;        // [D][10]
 };
 
+// MCSAgent decisions (sn_mcs_decide_exact), one wave each (sechs_mcs_wave.h):
+// the numpy key and pos in LDS, the playouts' draws decoded 64 words per instruction and
+// played 64 at a time in the lanes; same words, same order, same outputs.
 template <int N>
-__global__ __launch_bounds__(kBlock) void k_mcs_decide_exact(DecideArgs a) {
-    __shared__ uint8_t lds[kBlock * kDeckStride];
-    const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (d >= a.D) return;
-    uint8_t* mine = lds + threadIdx.x * kDeckStride;
-    uint32_t* st = a.mt_keys + d * kMtN;
-    const int32_t np_pos = a.mt_pos[d];
-    MtGen gen;
-    ByteBuf buf;
-    gen.load(st, mt_code_from_numpy(np_pos), buf);
+__global__ __launch_bounds__(64) void k_mcs_decide_wave(DecideArgs a) {
+    __shared__ WmcsLds L;
+    __shared__ uint32_t head[64];
+    const int64_t d = blockIdx.x;
+    const uint32_t lane = threadIdx.x;
+    uint32_t* key = a.mt_keys + d * kMtN;
+    WaveMt m{L.st, L.stage, 0u, 0u, 0u, 0u, false, head};
+    wmt_load(m, key, mt_code_from_numpy(a.mt_pos[d]), lane);
     u32x4 hs = {0u, 0u, 0u, 0u};
     for (int k = 0; k < kHand; k++) {
         const int c = a.hand[d * kHand + k];
@@ -259,20 +253,21 @@ __global__ __launch_bounds__(kBlock) void k_mcs_decide_exact(DecideArgs a) {
     b.hi = u32x4{hi[0], hi[1], hi[2], hi[3]};
     const u32x4 av = {a.avail[d * 4 + 0], a.avail[d * 4 + 1], a.avail[d * 4 + 2], a.avail[d * 4 + 3]};
     const uint32_t n = hand_len(me);
-    int32_t sum[kHand], cnt[kHand];
     bool q6 = false;
     uint32_t c = hand_get(me, 0u);
-    if (n > 1u) c = mcs_decide_exact<N>(gen, buf, mine, b, me, n, av, a.mc_per_card, a.mc_max, sum, cnt, &q6);
-    else
-#pragma unroll
-        for (int i = 0; i < kHand; i++) sum[i] = 0, cnt[i] = 0;
-    a.actions[d] = q6 ? -(int32_t)c - 2 : (int32_t)c;  // -(card)-2 flags quirk Q6
-#pragma unroll
-    for (int i = 0; i < kHand; i++) {
-        if (a.sums) a.sums[d * kHand + i] = sum[i];
-        if (a.counts) a.counts[d * kHand + i] = cnt[i];
+    int32_t* sums = a.sums ? a.sums + d * kHand : nullptr;
+    int32_t* counts = a.counts ? a.counts + d * kHand : nullptr;
+    if (n > 1u) {
+        c = wmcs_decide<N>(m, L, b, me, n, av, a.mc_per_card, a.mc_max, &q6, lane, sums, counts);
+    } else if (lane < (uint32_t)kHand) {
+        if (sums) sums[lane] = 0;
+        if (counts) counts[lane] = 0;
     }
-    a.mt_pos[d] = mt_export(st, gen.save(buf));
+    const int32_t pos = wmt_store_numpy(m, key, lane);
+    if (lane == 0u) {
+        a.actions[d] = q6 ? -(int32_t)c - 2 : (int32_t)c;  // -(card)-2 flags quirk Q6
+        a.mt_pos[d] = pos;
+    }
 }
 
 // ============================================================================
@@ -344,14 +339,15 @@ sn_status sn_mcs_play_exact(sn_env* e, uint32_t mcs_seats, int mc_per_card, int 
 sn_status sn_mcs_decide_exact(int device, int64_t D, int num_players, const int8_t* board, const int8_t* hand,
                               const uint32_t* avail, int mc_per_card, int mc_max, uint32_t* mt_keys, int32_t* mt_pos,
                               int32_t* actions, int32_t* sums, int32_t* counts, void* stream) {
-    if (D <= 0 || !board || !hand || !avail || !mt_keys || !mt_pos || !actions) return set_error(SN_EINVAL, "bad argument");
+    if (D <= 0 || D > 0x7FFFFFFF || !board || !hand || !avail || !mt_keys || !mt_pos || !actions)
+        return set_error(SN_EINVAL, "bad argument");
     if (mc_per_card < 0 || mc_max < 0) return set_error(SN_EINVAL, "mc_per_card and mc_max must be >= 0");
     HIP_TRY(hipSetDevice(device));
     DecideArgs a{};
     a.D = D, a.board = board, a.hand = hand, a.avail = avail, a.mc_per_card = mc_per_card, a.mc_max = mc_max;
     a.mt_keys = mt_keys, a.mt_pos = mt_pos, a.actions = actions, a.sums = sums, a.counts = counts;
     hipStream_t st = (hipStream_t)stream;
-    SN_DISPATCH_N(num_players, hipLaunchKernelGGL((k_mcs_decide_exact<NN>), dim3(grid_for(D)), dim3(kBlock), 0, st, a));
+    SN_DISPATCH_N(num_players, hipLaunchKernelGGL((k_mcs_decide_wave<NN>), dim3((unsigned)D), dim3(64), 0, st, a));
     HIP_TRY(hipGetLastError());
     return SN_OK;
 }

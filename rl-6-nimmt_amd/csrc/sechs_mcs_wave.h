@@ -33,6 +33,7 @@ struct WaveMt {
     uint8_t* stage;  // LDS [kWmStage], by stream word index
     uint32_t T, rd, wr, mt0;
     bool mt0_set;
+    uint32_t* head;  // LDS [64] or NULL: the previous round's slots 0..63 when a new round starts (numpy export)
 };
 
 // import a state code: the twisted-unconsumed words st[T - rem .. T) (mod
@@ -49,7 +50,7 @@ __device__ __forceinline__ void wmt_load(WaveMt& m, const uint32_t* gst, uint32_
         idx = (idx >= (uint32_t)kMtN) ? idx - kMtN : idx;
         m.stage[w] = (uint8_t)(mt_temper(m.st[idx]) & 0xFFu);
     }
-    m.T = T, m.rd = 0u, m.wr = rem, m.mt0 = 0u, m.mt0_set = false;
+    m.T = T, m.rd = 0u, m.wr = rem, m.mt0 = 0u, m.mt0_set = false;  // (head: the caller's)
     __syncthreads();
 }
 
@@ -68,6 +69,7 @@ __device__ __forceinline__ void wmt_twist(WaveMt& m, uint32_t lane) {
         v = mt_mix(a, b, c);
     }
     __syncthreads();
+    if (S == 0u && m.head) m.head[lane] = a;
     if (lane < len) {
         m.st[idx] = v;
         m.stage[(m.wr + lane) & (kWmStage - 1u)] = (uint8_t)(mt_temper(v) & 0xFFu);
@@ -132,6 +134,22 @@ __device__ __forceinline__ void wmt_store(const WaveMt& m, uint32_t* gst, uint32
     }
 }
 
+// export in numpy's (key, pos) form: a consumer still in the previous round
+// (the stream ran at most one 64-word chunk into the next) gets that round's
+// key back from the saved head; otherwise the current round is finished in
+// place, as numpy twists whole blocks (mt_export, sechs_mcs.hip)
+__device__ __forceinline__ int32_t wmt_store_numpy(WaveMt& m, uint32_t* key, uint32_t lane) {
+    const uint32_t u = m.wr - m.rd;  // staged, unconsumed
+    if (m.head && u > m.T) {         // straddle: T <= 64
+        for (uint32_t i = lane; i < (uint32_t)kMtN; i += 64u) key[i] = (i < m.T) ? m.head[i] : m.st[i];
+        return (int32_t)(kMtN - (u - m.T));
+    }
+    const uint32_t pos = m.T - u;
+    while (m.T < (uint32_t)kMtN) wmt_twist(m, lane);
+    for (uint32_t i = lane; i < (uint32_t)kMtN; i += 64u) key[i] = m.st[i];
+    return (int32_t)pos;
+}
+
 // One playout (mcts.py:108-154) from its decoded draws d: shuffle the unseen
 // cards (ascending, `sorted`) in this lane's deck, deal the k-1 opponents n
 // cards each, play n rounds with uniform moves for every seat.
@@ -192,7 +210,8 @@ struct WmcsLds {
 // legal move got no playout (the reference raises IndexError, quirk Q6)
 template <int K>
 __device__ uint32_t wmcs_decide(WaveMt& m, WmcsLds& L, const Board& root, const Hand& me, uint32_t n, u32x4 avail,
-                                int mc_per_card, int mc_max, bool* q6, uint32_t lane) {
+                                int mc_per_card, int mc_max, bool* q6, uint32_t lane, int32_t* sums_out = nullptr,
+                                int32_t* counts_out = nullptr) {
     int64_t fact = 1;
     for (uint32_t i = 2; i <= n; i++) fact *= i;
     const uint32_t n_mc = (uint32_t)min((int64_t)mc_max, (int64_t)mc_per_card * fact);
@@ -234,6 +253,13 @@ __device__ uint32_t wmcs_decide(WaveMt& m, WmcsLds& L, const Board& root, const 
         for (int off = 32; off >= 1; off >>= 1) {
             sum[i] += __shfl_xor(sum[i], off);
             cnt[i] += __shfl_xor(cnt[i], off);
+        }
+    }
+    if (lane == 0u) {
+#pragma unroll
+        for (int i = 0; i < kHand; i++) {
+            if (sums_out) sums_out[i] = sum[i];
+            if (counts_out) counts_out[i] = cnt[i];
         }
     }
     uint32_t best = 0;
