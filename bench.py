@@ -548,7 +548,7 @@ def bench_league_mixed(world, rank, slots, mc_max=200, rounds=1, warmup=1):
     return out
 
 
-def bench_dropin(mcs_games=3, puct_games=2, tour_games=3, mc_max_tour=200):
+def bench_dropin(mcs_games=3, puct_games=3, tour_games=3, mc_max_tour=200):
     """The drop-in search path a reference user runs: s per
     game of GameSession(MCSAgent(), DrunkHamster() x 3) and GameSession(
     PUCTAgent() [training], DrunkHamster() x 3) -- SURVEY §6's cProfile setups,
@@ -559,9 +559,10 @@ def bench_dropin(mcs_games=3, puct_games=2, tour_games=3, mc_max_tour=200):
     from rl_6_nimmt import GameSession, Tournament
     from rl_6_nimmt.agents import DrunkHamster, MCSAgent, PUCTAgent
 
-    def per_game(sess, n):
-        np.random.seed(0)
-        sess.play_game()  # warm-up
+    def per_game(sess, n, warmup=1):
+        for w in range(warmup):  # kernels; a PUCT agent's rollout graphs (captured at a shape's second use)
+            np.random.seed(1000 + w)
+            sess.play_game()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for g in range(n):
@@ -578,7 +579,7 @@ def bench_dropin(mcs_games=3, puct_games=2, tour_games=3, mc_max_tour=200):
     puct = PUCTAgent()
     puct.train()
     out["puct_train_3random_s_per_game"] = per_game(GameSession(puct, DrunkHamster(), DrunkHamster(), DrunkHamster()),
-                                                    puct_games)
+                                                    puct_games, warmup=2)
     out["puct_reference_s_per_game"] = [11.6, 14.7]
     tour = Tournament(min_players=2, max_players=4)
     for name, agent in run_py_league(mc_max_tour, with_random=False):
@@ -594,7 +595,8 @@ def bench_dropin(mcs_games=3, puct_games=2, tour_games=3, mc_max_tour=200):
     out["tournament_reference_s_per_game"] = [21.47, 46.95]
     out["workload"] = (f"drop-in (one game at a time, host loop over the one-game device env): GameSession(MCSAgent() "
                        f"[mc_max 100], DrunkHamster x3) x {mcs_games}, GameSession(PUCTAgent() [mc_max 100, training], "
-                       f"DrunkHamster x3) x {puct_games}, Tournament(2, 4) of run.py's agents at mc_max={mc_max_tour} "
+                       f"DrunkHamster x3) x {puct_games} after 2 untimed (its rollout graphs are captured at a shape's second "
+                       f"decision), Tournament(2, 4) of run.py's agents at mc_max={mc_max_tour} "
                        f"(training) x {tour_games} games")
     out["reference_source"] = ("SURVEY.md §6 cProfile runs of the reference on this image's CPU (MCS, PUCT) and "
                                "experiments/simple_tournament.ipynb:158-410 (tournament)")

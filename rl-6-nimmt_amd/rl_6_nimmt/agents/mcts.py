@@ -3,9 +3,10 @@
 `MCSAgent` is a drop-in for the reference's: same constructor, card memory,
 `forward(state, legal_actions) -> (card, {"log_prob": ...})` and `learn`.
 Its playouts run on the GPU (sn_mcs_decide_exact): the numpy global RNG
-state is copied to the device, one lane runs all n_mc playouts in the
-reference's exact draw order, and the advanced state is copied back -- so a
-seeded GameSession makes the same choices as the reference.
+state is copied to the device, one wave decodes the n_mc playouts' draws in
+the reference's exact order (64 stream words per instruction) and plays them
+in its lanes, and the advanced state is copied back -- so a seeded
+GameSession makes the same choices as the reference.
 
 Deviation: where a legal move received no playout the
 reference raises IndexError from a debug f-string (mcts.py:167-170); this
@@ -157,16 +158,30 @@ class PolicyMCSAgent(BaseMCAgent):
         (logits,) = self.actor(self.preprocessor(batch))
         return self.softmax(logits).flatten()
 
+    def __getstate__(self):
+        # the device search engines (a GPU env handle, captured graphs) are
+        # caches: a copy (Tournament.copy_player) builds its own
+        d = super().__getstate__() if hasattr(super(), "__getstate__") else dict(self.__dict__)
+        d = dict(d)
+        d["_engine"] = None
+        d.pop("_engines", None)
+        return d
+
     def _search_engine(self):
         from ..puct import BatchedPUCT
         from ..vec_env import VecSechsNimmtEnv
 
-        if self._engine is None or self._engine.env.num_players != self.num_players:
+        # one engine per player count (a Tournament seats 2..4): each keeps its
+        # captured rollout graphs across games
+        engines = self.__dict__.setdefault("_engines", {})
+        eng = engines.get(self.num_players)
+        if eng is None:
             env = VecSechsNimmtEnv(1, self.num_players, seed=0, rng="philox")
-            self._engine = BatchedPUCT(env, self.actor, mc_per_card=self.mc_per_card, mc_max=self.mc_max,
-                                       c_puct=getattr(self, "c_puct", 2.0), seed=self.search_seed, seats_mask=1,
-                                       puct_root=self._puct_root, net_dtype=torch.float32)
-        eng = self._engine
+            eng = engines[self.num_players] = BatchedPUCT(
+                env, self.actor, mc_per_card=self.mc_per_card, mc_max=self.mc_max, c_puct=getattr(self, "c_puct", 2.0),
+                seed=self.search_seed, seats_mask=1, puct_root=self._puct_root, net_dtype=torch.float32, graph=True)
+            eng.graph_after = 1  # a shape's second decision captures it
+        self._engine = eng
         eng.mc_per_card, eng.mc_max = self.mc_per_card, self.mc_max
         eng.c_puct = float(getattr(self, "c_puct", 2.0))
         return eng

@@ -62,6 +62,29 @@ class FusedMLP:
         wp[: w.shape[0]], bp[: b.shape[0]] = w, b
         return cls(net, layers, wp.t().contiguous(), bp, [h[0].out_features for h in heads])
 
+    def refresh_from(self, actor):
+        """copy new weights of the same architecture into this net's tensors
+        in place (every derived tensor too): addresses stay, so captured
+        hipGraphs stay valid.  False if the layout differs."""
+        src, dst = dict(actor.named_parameters()), dict(self.module.named_parameters())
+        if src.keys() != dst.keys() or any(src[k].shape != dst[k].shape for k in dst):
+            return False
+        with torch.no_grad():
+            for k, v in dst.items():
+                v.copy_(src[k])
+            if self.layers is not None:
+                fresh = FusedMLP.of(self.module)
+                self.head_w.copy_(fresh.head_w)
+                self.head_b.copy_(fresh.head_b)
+                if hasattr(self, "_split"):
+                    for old, new in zip(self._split_tensors(), fresh._split_tensors()):
+                        old.copy_(new)
+        return True
+
+    def _split_tensors(self):
+        sp = self.split()
+        return [sp[0], *sp[3], sp[4], sp[5]] if sp is not None else []
+
     def split(self):
         """the feature-major rollout form (sn_puct_seat_cols / sn_puct_h1_cols):
         augmented weights with each bias as the column against a ones feature
@@ -141,11 +164,16 @@ class BatchedPUCT:
         self._net_version = None
         self.rows_evaluated = 0
         # graph=True: a decision's rollout chain (n_mc x [deal, n x (rows,
-        # MLP, step)] launches) is captured once per (hand size, net version)
-        # as a hipGraph (torch.cuda.CUDAGraph) and replayed for every
-        # decision; the kernels read the decision counter from step_dev
+        # MLP, step)] launches) is captured once per hand size as a hipGraph
+        # (torch.cuda.CUDAGraph) and replayed for every decision; the kernels
+        # read the decision counter from step_dev, new weights are copied
+        # into the captured tensors in place (FusedMLP.refresh_from).
+        # graph_after: uses of a shape that run eagerly before it is captured
+        # (1 for one-game drop-in agents, whose one-off shapes would cost a
+        # capture each)
         self.graph = bool(graph) and max_decisions is None
-        self._graphs = {}
+        self.graph_after = 0
+        self._graphs, self._graphs_seen = {}, {}
         # the rollout rows' layer 1 split (FusedMLP.split): once per seat + the card column
         self.split_l1 = True
         self._step_dev = torch.zeros((1,), dtype=torch.int32, device=dev)
@@ -154,8 +182,12 @@ class BatchedPUCT:
     def sync_net(self):
         """(re)build the device copy of the actor in net_dtype"""
         version = tuple(p._version for p in self.actor.parameters())
+        if self._net is not None and version != self._net_version and self._net.refresh_from(self.actor):
+            self._net_version = version  # updated in place: the captured graphs still hold
         if self._net is None or version != self._net_version:
             import copy
+
+            self._graphs = {}
 
             net = copy.deepcopy(self.actor).to(self.env.device, self.net_dtype)
             net.eval()
@@ -220,13 +252,17 @@ class BatchedPUCT:
                 # the same 32-bit counter as the eager path's q.step, as int32 bits
                 sid = self.step_id & 0xFFFFFFFF
                 self._step_dev.fill_(sid - (1 << 32) if sid >= (1 << 31) else sid)
-                g = self._graphs.get((n, self._net_version))
-                if g is None:
+                key = (n, self.n_mc(n), self.c_puct, self.puct_root, self.D)  # everything a capture bakes in
+                g = self._graphs.get(key)
+                if g is None and self._graphs_seen.get(key, 0) >= self.graph_after:
                     g = self._capture(n)
-                    self._graphs = {k: v for k, v in self._graphs.items() if k[1] == self._net_version}
-                    self._graphs[(n, self._net_version)] = g
-                g[0].replay()
-                self.rows_evaluated += g[1]
+                    self._graphs[key] = g
+                if g is None:
+                    self._graphs_seen[key] = self._graphs_seen.get(key, 0) + 1
+                    self._rollouts(n, q)
+                else:
+                    g[0].replay()
+                    self.rows_evaluated += g[1]
             else:
                 self._rollouts(n, q)
         nat.check(L.sn_puct_choose(h, ctypes_ref(q), nat.ptr(self.actions), nat.ptr(self.best_index), st),

@@ -346,6 +346,30 @@ def test_puct_beats_random_seats():
     assert total[0] > total[1:].mean() + 2.0, total
 
 
+def test_dropin_puct_agent_copies_after_searching():
+    """Tournament.copy_player deep-copies agents: a PUCTAgent that has
+    searched (device engines, captured graphs) copies without them, and the
+    copy searches with its own engine and the same weights."""
+    import copy
+
+    from rl_6_nimmt import GameSession
+    from rl_6_nimmt.agents import DrunkHamster, PUCTAgent
+
+    torch.manual_seed(0)
+    agent = PUCTAgent(mc_max=8, mc_per_card=2)
+    agent.train()
+    np.random.seed(1)
+    GameSession(agent, DrunkHamster(), DrunkHamster()).play_game()
+    clone = copy.deepcopy(agent)
+    assert clone._engine is None and not getattr(clone, "_engines", None)
+    for a, b in zip(agent.actor.parameters(), clone.actor.parameters()):
+        assert torch.equal(a, b)
+    np.random.seed(2)
+    sess = GameSession(clone, DrunkHamster(), DrunkHamster(), DrunkHamster())
+    sess.play_game()
+    assert (sess.results[0] <= 0).all()
+
+
 def test_dropin_puct_agent_session_and_learning():
     from rl_6_nimmt import GameSession
     from rl_6_nimmt.agents import DrunkHamster, PUCTAgent
