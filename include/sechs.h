@@ -157,17 +157,9 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          are in lockstep (after sn_reset; N <= 4, auto-reset):
                          1 (default) or 0 (never).  Measured (65 536 x 4p):
                          74 -> 59 us per 10 env-steps.  Numpy-compat handles
-                         always use the pipelined one-wave k_play.
-     SN_OPT_PIPE_DECODE  1: the pipelined twist-ahead also decodes every
-                         DrunkHamster draw of the next launches (numpy's masked
-                         rejection resolved 64 words at a time per game), so
-                         k_play reads policy indices and deal targets instead
-                         of words; 0 (default): k_play decodes the words itself.
-                         Measured (65 536 x 4p): k_play 74 -> 61 us, but the
-                         twist-ahead 65 -> 113 us, so the step is slower.
-                         Tournament handles and SN_OPT_PIPE_GPW 32 never decode. */
+                         always use the pipelined one-wave k_play. */
 enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3, SN_OPT_TIMING = 4, SN_OPT_PIPE_GPW = 5,
-       SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7, SN_OPT_PIPE_DECODE = 8 };
+       SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7 };
 sn_status sn_set_option(sn_env* env, int option, int value);
 /* pipelined rollouts whose draws ran past the twisted words (must be 0; a
    nonzero count means those games' draws are wrong) [sync].  The count is

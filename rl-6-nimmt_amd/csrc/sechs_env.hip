@@ -263,44 +263,16 @@ struct AheadArgs {
     int tout;  // ptend parity written
     int lead;  // words to keep twisted past the consumer (kPipeLead; smaller only to test the overrun path)
     uint32_t* perr_mirror;  // host-mapped copy of *perr, refreshed at launch start (off the play stream)
-    // DEC: decode the DrunkHamster draws ahead (k_play<RNG_NUMPY_DEC> consumes them)
-    int N, C1, P, R;  // seats, deal draws (C - 1), draws per record, record bytes
-    uint32_t invN;    // ceil(65536 / N): q / N for q < 9N as (q * invN) >> 16
-    int span;         // records' worth of draws to have decoded past the consumer of the launch before last
 };
 
-// Decoded-draw records.  Every random decision of the in-kernel DrunkHamster
-// self-play is a numpy random_interval whose maximum is known in advance:
-// the deal's Fisher-Yates draws j = random_interval(i), i = C-1 .. 1
-// (env.py:99-112), then per step with n cards left each seat's
-// legal[random_interval(n-1)] (agents/random.py:9) for n = 10 .. 2.  So the
-// draw sequence of a game is a fixed pattern of P = C-1 + 9N maxima per
-// episode ("record"), and decoding it needs the words only.  k_mt_ahead
-// decodes one game per wave, 64 consecutive stream words per instruction: a
-// word's draw index is its prefix count of accepted words, and whether it is
-// accepted depends on that index (numpy's masked rejection), so the wave
-// iterates acceptance -> ballot -> prefix counts (v_mbcnt) to the fixed point
-// (unique, and reached from the left; ~5.5 evaluations per 64 words).  The
-// accepted words' masked values go to the game's record ring (byte o of
-// record d / P for draw d: targets at o < C-1, step draws at kDecDP + ...),
-// the stream position after the last draw of every step to wpos (the numpy
-// state a consumer at that step boundary exports).
-__device__ __forceinline__ void dec_pattern(const AheadArgs& a, uint32_t o, uint32_t& m) {
-    const uint32_t q = o - (uint32_t)a.C1;
-    m = (o < (uint32_t)a.C1) ? (uint32_t)a.C1 - o : 9u - ((q * a.invN) >> 16);
-}
-
-template <bool INIT, bool DEC>
+template <bool INIT>
 __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
     constexpr uint32_t D = kMtN - kMtM;  // 227
     constexpr uint32_t P1 = 224;          // words twisted before any store (all inputs already in memory)
-    constexpr int kStage = 640;           // DEC: low bytes of this launch's words (and INIT's replayed ones)
-    __shared__ uint8_t stage_all[DEC ? (kBlock / 64) * kStage : 1];
     const int64_t g = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     if (g >= s.B) return;  // whole waves
     const uint32_t lane = threadIdx.x & 63u;
     const int64_t B = s.B;
-    uint8_t* stage = stage_all + (DEC ? (threadIdx.x >> 6) * kStage : 0);
     // publish the overrun count so far (every k_play before the running one)
     // to the host without a sync; sn_rollout reads it at entry
     if (g == 0 && lane == 0u && a.perr_mirror)
@@ -308,35 +280,11 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t* st = s.mt + g * kMtN;
     uint8_t* ring = (uint8_t*)s.pring;
-    uint32_t Tp, t0, c, rem = 0u;
-    // DEC: the decoder's words twisted by earlier launches, [dword, ptend) --
-    // in steady state ~212 (the twist leads the consumer by 600, the decoder
-    // it by two records): up to kOld of them staged (13 sd past the mean)
-    constexpr uint32_t kOld = 384;
-    uint32_t sbase = 0u, dw0 = 0u, old[kOld / 64];
-    uint32_t cd0 = 0u, dd0 = 0u;                            // DEC: consumer draw (launch before last), decoder draw
-    auto ring_at = [&](uint32_t pos) -> uint32_t {
-        const uint32_t ri = pos & (uint32_t)(kPipeRing - 1);
-        return ring[((int64_t)(ri >> 4) * B + g) * 16 + (ri & 15u)];
-    };
-    if (DEC && !INIT) {
-        // the decoder's words twisted by earlier launches, [dword, ptend): their
-        // loads go out before the twist's, land in the stage after it, so that
-        // the decode reads LDS only (a global load there would wait behind the
-        // twist's stores: vmcnt counts both in order)
-        dw0 = __builtin_amdgcn_readfirstlane(s.dword[g]);
-        cd0 = __builtin_amdgcn_readfirstlane(s.pcdraw[(int64_t)a.cin * B + g]);  // loaded here: a load after the
-        dd0 = __builtin_amdgcn_readfirstlane(s.ddraw[g]);                        // twist waits for its stores
-        const uint32_t te = __builtin_amdgcn_readfirstlane(s.ptend[(int64_t)a.tin * B + g]);
-        const int32_t nold = (int32_t)(te - dw0);
-        sbase = (nold > 0) ? min((uint32_t)nold, kOld) : 0u;
-#pragma unroll
-        for (uint32_t q = 0; q < kOld / 64; q++) old[q] = (64u * q + lane < sbase) ? ring_at(dw0 + 64u * q + lane) : 0u;
-    }
+    uint32_t Tp, t0, c;
     if (INIT) {
         const uint32_t code = s.mt_pos[g];
         Tp = code & 0x7FFu;
-        rem = (code >> 16) & kMtCntMask;
+        const uint32_t rem = (code >> 16) & kMtCntMask;
         t0 = 0u;
         c = 0u - rem;
         for (uint32_t k0 = 0; k0 < rem; k0 += 64u) {  // twisted, unconsumed: stream index Tp - rem + k (mod 624)
@@ -344,16 +292,14 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
             if (k < rem) {
                 const uint32_t v = st[(Tp + kMtN - rem + k) % (uint32_t)kMtN];
                 const uint32_t ri = (c + k) & (uint32_t)(kPipeRing - 1);
-                const uint8_t y = (uint8_t)(mt_temper(v) & 0xFFu);
-                ring[((int64_t)(ri >> 4) * B + g) * 16 + (ri & 15u)] = y;
-                if (DEC && k < (uint32_t)kStage) stage[k] = y;
+                ring[((int64_t)(ri >> 4) * B + g) * 16 + (ri & 15u)] = (uint8_t)(mt_temper(v) & 0xFFu);
             }
         }
         if (lane == 0u) s.pabsc[(int64_t)a.cin * B + g] = c;
     } else {
-        Tp = __builtin_amdgcn_readfirstlane(s.ptp[g]);
-        t0 = __builtin_amdgcn_readfirstlane(s.ptend[(int64_t)a.tin * B + g]);
-        c = __builtin_amdgcn_readfirstlane(s.pabsc[(int64_t)a.cin * B + g]);
+        Tp = s.ptp[g];
+        t0 = s.ptend[(int64_t)a.tin * B + g];
+        c = s.pabsc[(int64_t)a.cin * B + g];
     }
     // signed: a consumer past the twisted end means a play lane overran
     // (counted there too); twist nothing rather than underflow the lead
@@ -366,7 +312,6 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
         const uint32_t d = y | (__shfl_down(y, 1) << 8) | (__shfl_down(y, 2) << 16) | (__shfl_down(y, 3) << 24);
         const uint32_t ri = (t0 + j) & (uint32_t)(kPipeRing - 1);
         if ((lane & 3u) == 0u && j < n) st_nt((uint32_t*)(ring + ((int64_t)(ri >> 4) * B + g) * 16 + (ri & 12u)), d, SECHS_NT_MORE);
-        if (DEC && j < n && rem + sbase + j < (uint32_t)kStage) stage[rem + sbase + j] = (uint8_t)y;
     };
     // phase 1: words 0 .. min(n, 224)
     uint32_t A[4], Bv[4], Cv[4], IX[4];
@@ -381,14 +326,6 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
             Bv[b] = st[(idx + 1u == (uint32_t)kMtN) ? 0u : idx + 1u];
             Cv[b] = st[(idx < D) ? idx + kMtM : idx - D];
         }
-    }
-    if (DEC && !INIT) {
-        // every load so far has landed once phase 1 may start (and no store is
-        // in flight yet): stage the old words now, not behind the twist's stores
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-#pragma unroll
-        for (uint32_t q = 0; q < kOld / 64; q++)
-            if (64u * q + lane < sbase) stage[64u * q + lane] = (uint8_t)old[q];
     }
 #pragma unroll
     for (int b = 0; b < 4; b++) {
@@ -423,97 +360,6 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
         }
         s.ptp[g] = Tn;
         s.ptend[(int64_t)a.tout * B + g] = t0 + n;
-    }
-    if constexpr (DEC) {
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the staged bytes, written by other lanes
-        const uint32_t P = (uint32_t)a.P, C1 = (uint32_t)a.C1, NCH = (uint32_t)a.R >> 4;
-        uint32_t cd, dd, dw;  // wave-uniform (one game per wave): scalar registers
-        if (INIT) {
-            // the consumer's place in the draw pattern from its hand size (every
-            // seat holds n cards; a finished game without auto-reset draws no more)
-            const uint32_t hn = __builtin_amdgcn_readfirstlane(hand_len(load_hand(s, 0, g)));
-            const uint32_t phase = (hn >= 1u) ? kHand - hn : 9u;
-            cd = (phase >= 9u) ? P : C1 + phase * (uint32_t)a.N;
-            dd = cd, dw = c;
-            if (lane == 0u) {
-                s.pcdraw[(int64_t)a.cin * B + g] = cd;
-                const uint32_t r = cd / P, oo = cd - r * P;
-                const uint32_t b = (oo == 0u) ? 10u * r - 1u : 10u * r + (((oo - C1) * a.invN) >> 16);
-                s.wpos[(int64_t)(b & (kDecWB - 1)) * B + g] = c;
-            }
-        } else {
-            cd = cd0, dd = dd0, dw = dw0;
-        }
-        // the stage holds the words [lbase, wend): INIT from the replayed ones,
-        // steady from the decoder's first word (sbase old words, then this launch's)
-        const uint32_t target = cd + (uint32_t)a.span * P;
-        // (more than kOld old words: the stage ends there -- an overrun, counted)
-        const uint32_t wend = (!INIT && (int32_t)(t0 - dw) > (int32_t)kOld) ? dw + kOld : t0 + n, lbase = INIT ? c : dw;
-        uint32_t r0 = dd / P, o0 = dd - r0 * P;
-        // Per evaluation: ~12 VALU, the ballot, one compare + branch on the
-        // scalar unit (shared by the CU's 4 SIMDs: the first form of this loop,
-        // with the pattern as a branch and an iteration counter, spent ~250
-        // SALU per wave and made the kernel scalar-issue bound)
-        const uint32_t invN = a.invN, Nn = (uint32_t)a.N;
-        while ((int32_t)(target - dd) > 0) {
-            const uint32_t p = dw + lane;
-            const bool valid = (int32_t)(wend - p) > 0;
-            const uint64_t V = __ballot(valid);
-            const uint32_t x = (uint32_t)stage[min(p - lbase, (uint32_t)kStage - 1u)];
-            auto eval = [&](uint32_t pre, uint32_t& o, uint32_t& m) -> bool {
-                const uint32_t oa = o0 + pre;
-                o = min(oa, oa - P);  // oa < P: oa - P wraps above it (P >= 64: one record boundary at most)
-                const uint32_t t = __umul24((o - C1) & 0xFFu, invN) >> 16;  // (o - C1) / N, used when o >= C1
-                m = (o < C1) ? C1 - o : 9u - t;
-                return (x & (0xFFFFFFFFu >> __builtin_clz(m))) <= m;
-            };
-            uint32_t o, m;
-            // first guess: about 3 of 4 words accepted; then to the fixed point
-            uint64_t Acc = __ballot(eval((lane * 3u) >> 2, o, m)) & V;
-            while (true) {
-                const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(Acc >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)Acc, 0u));
-                const uint64_t A2 = __ballot(eval(pre, o, m)) & V;
-                if (A2 == Acc) break;
-                Acc = A2;
-            }
-            const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(Acc >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)Acc, 0u));
-            const bool acc = ((Acc >> lane) & 1ull) != 0ull;
-            (void)eval(pre, o, m);  // this lane's (o, m) at its draw
-            const uint32_t room = target - dd;  // draws still to decode (> 0)
-            const bool commit = acc && pre < room;
-            if (commit) {
-                const uint32_t r = r0 + ((o0 + pre >= P) ? 1u : 0u);
-                const uint32_t bo = (o < C1) ? o : (uint32_t)kDecDP + (o - C1);
-                const uint32_t slot = r & (uint32_t)(kDecRecs - 1);
-                s.drec[(((int64_t)slot * NCH + (bo >> 4)) * B + g) * 16 + (bo & 15u)] = (uint8_t)(x & (0xFFFFFFFFu >> __builtin_clz(m)));
-                // the step boundary this draw completes: after the deal (o == C-2), after a step's N draws
-                const uint32_t q1 = o - C1 + 1u;
-                const uint32_t t1 = __umul24(q1 & 0xFFu, invN) >> 16;
-                const bool endd = o + 1u == C1, ends = o >= C1 && t1 * Nn == q1;
-                if (endd || ends) s.wpos[(int64_t)((10u * r + (endd ? 0u : t1)) & (kDecWB - 1)) * B + g] = p + 1u;
-            }
-            const uint32_t na = (uint32_t)__popcll(Acc);
-            if (na >= room) {  // the target is in this batch: stop past the word of its last draw
-                const uint64_t Cm = __ballot(commit);
-                dw += 64u - (uint32_t)__builtin_clzll(Cm);
-                dd += room;
-                break;
-            }
-            const uint32_t nv = (uint32_t)__popcll(V);
-            dd += na;
-            dw += nv;
-            o0 += na;
-            if (o0 >= P) o0 -= P, r0 += 1u;
-            if (nv < 64u) {  // the twisted words ran out before the target: the consumer would overrun
-                if (lane == 0u) atomicAdd(s.perr, 1u);
-                break;
-            }
-        }
-        if (lane == 0u) {
-            s.ddraw[g] = dd;
-            s.dword[g] = dw;
-            s.dend[(int64_t)a.tout * B + g] = dd;
-        }
     }
 }
 
@@ -586,7 +432,6 @@ struct PlayArgs {
     int32_t* league_rec;     // league: [episodes][B][1 + N] per finished game: seats word, results
     int step0;               // league: env-steps of this rollout before this launch (episode index of a record)
     int n0;                  // k_play_split: every game's hand size at the launch's start (aligned handle)
-    int dec_P, dec_R;        // RNG_NUMPY_DEC: draws per record, record bytes
 };
 
 // The env-step loop of one lane (game g).  R supplies the random words
@@ -624,48 +469,6 @@ struct StreamSrc {
         shuffle_apply(deck, deck + kDeckStride, s.C);
         pp.mark(PH_APPLY);
         deal_from_deck<N>(deck, s.C, G);
-    }
-};
-
-// DecSrc: the draws k_mt_ahead decoded ahead (RNG_NUMPY_DEC).  The lane
-// copies the two records its launch can touch (the current one and the
-// next: a launch of <= 10 steps crosses at most one deal) to LDS at start;
-// a step's N policy indices are N consecutive bytes, the deal's Fisher-Yates
-// targets the next record's first C-1 bytes -- shuffle_apply reads them in
-// place.  No random word, rejection test or byte buffer in the step loop.
-template <int N>
-struct DecSrc {
-    uint8_t* win;   // LDS: records R0 and R0 + 1 (R bytes each)
-    uint8_t* deck;  // LDS deck slot
-    uint32_t cdraw, rb, o, P, C1, R;
-    __device__ __forceinline__ void load(const DevState& s, const PlayArgs& a, int64_t g, uint8_t* w, uint8_t* d);
-    __device__ __forceinline__ void draws(const Game<N>& G, int, uint32_t, bool, uint32_t (&idx)[N]) {
-        if (G.n <= 1u) {  // n == 1: legal[random_interval(0)] draws nothing
-#pragma unroll
-            for (int p = 0; p < N; p++) idx[p] = 0u;
-            return;
-        }
-        const uint8_t* q = win + rb + kDecDP + (o - C1);
-        if (N == 4) {  // kDecDP + 4t: one aligned dword
-            const uint32_t v = *(const uint32_t*)q;
-#pragma unroll
-            for (int p = 0; p < N; p++) idx[p] = (v >> (8 * p)) & 0xFFu;
-        } else {
-#pragma unroll
-            for (int p = 0; p < N; p++) idx[p] = q[p];
-        }
-        o += N;
-        cdraw += N;
-    }
-    __device__ __forceinline__ uint32_t league(const DevState&) { return 0u; }
-    __device__ __forceinline__ void deal(const DevState& s, Game<N>& G, PhaseProf& pp) {
-        if (o == P) rb += R, o = 0u;  // the next record (a launch that starts at a record's first draw reads its own)
-        for (int i = 0; i < s.C; i += 4) *(uint32_t*)(deck + i) = (uint32_t)i * 0x01010101u + 0x03020100u;
-        shuffle_apply(deck, win + rb, s.C);
-        pp.mark(PH_APPLY);
-        deal_from_deck<N>(deck, s.C, G);
-        o = C1;
-        cdraw += C1;
     }
 };
 
@@ -855,20 +658,7 @@ __device__ __forceinline__ void play_body(const DevState& s, const PlayArgs& a, 
     load_results<N>(s, g, a.flags, sum_res, episodes);
     uint32_t lg = LG ? s.lgs[g] : 0u;
     ByteBuf buf;
-    if constexpr (MODE == RNG_NUMPY_DEC) {
-        DecSrc<N> src;
-        src.load(s, a, g, wave_lds + a.wave_lds - 64 * a.ring_lds + lane * a.ring_lds, wave_lds + lane * kDealStride);
-        pp.mark(PH_PROLOGUE);
-        play_steps<N, DecSrc<N>, 64, false>(s, a, g, lane, wave_lds, G, src, sum_res, episodes, pp, lg, 0, a.steps);
-        // the consumer state the next twist-ahead leads: draw index, and the
-        // stream position of its step boundary (what the numpy state exports)
-        const int64_t B = s.B;
-        if ((int32_t)(src.cdraw - s.dend[(int64_t)a.pipe_t * B + g]) > 0) atomicAdd(s.perr, 1u);  // past the decoded draws
-        const uint32_t r = src.cdraw / src.P, oo = src.cdraw - r * src.P;
-        const uint32_t b = (oo == 0u) ? 10u * r - 1u : 10u * r + (oo - src.C1) / (uint32_t)N;
-        s.pcdraw[(int64_t)a.pipe_cout * B + g] = src.cdraw;
-        s.pabsc[(int64_t)a.pipe_cout * B + g] = s.wpos[(int64_t)(b & (kDecWB - 1)) * B + g];
-    } else if constexpr (MODE == RNG_NUMPY_PIPE) {
+    if constexpr (MODE == RNG_NUMPY_PIPE) {
         RingPipe rng;
         rng.load(s, g, buf, wave_lds + a.wave_lds - GPW * a.ring_lds + lane * a.ring_lds, a.pipe_cin, a.pipe_t);
         pp.mark(PH_PROLOGUE);
@@ -895,24 +685,6 @@ __device__ __forceinline__ void play_body(const DevState& s, const PlayArgs& a, 
     if (LG) s.lgs[g] = lg;
     pp.mark(PH_EPILOGUE);
     pp.flush(lane);
-}
-
-template <int N>
-__device__ __forceinline__ void DecSrc<N>::load(const DevState& s, const PlayArgs& a, int64_t g, uint8_t* w, uint8_t* d) {
-    win = w, deck = d;
-    P = (uint32_t)a.dec_P, R = (uint32_t)a.dec_R, C1 = (uint32_t)s.C - 1u;
-    cdraw = s.pcdraw[(int64_t)a.pipe_cin * s.B + g];
-    const uint32_t R0 = cdraw / P;
-    o = cdraw - R0 * P;
-    rb = 0u;
-    const uint32_t nch = R >> 4;
-#pragma unroll 4
-    for (uint32_t i = 0; i < 2u * nch; i++) {  // record R0 then R0 + 1: 16-B chunks, coalesced over the wave
-        const uint32_t slot = (R0 + (i >= nch ? 1u : 0u)) & (uint32_t)(kDecRecs - 1), q = (i >= nch) ? i - nch : i;
-        const u32x4 c = *(const u32x4*)(s.drec + (((int64_t)slot * nch + q) * s.B + g) * 16);
-        *(uint64_t*)(w + 16u * i) = (uint64_t)c.x | ((uint64_t)c.y << 32);  // 8-B aligned window (stride 2R + 8)
-        *(uint64_t*)(w + 16u * i + 8u) = (uint64_t)c.z | ((uint64_t)c.w << 32);
-    }
 }
 
 template <int N, int MODE, int GPW = 64, bool LG = false>
@@ -1466,9 +1238,6 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
     }
     e->chunk_steps = 10;
     e->pipe = 1;
-    e->pipe_dec = 0;  // measured: k_play 74 -> 61 us, but the decoding twist-ahead 65 -> 113 us
-    s.dec_P = num_cards - 1 + 9 * num_players;
-    s.dec_R = ((kDecDP + 9 * num_players) + 15) & ~15;
     e->pipe_gpw = 64;
     e->pipe_lead = kPipeLead;
     e->phase = -1;
@@ -1481,10 +1250,7 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
             size_t bytes;
         } pal[] = {{(void**)&s.pring, (size_t)kPipeRing * B}, {(void**)&s.pabsc, sizeof(uint32_t) * 2 * B},
                    {(void**)&s.ptend, sizeof(uint32_t) * 2 * B}, {(void**)&s.ptp, sizeof(uint32_t) * B},
-                   {(void**)&s.perr, sizeof(uint32_t)},
-                   {(void**)&s.drec, (size_t)kDecRecs * s.dec_R * B}, {(void**)&s.wpos, sizeof(uint32_t) * kDecWB * B},
-                   {(void**)&s.ddraw, sizeof(uint32_t) * B}, {(void**)&s.dword, sizeof(uint32_t) * B},
-                   {(void**)&s.dend, sizeof(uint32_t) * 2 * B}, {(void**)&s.pcdraw, sizeof(uint32_t) * 2 * B}};
+                   {(void**)&s.perr, sizeof(uint32_t)}};
         for (auto& a : pal) {
             if (hipMalloc(a.p, a.bytes) != hipSuccess) {
                 sn_destroy(e);
@@ -1544,8 +1310,7 @@ sn_status sn_destroy(sn_env* e) {
     if (e->side) (void)hipStreamDestroy(e->side);
     free_timing(e);
     void* ps[] = {s.hand, s.row_lo, s.row_hi, s.score, s.sum_res, s.episodes, s.mt_pos, s.ctr, s.mt, s.mt0, s.ring,
-                  s.pring, s.pabsc, s.ptend, s.ptp, s.perr, s.lgs, s.lmem, s.drec, s.wpos, s.ddraw, s.dword,
-                  s.dend, s.pcdraw};
+                  s.pring, s.pabsc, s.ptend, s.ptp, s.perr, s.lgs, s.lmem};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     delete e;
@@ -1590,10 +1355,6 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
         case SN_OPT_PIPE_GPW:
             if (value != 32 && value != 64) return fail(SN_EINVAL, "games per wave must be 32 or 64");
             e->pipe_gpw = value;
-            return SN_OK;
-        case SN_OPT_PIPE_DECODE:
-            if (value != 0 && value != 1) return fail(SN_EINVAL, "pipe decode must be 0 or 1");
-            e->pipe_dec = value;
             return SN_OK;
         case SN_OPT_PLAY_SPLIT:
             if (value < 0 || value > 1) return fail(SN_EINVAL, "play split must be 0 or 1");
@@ -1783,23 +1544,13 @@ sn_status sn_pipe_sync(sn_env* e, hipStream_t st) {
 // launches (one episode per pair) it is <= 6.1e-73 for every N <= 10.
 static int pipe_max_chunk(int N) { return N <= 4 ? 10 : 5; }
 
-// LDS a pipelined k_play block needs (obs staging / deck + the RingPipe windows,
-// or with decoded draws the two records' window, stride 2R + 8)
-static size_t pipe_lds(const DevState& s, const PlayArgs& a, int gpw, int* wave_out, bool dec = false) {
+// LDS a pipelined k_play block needs (obs staging / deck + the RingPipe windows)
+static size_t pipe_lds(const DevState& s, const PlayArgs& a, int gpw, int* wave_out) {
     int wave = gpw * kDealStride;
     if (a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15) == 0) wave = max(wave, gpw * s.N * 48);
-    wave += gpw * (dec ? 2 * s.dec_R + 8 : kPipeSlot);
+    wave += gpw * kPipeSlot;
     *wave_out = wave;
     return (size_t)wave * (kBlock / 64);
-}
-
-// decoded draws (k_mt_ahead<.., true> + k_play<RNG_NUMPY_DEC>) for a pipelined
-// handle: DrunkHamster games (not a tournament), 64 games per wave, at least
-// 64 draws per record (one record boundary per decode batch), LDS to spare
-static bool dec_ok(const sn_env* e, const PlayArgs& a) {
-    int wave;
-    return e->pipe_dec && !e->s.lg_K && e->pipe_gpw == 64 && e->s.dec_P >= 64 &&
-           pipe_lds(e->s, a, 64, &wave, true) <= (size_t)kLdsBytes;
 }
 
 // The pipelined numpy-MT rollout: per launch of <= 10 env-steps, k_play (on
@@ -1809,42 +1560,23 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     DevState& s = e->s;
     int wave;
     const int gpw = e->pipe_gpw;
-    // a tournament game adds its seat draw (<= K - 1 + 1 draws): 10-step
-    // launches keep the pair tail < 1e-26 up to K = 8 agents at N <= 4
-    // (tools/pipe_tail.py), beyond that 5-step launches
-    const int chunk = min(e->chunk_steps, (s.lg_K > 8) ? 5 : pipe_max_chunk(s.N));
-    if (!e->pvalid) e->pdec = dec_ok(e, a);  // the pipeline's mode is fixed until the next sn_pipe_sync
-    else if (e->pdec && !dec_ok(e, a)) {     // this launch needs the other mode (LDS): restart the pipeline
-        const sn_status r = sn_pipe_sync(e, st);
-        if (r != SN_OK) return r;
-        e->pdec = 0;
-    }
-    const bool dec = e->pdec != 0;
-    const size_t shmem = pipe_lds(s, a, gpw, &wave, dec);
+    const size_t shmem = pipe_lds(s, a, gpw, &wave);
     a.wave_lds = wave;
-    a.ring_lds = dec ? 2 * s.dec_R + 8 : kPipeSlot;
-    a.dec_P = s.dec_P, a.dec_R = s.dec_R;
+    a.ring_lds = kPipeSlot;
     a.vec_out = ((((uintptr_t)a.rewards) & 15) == 0) && ((((uintptr_t)a.actions_out) & 3) == 0);
     const dim3 pg((unsigned)((s.B + kBlock / 64 - 1) / (kBlock / 64)));
-    // decoded draws: every launch's twist-ahead decodes until the draws of
-    // the next two launches (from the consumer position of the launch
-    // before last) are in the records: ceil(2 chunk / 10) records' worth
-    auto ahead_args = [&](int cin, int tin, int tout) {
-        AheadArgs x{cin, tin, tout, e->pipe_lead, e->perr_host_dev};
-        x.N = s.N, x.C1 = s.C - 1, x.P = s.dec_P, x.R = s.dec_R;
-        x.invN = (65536u + (uint32_t)s.N - 1u) / (uint32_t)s.N;
-        x.span = (2 * chunk + kHand - 1) / kHand;
-        return x;
-    };
     if (!e->pvalid) {  // start the pipeline from mt_pos: twist kPipeLead ahead, synchronously
         const int p = (int)(e->pcount & 1u);
-        if (dec) hipLaunchKernelGGL((k_mt_ahead<true, true>), pg, dim3(kBlock), 0, st, s, ahead_args(1 - p, 0, p));
-        else hipLaunchKernelGGL((k_mt_ahead<true, false>), pg, dim3(kBlock), 0, st, s, ahead_args(1 - p, 0, p));
+        hipLaunchKernelGGL(k_mt_ahead<true>, pg, dim3(kBlock), 0, st, s, AheadArgs{1 - p, 0, p, e->pipe_lead, e->perr_host_dev});
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(e->ev_prep, st));
         e->pvalid = 1;
     }
     const int64_t B = s.B, N = s.N;
+    // a tournament game adds its seat draw (<= K - 1 + 1 draws): 10-step
+    // launches keep the pair tail < 1e-26 up to K = 8 agents at N <= 4
+    // (tools/pipe_tail.py), beyond that 5-step launches
+    const int chunk = min(e->chunk_steps, (s.lg_K > 8) ? 5 : pipe_max_chunk(s.N));
     for (int t0 = 0; t0 < a.steps; t0 += chunk) {
         PlayArgs c = a;
         c.steps = min(chunk, a.steps - t0);
@@ -1860,11 +1592,7 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
         if (tv) HIP_TRY(hipEventRecord(tv[0], st));
         SN_DISPATCH_N(s.N, {
-            if (dec) {
-                HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_DEC>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
-                hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_DEC>), dim3(grid_for(s.B)), dim3(kBlock), shmem, st, s, c);
-            } else if (gpw == 32) {
+            if (gpw == 32) {
                 HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_PIPE, 32>,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
                 hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_PIPE, 32>), dim3((unsigned)((s.B + 32 * (kBlock / 64) - 1) / (32 * (kBlock / 64)))),
@@ -1886,8 +1614,7 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         // the next launch's twist, beside this one: leads the consumer of the launch before
         HIP_TRY(hipStreamWaitEvent(e->side, e->ev_main, 0));
         if (tv) HIP_TRY(hipEventRecord(tv[2], e->side));
-        if (dec) hipLaunchKernelGGL((k_mt_ahead<false, true>), pg, dim3(kBlock), 0, e->side, s, ahead_args(1 - p, p, 1 - p));
-        else hipLaunchKernelGGL((k_mt_ahead<false, false>), pg, dim3(kBlock), 0, e->side, s, ahead_args(1 - p, p, 1 - p));
+        hipLaunchKernelGGL(k_mt_ahead<false>, pg, dim3(kBlock), 0, e->side, s, AheadArgs{1 - p, p, 1 - p, e->pipe_lead, e->perr_host_dev});
         HIP_TRY(hipGetLastError());
         if (tv) HIP_TRY(hipEventRecord(tv[3], e->side));
         HIP_TRY(hipEventRecord(e->ev_prep, e->side));
@@ -1978,7 +1705,6 @@ sn_status sn_league_config(sn_env* e, int num_agents, int min_players, int max_p
     if (!e) return fail(SN_EINVAL, "env is NULL");
     DevState& s = e->s;
     HIP_TRY(hipSetDevice(e->device));
-    if (sn_pipe_sync(e, 0) != SN_OK) return SN_EHIP;  // the pipeline's mode (decoded draws) depends on it
     if (num_agents == 0) {
         HIP_TRY(hipDeviceSynchronize());
         if (s.lgs) (void)hipFree(s.lgs);

@@ -48,17 +48,6 @@ struct DevState {
     uint32_t* ptend; // [2][B] end of the twisted words after a prep launch (by launch parity)
     uint32_t* ptp;   // [B] twist pointer (MtGen's pos field), owned by k_mt_ahead
     uint32_t* perr;  // [1] play lanes that ran past the twisted words (must stay 0)
-    // decoded draws (k_mt_ahead<.., DEC>, k_play<RNG_NUMPY_DEC>): every random
-    // decision of the DrunkHamster self-play, decoded from the words ahead of
-    // play.  Draw d of a game is decision d % P of record d / P (P = C-1 + 9N:
-    // the deal's C-1 Fisher-Yates targets, then 9 steps x N policy indices).
-    uint8_t* drec;   // [kDecRecs][rec_chunks][B][16] record bytes: targets at 0.., step draws at kDecDP..
-    uint32_t* wpos;  // [kDecWB][B] stream word position at step boundary b (10 per record)
-    uint32_t* ddraw; // [B] decoder: next draw to decode (absolute)
-    uint32_t* dword; // [B] decoder: stream position of the next undecoded word
-    uint32_t* dend;  // [2][B] draws decoded through, by launch parity (as ptend)
-    uint32_t* pcdraw;// [2][B] consumer draw index after a play launch, by launch parity (as pabsc)
-    int dec_P, dec_R;  // draws per record, record bytes (multiple of 16)
     // batched tournament (sn_league_config): per game the current game's
     // player count k and seat agents, k | agent(seat p) << (4 + 4p)
     uint32_t* lgs;   // [B]
@@ -71,9 +60,6 @@ struct DevState {
 constexpr int kPipeRing = 1024;  // ring bytes per game (>= lead + one launch)
 constexpr int kPipeLead = 600;   // words k_mt_ahead keeps twisted ahead of the consumer (<= 624)
 constexpr int kPipeWin = 304;    // of them, copied to LDS per lane at a k_play launch
-constexpr int kDecRecs = 4;      // decoded records per game (a launch reads 2, the decoder writes ahead)
-constexpr int kDecWB = 32;       // step-boundary word positions per game (ring)
-constexpr int kDecDP = 104;      // record byte offset of the step draws (after the deal's <= 103 targets)
 
 constexpr int kBlock = 256;
 constexpr int kLeagueMaxPlayers = 6;  // tournament handles: 2..6 seats (agent ids packed 4 bits per seat)
@@ -834,8 +820,6 @@ struct sn_env {
     int chunk_steps;  // SN_OPT_CHUNK_STEPS
     int pipe;         // SN_OPT_PIPELINE
     int pipe_gpw;     // SN_OPT_PIPE_GPW: games per k_play wave on the pipelined path (32 or 64)
-    int pipe_dec;     // SN_OPT_PIPE_DECODE: decode the draws in the twist-ahead (k_play<RNG_NUMPY_DEC>)
-    int pdec;         // the live pipeline decodes (fixed from its start to the next sn_pipe_sync)
     int pipe_lead;    // SN_OPT_PIPE_LEAD: words k_mt_ahead keeps twisted ahead (kPipeLead; tests lower it)
     int lg_phase;     // tournament handle: env-steps since the games were dealt, mod 10 (-1: not dealt yet)
     int lg_kind[16];  // tournament handle: per agent SN_AGENT_* (sn_league_agents; all RANDOM by default)

@@ -317,12 +317,12 @@ def test_mt_state_across_round_boundaries_every_step():
             assert p == rp and np.array_equal(k, rk), (t, g)
 
 
-@pytest.mark.parametrize("ring_words,chunk_steps,pipeline,gpw,dec", [
-    (0, 10, 0, 64, 1), (64, 10, 0, 64, 1), (64, 1, 0, 64, 1), (128, 3, 0, 64, 1), (512, 25, 0, 64, 1),
-    (256, 7, 0, 64, 1), (256, 10, 1, 64, 1), (256, 3, 1, 64, 1), (0, 1, 1, 64, 1), (512, 25, 1, 64, 1),
-    (256, 10, 1, 32, 1), (0, 3, 1, 32, 1), (0, 25, 1, 32, 1), (256, 10, 1, 64, 0), (0, 1, 1, 64, 0),
-    (0, 3, 1, 64, 0)])
-def test_ring_options_do_not_change_results(ring_words, chunk_steps, pipeline, gpw, dec):
+@pytest.mark.parametrize("ring_words,chunk_steps,pipeline,gpw", [(0, 10, 0, 64), (64, 10, 0, 64), (64, 1, 0, 64),
+                                                                  (128, 3, 0, 64), (512, 25, 0, 64), (256, 7, 0, 64),
+                                                                  (256, 10, 1, 64), (256, 3, 1, 64), (0, 1, 1, 64),
+                                                                  (512, 25, 1, 64), (256, 10, 1, 32), (0, 3, 1, 32),
+                                                                  (0, 25, 1, 32)])
+def test_ring_options_do_not_change_results(ring_words, chunk_steps, pipeline, gpw):
     """The twist-ahead paths are optimisations only: every ring size (0 =
     lazy per-lane MT19937; 64 runs k_mt_prep's ring dry inside every
     episode, so the slow path continues mid-launch), launch chunking, and
@@ -330,7 +330,7 @@ def test_ring_options_do_not_change_results(ring_words, chunk_steps, pipeline, g
     oracle's actions, rewards, obs and final numpy MT states."""
     B, N, T, seed = 300, 4, 37, 21
     env = venv(B, N, seed=seed, rng="numpy")
-    env.set_option(ring_words=ring_words, chunk_steps=chunk_steps, pipeline=pipeline, pipe_gpw=gpw, pipe_decode=dec)
+    env.set_option(ring_words=ring_words, chunk_steps=chunk_steps, pipeline=pipeline, pipe_gpw=gpw)
     env.reset()
     ref = O.VecOracle(B, N, rng_mode=O.RNG_NUMPY_MT, seed=seed)
     ref.reset()
@@ -524,7 +524,7 @@ def test_pipelined_overrun_is_an_error(N, lead):
     the next rollout raises from the asynchronous mirror (sticky)."""
     from rl_6_nimmt._native import PipeOverrunError
 
-    env = venv(4096, N, seed=1, rng="numpy")  # N = 4: the decoding twist-ahead runs out of words
+    env = venv(4096, N, seed=1, rng="numpy")
     env.set_option(pipe_lead=lead)
     env.reset()
     with pytest.raises(PipeOverrunError):
