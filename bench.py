@@ -56,7 +56,7 @@ ALGO_BYTES_PER_STEP = (33 * N_PLAYERS + 57) + 47 * N_PLAYERS  # 377 B at N = 4
 # applied by tools/pmc_traffic.py.  PMC counters cannot be read inside a plain
 # run, so the committed summary of the current kernels is reported beside the
 # live timing.
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02_pmc_traffic_{rng}.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r03_pmc_traffic_{rng}.json")
 
 
 def parse():

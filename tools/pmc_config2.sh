@@ -10,7 +10,7 @@ TAG=${1:-cur}
 OUT=$R/gpurun_out/pmc_$TAG
 mkdir -p $OUT
 for mode in numpy philox; do
-  B="python3 bench.py --steps 5 --warmup 1 --no-cpu --no-mcs --no-puct --no-scalar --no-league --no-philox --rng $mode"
+  B="python3 bench.py --steps 5 --warmup 1 --no-cpu --no-mcs --no-puct --no-scalar --no-league --no-mixed-league --no-dropin --no-philox --rng $mode"
   timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_play|k_mt_ahead|k_mt_prep" --output-format csv -d $OUT/fetch_$mode -o run -- $B > $OUT/fetch_$mode.log 2>&1 || { tail $OUT/fetch_$mode.log; exit 1; }
   timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_play|k_mt_ahead|k_mt_prep" --output-format csv -d $OUT/write_$mode -o run -- $B > $OUT/write_$mode.log 2>&1 || { tail $OUT/write_$mode.log; exit 1; }
   timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS --kernel-include-regex "k_play|k_mt_ahead|k_mt_prep" --output-format csv -d $OUT/sq_$mode -o run -- $B > $OUT/sq_$mode.log 2>&1 || { tail $OUT/sq_$mode.log; exit 1; }
