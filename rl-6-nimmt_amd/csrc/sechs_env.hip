@@ -472,6 +472,11 @@ struct StreamSrc {
     }
 };
 
+// 16-B pieces per lane in the obs staging rows: 3N padded to an odd count, so
+// the 64 lanes' ds_write_b128 at a common piece index spread over all banks
+// (an even stride -- 12 pieces = 192 B at N = 4 -- serialised them)
+__host__ __device__ constexpr int obs_stage_pieces(int N) { return 3 * N + ((N & 1) ? 0 : 1); }
+
 template <int N, class Src, int GPW = 64, bool LG = false>
 __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a, int64_t g, int lane, uint8_t* wave_lds,
                                            Game<N>& G, Src& src, int32_t (&sum_res)[N], int32_t& episodes,
@@ -493,7 +498,8 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
             const int nobs = LG ? (int)kp : N;
             const GameWords gw = summ ? game_words<true>(nobs, G.b, w2hi) : game_words<false>(nobs, G.b, w2hi);
             if (staged) {
-                u32x4* row = (u32x4*)(wave_lds + lane * N * 48);
+                constexpr int P = obs_stage_pieces(N);  // odd: lanes' rows land on distinct bank groups
+                u32x4* row = (u32x4*)wave_lds + lane * P;
 #pragma unroll
                 for (int p = 0; p < N; p++) {
                     const Hand& h = G.hand[p];
@@ -507,7 +513,10 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
                 if (wave_games == GPW) {  // all reads, one wait, all stores
                     u32x4 pc[3 * N];
 #pragma unroll
-                    for (int j = 0; j < 3 * N; j++) pc[j] = src[lane + GPW * j];
+                    for (int j = 0; j < 3 * N; j++) {
+                        const int c = lane + GPW * j;  // piece c of the wave's contiguous obs block
+                        pc[j] = src[(c / (3 * N)) * P + c % (3 * N)];
+                    }
 #pragma unroll
                     for (int j = 0; j < 3 * N; j++) {
                         if (SECHS_NT_OBS) __builtin_nontemporal_store(pc[j], &dst[lane + GPW * j]);
@@ -515,7 +524,7 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
                     }
                 } else {
                     const int pieces = wave_games * N * 3;
-                    for (int i = lane; i < pieces; i += wave_games) dst[i] = src[i];
+                    for (int i = lane; i < pieces; i += wave_games) dst[i] = src[(i / (3 * N)) * P + i % (3 * N)];
                 }
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             } else {
@@ -1005,7 +1014,7 @@ __device__ __forceinline__ void produce_draws(R& rng, ByteBuf& buf, uint16_t* id
 // LDS of a k_play_split block: play staging | decks | index words | dealt games
 __host__ __device__ __forceinline__ int split_deal_words(int N) { return 3 * N + 1; }
 __host__ __device__ __forceinline__ size_t split_lds(int N, int steps) {
-    return (size_t)4 * 64 * N * 48 + (size_t)4 * 64 * kDealStride + (size_t)4 * steps * 64 * 2 +
+    return (size_t)4 * 64 * obs_stage_pieces(N) * 16 + (size_t)4 * 64 * kDealStride + (size_t)4 * steps * 64 * 2 +
            (size_t)4 * split_deal_words(N) * 64 * 4;
 }
 
@@ -1017,8 +1026,8 @@ __global__ __launch_bounds__(2 * kBlock) void k_play_split(DevState s, PlayArgs 
     const int tid = (int)threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, w = wave & 3;
     const int64_t g = ((int64_t)blockIdx.x * 4 + w) * 64 + lane;
     const bool live = g < s.B;
-    uint8_t* staging = lds_dyn + (size_t)w * 64 * N * 48;
-    uint8_t* decks = lds_dyn + (size_t)4 * 64 * N * 48;
+    uint8_t* staging = lds_dyn + (size_t)w * 64 * obs_stage_pieces(N) * 16;
+    uint8_t* decks = lds_dyn + (size_t)4 * 64 * obs_stage_pieces(N) * 16;
     uint16_t* idx = (uint16_t*)(decks + (size_t)4 * 64 * kDealStride) + (size_t)w * a.steps * 64 + lane;
     uint32_t* dealt = (uint32_t*)((uint8_t*)((uint16_t*)(decks + (size_t)4 * 64 * kDealStride) + (size_t)4 * a.steps * 64)) +
                       (size_t)w * split_deal_words(N) * 64 + lane;
@@ -1442,7 +1451,7 @@ static sn_status launch_play_one(sn_env* e, PlayArgs a, hipStream_t st) {
     const DevState& s = e->s;
     const bool ring = (s.rng_mode == SN_RNG_NUMPY_MT) && !a.actions && s.ring_w > 0;
     int wave = 64 * kDealStride;
-    if (a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15) == 0) wave = max(wave, 64 * s.N * 48);
+    if (a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15) == 0) wave = max(wave, 64 * obs_stage_pieces(s.N) * 16);
     a.ring_lds = 0;
     const int ring_stride = ring_lds_stride(s.ring_w);
     const bool ring_in_lds = ring && (wave + 64 * ring_stride) * (kBlock / 64) <= kLdsBytes;
@@ -1547,7 +1556,7 @@ static int pipe_max_chunk(int N) { return N <= 4 ? 10 : 5; }
 // LDS a pipelined k_play block needs (obs staging / deck + the RingPipe windows)
 static size_t pipe_lds(const DevState& s, const PlayArgs& a, int gpw, int* wave_out) {
     int wave = gpw * kDealStride;
-    if (a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15) == 0) wave = max(wave, gpw * s.N * 48);
+    if (a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15) == 0) wave = max(wave, gpw * obs_stage_pieces(s.N) * 16);
     wave += gpw * kPipeSlot;
     *wave_out = wave;
     return (size_t)wave * (kBlock / 64);
