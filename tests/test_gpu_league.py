@@ -236,3 +236,61 @@ def test_league_records_equal_oracle_shards():
         rec = t.play_games(3).cpu().numpy()
         assert np.array_equal(rec, O.league_records(5, 2, 4, seed=0, game_offset=off, slots=96, games=3))
         t.close()
+
+
+def _rank_league(rank, world, port, q, B, G):
+    """one rank of the distributed league on cuda:0: its shard of device
+    slots, the per-agent all_reduce and the record all_gather (gloo here --
+    two ranks cannot share one GPU under RCCL; bench.py uses nccl = RCCL)"""
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rl_6_nimmt.distributed import gather_league_records, reduce_agent_stats, shard
+
+    off, cnt = shard(rank, world, B)
+    t = _league(cnt, 5, 2, 4, seed=3, game_offset=off)
+    t.play_games(G)
+    stats = reduce_agent_stats(t.agent_stats().cpu())
+    allrec = gather_league_records(t.all_records().cpu())
+    errs = t.env.pipe_errors()
+    t.close()
+    if rank == 0:
+        q.put((stats.numpy(), allrec.numpy(), errs))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_device_league_gather_equals_one_handle():
+    """world_size 2 with DEVICE records: each rank plays its shard of slots
+    on the GPU; the gathered records and the reduced per-agent sums equal one
+    handle holding every slot (the CPU gloo test gathers oracle records)."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    from rl_6_nimmt.league import replay_league_elo
+
+    B, G = 512, 3
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_league, args=(r, 2, port, q, B, G)) for r in range(2)]
+    for p in procs:
+        p.start()
+    stats, allrec, errs = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    t = _league(2 * B, 5, 2, 4, seed=3)
+    t.play_games(G)
+    ref = t.all_records().cpu().numpy()
+    assert errs == 0 and t.env.pipe_errors() == 0
+    assert allrec.shape == ref.shape and np.array_equal(allrec, ref)
+    assert np.allclose(stats, t.agent_stats().cpu().numpy())
+    assert np.allclose(replay_league_elo(torch.from_numpy(allrec), 5, 4), t.replay_elo(), rtol=0, atol=1e-9)
+    t.close()
