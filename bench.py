@@ -70,8 +70,6 @@ def parse():
     ap.add_argument("--pipe-gpw", type=int, default=64, choices=[32, 64], help="games per k_play wave (pipelined path)")
     ap.add_argument("--play-split", type=int, default=None, choices=[0, 1],
                     help="SN_OPT_PLAY_SPLIT (default: the library's)")
-    ap.add_argument("--pipe-dec", type=int, default=None, choices=[0, 1],
-                    help="SN_OPT_PIPE_DEC decode-ahead pipeline (default: the library's)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-philox", action="store_true", help="skip the philox-mode leg of config 2")
@@ -761,7 +759,7 @@ def main():
     B = args.games
     env = VecSechsNimmtEnv(B, N_PLAYERS, seed=0, game_offset=rank * B, rng=args.rng)
     if args.rng == "numpy":
-        env.set_option(pipe_gpw=args.pipe_gpw, play_split=args.play_split, pipe_dec=args.pipe_dec)
+        env.set_option(pipe_gpw=args.pipe_gpw, play_split=args.play_split)
     env.reset()
     out = make_out(env, B, not args.no_obs)
     wall, kern_ms, kt = time_rollouts(env, out, args.steps, args.warmup, world)

@@ -157,17 +157,9 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          are in lockstep (after sn_reset; N <= 4, auto-reset):
                          1 (default) or 0 (never).  Measured (65 536 x 4p):
                          74 -> 59 us per 10 env-steps.  Numpy-compat handles
-                         always use the pipelined one-wave k_play.
-     SN_OPT_PIPE_DEC     decode-ahead pipeline for numpy-compat in-kernel
-                         DrunkHamster rollouts with auto-reset (N <= 4, not a
-                         tournament handle): k_play_dec plays a launch from
-                         per-game records of its draws and deal decoded by the
-                         launch before, and decodes the next launch in other
-                         waves of the same blocks.  1 or 0.  Same words, same
-                         results; the last decode of a rollout is speculative
-                         and is dropped by any other use of the handle. */
+                         always use the pipelined one-wave k_play. */
 enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3, SN_OPT_TIMING = 4, SN_OPT_PIPE_GPW = 5,
-       SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7, SN_OPT_PIPE_DEC = 8 };
+       SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7 };
 sn_status sn_set_option(sn_env* env, int option, int value);
 /* pipelined rollouts whose draws ran past the twisted words (must be 0; a
    nonzero count means those games' draws are wrong) [sync].  The count is

@@ -702,179 +702,6 @@ __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
     play_body<N, MODE, GPW, LG>(s, a, lds_dyn, (int)threadIdx.x);
 }
 
-// ============================================================================
-// Decode-ahead pipeline (SN_OPT_PIPE_DEC, numpy-MT DrunkHamster rollouts with
-// auto-reset, N <= 4).  Every random decision of such a rollout depends on
-// the game's word stream and its hand size only: step t's draws are
-// random_interval(n - 1) per seat, and when the hand runs out the deal is a
-// shuffle of the next words.  So they can be decoded a launch AHEAD of the
-// game: a k_play_dec block holds 4 play waves (256 games, launch i) and 4
-// decode waves (the same games, launch i + 1).  The decode waves read the
-// pipelined ring exactly as k_play<RNG_NUMPY_PIPE> does (they are now the
-// ring's consumer: k_mt_ahead leads their position) and write per-game
-// records: the packed draw indices of every step and the next deal's sorted
-// hands and row cards.  The play waves of the next launch load those records
-// in their prologue and run no RNG code at all -- the SIMD interleaves a play
-// wave and a decode wave instead of running one wave's whole serial chain.
-// Record of a game (slot = decode launch parity, word-major [slot][kDecRecW][B]):
-//   words 0..4  draw indices: step t in bits 16 (t & 1) of word t >> 1, seat p
-//               in nibble p (N <= 4, <= 10 steps)
-//   word 5      hand size at the decode's start | steps << 8 (checked by play)
-//   words 6..   the deal: hand p as 3 words (Hand lo.lo32, lo.hi32, hi), then
-//               the four row cards packed in one word
-// The decode of the LAST launch of a rollout is speculative (the next rollout
-// is assumed to start the same way); the host drops it (dec_drop: restores the
-// consumer position of the launch before) whenever the next use differs.
-// ============================================================================
-#ifndef SECHS_DEC_WPE
-#define SECHS_DEC_WPE 3  // waves per SIMD k_play_dec is compiled for (<= 168 VGPRs: room for k_mt_ahead waves)
-#endif
-constexpr int kDecMaxPlayers = 4;
-constexpr int kDecIdxW = 5;
-constexpr int kDecRecW = kDecIdxW + 1 + 3 * kDecMaxPlayers + 1;  // 19
-constexpr int kDecDeck = kDeckStride;                             // 108 B per lane, odd dword stride
-constexpr int kDecWave = 64 * (kPipeSlot + kDecDeck);              // LDS of a decode wave
-
-struct DecArgs {
-    int steps;  // env-steps the decode waves decode (0: none)
-    int init;   // hand sizes from the game state (no decode launch before this one)
-    int p;      // parity: ring consumer reads pabsc[1-p], writes pabsc[p], reads ptend[p];
-                // records / hand sizes written to slot p, the play waves read slot 1-p
-};
-
-template <int N>
-struct DecSrc {
-    // the draw words as a 160-bit shift register (no indexed register array:
-    // LLVM would put one in scratch); `front` = the step in its low 16 bits
-    uint64_t i01, i23;
-    uint32_t i4;
-    int front;
-    uint32_t dw[3 * N + 1];
-    __device__ __forceinline__ void load(const DevState& s, const uint32_t* rec, int64_t g) {
-        const int64_t B = s.B;
-        i01 = (uint64_t)rec[g] | ((uint64_t)rec[B + g] << 32);
-        i23 = (uint64_t)rec[2 * B + g] | ((uint64_t)rec[3 * B + g] << 32);
-        i4 = rec[4 * B + g];
-        front = 0;
-#pragma unroll
-        for (int k = 0; k < 3 * N + 1; k++) dw[k] = rec[(int64_t)(kDecIdxW + 1 + k) * B + g];
-    }
-    __device__ __forceinline__ void draws(const Game<N>&, int t, uint32_t, bool, uint32_t (&idx)[N]) {
-        while (front < t) {  // wave-uniform; one pass per step (more only after skipped steps)
-            i01 = (i01 >> 16) | (i23 << 48);
-            i23 = (i23 >> 16) | ((uint64_t)i4 << 48);
-            i4 >>= 16;
-            front++;
-        }
-        const uint32_t w = (uint32_t)i01;
-#pragma unroll
-        for (int p = 0; p < N; p++) idx[p] = (w >> (4 * p)) & 15u;
-    }
-    __device__ __forceinline__ uint32_t league(const DevState&) { return 0u; }
-    __device__ __forceinline__ void deal(const DevState&, Game<N>& G, PhaseProf&) {
-#pragma unroll
-        for (int p = 0; p < N; p++) {
-            G.hand[p].lo = (uint64_t)dw[3 * p] | ((uint64_t)dw[3 * p + 1] << 32);
-            G.hand[p].hi = dw[3 * p + 2];
-            G.score[p] = 0;
-        }
-        const uint32_t r = dw[3 * N];
-        const uint32_t r0 = r & 0xFFu, r1 = (r >> 8) & 0xFFu, r2 = (r >> 16) & 0xFFu, r3 = r >> 24;
-        G.b.lo.x = r0, G.b.lo.y = r1, G.b.lo.z = r2, G.b.lo.w = r3;
-        G.b.hi.x = meta_row(r0), G.b.hi.y = meta_row(r1), G.b.hi.z = meta_row(r2), G.b.hi.w = meta_row(r3);
-        G.n = kHand;
-    }
-};
-
-// a decode wave: launch i+1's draws and deal for 64 games, from the ring
-template <int N>
-__device__ __forceinline__ void dec_body(const DevState& s, const DecArgs& d, uint8_t* win, uint8_t* deck, int64_t g) {
-    const int64_t B = s.B;
-    ByteBuf buf;
-    RingPipe rng;
-    rng.load(s, g, buf, win, 1 - d.p, d.p);
-    uint32_t n = d.init ? hand_len(load_hand(s, 0, g)) : s.dn[(int64_t)(1 - d.p) * B + g];
-    uint32_t* rec = s.drec + (int64_t)d.p * kDecRecW * B + g;
-    rec[(int64_t)kDecIdxW * B] = n | ((uint32_t)d.steps << 8);
-    uint32_t cur = 0u;
-    for (int t = 0; t < d.steps; t++) {
-        uint32_t idx[N];
-        if (n != 0u) {  // a finished game without a deal plays nothing (k_play: bad = 0)
-            rng_draws<N>(rng, buf, n - 1u, idx);
-#pragma unroll
-            for (int p = 0; p < N; p++) cur |= idx[p] << (16 * (t & 1) + 4 * p);
-        }
-        if ((t & 1) || t + 1 == d.steps) {
-            rec[(int64_t)(t >> 1) * B] = cur;
-            cur = 0u;
-        }
-        if (n != 0u && --n == 0u) {  // env.py:99-112, the auto-reset deal after the last card
-            deck_shuffle(rng, buf, deck, s.C);
-            Game<N> G;
-            deal_from_deck<N>(deck, s.C, G);
-#pragma unroll
-            for (int p = 0; p < N; p++) {
-                rec[(int64_t)(kDecIdxW + 1 + 3 * p) * B] = (uint32_t)G.hand[p].lo;
-                rec[(int64_t)(kDecIdxW + 2 + 3 * p) * B] = (uint32_t)(G.hand[p].lo >> 32);
-                rec[(int64_t)(kDecIdxW + 3 + 3 * p) * B] = G.hand[p].hi;
-            }
-            rec[(int64_t)(kDecIdxW + 1 + 3 * N) * B] = G.b.lo.x | (G.b.lo.y << 8) | (G.b.lo.z << 16) | (G.b.lo.w << 24);
-            n = kHand;
-        }
-    }
-    s.pabsc[(int64_t)d.p * B + g] = rng.consumed(buf);
-    s.dn[(int64_t)d.p * B + g] = n;
-}
-
-// a play wave: launch i from the records the previous launch decoded
-template <int N>
-__device__ __forceinline__ void play_dec_body(const DevState& s, const PlayArgs& a, const DecArgs& d, uint8_t* wave_lds,
-                                              int64_t g, int lane) {
-    __builtin_amdgcn_s_setprio(1);
-    PhaseProf pp;
-    pp.start();
-    Game<N> G;
-    load_game<N>(s, g, G);
-    int32_t sum_res[N], episodes;
-    load_results<N>(s, g, a.flags, sum_res, episodes);
-    const uint32_t* rec = s.drec + (int64_t)(1 - d.p) * kDecRecW * s.B;
-    DecSrc<N> src;
-    src.load(s, rec, g);
-    // records decoded for another start (a host bookkeeping bug) fail loudly
-    if (rec[(int64_t)kDecIdxW * s.B + g] != (G.n | ((uint32_t)a.steps << 8))) atomicAdd(s.perr, 1u);
-    pp.mark(PH_PROLOGUE);
-    uint32_t lg = 0u;
-    play_steps<N, DecSrc<N>, 64, false>(s, a, g, lane, wave_lds, G, src, sum_res, episodes, pp, lg, 0, a.steps);
-    store_game<N>(s, g, G);
-    store_results<N>(s, g, a.flags, sum_res, episodes);
-    pp.mark(PH_EPILOGUE);
-    pp.flush(lane);
-}
-
-// 512 threads: waves 0..3 play games [256 b, 256 b + 256) (a.steps of them,
-// 0 = none), waves 4..7 decode the same games' next launch (d.steps, 0 = none)
-template <int N>
-__global__ __launch_bounds__(2 * kBlock, SECHS_DEC_WPE) void k_play_dec(DevState s, PlayArgs a, DecArgs d) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
-    const int tid = (int)threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int64_t g = (int64_t)blockIdx.x * kBlock + (tid & (kBlock - 1));
-    if (g >= s.B) return;
-    if (wave < kBlock / 64) {
-        if (a.steps > 0) play_dec_body<N>(s, a, d, lds_dyn + wave * a.wave_lds, g, lane);
-    } else if (d.steps > 0) {
-        uint8_t* dl = lds_dyn + (kBlock / 64) * a.wave_lds + (wave - kBlock / 64) * kDecWave;
-        dec_body<N>(s, d, dl + lane * kPipeSlot, dl + 64 * kPipeSlot + lane * kDecDeck, g);
-    }
-}
-
-// drop a speculative decode: its consumer position and hand sizes become
-// those of the decode launch before it
-__global__ void k_dec_drop(DevState s, int p) {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= s.B) return;
-    s.pabsc[(int64_t)p * s.B + g] = s.pabsc[(int64_t)(1 - p) * s.B + g];
-}
-
 // ---- one-game fast path (the scalar drop-in SechsNimmtEnv, B == 1) -------
 // One launch per env.step / env.reset: the actions arrive as kernel
 // arguments, the results (invalid seat, done, rewards, scores, int8 obs rows)
@@ -1424,9 +1251,6 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
     e->pipe_lead = kPipeLead;
     e->phase = -1;
     e->play_split = 1;
-    e->pipe_dec = 0;
-    e->dec_pending = 0;
-    e->dec_steps = 0;
     e->pvalid = 0;
     e->pcount = 0;
     if (rng_mode == SN_RNG_NUMPY_MT) {
@@ -1435,9 +1259,7 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
             size_t bytes;
         } pal[] = {{(void**)&s.pring, (size_t)kPipeRing * B}, {(void**)&s.pabsc, sizeof(uint32_t) * 2 * B},
                    {(void**)&s.ptend, sizeof(uint32_t) * 2 * B}, {(void**)&s.ptp, sizeof(uint32_t) * B},
-                   {(void**)&s.perr, sizeof(uint32_t)},
-                   {(void**)&s.drec, N <= kDecMaxPlayers ? sizeof(uint32_t) * 2 * kDecRecW * B : 4},
-                   {(void**)&s.dn, sizeof(uint32_t) * 2 * B}};
+                   {(void**)&s.perr, sizeof(uint32_t)}};
         for (auto& a : pal) {
             if (hipMalloc(a.p, a.bytes) != hipSuccess) {
                 sn_destroy(e);
@@ -1497,7 +1319,7 @@ sn_status sn_destroy(sn_env* e) {
     if (e->side) (void)hipStreamDestroy(e->side);
     free_timing(e);
     void* ps[] = {s.hand, s.row_lo, s.row_hi, s.score, s.sum_res, s.episodes, s.mt_pos, s.ctr, s.mt, s.mt0, s.ring,
-                  s.pring, s.pabsc, s.ptend, s.ptp, s.perr, s.drec, s.dn, s.lgs, s.lmem};
+                  s.pring, s.pabsc, s.ptend, s.ptp, s.perr, s.lgs, s.lmem};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     delete e;
@@ -1546,10 +1368,6 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
         case SN_OPT_PLAY_SPLIT:
             if (value < 0 || value > 1) return fail(SN_EINVAL, "play split must be 0 or 1");
             e->play_split = value;
-            return SN_OK;
-        case SN_OPT_PIPE_DEC:
-            if (value != 0 && value != 1) return fail(SN_EINVAL, "pipe decode must be 0 or 1");
-            e->pipe_dec = value;
             return SN_OK;
         case SN_OPT_PIPE_LEAD:
             if (value < 64 || value > kPipeLead) return fail(SN_EINVAL, "pipe lead must be in 64..600");
@@ -1609,13 +1427,10 @@ sn_status sn_reset(sn_env* e, const uint8_t* decks, void* stream) {
     return SN_OK;
 }
 
-static sn_status dec_drop(sn_env* e, hipStream_t st);
-
 sn_status sn_reset_to(sn_env* e, const int8_t* board, const int8_t* hands, void* stream) {
     if (!e || !board || !hands) return fail(SN_EINVAL, "NULL argument");
     e->phase = -1;
     hipStream_t st = (hipStream_t)stream;
-    if (e->pvalid && dec_drop(e, st) != SN_OK) return SN_EHIP;  // new hands: a decoded launch no longer applies
     const DevState& s = e->s;
     SN_DISPATCH_N(s.N, hipLaunchKernelGGL((k_reset_to<NN>), dim3(grid_for(s.B)), dim3(kBlock), 0, st, s, board, hands));
     HIP_TRY(hipGetLastError());
@@ -1713,23 +1528,8 @@ static sn_status launch_play_one(sn_env* e, PlayArgs a, hipStream_t st) {
 // A ring-fed (numpy-MT, in-kernel DrunkHamster) rollout runs in launches of
 // at most chunk_steps env-steps, each behind its own k_mt_prep, so that one
 // ring covers a launch's draws (a 4-player episode: 193.5 +- 9.3 words).
-static sn_status dec_drop(sn_env* e, hipStream_t st) {
-    if (!e->dec_pending) return SN_OK;
-    HIP_TRY(hipStreamWaitEvent(st, e->ev_play, 0));  // the speculative decode has run
-    const int p = (int)((e->pcount - 1u) & 1u);
-    hipLaunchKernelGGL(k_dec_drop, dim3(grid_for(e->s.B)), dim3(kBlock), 0, st, e->s, p);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(e->ev_play, st));
-    e->dec_pending = 0;
-    return SN_OK;
-}
-
 sn_status sn_pipe_sync(sn_env* e, hipStream_t st) {
     if (!e || !e->pvalid) return SN_OK;
-    {
-        const sn_status r = dec_drop(e, st);
-        if (r != SN_OK) return r;
-    }
     // k_pipe_code reads the last k_play's consumer position (pabsc) and the
     // last k_mt_ahead's twisted end: wait for both, whatever stream `st` is
     // (the null stream does not order behind a non-blocking caller stream)
@@ -1774,10 +1574,6 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     a.ring_lds = kPipeSlot;
     a.vec_out = ((((uintptr_t)a.rewards) & 15) == 0) && ((((uintptr_t)a.actions_out) & 3) == 0);
     const dim3 pg((unsigned)((s.B + kBlock / 64 - 1) / (kBlock / 64)));
-    {
-        const sn_status r = dec_drop(e, st);
-        if (r != SN_OK) return r;
-    }
     if (!e->pvalid) {  // start the pipeline from mt_pos: twist kPipeLead ahead, synchronously
         const int p = (int)(e->pcount & 1u);
         hipLaunchKernelGGL(k_mt_ahead<true>, pg, dim3(kBlock), 0, st, s, AheadArgs{1 - p, 0, p, e->pipe_lead, e->perr_host_dev});
@@ -1837,89 +1633,6 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     return SN_OK;
 }
 
-// Decode-ahead rollout (k_play_dec, see the kernel): each launch plays chunk
-// i from the records decoded by the launch before and decodes chunk i + 1
-// (the last one: the first chunk of a rollout like this one, speculatively).
-// The ring protocol is launch_pipe's with the decode waves as the consumer.
-static bool dec_ok(const sn_env* e, const PlayArgs& a) {
-    const DevState& s = e->s;
-    return e->pipe_dec && s.N <= kDecMaxPlayers && !s.lg_K && (a.flags & SN_AUTO_RESET) && !a.actions && !a.invalid &&
-           e->pipe_gpw == 64 && !(a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15));
-}
-
-static sn_status launch_pipe_dec(sn_env* e, PlayArgs a, hipStream_t st) {
-    if (a.steps <= 0) return SN_OK;
-    DevState& s = e->s;
-    const int64_t B = s.B, N = s.N;
-    const int chunk = min(e->chunk_steps, pipe_max_chunk(s.N));
-    const int first = min(chunk, a.steps);
-    const int staged = a.obs && a.obs_stride == 48;
-    a.wave_lds = staged ? 64 * obs_stage_pieces(s.N) * 16 : 0;
-    a.ring_lds = 0;
-    a.vec_out = ((((uintptr_t)a.rewards) & 15) == 0) && ((((uintptr_t)a.actions_out) & 3) == 0);
-    const size_t shmem = (size_t)(kBlock / 64) * (a.wave_lds + kDecWave);
-    const dim3 pg((unsigned)((B + kBlock / 64 - 1) / (kBlock / 64)));
-    if (e->dec_pending && e->dec_steps != first) {
-        const sn_status r = dec_drop(e, st);
-        if (r != SN_OK) return r;
-    }
-    if (!e->pvalid) {
-        const int p = (int)(e->pcount & 1u);
-        hipLaunchKernelGGL(k_mt_ahead<true>, pg, dim3(kBlock), 0, st, s, AheadArgs{1 - p, 0, p, e->pipe_lead, e->perr_host_dev});
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(e->ev_prep, st));
-        e->pvalid = 1;
-        e->dec_pending = 0;
-    }
-    // one ring consumer launch (play of `c` if c.steps > 0 + decode of dsteps)
-    auto consumer = [&](const PlayArgs& c, int dsteps, int init) -> sn_status {
-        const int p = (int)(e->pcount & 1u);
-        HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));
-        HIP_TRY(hipEventRecord(e->ev_main, st));
-        hipEvent_t* tv = (c.steps > 0 && e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
-        if (tv) HIP_TRY(hipEventRecord(tv[0], st));
-        const DecArgs d{dsteps, init, p};
-        SN_DISPATCH_N(s.N, {
-            if constexpr (NN <= kDecMaxPlayers) {
-                HIP_TRY(hipFuncSetAttribute((const void*)k_play_dec<NN>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
-                hipLaunchKernelGGL((k_play_dec<NN>), dim3((unsigned)((B + kBlock - 1) / kBlock)), dim3(2 * kBlock), shmem, st, s, c, d);
-            }
-        });
-        HIP_TRY(hipGetLastError());
-        if (tv) HIP_TRY(hipEventRecord(tv[1], st));
-        HIP_TRY(hipStreamWaitEvent(e->side, e->ev_main, 0));
-        if (tv) HIP_TRY(hipEventRecord(tv[2], e->side));
-        hipLaunchKernelGGL(k_mt_ahead<false>, pg, dim3(kBlock), 0, e->side, s, AheadArgs{1 - p, p, 1 - p, e->pipe_lead, e->perr_host_dev});
-        HIP_TRY(hipGetLastError());
-        if (tv) HIP_TRY(hipEventRecord(tv[3], e->side));
-        HIP_TRY(hipEventRecord(e->ev_prep, e->side));
-        e->pcount++;
-        return SN_OK;
-    };
-    if (!e->dec_pending) {  // prime: decode the first chunk, play nothing
-        PlayArgs c = a;
-        c.steps = 0;
-        const sn_status r = consumer(c, first, 1);
-        if (r != SN_OK) return r;
-    }
-    for (int t0 = 0; t0 < a.steps; t0 += chunk) {
-        PlayArgs c = a;
-        c.steps = min(chunk, a.steps - t0);
-        c.step0 = a.step0 + t0;
-        if (a.rewards) c.rewards = a.rewards + (int64_t)t0 * B * N;
-        if (a.done) c.done = a.done + (int64_t)t0 * B;
-        if (a.actions_out) c.actions_out = a.actions_out + (int64_t)t0 * B * N;
-        if (a.obs) c.obs = a.obs + (int64_t)t0 * B * N * a.obs_stride;
-        const int next = (t0 + chunk < a.steps) ? min(chunk, a.steps - t0 - chunk) : first;
-        const sn_status r = consumer(c, next, 0);
-        if (r != SN_OK) return r;
-        e->dec_steps = next;
-    }
-    e->dec_pending = 1;
-    HIP_TRY(hipEventRecord(e->ev_play, st));
-    return SN_OK;
-}
-
 static sn_status launch_play(sn_env* e, PlayArgs a, hipStream_t st) {
     const DevState& s = e->s;
     if (s.lg_K) {  // tournament handles: in-kernel DrunkHamster seats, pipelined numpy-MT or philox
@@ -1934,7 +1647,6 @@ static sn_status launch_play(sn_env* e, PlayArgs a, hipStream_t st) {
         return launch_play_one(e, a, st);
     }
     if (s.rng_mode == SN_RNG_NUMPY_MT && !a.actions && e->pipe) {
-        if (dec_ok(e, a)) return launch_pipe_dec(e, a, st);
         int wave;
         if (pipe_lds(s, a, e->pipe_gpw, &wave) <= (size_t)kLdsBytes) return launch_pipe(e, a, st);
     }
@@ -2244,7 +1956,6 @@ sn_status sn_step1(sn_env* e, const int32_t* actions_host, int32_t* out_host, in
     if (h1_ready(e) != SN_OK) return SN_ENOMEM;
     if (e->s.lg_K) return fail(SN_EUNSUPPORTED, "a tournament handle plays whole games with sn_league_rollout");
     e->phase = -1;
-    if (e->pvalid && dec_drop(e, 0) != SN_OK) return SN_EHIP;
     Acts1 a{};
     for (int p = 0; p < e->s.N; p++) a.a[p] = actions_host[p];
     const int summ = !(flags & SN_NO_SUMMARIES);

@@ -48,9 +48,6 @@ struct DevState {
     uint32_t* ptend; // [2][B] end of the twisted words after a prep launch (by launch parity)
     uint32_t* ptp;   // [B] twist pointer (MtGen's pos field), owned by k_mt_ahead
     uint32_t* perr;  // [1] play lanes that ran past the twisted words (must stay 0)
-    // decode-ahead pipeline (k_play_dec, SN_OPT_PIPE_DEC):
-    uint32_t* drec;  // [2][kDecRecW][B] per-game records of a decode launch (by its parity)
-    uint32_t* dn;    // [2][B] hand size after a decode launch (by its parity)
     // batched tournament (sn_league_config): per game the current game's
     // player count k and seat agents, k | agent(seat p) << (4 + 4p)
     uint32_t* lgs;   // [B]
@@ -831,9 +828,6 @@ struct sn_env {
     int lg_mpc[16], lg_mmax[16];  // MCSAgent agents: mc_per_card, mc_max
     int phase;        // every game's env-steps since its deal, mod 10, when they are in lockstep; -1 unknown
     int play_split;   // SN_OPT_PLAY_SPLIT: role-split k_play for lockstep DrunkHamster rollouts
-    int pipe_dec;     // SN_OPT_PIPE_DEC: decode-ahead k_play_dec for numpy DrunkHamster rollouts
-    int dec_pending;  // the last ring consumer decoded dec_steps env-steps not played yet
-    int dec_steps;
     sechs::DevState s;
     // pipelined twist-ahead (sechs_env.hip launch_pipe): a k_mt_ahead for the
     // next play launch may be in flight on `side` (ev_prep) after a rollout

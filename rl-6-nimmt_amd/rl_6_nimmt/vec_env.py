@@ -186,12 +186,10 @@ class VecSechsNimmtEnv:
 
     # ------------------------------------------------------------ numpy RNG bridge
     def set_option(self, ring_words=None, chunk_steps=None, pipeline=None, pipe_gpw=None, pipe_lead=None,
-                   play_split=None, pipe_dec=None):
+                   play_split=None):
         """rollout tuning (include/sechs.h SN_OPT_*; all numpy-compat only except play_split,
         the role-split kernel of philox handles); results never depend on it
         (except pipe_lead < 600, a test knob that makes overruns -- PipeOverrunError -- likely)"""
-        if pipe_dec is not None:
-            nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPE_DEC, int(pipe_dec)), "sn_set_option")
         if pipe_lead is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPE_LEAD, int(pipe_lead)), "sn_set_option")
         if pipe_gpw is not None:
