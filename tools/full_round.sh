@@ -14,6 +14,6 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smok
 rc=$?; tail -2 $OUT/smoke.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 900 python bench.py > $OUT/bench.json 2> $OUT/bench.err
 rc=$?; tail -2 $OUT/bench.err; [ $rc -ne 0 ] && exit $rc
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 $R/bench.py --no-cpu --no-mcs --no-puct --no-scalar --no-league --no-mixed-league --no-dropin --steps 50 --warmup 10 > $OUT/prof_bench.json 2> $OUT/prof_bench.err
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $R/bench.py --no-cpu --no-mcs --no-puct --no-scalar --no-league --no-mixed-league --no-dropin --steps 50 --warmup 10 > $OUT/prof_bench.json 2> $OUT/prof_bench.err
 rc=$?; [ $rc -ne 0 ] && { echo "prof rc=$rc"; exit $rc; }
 echo done
