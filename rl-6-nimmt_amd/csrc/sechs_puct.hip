@@ -18,6 +18,8 @@
 // same input, so the probabilities are the same.
 #include <hip/hip_bf16.h>
 
+#include <algorithm>
+
 #include "sechs_state.h"
 
 using namespace sechs;
@@ -276,15 +278,16 @@ __global__ void k_puct_seat_cols(PuctArgs a, int N, int n_cur, T* cols, int ks, 
 // (one 8-B store per feature in bf16) when R % 4 == 0
 template <typename T>
 __global__ __launch_bounds__(256) void k_puct_h1_cols4(uint32_t R, uint32_t S, int H, int kp, int n_cur, const T* baseT,
-                                                       const float* cards, const float* w1c, T* h1T) {
+                                                       const float* cards, const float* w1c, T* h1T, int fch) {
     const uint32_t r = 4u * (blockIdx.x * blockDim.x + threadIdx.x);
     if (r >= R) return;
+    const int j0 = (int)blockIdx.y * fch, j1 = min(kp, j0 + fch);  // this block's feature slice
     uint32_t sd[4];
     float x[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) sd[u] = (r + u) / (uint32_t)n_cur, x[u] = cards[r + u];
 #pragma unroll 4
-    for (int j = 0; j < kp; j++) {
+    for (int j = j0; j < j1; j++) {
         float v[4];
         if (j < H) {
             const float w = w1c[j];
@@ -313,15 +316,16 @@ __global__ __launch_bounds__(256) void k_puct_h1_cols4(uint32_t R, uint32_t S, i
 // the general form: two rows per thread
 template <typename T>
 __global__ __launch_bounds__(256) void k_puct_h1_cols(uint32_t R, uint32_t S, int H, int kp, int n_cur, const T* baseT,
-                                                      const float* cards, const float* w1c, T* h1T) {
+                                                      const float* cards, const float* w1c, T* h1T, int fch) {
     const uint32_t r = 2u * (blockIdx.x * blockDim.x + threadIdx.x);
     if (r >= R) return;
+    const int j0 = (int)blockIdx.y * fch, j1 = min(kp, j0 + fch);
     const bool two = r + 1u < R;
     const uint32_t s0 = r / (uint32_t)n_cur, s1 = (r + 1u) / (uint32_t)n_cur;
     const float x0 = cards[r], x1 = two ? cards[r + 1u] : 0.f;
     const bool pack = (sizeof(T) == 2) && ((R & 1u) == 0u);  // 4-B aligned row pairs
 #pragma unroll 4
-    for (int j = 0; j < kp; j++) {
+    for (int j = j0; j < j1; j++) {
         float v0, v1;
         if (j < H) {
             const float w = w1c[j];
@@ -738,23 +742,33 @@ sn_status sn_puct_h1_cols(sn_env* e, const sn_puct* q, int n_cur, const void* ba
     if (R * kp >= (1ll << 40) || R >= (1ll << 31)) return set_error(SN_EINVAL, "too many rows");
     hipStream_t s = (hipStream_t)stream;
     const int64_t threads = (R + 1) / 2;
+    // the features are split over blockIdx.y so that a launch has >= ~4 waves
+    // per SIMD (a thread's feature loop is a latency chain of small gathers:
+    // at 8192 x 4 x 10 rows one 4-row thread per row group is 1.25 waves per SIMD)
+    auto slices = [&](int64_t thr) {
+        const int64_t waves = (thr + 63) / 64;
+        return (int)std::max<int64_t>(1, std::min<int64_t>((kp + 7) / 8, (4096 + waves - 1) / waves));
+    };
     if ((R & 3) == 0 && (((uintptr_t)h1T) & 15) == 0) {  // 4-row groups: 8-B (bf16) / 16-B (f32) aligned stores
+        const int G = slices(R / 4), fch = (kp + G - 1) / G;
+        const dim3 grid((unsigned)grid_for(R / 4), (unsigned)((kp + fch - 1) / fch));
         if (bf16)
-            hipLaunchKernelGGL(k_puct_h1_cols4<__hip_bfloat16>, dim3(grid_for(R / 4)), dim3(kBlock), 0, s, (uint32_t)R,
-                               (uint32_t)S, hidden, kp, n_cur, (const __hip_bfloat16*)baseT, cards, w1c,
-                               (__hip_bfloat16*)h1T);
+            hipLaunchKernelGGL(k_puct_h1_cols4<__hip_bfloat16>, grid, dim3(kBlock), 0, s, (uint32_t)R, (uint32_t)S, hidden,
+                               kp, n_cur, (const __hip_bfloat16*)baseT, cards, w1c, (__hip_bfloat16*)h1T, fch);
         else
-            hipLaunchKernelGGL(k_puct_h1_cols4<float>, dim3(grid_for(R / 4)), dim3(kBlock), 0, s, (uint32_t)R, (uint32_t)S,
-                               hidden, kp, n_cur, (const float*)baseT, cards, w1c, (float*)h1T);
+            hipLaunchKernelGGL(k_puct_h1_cols4<float>, grid, dim3(kBlock), 0, s, (uint32_t)R, (uint32_t)S, hidden, kp, n_cur,
+                               (const float*)baseT, cards, w1c, (float*)h1T, fch);
         HIP_TRY(hipGetLastError());
         return SN_OK;
     }
+    const int G = slices(threads), fch = (kp + G - 1) / G;
+    const dim3 grid((unsigned)grid_for(threads), (unsigned)((kp + fch - 1) / fch));
     if (bf16)
-        hipLaunchKernelGGL(k_puct_h1_cols<__hip_bfloat16>, dim3(grid_for(threads)), dim3(kBlock), 0, s, (uint32_t)R,
-                           (uint32_t)S, hidden, kp, n_cur, (const __hip_bfloat16*)baseT, cards, w1c, (__hip_bfloat16*)h1T);
+        hipLaunchKernelGGL(k_puct_h1_cols<__hip_bfloat16>, grid, dim3(kBlock), 0, s, (uint32_t)R, (uint32_t)S, hidden, kp,
+                           n_cur, (const __hip_bfloat16*)baseT, cards, w1c, (__hip_bfloat16*)h1T, fch);
     else
-        hipLaunchKernelGGL(k_puct_h1_cols<float>, dim3(grid_for(threads)), dim3(kBlock), 0, s, (uint32_t)R, (uint32_t)S,
-                           hidden, kp, n_cur, (const float*)baseT, cards, w1c, (float*)h1T);
+        hipLaunchKernelGGL(k_puct_h1_cols<float>, grid, dim3(kBlock), 0, s, (uint32_t)R, (uint32_t)S, hidden, kp, n_cur,
+                           (const float*)baseT, cards, w1c, (float*)h1T, fch);
     HIP_TRY(hipGetLastError());
     return SN_OK;
 }
