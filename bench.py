@@ -61,7 +61,9 @@ PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r03_pmc_traffic_{rng}.json")
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of this node, one rank each (default: WORLD_SIZE, else 1); without a launcher, N > 1 "
+                         "starts torch.distributed.run over N ranks as a child process")
     ap.add_argument("--steps", type=int, default=100, help="timed launches (episodes)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--games", type=int, default=65536, help="games per GPU")
@@ -90,6 +92,45 @@ def parse():
     return ap.parse_args()
 
 
+def launch_ranks(n):
+    """`python bench.py --gpus N` without a launcher (N > 1): run this same
+    command under torch.distributed.run, one rank per GPU on this node, as a
+    child process -- started before this process touches the GPU (no exec
+    from a process that has) -- and hand back its exit code; rank 0 of the
+    child prints the JSON line to the inherited stdout."""
+    import socket
+
+    try:
+        avail = torch.cuda.device_count()  # does not initialise the GPU on this image
+    except Exception:
+        avail = None
+    if avail is not None and avail < n and not os.environ.get("SECHS_BENCH_SHARED_GPU"):
+        # SECHS_BENCH_SHARED_GPU=1: rehearse the N-rank path on fewer GPUs
+        # (ranks share the visible devices; RCCL itself refuses two ranks on
+        # one GPU, SECHS_BENCH_BACKEND=gloo runs the whole path)
+        raise SystemExit(f"bench: --gpus {n} but {avail} GPU(s) visible (one rank per GPU)")
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
+def resolve_world(args):
+    """(ranks to use, True when this process must launch them itself)"""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if args.gpus is not None and args.gpus != int(env_world):
+            raise SystemExit(f"bench: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks")
+        return int(env_world), False
+    n = 1 if args.gpus is None else int(args.gpus)
+    if n < 1:
+        raise SystemExit("bench: --gpus must be >= 1")
+    return n, n > 1
+
+
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -102,8 +143,9 @@ def dist_setup(args):
         # driver's runs use the default, nccl (= RCCL), one GPU per rank
         backend = os.environ.get("SECHS_BENCH_BACKEND", "nccl")
         if backend == "nccl":
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dev = local % torch.cuda.device_count() if os.environ.get("SECHS_BENCH_SHARED_GPU") else local
+            torch.cuda.set_device(dev)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             torch.cuda.set_device(local % torch.cuda.device_count())
             dist.init_process_group(backend)
@@ -382,9 +424,7 @@ def bench_league(world, rank, slots, rounds, warmup=2, K=5, lo=2, hi=4):
     rank.  Then the RCCL score gather: all_reduce of the per-agent sums and
     all_gather of every game's record, Elo replayed on rank 0 (host C++) in
     canonical order -- timed separately."""
-    import torch.distributed as dist
-
-    from rl_6_nimmt.distributed import gather_league_records, reduce_agent_stats
+    from rl_6_nimmt.distributed import gather_league_records, max_over_ranks, reduce_agent_stats
     from rl_6_nimmt.league import BatchedTournament, replay_league_elo
 
     t = BatchedTournament(slots, lo, hi, seed=0, game_offset=rank * slots, rng="numpy")
@@ -392,7 +432,7 @@ def bench_league(world, rank, slots, rounds, warmup=2, K=5, lo=2, hi=4):
         t.add_player(f"DrunkHamster_{i}")
     t.play_games(warmup)
     t.agent_stats()  # first use of the scoring kernels, outside the timing
-    t.records.clear()
+    t.clear_records()
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
@@ -405,14 +445,17 @@ def bench_league(world, rank, slots, rounds, warmup=2, K=5, lo=2, hi=4):
     if t.env.pipe_errors():
         raise SystemExit("bench: tournament draws ran past the twisted words")
     tg = time.perf_counter()
-    stats = reduce_agent_stats(t.agent_stats())
-    allrec = gather_league_records(t.all_records())
+    # per-rank sums (host float64) and device records: the helpers place each
+    # on the device the group's backend takes (RCCL: the GPU)
+    from rl_6_nimmt.league import league_agent_stats
+
+    timed = t.all_records()  # the timed rounds only
+    stats = reduce_agent_stats(league_agent_stats(timed, K, hi))
+    allrec = gather_league_records(timed)
     torch.cuda.synchronize()
     gather_ms = (time.perf_counter() - tg) * 1e3
     if world > 1:
-        w = torch.tensor([wall, gather_ms], dtype=torch.float64, device=t.env.device)
-        dist.all_reduce(w, op=dist.ReduceOp.MAX)
-        wall, gather_ms = float(w[0].item()), float(w[1].item())
+        wall, gather_ms = max_over_ranks([wall, gather_ms], device=t.env.device)
     out = None
     if rank == 0:
         te = time.perf_counter()
@@ -471,9 +514,7 @@ def bench_league_mixed(world, rank, slots, mc_max=200, rounds=1, warmup=1):
     whole game, then every net agent's batched update), then the RCCL
     gather of the per-agent sums and every game record + the rank-0 Elo
     replay."""
-    import torch.distributed as dist
-
-    from rl_6_nimmt.distributed import gather_league_records, reduce_agent_stats
+    from rl_6_nimmt.distributed import gather_league_records, max_over_ranks, reduce_agent_stats
     from rl_6_nimmt.league import BatchedTournament, replay_league_elo
 
     # warm-up on a small league of the same agents (kernels, GEMM heuristics,
@@ -511,9 +552,7 @@ def bench_league_mixed(world, rank, slots, mc_max=200, rounds=1, warmup=1):
     torch.cuda.synchronize()
     gather_ms = (time.perf_counter() - tg) * 1e3
     if world > 1:
-        w = torch.tensor([wall, gather_ms], dtype=torch.float64, device=t.env.device)
-        dist.all_reduce(w, op=dist.ReduceOp.MAX)
-        wall, gather_ms = float(w[0].item()), float(w[1].item())
+        wall, gather_ms = max_over_ranks([wall, gather_ms], device=t.env.device)
     out = None
     if rank == 0:
         te = time.perf_counter()
@@ -731,6 +770,9 @@ def pmc_traffic(rng, games):
 
 def main():
     args = parse()
+    n, spawn = resolve_world(args)
+    if spawn:
+        sys.exit(launch_ranks(n))
     world, rank, local = dist_setup(args)
     legs = set(x for x in args.only.split(",") if x)
 
@@ -773,17 +815,13 @@ def main():
     sums, eps = env.results()
     tot = sums.to(torch.float64).sum(dim=0)
     if world > 1:
-        import torch.distributed as dist
+        from rl_6_nimmt.distributed import max_over_ranks, reduce_agent_stats
 
-        walls = torch.tensor([wall], dtype=torch.float64, device=env.device)
-        dist.all_reduce(walls, op=dist.ReduceOp.MAX)
-        wall = float(walls.item())
-        kms = torch.tensor([kern_ms, kt["k_play"], kt.get("k_mt_ahead", 0.0)], dtype=torch.float64, device=env.device)
-        dist.all_reduce(kms, op=dist.ReduceOp.MAX)
-        kern_ms, kt["k_play"] = float(kms[0].item()), float(kms[1].item())
+        wall, kern_ms, kt["k_play"], ahead = max_over_ranks([wall, kern_ms, kt["k_play"], kt.get("k_mt_ahead", 0.0)],
+                                                           device=env.device)
         if "k_mt_ahead" in kt:
-            kt["k_mt_ahead"] = float(kms[2].item())
-        dist.all_reduce(tot)
+            kt["k_mt_ahead"] = ahead
+        reduce_agent_stats(tot)
 
     total_steps = world * B * STEPS_PER_LAUNCH * args.steps
     value = total_steps / wall

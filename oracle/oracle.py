@@ -321,3 +321,28 @@ def league_records(num_agents, min_players, max_players, seed=0, game_offset=0, 
             out[e, j, 0] = w  # < 2^28: K <= 16 agents, k <= 6 seats
             out[e, j, 1: 1 + k] = [-s for s in g.scores]
     return out
+
+
+def league_mixed_records(kinds, min_players, max_players, mc_per_card=10, mc_max=100, seed=0, game_offset=0, slots=1,
+                         games=1, nthreads=None):
+    """Tournament streams of DrunkHamster ('R') and MCSAgent ('M') agents
+    (tournament.py:132-177, mcts.py:43-188): slot g replays np.random.seed(
+    seed + game_offset + g); Tournament(min, max) over the agents in `kinds`;
+    play_game() x games -- the MCS seats search on the same global stream,
+    in seat order.  Returns (records int32 [games, slots, 1 + max_players] in
+    the device's format, q6 int32 [slots]: MCS decisions where a legal move
+    got no playout -- quirk Q6, the best sampled move is played)."""
+    K = len(kinds)
+    mpc = np.ascontiguousarray(np.broadcast_to(np.asarray(mc_per_card, dtype=np.int32), (K,)))
+    mmx = np.ascontiguousarray(np.broadcast_to(np.asarray(mc_max, dtype=np.int32), (K,)))
+    rec = np.zeros((games, slots, 1 + max_players), dtype=np.int32)
+    st = np.zeros(slots, dtype=np.int32)
+    L = lib()
+    P = ctypes.c_void_p
+    L.or_league_mixed.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, ctypes.c_uint64,
+                                  ctypes.c_uint64, ctypes.c_int, ctypes.c_int, P, P, ctypes.c_int]
+    if nthreads is None:
+        nthreads = max(1, min(16, len(os.sched_getaffinity(0))))
+    L.or_league_mixed(kinds.encode(), K, min_players, max_players, _p(mpc), _p(mmx), seed, game_offset, slots, games,
+                      _p(rec), _p(st), nthreads)
+    return rec, st

@@ -406,7 +406,8 @@ static long long factorial_capped(int n, long long cap) {
     return f;
 }
 
-int or_mcs_forward(or_mcs* m, or_rng* r, const int64_t* state, int include_summaries, const int* legal, int n) {
+static int mcs_forward_q6(or_mcs* m, or_rng* r, const int64_t* state, int include_summaries, const int* legal, int n,
+                          int* q6) {
     const int L = or_obs_len(include_summaries);
     const int64_t* board = state + L - OR_ROWS * OR_THRESHOLD; /* _board_from_state: state[-24:] (mcts.py:75-85) */
     if (n == OR_HAND) {                                          /* _initialize_game (mcts.py:62-64) */
@@ -465,16 +466,25 @@ int or_mcs_forward(or_mcs* m, or_rng* r, const int64_t* state, int include_summa
     }
     /* _choose_action_from_outcomes (mcts.py:156-172); the debug f-string at
        :170 indexes log_probs[a][0] for every action -> IndexError if any
-       action got no rollout (quirk Q6) */
-    for (int i = 0; i < n; i++)
-        if (cnt[i] == 0) return -2;
+       action got no rollout (quirk Q6): flagged in *q6, and the best mean
+       over the moves that got playouts is returned (the device's choice) */
     int best = legal[0];
     double best_mean = -1.0 / 0.0;
     for (int i = 0; i < n; i++) {
+        if (cnt[i] == 0) {
+            *q6 = 1;
+            continue;
+        }
         double mean = sum[i] / (double)cnt[i];
         if (mean > best_mean) best_mean = mean, best = legal[i];
     }
     return best;
+}
+
+int or_mcs_forward(or_mcs* m, or_rng* r, const int64_t* state, int include_summaries, const int* legal, int n) {
+    int q6 = 0;
+    const int a = mcs_forward_q6(m, r, state, include_summaries, legal, n, &q6);
+    return q6 ? -2 : a;
 }
 
 int or_mcs_game(const char* seats, int num_players, int mc_per_card, int mc_max, uint32_t seed, int* actions,
@@ -569,6 +579,55 @@ void or_mcs_stratified(const or_game* root, int seat, const int* avail, int n_av
                 outcome += rw[0];
             }
             sums[a] += outcome;
+        }
+    }
+}
+
+/* ===================================================================== */
+/* Tournament of DrunkHamster and MCSAgent agents (tournament.py:132-177,  */
+/* play.py:23-75, agents/random.py:8-10, agents/mcts.py:43-188)            */
+/* ===================================================================== */
+void or_league_mixed(const char* kinds, int K, int lo, int hi, const int* mc_per_card, const int* mc_max, uint64_t seed,
+                     uint64_t game_offset, int slots, int games, int32_t* rec, int32_t* status, int nthreads) {
+#pragma omp parallel for schedule(dynamic) num_threads(nthreads > 0 ? nthreads : 1)
+    for (int j = 0; j < slots; j++) {
+        or_rng r;
+        or_rng_init_mt(&r, (uint32_t)(seed + game_offset + (uint64_t)j)); /* np.random.seed(seed + g) */
+        status[j] = 0;
+        for (int e = 0; e < games; e++) {
+            /* _choose_players (tournament.py:166-177): choice(range(lo, hi + 1))
+               = lo + random_interval(hi - lo); choice(K, k, replace=False) =
+               permutation(K)[:k] */
+            const int k = lo + (int)or_rng_interval(&r, (uint32_t)(hi - lo));
+            int perm[16];
+            for (int i = 0; i < K; i++) perm[i] = i;
+            or_shuffle_int(&r, perm, K);
+            /* GameSession(*agents).play_game(): a k-player env, reset (the deal) */
+            or_game g;
+            or_reset(&g, k, OR_MAX_CARDS, &r);
+            or_mcs mcs[OR_MAX_PLAYERS];
+            for (int p = 0; p < k; p++) or_mcs_init(&mcs[p], mc_per_card[perm[p]], mc_max[perm[p]]);
+            int64_t st[64];
+            while (!or_is_done(&g)) {
+                int a[OR_MAX_PLAYERS];
+                for (int p = 0; p < k; p++) { /* agents in seat order (play.py:38-41) */
+                    if (kinds[perm[p]] == 'M') {
+                        int q6 = 0;
+                        or_obs(&g, p, 1, st);
+                        a[p] = mcs_forward_q6(&mcs[p], &r, st, 1, g.hands[p], g.hand_len[p], &q6);
+                        status[j] += q6;
+                    } else {
+                        a[p] = or_random_policy(&r, &g, p);
+                    }
+                }
+                int32_t rw[OR_MAX_PLAYERS];
+                or_step(&g, a, rw);
+            }
+            int32_t* out = rec + ((int64_t)e * slots + j) * (1 + hi);
+            uint32_t w = (uint32_t)k;
+            for (int p = 0; p < k; p++) w |= (uint32_t)perm[p] << (4 + 4 * p);
+            out[0] = (int32_t)w;
+            for (int p = 0; p < hi; p++) out[1 + p] = (p < k) ? -g.scores[p] : 0;
         }
     }
 }

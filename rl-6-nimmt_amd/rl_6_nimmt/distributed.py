@@ -10,7 +10,14 @@ data path).  After a block of games:
     (tournament.py:157-164) in global game-id order;
   * `gather_league_records`: the same for the batched tournament's records
     (league.py), which carry no id column: rank order is global slot order.
-Works with any torch.distributed backend (nccl = RCCL on the GPUs, gloo on CPU).
+Works with any torch.distributed backend (nccl = RCCL on the GPUs, gloo on
+CPU): every helper hands the collective a tensor on the device the process
+group's backend takes (`collective_device`: RCCL takes device tensors only,
+`Backend.backend_capability['nccl'] == ['cuda']`) and returns the result on
+the caller's device, so callers may pass host or device tensors alike.
+The helpers run the collective whenever a process group is initialised,
+world size 1 included (a one-rank RCCL group then exercises the same
+device placement the N-rank run needs).
 """
 import numpy as np
 import torch
@@ -22,20 +29,55 @@ def shard(rank, world, games_per_rank):
     return rank * games_per_rank, games_per_rank
 
 
-def reduce_agent_stats(stats):
-    """stats: float64 tensor [K, F] of per-agent sums (games, score, wins, position)."""
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(stats, op=dist.ReduceOp.SUM)
+def group_active():
+    return dist.is_available() and dist.is_initialized()
+
+
+def world_size():
+    return dist.get_world_size() if group_active() else 1
+
+
+def collective_device(group=None):
+    """the device the process group's collectives take tensors on: the
+    current GPU for backends that only take device tensors (nccl = RCCL),
+    else the host (gloo and the other host-capable backends)"""
+    backend = str(dist.get_backend(group))
+    caps = dist.Backend.backend_capability.get(backend, ["cpu"])
+    if "cpu" in caps:
+        return torch.device("cpu")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def _on(t, dev):
+    return t if t.device == dev else t.to(dev)
+
+
+def reduce_agent_stats(stats, op=None):
+    """stats: float64 tensor [K, F] of per-agent sums (games, score, wins,
+    position), reduced in place over the ranks (and returned)."""
+    if group_active():
+        c = _on(stats.contiguous(), collective_device())
+        dist.all_reduce(c, op=dist.ReduceOp.SUM if op is None else op)
+        if c.data_ptr() != stats.data_ptr():
+            stats.copy_(c.to(stats.device))
     return stats
+
+
+def all_gather_cat(t, dim=0):
+    """every rank's `t` (same shape on every rank) concatenated along `dim`
+    in rank order, on t's device"""
+    if not group_active():
+        return t
+    c = _on(t.contiguous(), collective_device())
+    parts = [torch.empty_like(c) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, c)
+    return torch.cat(parts, dim=dim).to(t.device)
 
 
 def gather_game_records(records):
     """records: int32 tensor [G, 1 + 2*N] rows (global game id, seat agent ids, seat scores),
     same G on every rank.  Returns all ranks' rows sorted by global game id."""
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        parts = [torch.empty_like(records) for _ in range(dist.get_world_size())]
-        dist.all_gather(parts, records)
-        records = torch.cat(parts, dim=0)
+    records = all_gather_cat(records, dim=0)
     order = torch.argsort(records[:, 0].to(torch.int64), stable=True)
     return records[order]
 
@@ -45,11 +87,15 @@ def gather_league_records(records):
     (rank r owns global slots [r*slots, (r+1)*slots)), all_gather'ed (RCCL on
     the GPUs) into [games, world*slots, 1 + N]: round major, then global slot
     id -- the canonical order of the Elo replay (league.replay_league_elo)."""
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        parts = [torch.empty_like(records) for _ in range(dist.get_world_size())]
-        dist.all_gather(parts, records.contiguous())
-        records = torch.cat(parts, dim=1)
-    return records
+    return all_gather_cat(records, dim=1)
+
+
+def max_over_ranks(values, device=None):
+    """elementwise max of a list of floats over the ranks (wall times)"""
+    t = torch.tensor(list(values), dtype=torch.float64, device=device)
+    if group_active():
+        reduce_agent_stats(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.tolist()]
 
 
 def replay_elo(records, num_agents, num_players, elo_initial=1600.0, elo_k=32.0):

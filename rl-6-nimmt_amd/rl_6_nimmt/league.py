@@ -56,12 +56,14 @@ logger = logging.getLogger(__name__)
 
 STAT_GAMES, STAT_SCORE, STAT_POSITION, STAT_WINS = range(4)
 KIND_RANDOM, KIND_MCS, KIND_PUCT, KIND_CUSTOMED, KIND_ACER = "random", "mcs", "puct", "customed", "acer"
+KIND_REINFORCE = "reinforce"
+NET_KINDS = (KIND_PUCT, KIND_CUSTOMED, KIND_ACER, KIND_REINFORCE)
 T_STEPS = 10
 
 
 def agent_kind(agent):
     """the batched engine that plays `agent` (tournament.py seats any Agent)"""
-    from .agents import BatchedACERAgent, DrunkHamster, MCSAgent, PolicyMCSAgent, PUCTCustomedAgent
+    from .agents import BatchedACERAgent, BatchedReinforceAgent, DrunkHamster, MCSAgent, PolicyMCSAgent, PUCTCustomedAgent
 
     if isinstance(agent, PUCTCustomedAgent):
         return KIND_CUSTOMED
@@ -71,6 +73,8 @@ def agent_kind(agent):
         return KIND_MCS
     if isinstance(agent, BatchedACERAgent):
         return KIND_ACER
+    if isinstance(agent, BatchedReinforceAgent):
+        return KIND_REINFORCE
     if isinstance(agent, DrunkHamster):
         return KIND_RANDOM
     raise NotImplementedError(f"the batched tournament has no engine for {type(agent).__name__}")
@@ -114,21 +118,37 @@ class BatchedTournament:
     (one rank's shard: global slot ids game_offset .. game_offset + num_slots - 1)."""
 
     def __init__(self, num_slots, min_players=2, max_players=4, seed=0, game_offset=0, rng="numpy", device=None,
-                 elo_initial=1600, elo_k=32, net_dtype=torch.bfloat16, train=False, fused=True):
+                 elo_initial=1600, elo_k=32, net_dtype=torch.bfloat16, train=False, fused=True, distributed=False):
+        """distributed=True: this handle is one rank's shard of ONE tournament
+        over the initialised process group (every rank constructs it with the
+        same roster and calls the same methods): the tallies and Elo that
+        evolve / agent_stats / replay_elo use are folded from every rank's
+        records (all_gather, canonical order), so every rank keeps the same
+        roster.  False: the tallies are this rank's own (reduce them with
+        distributed.reduce_agent_stats), and evolve refuses to run on more
+        than one rank."""
         assert 0 < min_players <= max_players
         self.num_slots, self.min_players, self.max_players = int(num_slots), int(min_players), int(max_players)
         self.seed, self.game_offset, self.rng, self.device = int(seed), int(game_offset), rng, device
         self.elo_initial, self.elo_k = float(elo_initial), float(elo_k)
         self.net_dtype, self.train, self.fused = net_dtype, bool(train), bool(fused)
+        self.distributed = bool(distributed)
         # the roster, in the reference's dict order (tournament.py:25-35)
         self.names, self.agents, self.active, self.descendants, self.kinds = [], {}, {}, {}, {}
         self.env = None
         self.mode = None  # "fused" (all DrunkHamster, sn_league_rollout) or "step" (sn_league_step)
         self.engines = {}  # net agent name -> batched engine
         self.records = []  # (int32 [games, slots, 1 + N] on the device, roster index of each active agent)
+        self.record_names = []  # the active agents' names of each records block (roster indices shift on deletes)
         self.stats = np.zeros((0, 4), dtype=np.float64)  # per roster agent: games, score, position, wins
         self.elos = np.zeros((0,), dtype=np.float64)     # current Elo per roster agent
+        # per roster agent, its relative positions as the reference keeps them
+        # (float32, tournament.py:249-256) in play order -- (round, global
+        # slot) order here: evolve's "tournament_positions" key and winner()
+        # are np.mean over exactly this sequence, as the reference's are
+        self.positions = {}
         self.total_games = 0
+        self.q6_slot_rounds = 0  # (slot, round) pairs with an MCS decision where a legal move got no playout (Q6)
         self._seen = 0  # records already folded into stats / elos
 
     # ------------------------------------------------------------ roster (tournament.py:36-76)
@@ -147,6 +167,7 @@ class BatchedTournament:
         self.active[name], self.descendants[name] = True, name
         self.stats = np.concatenate((self.stats, np.zeros((1, 4))), axis=0)
         self.elos = np.concatenate((self.elos, [self.elo_initial]))
+        self.positions[name] = []
         if self.env is not None:
             self._configure()
 
@@ -168,6 +189,7 @@ class BatchedTournament:
         self.active[new_name], self.descendants[new_name] = self.active[old_name], self.descendants[old_name]
         self.stats = np.concatenate((self.stats, self.stats[i: i + 1]), axis=0)
         self.elos = np.concatenate((self.elos, self.elos[i: i + 1]))
+        self.positions[new_name] = list(self.positions[old_name])
 
     def remove_player(self, name, full_delete=False):
         """tournament.py:62-76"""
@@ -175,7 +197,7 @@ class BatchedTournament:
         if full_delete:
             i = self.names.index(name)
             self.names.pop(i)
-            for d in (self.agents, self.kinds, self.active, self.descendants):
+            for d in (self.agents, self.kinds, self.active, self.descendants, self.positions):
                 del d[name]
             self.stats = np.delete(self.stats, i, axis=0)
             self.elos = np.delete(self.elos, i)
@@ -196,6 +218,11 @@ class BatchedTournament:
         if self.mode == "fused":
             raise NotImplementedError("evolve needs the per-game round (BatchedTournament(..., fused=False)): the fused "
                                       "rollout draws each slot's next seats at the end of the game before")
+        from .distributed import world_size
+
+        if world_size() > 1 and not self.distributed:
+            raise RuntimeError("evolve on one rank's shard would rank the agents by that rank's games only and let "
+                               "the ranks' rosters diverge: construct the tournament with distributed=True")
         self._fold()
         s = self.stats
         table = {"tournament_scores": (STAT_SCORE, True, True), "tournament_positions": (STAT_POSITION, False, True),
@@ -205,11 +232,20 @@ class BatchedTournament:
         col, reverse, use_mean = table[metric]
 
         def key(name):
+            # the reference's keys (tournament.py:98-101): np.mean of the
+            # agent's list, 0. when empty; Elo: the latest value.  Scores and
+            # wins are integers / 0-1 floats, so their float64 mean is the sum
+            # over the count exactly; positions are float32 values whose
+            # float32 np.mean depends on their order, kept in self.positions
             i = self.names.index(name)
             if not use_mean:
                 return float(self.elos[i])  # the latest Elo (never empty)
             g = s[i, STAT_GAMES]
-            return float(s[i, col] / g) if g > 0 else 0.0
+            if g == 0:
+                return 0.0
+            if col == STAT_POSITION:
+                return np.mean(np.concatenate(self.positions[name]))
+            return float(s[i, col] / g)
 
         ranking = sorted(self.active_agents(), key=key, reverse=reverse)
         kept, per_family = 0, {}
@@ -267,7 +303,7 @@ class BatchedTournament:
         self._ids = torch.tensor([self.names.index(n) for n in act], dtype=torch.long)
         keep = {}
         for n in act:
-            if self.kinds[n] in (KIND_PUCT, KIND_CUSTOMED, KIND_ACER):
+            if self.kinds[n] in NET_KINDS:
                 keep[n] = self.engines.get(n) or self._engine(n)
         self.engines = keep
 
@@ -275,6 +311,7 @@ class BatchedTournament:
         """the batched engine of one net agent over this handle (decision-list mode)"""
         from .acer import BatchedACER
         from .puct import BatchedPUCT, BatchedPUCTCustomed
+        from .reinforce import BatchedReinforce
 
         agent, kind, env = self.agents[name], self.kinds[name], self.env
         agent.to(env.device)
@@ -287,6 +324,10 @@ class BatchedTournament:
                                net_dtype=self.net_dtype, mcs_num_cards=agent.num_cards, max_decisions=B)
         if kind == KIND_CUSTOMED:
             return BatchedPUCTCustomed(env, agent.actor, net_dtype=self.net_dtype, seed=seed, max_decisions=B)
+        if kind == KIND_REINFORCE:
+            return BatchedReinforce(env, agent.actor, net_dtype=self.net_dtype, seed=seed, gamma=agent.gamma,
+                                    r_factor=agent.r_factor, actor_weight=agent.actor_weight,
+                                    entropy_weight=agent.entropy_weight, max_decisions=B)
         return BatchedACER(env, agent.actor_critic, net_dtype=self.net_dtype, seed=seed, gamma=agent.gamma,
                            rollout_len=agent.rollout_len, minibatch=agent.batchsize, truncate=agent.truncate,
                            warmup=agent.warmup, r_factor=agent.r_factor, critic_weight=agent.critic_weight,
@@ -316,6 +357,7 @@ class BatchedTournament:
             rec = torch.stack(recs, dim=0)
             rew = torch.cat(rews, dim=0) if rewards else None
         self.records.append((rec, self._ids.clone()))
+        self.record_names.append(tuple(self.active_agents()))
         self.total_games += int(games) * self.num_slots
         return (rec, rew) if rewards else rec
 
@@ -352,7 +394,9 @@ class BatchedTournament:
         bad = int((invalid >= 0).sum())
         if bad:
             raise RuntimeError(f"sn_league_step: {bad} illegal moves of the net agents' engines")
-        if int(status.sum()):
+        q6 = int(status.sum())
+        if q6:
+            self.q6_slot_rounds += q6
             logger.warning("MCS: a legal move got no playout (the reference raises IndexError here, quirk Q6)")
         if self.train:
             self._learn(per_step)
@@ -362,6 +406,7 @@ class BatchedTournament:
         """one Adam step per net agent on its loss over the round's games"""
         from .acer import BatchedACER
         from .puct import BatchedPUCTCustomed
+        from .reinforce import BatchedReinforce
 
         for name, eng in self.engines.items():
             agent = self.agents[name]
@@ -374,7 +419,10 @@ class BatchedTournament:
                 continue
             if eng.D == 0 or not eng.decisions:
                 continue
-            loss = eng.loss(per_step) if isinstance(eng, BatchedPUCTCustomed) else eng.policy_loss()
+            if isinstance(eng, (BatchedPUCTCustomed, BatchedReinforce)):
+                loss = eng.loss(per_step)
+            else:
+                loss = eng.policy_loss()
             agent.optimizer.zero_grad()
             loss.backward()
             agent.optimizer.step()
@@ -392,31 +440,89 @@ class BatchedTournament:
         play order: the Elo is sequential, tournament.py:157-164)"""
         while self._seen < len(self.records):
             rec, ids = self.records[self._seen]
+            if self.distributed:  # every rank's games of this block, in global slot order
+                from .distributed import gather_league_records
+
+                rec = gather_league_records(rec)
             K = int(ids.numel())
             s = league_agent_stats(rec, K, self.max_players).cpu().numpy()
             np.add.at(self.stats, ids.numpy(), s)
+            for name, pos in zip(self.record_names[self._seen], league_positions32(rec, K, self.max_players)):
+                self.positions[name].append(pos)
             sub = replay_league_elo(rec, K, self.max_players, 0.0, self.elo_k, initial=self.elos[ids.numpy()])
             self.elos[ids.numpy()] = sub
             self._seen += 1
 
     def all_records(self):
-        """every game played so far, [games, slots, 1 + N] (round major;
-        seat ids index the active list of their round -- see records)"""
-        return torch.cat([r for r, _ in self.records], dim=0) if self.records else torch.zeros(
-            (0, self.num_slots, 1 + self.max_players), dtype=torch.int32)
+        """every game played so far, [games, slots, 1 + N] (round major).
+        Seat ids index the active list of their round, so the blocks of
+        rounds played under different rosters (evolve, copy_player,
+        remove_player in between) cannot share one tensor: use
+        `records_by_roster()` then."""
+        if not self.records:
+            return torch.zeros((0, self.num_slots, 1 + self.max_players), dtype=torch.int32)
+        ids0 = self.records[0][1]
+        if any(not torch.equal(ids, ids0) for _, ids in self.records[1:]):
+            raise ValueError("the records span a roster change (seat ids index each round's active list): use "
+                             "records_by_roster()")
+        return torch.cat([r for r, _ in self.records], dim=0)
+
+    def clear_records(self):
+        """fold the records so far into the tallies, then drop them (the
+        tallies, Elo and position lists keep every game)"""
+        self._fold()
+        self.records.clear()
+        self.record_names.clear()
+        self._seen = 0
+
+    def records_by_roster(self):
+        """[(records [games, slots, 1 + N], the names of the active agents the
+        seat ids of those records index)] -- one entry per play_games call"""
+        return [(r, list(names)) for (r, _), names in zip(self.records, self.record_names)]
+
+    def winner(self):
+        """tournament.py:197-206: the agent (active or not) with the best mean
+        relative position, first in roster order on ties; agents without
+        games have a NaN mean and never win"""
+        self._fold()
+        best, best_agent = -float("inf"), None
+        for name in self.names:
+            p = self.positions[name]
+            with np.errstate(all="ignore"):
+                m = np.mean(np.concatenate(p)) if p else np.float64("nan")
+            if m > best:
+                best, best_agent = m, self.agents[name]
+        return best_agent
+
+    def _to_roster(self, active_vals, fill):
+        """values per active agent (this roster's current active list) -> roster rows"""
+        out = np.full((len(self.names),) + tuple(active_vals.shape[1:]), fill, dtype=np.float64)
+        out[self._active_ids().numpy()] = active_vals
+        return out
+
+    def _active_ids(self):
+        return torch.tensor([self.names.index(n) for n in self.active_agents()], dtype=torch.long)
 
     def agent_stats(self, records=None):
-        """per-agent sums float64 [roster, 4]: games played, score, relative position, wins"""
+        """per-agent sums float64 [roster, 4]: games played, score, relative
+        position, wins.  `records` (seat ids indexing the CURRENT active
+        list) are mapped onto the roster rows through it."""
         if records is not None:
-            return league_agent_stats(records, len(self.names), self.max_players)
+            K = len(self.active_agents())
+            s = league_agent_stats(records, K, self.max_players).cpu().numpy()
+            return torch.from_numpy(self._to_roster(s, 0.0))
         self._fold()
         return torch.from_numpy(self.stats.copy())
 
     def replay_elo(self, records=None):
         """Elo of every roster agent after the games so far (round major, then
-        global slot id -- sn_elo_replay, host C++)"""
+        global slot id -- sn_elo_replay, host C++).  With `records` (seat ids
+        indexing the current active list): the Elo those games alone give,
+        every agent starting from elo_initial."""
         if records is not None:
-            return replay_league_elo(records, len(self.names), self.max_players, self.elo_initial, self.elo_k)
+            K = len(self.active_agents())
+            e = replay_league_elo(records, K, self.max_players, self.elo_initial, self.elo_k)
+            return self._to_roster(e, self.elo_initial)
         self._fold()
         return self.elos.copy()
 
@@ -425,7 +531,7 @@ class BatchedTournament:
         stats = self.agent_stats() if stats is None else stats
         elos = self.replay_elo() if elos is None else elos
         s = stats.cpu().numpy() if hasattr(stats, "cpu") else np.asarray(stats)
-        total = int(s[:, STAT_WINS].sum())  # one winner per game
+        total = self.total_games  # tournament.py:211 (clones inherit tallies: a sum over rows would double count)
         bar = "-----------------------------------------------------------------"
         out = [f"Tournament after {total} games:", bar,
                " Agent                | Games | Mean score | Win fraction |  ELO ", bar]
@@ -469,6 +575,17 @@ def league_agent_stats(records, num_agents, max_players):
     # atomics on K addresses (index_add_ serialises millions of them)
     onehot = ((ids.reshape(-1, 1) == torch.arange(K, device=rec.device)[None, :]) & valid.reshape(-1, 1)).to(torch.float64)
     return onehot.T @ vals.reshape(-1, 4)
+
+
+def league_positions32(records, num_agents, max_players):
+    """per active agent id, the float32 relative positions of its seats in
+    records [..., 1 + N], in row order (the reference's tournament_positions
+    entries: _compute_relative_positions in float32, tournament.py:249-256)"""
+    rec = records.reshape(-1, 1 + max_players)
+    k, ids = decode_seats(rec[:, 0], max_players)
+    rel = relative_positions(rec[:, 1:], k).to(torch.float32).cpu().numpy()
+    ids = ids.cpu().numpy()
+    return [rel[ids == a] for a in range(num_agents)]
 
 
 def replay_league_elo(records, num_agents, max_players, elo_initial=1600.0, elo_k=32.0, initial=None):

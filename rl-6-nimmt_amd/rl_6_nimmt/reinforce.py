@@ -26,18 +26,21 @@ from .puct import ROW, BatchedPUCT, ctypes_ref, make_actor
 
 class BatchedReinforce(BatchedPUCT):
     def __init__(self, env, actor=None, seats_mask=None, net_dtype=torch.bfloat16, seed=0, gamma=0.99, r_factor=1.0,
-                 actor_weight=1.0, entropy_weight=0.0):
+                 actor_weight=1.0, entropy_weight=0.0, max_decisions=None):
         super().__init__(env, actor if actor is not None else make_actor(), seed=seed, seats_mask=seats_mask,
-                         puct_root=False, net_dtype=net_dtype)
+                         puct_root=False, net_dtype=net_dtype, max_decisions=max_decisions)
         self.gamma, self.r_factor = float(gamma), float(r_factor)
         self.actor_weight, self.entropy_weight = float(actor_weight), float(entropy_weight)
-        D = self.D
+        D = self.D_max
         self.log_prob = torch.zeros((D,), dtype=torch.float32, device=env.device)
         self.entropy = torch.zeros((D,), dtype=torch.float32, device=env.device)
 
     def decide(self, n, memorize=False, record=False):
         """sample every deciding seat's card at hand size n: actions [B, N] int32"""
         L, h, st = nat.lib(), self.env._h, self.env._stream()
+        if self.D == 0:  # tournament mode: no seat of this agent in the current games
+            self.step_id += 1
+            return self.actions
         bf16 = int(self.net_dtype == torch.bfloat16)
         q = self._params(n)
         self.sync_net()
@@ -47,7 +50,7 @@ class BatchedReinforce(BatchedPUCT):
         nat.check(L.sn_policy_sample(h, ctypes_ref(q), nat.ptr(logits), nat.ptr(self.actions), nat.ptr(self.best_index),
                                      nat.ptr(self.log_prob), nat.ptr(self.entropy), st), "sn_policy_sample")
         if record:
-            self.decisions.append((self._train_rows(q, n, rows), n, self.best_index.clone()))
+            self.decisions.append((self._train_rows(q, n, rows), n, self.best_index[: self.D].clone()))
         self.step_id += 1
         return self.actions
 
@@ -71,8 +74,11 @@ class BatchedReinforce(BatchedPUCT):
 
     def returns(self, per_step):
         """discounted returns [D, T] of the rewards learn() would see"""
-        seats = [p for p in range(self.env.num_players) if (self.seats_mask >> p) & 1]
-        r = per_step[:, :, seats].reshape(per_step.shape[0], -1).T.double() * self.r_factor  # [D, T]
+        if self.dec is not None:  # tournament mode: the decision list's seats
+            r = per_step.reshape(per_step.shape[0], -1)[:, self.dec.long()].T.double() * self.r_factor
+        else:
+            seats = [p for p in range(self.env.num_players) if (self.seats_mask >> p) & 1]
+            r = per_step[:, :, seats].reshape(per_step.shape[0], -1).T.double() * self.r_factor  # [D, T]
         seen = torch.zeros_like(r)
         seen[:, 1:] = r[:, :-1]  # learn() at step t gets step t-1's reward
         G = torch.zeros_like(seen)

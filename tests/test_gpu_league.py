@@ -294,3 +294,188 @@ def test_two_rank_device_league_gather_equals_one_handle():
     assert np.allclose(stats, t.agent_stats().cpu().numpy())
     assert np.allclose(replay_league_elo(torch.from_numpy(allrec), 5, 4), t.replay_elo(), rtol=0, atol=1e-9)
     t.close()
+
+
+def _rccl_one_rank(port, q):
+    """a one-rank RCCL (backend 'nccl') group: the bench's config-5 legs run
+    their score gathers through it -- the collectives then take exactly the
+    device placement an N-rank RCCL run needs"""
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, init_method=f"tcp://127.0.0.1:{port}",
+                           device_id=torch.device("cuda", 0))
+    import bench
+    from rl_6_nimmt import distributed as D
+
+    assert D.collective_device().type == "cuda"
+    host = D.reduce_agent_stats(torch.ones((3, 4), dtype=torch.float64))  # a host tensor through RCCL
+    assert host.device.type == "cpu" and bool((host == 1).all())
+    league = bench.bench_league(1, 0, 2048, 2)
+    mixed = bench.bench_league_mixed(1, 0, 256, mc_max=10)
+    wall = D.max_over_ranks([1.5, 2.5], device=torch.device("cuda", 0))
+    dist.destroy_process_group()
+    q.put((league["agents"], mixed["agents"], wall))
+
+
+def test_rccl_group_runs_the_bench_score_gathers():
+    """round 3 handed RCCL a host tensor (BatchedTournament.agent_stats) and
+    the N>1 bench died at its config-5 leg; every collective of the bench's
+    league legs now goes through a one-rank RCCL group on the GPU"""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_one_rank, args=(port, q))
+    p.start()
+    league, mixed, wall = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert sum(a["games"] for a in league.values()) > 0 and sum(a["games"] for a in mixed.values()) > 0
+    assert wall == [1.5, 2.5]
+
+
+def _f13():
+    return load("evolve_games.json")["cases"]
+
+
+def _roster_names(roster):
+    return [r["name"] for r in roster]
+
+
+@pytest.mark.parametrize("ci", range(5))
+def test_batched_league_with_evolve_replays_reference(ci):
+    """golden F13 end to end on the GPU: a one-slot tournament handle
+    (np.random.seed(seed) stream: seat draws over the CURRENT active list,
+    deals and DrunkHamster moves in-kernel) plays every block's games, evolve
+    runs between blocks -- every game's seats and results and the roster
+    after every evolve equal the reference tournament's
+    (tournament.py:54-177)"""
+    from rl_6_nimmt.league import decode_seats
+
+    case = _f13()[ci]
+    hi = case["max_players"]
+    from rl_6_nimmt.agents import DrunkHamster
+
+    t = _mixed(1, [(f"a{i}", DrunkHamster())
+                   for i in range(case["num_agents"])], case["min_players"], hi, seed=case["seed"])
+    for block in case["blocks"]:
+        active = t.active_agents()
+        rec = t.play_games(len(block["games"])).cpu()
+        k, ids = decode_seats(rec[..., 0], hi)
+        for e, g in enumerate(block["games"]):
+            kk = len(g["names"])
+            assert int(k[e, 0]) == kk
+            assert [active[i] for i in ids[e, 0, :kk].tolist()] == g["names"], (ci, e)
+            assert rec[e, 0, 1: 1 + kk].tolist() == g["results"], (ci, e)
+        if "evolve" in block:
+            ev = dict(block["evolve"])
+            ev["copies"] = tuple(ev["copies"])
+            t.evolve(**ev)
+            assert t.names == _roster_names(block["after"])
+            assert [t.active[n] for n in t.names] == [r["active"] for r in block["after"]]
+            st = t.agent_stats().numpy()
+            assert st[:, 0].tolist() == [r["played_games"] for r in block["after"]]
+            assert t.elos.tolist() == [r["elo"] for r in block["after"]]
+    assert t.env.pipe_errors() == 0
+    t.close()
+
+
+def test_dropin_tournament_with_evolve_replays_reference():
+    """the drop-in Tournament (host league over the one-game device env) on
+    golden F13: np.random.seed(seed), play_game x games, evolve between blocks"""
+    from rl_6_nimmt import Tournament
+    from rl_6_nimmt.agents import DrunkHamster
+
+    for case in _f13()[:3]:
+        np.random.seed(case["seed"])
+        t = Tournament(case["min_players"], case["max_players"])
+        for i in range(case["num_agents"]):
+            t.add_player(f"a{i}", DrunkHamster())
+        for block in case["blocks"]:
+            for g in block["games"]:
+                t.play_game()
+            if "evolve" in block:
+                ev = dict(block["evolve"])
+                ev["copies"] = tuple(ev["copies"])
+                for r in block["before"]:
+                    assert [int(x) for x in t.tournament_scores[r["name"]]] == r["scores"]
+                t.evolve(**ev)
+                assert list(t.agents.keys()) == _roster_names(block["after"])
+                assert [t.elos[n][-1] for n in t.agents] == [r["elo"] for r in block["after"]]
+
+
+def test_mixed_league_every_slot_equals_oracle():
+    """DrunkHamster + MCSAgent league (reference-exact MCS on each slot's
+    numpy stream, sn_league_step) at 512 slots x 3 games: EVERY slot's
+    records equal the oracle's restatement (oracle.league_mixed_records,
+    itself pinned to golden F11's seeded reference tournaments)"""
+    from oracle import oracle as O
+    from rl_6_nimmt.agents import DrunkHamster, MCSAgent
+
+    kinds, B, G = "RMRMR", 512, 3
+    specs = [(f"{c}{i}", MCSAgent(mc_max=100) if c == "M" else DrunkHamster()) for i, c in enumerate(kinds)]
+    t = _mixed(B, specs, 2, 4, seed=77)
+    rec = t.play_games(G).cpu().numpy()
+    ref, q6 = O.league_mixed_records(kinds, 2, 4, mc_per_card=10, mc_max=100, seed=77, slots=B, games=G)
+    assert t.mode == "step"
+    bad = np.nonzero((rec != ref).any(axis=(0, 2)))[0]
+    assert bad.size == 0, f"slots differing from the oracle: {bad[:10].tolist()}"
+    assert (t.q6_slot_rounds > 0) == (int(q6.sum()) > 0)
+    assert t.env.pipe_errors() == 0
+    t.close()
+
+
+def test_mixed_league_full_size_sharding_invariance():
+    """65 536-slot DrunkHamster + MCSAgent league: two half-size handles
+    (game_offset) give exactly the records of one full handle, and a sample
+    of slots equals the oracle"""
+    from oracle import oracle as O
+    from rl_6_nimmt.agents import DrunkHamster, MCSAgent
+
+    kinds, B = "RMRRM", 65536
+
+    def specs():
+        return [(f"{c}{i}", MCSAgent(mc_max=100) if c == "M" else DrunkHamster()) for i, c in enumerate(kinds)]
+
+    t = _mixed(B, specs(), 2, 4, seed=9)
+    rec = t.play_games(1)
+    h = [_mixed(B // 2, specs(), 2, 4, seed=9, game_offset=o) for o in (0, B // 2)]
+    halves = torch.cat([x.play_games(1) for x in h], dim=1)
+    assert torch.equal(rec, halves)
+    ref, _ = O.league_mixed_records(kinds, 2, 4, seed=9, game_offset=B - 64, slots=64, games=1)
+    assert np.array_equal(rec[:, B - 64:].cpu().numpy(), ref)
+    for x in [t] + h:
+        assert x.env.pipe_errors() == 0
+        x.close()
+
+
+def test_league_seats_a_reinforce_agent_and_trains_it():
+    """BatchedReinforceAgent (agents/policy.py:109-201) takes a seat in the
+    batched tournament: its engine samples on its seats' decision list, every
+    move is legal (sn_league_step checks), and one REINFORCE step per round
+    moves its weights"""
+    from rl_6_nimmt.agents import BatchedReinforceAgent, DrunkHamster, MCSAgent
+
+    torch.manual_seed(1)
+    rf = BatchedReinforceAgent()
+    rf.train()
+    before = [p.detach().clone() for p in rf.parameters()]
+    specs = [("R0", DrunkHamster()), ("REINFORCE", rf), ("M", MCSAgent(mc_max=20)), ("R1", DrunkHamster())]
+    t = _mixed(256, specs, 2, 4, seed=12, train=True)
+    rec = t.play_games(2)
+    from rl_6_nimmt.league import decode_seats
+
+    k, ids = decode_seats(rec[..., 0], 4)
+    assert int((ids == 1).sum()) > 0  # the REINFORCE agent was seated
+    st = t.agent_stats()
+    assert int(st[:, 0].sum()) == int(k.sum()) and int(st[1, 0]) > 0
+    assert any(not torch.equal(a.detach().cpu(), b.cpu()) for a, b in zip(t.agents["REINFORCE"].parameters(), before))
+    assert t.env.pipe_errors() == 0
+    t.close()

@@ -18,7 +18,8 @@ def _pair(names, scores, positions, wins, elos):
         ref.add_player(n, DrunkHamster())
         bt.add_player(n, DrunkHamster())
         ref.tournament_scores[n] = list(scores[i])
-        ref.tournament_positions[n] = list(positions[i])
+        ref.tournament_positions[n] = list(np.asarray(positions[i], dtype=np.float32))  # float32, as the reference's
+        bt.positions[n] = [np.asarray(positions[i], dtype=np.float32)]
         ref.tournament_wins[n] = list(wins[i])
         ref.played_games[n] = len(scores[i])
         ref.elos[n] = [1600.0, elos[i]]
@@ -59,5 +60,12 @@ def test_agent_kinds():
     assert agent_kind(PUCTAgent()) == "puct" and agent_kind(PolicyMCSAgent()) == "puct"
     assert agent_kind(PUCTCustomedAgent()) == "customed"
     assert agent_kind(BatchedACERAgent()) == "acer"
-    with pytest.raises(NotImplementedError):
-        agent_kind(BatchedReinforceAgent())
+    assert agent_kind(BatchedReinforceAgent()) == "reinforce"
+    from rl_6_nimmt.agents import AGENTS
+
+    for name, cls in AGENTS.items():  # every registered agent the drop-in has takes a seat
+        try:
+            agent = cls()
+        except TypeError:
+            continue
+        assert agent_kind(agent) in ("random", "mcs", "puct", "customed", "acer", "reinforce"), name

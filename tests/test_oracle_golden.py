@@ -197,3 +197,25 @@ def test_league_records_replay_reference_tournaments():
                 assert w & 15 == len(seats)
                 assert [(w >> (4 + 4 * p)) & 15 for p in range(len(seats))] == seats
                 assert out[e, j, 1: 1 + len(seats)].tolist() == res
+
+
+def test_mixed_league_restatement_replays_reference_tournaments():
+    """the oracle's DrunkHamster + MCSAgent tournament streams
+    (league_mixed_records) replay golden F11's "dropin" leagues -- seeded
+    reference Tournament.play_game() sequences with MCS seats searching on the
+    same global numpy stream (tournament.py:132-177, mcts.py:43-188): seat
+    draws, results; no Q6 decision in them"""
+    for lg in load("tournament_games.json")["dropin"]:
+        G, hi = len(lg["games"]), lg["max_players"]
+        rec, q6 = O.league_mixed_records(lg["kinds"], lg["min_players"], hi, lg["mc_per_card"], lg["mc_max"],
+                                         seed=lg["seed"], slots=1, games=G)
+        assert int(q6.sum()) == 0
+        for e, g in enumerate(lg["games"]):
+            k = len(g["names"])
+            w = int(rec[e, 0, 0])
+            assert w & 15 == k
+            assert [lg["agents"][(w >> (4 + 4 * p)) & 15] for p in range(k)] == g["names"], (lg["kinds"], e)
+            assert rec[e, 0, 1: 1 + k].tolist() == g["results"], (lg["kinds"], e)
+    # an all-DrunkHamster roster is the DrunkHamster restatement
+    r, _ = O.league_mixed_records("RRRRR", 2, 4, seed=5, slots=32, games=3)
+    assert np.array_equal(r, O.league_records(5, 2, 4, seed=5, slots=32, games=3))

@@ -47,6 +47,10 @@ Fixture families (SURVEY.md §4 "What the build must add"):
                            seeded stream per slot (the batched league).
                            Tournament._compute_elos is replaced by a no-op
                            (multi_elo is absent: Elo stays unpinned).
+  F13 evolve_games.json  seeded Tournament games with evolve() between blocks
+                           (every metric, copies / max_players /
+                           max_per_descendant combinations, two or three
+                           evolves): games and the roster after each evolve
 """
 import argparse
 import json
@@ -838,6 +842,108 @@ def gen_tournament(ref, out):
                    "dropin": dropin, "league": league}, f)
 
 
+def _restated_elo():
+    """the build's multi_elo restatement (rl-6-nimmt_amd/rl_6_nimmt/elo.py),
+    loaded by path: multi_elo is absent, so F13's Elo values are that
+    restatement's (Elo arithmetic parity stays unpinned), while what F13 pins
+    -- evolve's ranking, cloning and pruning over them -- is the reference's"""
+    import importlib.util
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "rl-6-nimmt_amd", "rl_6_nimmt", "elo.py")
+    spec = importlib.util.spec_from_file_location("sechs_elo_restated", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _roster(t):
+    """the reference tournament's roster in its dict order, with every tally"""
+    return [{"name": n, "active": bool(t.active[n]), "descendant": t.descendants[n],
+             "played_games": int(t.played_games[n]), "scores": [int(x) for x in t.tournament_scores[n]],
+             "positions": [float(x) for x in t.tournament_positions[n]],
+             "wins": [float(x) for x in t.tournament_wins[n]], "elo": float(t.elos[n][-1]),
+             "elos": [float(x) for x in t.elos[n]]} for n in t.agents]
+
+
+def gen_evolve(ref, out):
+    """F13.  Seeded reference tournaments of DrunkHamster agents with
+    `evolve` between blocks of games (tournament.py:54-130): np.random.seed(
+    seed); Tournament(lo, hi); add_player a0..a{K-1}; then per block
+    play_game() x games followed by evolve(copies, max_players,
+    max_per_descendant, metric).  copy_player round-trips the agent through
+    temp_model.pt in the working directory (run here in a temporary one;
+    torch.load of that file, which torch.save wrote a line before in this
+    process, needs weights_only=False on torch >= 2.6).  Elo: the build's
+    restatement of multi_elo stands in (see _restated_elo).  Recorded: every
+    game (seat names, results) and the roster after each evolve (dict order,
+    active flags, families, tallies, Elo), plus the ranking keys."""
+    import functools
+
+    import torch
+    from rl_6_nimmt.agents import DrunkHamster
+    from rl_6_nimmt.tournament import Tournament
+
+    E = _restated_elo()
+    cases_in = [
+        # seed, K, lo, hi, [(games, evolve kwargs or None)]
+        (500, 5, 2, 4, [(6, dict(copies=(2,), max_players=None, max_per_descendant=2, metric="elo")),
+                        (6, dict(copies=(2, 1), max_players=5, max_per_descendant=2, metric="tournament_scores")),
+                        (4, None)]),
+        (501, 5, 2, 4, [(8, dict(copies=(2,), max_players=4, max_per_descendant=2, metric="tournament_positions")),
+                        (8, dict(copies=(3,), max_players=6, max_per_descendant=1, metric="tournament_wins")),
+                        (4, None)]),
+        (502, 6, 3, 4, [(10, dict(copies=(2, 2), max_players=None, max_per_descendant=None, metric="tournament_wins")),
+                        (6, dict(copies=(1,), max_players=5, max_per_descendant=3, metric="elo")),
+                        (5, dict(copies=(2,), max_players=6, max_per_descendant=2, metric="tournament_positions")),
+                        (3, None)]),
+        (503, 4, 2, 3, [(12, dict(copies=(2,), max_players=None, max_per_descendant=2, metric="tournament_positions")),
+                        (7, dict(copies=(), max_players=4, max_per_descendant=1, metric="tournament_scores")),
+                        (4, None)]),
+        (504, 8, 2, 4, [(16, dict(copies=(2, 2, 1), max_players=7, max_per_descendant=2, metric="elo")),
+                        (10, dict(copies=(2,), max_players=None, max_per_descendant=1, metric="tournament_scores")),
+                        (5, None)]),
+    ]
+    real_load = torch.load
+    cwd = os.getcwd()
+    tmp = tempfile.mkdtemp(prefix="sechs_evolve_")
+    cases = []
+    try:
+        os.chdir(tmp)
+        torch.load = functools.partial(real_load, weights_only=False)
+        for seed, K, lo, hi, blocks in cases_in:
+            np.random.seed(seed)
+            t = Tournament(min_players=lo, max_players=hi)
+            for i in range(K):
+                t.add_player(f"a{i}", DrunkHamster())
+
+            def elos(names, scores, t=t):
+                places = t._compute_absolute_positions(scores)
+                return E.calc_elo([E.EloPlayer(place=pl, elo=t.elos[n][-1]) for pl, n in zip(places, names)], t.elo_k)
+
+            t._compute_elos = elos
+            rec = []
+            for games, ev in blocks:
+                played = _play_recorded_games(t, games)
+                entry = {"games": played}
+                if ev is not None:
+                    entry["evolve"] = {k: (list(v) if isinstance(v, tuple) else v) for k, v in ev.items()}
+                    entry["before"] = _roster(t)
+                    t.evolve(**ev)
+                    entry["after"] = _roster(t)
+                rec.append(entry)
+            cases.append({"seed": seed, "num_agents": K, "min_players": lo, "max_players": hi, "blocks": rec,
+                          "total_games": int(t.total_games)})
+            print(f"  evolve seed={seed}: roster {[r['name'] for r in _roster(t) if r['active']]}", flush=True)
+    finally:
+        torch.load = real_load
+        os.chdir(cwd)
+    with open(os.path.join(out, "evolve_games.json"), "w") as f:
+        json.dump({"protocol": "np.random.seed(seed); t = Tournament(min_players, max_players); add_player(a{i}, "
+                               "DrunkHamster()) for i < num_agents; per block: t.play_game() x len(games), then "
+                               "t.evolve(**evolve) when given; Elo by the build's multi_elo restatement (elo.py); "
+                               "rosters in the reference's dict order", "cases": cases}, f)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests", "golden"))
@@ -858,6 +964,7 @@ def main():
         ("reinforce", gen_reinforce),
         ("acer", gen_acer),
         ("tournament", gen_tournament),
+        ("evolve", gen_evolve),
     ]
     for name, fn in steps:
         if args.only and name not in args.only.split(","):
