@@ -157,9 +157,16 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          are in lockstep (after sn_reset; N <= 4, auto-reset):
                          1 (default) or 0 (never).  Measured (65 536 x 4p):
                          74 -> 59 us per 10 env-steps.  Numpy-compat handles
-                         always use the pipelined one-wave k_play. */
+                         always use the pipelined one-wave k_play.
+     SN_OPT_PIPE_FLAGS   hand-off between the pipelined play launches (caller's
+                         stream) and the twist-ahead launches (side stream):
+                         1 (default where hipStreamWaitValue64 is supported):
+                         device flags -- a play lane polls its game's
+                         generation word, the side stream's CP waits on a
+                         block count -- so consecutive play launches have no
+                         packet between them; 0: HIP events both ways. */
 enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3, SN_OPT_TIMING = 4, SN_OPT_PIPE_GPW = 5,
-       SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7 };
+       SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7, SN_OPT_PIPE_FLAGS = 8 };
 sn_status sn_set_option(sn_env* env, int option, int value);
 /* pipelined rollouts whose draws ran past the twisted words (must be 0; a
    nonzero count means those games' draws are wrong) [sync].  The count is
@@ -373,6 +380,25 @@ sn_status sn_puct_seat_cols(sn_env* env, const sn_puct* q, int n_cur, void* cols
                             void* stream);
 sn_status sn_puct_h1_cols(sn_env* env, const sn_puct* q, int n_cur, const void* baseT, int hidden, const float* w1c,
                           const float* cards, void* h1T, int kp, int bf16, void* stream);
+/* Fused rollout MLP (replaces sn_puct_h1_cols + the PyTorch GEMMs of the
+   later layer and the head for MultiHeadedMLP(48, (H, H2), (1,)), H <= 111,
+   H2 <= 127 -- the reference's policy net, utils/nets.py:100-132, evaluated
+   in mcts.py:219-228):
+     sn_puct_seat_rows  rows [D*N][ks] bf16: seat-major form of sn_puct_seat_cols
+                        (same features, same cards output)
+     (caller, PyTorch)  base [D*N][ldb] bf16 = rows @ W1t (W1t [ks][ldb]: the
+                        transposed [W1 | b1 | 0] in columns < H, 1 at (48, H): the
+                        ones feature; ldb >= 112)
+     sn_puct_mlp        logits [D*N*n_cur] f32 (packed, for sn_puct_step with
+                        logit_stride 1, logit_bf16 0) = head . relu(w2 . h1),
+                        h1[k] = bf16(relu(base[seat][k] + card * w1c[k])) for k < 112,
+                        w2 [128][112] bf16 = [W2 | b2 | 0] rows (the row after the
+                        last output: the ones pass-through), head [128] f32 = [wh |
+                        bh | 0]: one v_mfma_f32_32x32x16_bf16 kernel, no activation
+                        in HBM.  base, w2, w1c, head 16-B aligned. */
+sn_status sn_puct_seat_rows(sn_env* env, const sn_puct* q, int n_cur, void* rows, int ks, float* cards, void* stream);
+sn_status sn_puct_mlp(sn_env* env, const sn_puct* q, int n_cur, const void* base, int ldb, const float* w1c,
+                      const float* cards, const void* w2, const float* head, float* logits, void* stream);
 /* best_index [D] (optional): index of the chosen card in the root legal list */
 sn_status sn_puct_choose(sn_env* env, const sn_puct* q, int32_t* actions, int32_t* best_index, void* stream);
 /* PUCTCustomedAgent (agents/mcts.py:325-451, replaces _mcts /

@@ -263,6 +263,7 @@ struct AheadArgs {
     int tout;  // ptend parity written
     int lead;  // words to keep twisted past the consumer (kPipeLead; smaller only to test the overrun path)
     uint32_t* perr_mirror;  // host-mapped copy of *perr, refreshed at launch start (off the play stream)
+    uint32_t gen;           // != 0: store it to pgen[g] once this game's ring bytes and twisted end are out
 };
 
 template <bool INIT>
@@ -299,7 +300,7 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
     } else {
         Tp = s.ptp[g];
         t0 = s.ptend[(int64_t)a.tin * B + g];
-        c = s.pabsc[(int64_t)a.cin * B + g];
+        c = ld_sc1(&s.pabsc[(int64_t)a.cin * B + g]);  // the play launch before last (other queue)
     }
     // signed: a consumer past the twisted end means a play lane overran
     // (counted there too); twist nothing rather than underflow the lead
@@ -311,7 +312,8 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
         const uint32_t y = mt_temper(v) & 0xFFu;
         const uint32_t d = y | (__shfl_down(y, 1) << 8) | (__shfl_down(y, 2) << 16) | (__shfl_down(y, 3) << 24);
         const uint32_t ri = (t0 + j) & (uint32_t)(kPipeRing - 1);
-        if ((lane & 3u) == 0u && j < n) st_nt((uint32_t*)(ring + ((int64_t)(ri >> 4) * B + g) * 16 + (ri & 12u)), d, SECHS_NT_MORE);
+        // sc1 (write-through): handed off to the next k_play on the other queue
+        if ((lane & 3u) == 0u && j < n) st_sc1((uint32_t*)(ring + ((int64_t)(ri >> 4) * B + g) * 16 + (ri & 12u)), d);
     };
     // phase 1: words 0 .. min(n, 224)
     uint32_t A[4], Bv[4], Cv[4], IX[4];
@@ -359,7 +361,11 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
             while (Tn > (uint32_t)kMtN) Tn -= kMtN;
         }
         s.ptp[g] = Tn;
-        s.ptend[(int64_t)a.tout * B + g] = t0 + n;
+        st_sc1(&s.ptend[(int64_t)a.tout * B + g], t0 + n);
+    }
+    if (a.gen) {  // every lane's ring / ptend stores drained, then the flag
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0u) st_sc1(&s.pgen[g], a.gen);
     }
 }
 
@@ -432,7 +438,26 @@ struct PlayArgs {
     int32_t* league_rec;     // league: [episodes][B][1 + N] per finished game: seats word, results
     int step0;               // league: env-steps of this rollout before this launch (episode index of a record)
     int n0;                  // k_play_split: every game's hand size at the launch's start (aligned handle)
+    uint32_t pgen_want;      // RNG_NUMPY_PIPE, device-flag mode: wait until pgen[g] reaches it (0: no wait)
+    unsigned long long* pdone;  // RNG_NUMPY_PIPE, device-flag mode: each block adds 1 when its stores are out
 };
+
+// device-flag pipeline: this lane's game waits for its twist-ahead words
+// (pgen[g] >= want, sc1 poll, wave-uniform exit).  Bounded: past ~1 s (the
+// wall clock runs at <= 100 MHz) the lane counts an overrun (perr, surfaced
+// as SN_ERNG) and goes on, so a lost hand-off can never hang the GPU.
+__device__ __noinline__ void pipe_wait(const DevState& s, int64_t g, uint32_t want) {
+    const uint64_t t0 = wall_clock64();
+    for (;;) {
+        const bool ok = (int32_t)(ld_sc1(&s.pgen[g]) - want) >= 0;
+        if (__all(ok)) return;
+        if (wall_clock64() - t0 > (1ull << 27)) {
+            if (!ok) atomicAdd(s.perr, 1u);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
 
 // The env-step loop of one lane (game g).  R supplies the random words
 // (topup/force, sechs_device.h).  Each wave
@@ -668,13 +693,15 @@ __device__ __forceinline__ void play_body(const DevState& s, const PlayArgs& a, 
     uint32_t lg = LG ? s.lgs[g] : 0u;
     ByteBuf buf;
     if constexpr (MODE == RNG_NUMPY_PIPE) {
+        if (a.pgen_want) pipe_wait(s, g, a.pgen_want);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);  // no ring load above the poll
         RingPipe rng;
         rng.load(s, g, buf, wave_lds + a.wave_lds - GPW * a.ring_lds + lane * a.ring_lds, a.pipe_cin, a.pipe_t);
         pp.mark(PH_PROLOGUE);
         StreamSrc<N, RingPipe> src{rng, buf, wave_lds + lane * kDealStride};
         play_steps<N, StreamSrc<N, RingPipe>, GPW, LG>(s, a, g, lane, wave_lds, G, src, sum_res, episodes, pp, lg, 0,
                                                        a.steps);
-        s.pabsc[(int64_t)a.pipe_cout * s.B + g] = rng.consumed(buf);
+        st_sc1(&s.pabsc[(int64_t)a.pipe_cout * s.B + g], rng.consumed(buf));  // read by k_mt_ahead on the other queue
     } else {
         typename RngOf<MODE, kPlayPrefetch>::T rng;
         if constexpr (MODE == RNG_NUMPY_RING || MODE == RNG_NUMPY_RING_HBM) {
@@ -700,6 +727,13 @@ template <int N, int MODE, int GPW = 64, bool LG = false>
 __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
     play_body<N, MODE, GPW, LG>(s, a, lds_dyn, (int)threadIdx.x);
+    if constexpr (MODE == RNG_NUMPY_PIPE) {
+        if (a.pdone) {  // device-flag pipeline: this block's pabsc stores are out -> count it (CP-polled)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0) __hip_atomic_fetch_add(a.pdone, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 // ---- one-game fast path (the scalar drop-in SechsNimmtEnv, B == 1) -------
@@ -1259,7 +1293,7 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
             size_t bytes;
         } pal[] = {{(void**)&s.pring, (size_t)kPipeRing * B}, {(void**)&s.pabsc, sizeof(uint32_t) * 2 * B},
                    {(void**)&s.ptend, sizeof(uint32_t) * 2 * B}, {(void**)&s.ptp, sizeof(uint32_t) * B},
-                   {(void**)&s.perr, sizeof(uint32_t)}};
+                   {(void**)&s.perr, sizeof(uint32_t)}, {(void**)&s.pgen, sizeof(uint32_t) * B}};
         for (auto& a : pal) {
             if (hipMalloc(a.p, a.bytes) != hipSuccess) {
                 sn_destroy(e);
@@ -1285,6 +1319,16 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
             return fail(SN_ENOMEM, "pinned overrun mirror allocation failed");
         }
         *e->perr_host = 0u;
+        // device-flag hand-off (default where the device supports CP-side
+        // stream waits on memory and the ring fits 32-bit buffer offsets)
+        int can_wait = 0;
+        (void)hipDeviceGetAttribute(&can_wait, hipDeviceAttributeCanUseStreamWaitValue, device);
+        if (can_wait && (uint64_t)kPipeRing * (uint64_t)B < (1ull << 32) &&
+            hipExtMallocWithFlags((void**)&e->pdone, sizeof(unsigned long long), hipMallocSignalMemory) == hipSuccess) {
+            (void)hipMemset(e->pdone, 0, sizeof(unsigned long long));
+            const char* pf = getenv("SECHS_PIPE_FLAGS");
+            e->pflags = (pf && pf[0] == '0') ? 0 : 1;
+        }
     }
     if (rng_mode == SN_RNG_NUMPY_MT) {
         const sn_status r = sn_set_option(e, SN_OPT_RING_WORDS, N <= 4 ? 256 : 512);
@@ -1315,11 +1359,12 @@ sn_status sn_destroy(sn_env* e) {
     if (e->ev_main) (void)hipEventDestroy(e->ev_main);
     if (e->ev_play) (void)hipEventDestroy(e->ev_play);
     if (e->perr_host) (void)hipHostFree(e->perr_host);
+    if (e->pdone) (void)hipFree(e->pdone);
     if (e->hbuf) (void)hipHostFree(e->hbuf);
     if (e->side) (void)hipStreamDestroy(e->side);
     free_timing(e);
     void* ps[] = {s.hand, s.row_lo, s.row_hi, s.score, s.sum_res, s.episodes, s.mt_pos, s.ctr, s.mt, s.mt0, s.ring,
-                  s.pring, s.pabsc, s.ptend, s.ptp, s.perr, s.lgs, s.lmem};
+                  s.pring, s.pabsc, s.ptend, s.ptp, s.perr, s.pgen, s.lgs, s.lmem};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     delete e;
@@ -1368,6 +1413,12 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
         case SN_OPT_PLAY_SPLIT:
             if (value < 0 || value > 1) return fail(SN_EINVAL, "play split must be 0 or 1");
             e->play_split = value;
+            return SN_OK;
+        case SN_OPT_PIPE_FLAGS:
+            if (value != 0 && value != 1) return fail(SN_EINVAL, "pipe flags must be 0 or 1");
+            if (value && !e->pdone) return fail(SN_EUNSUPPORTED, "no device-flag hand-off on this handle (numpy mode, "
+                                                                 "hipStreamWaitValue64 support, B * 1024 < 2^32)");
+            e->pflags = value;
             return SN_OK;
         case SN_OPT_PIPE_LEAD:
             if (value < 64 || value > kPipeLead) return fail(SN_EINVAL, "pipe lead must be in 64..600");
@@ -1532,8 +1583,12 @@ sn_status sn_pipe_sync(sn_env* e, hipStream_t st) {
     if (!e || !e->pvalid) return SN_OK;
     // k_pipe_code reads the last k_play's consumer position (pabsc) and the
     // last k_mt_ahead's twisted end: wait for both, whatever stream `st` is
-    // (the null stream does not order behind a non-blocking caller stream)
+    // (the null stream does not order behind a non-blocking caller stream).
+    // The events are recorded here, behind everything enqueued so far on
+    // the play stream and the side stream, not once per launch.
+    HIP_TRY(hipEventRecord(e->ev_play, e->pstream));
     HIP_TRY(hipStreamWaitEvent(st, e->ev_play, 0));
+    HIP_TRY(hipEventRecord(e->ev_prep, e->side));
     HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));
     const int p = (int)(e->pcount & 1u);
     hipLaunchKernelGGL(k_pipe_code, dim3(grid_for(e->s.B)), dim3(kBlock), 0, st, e->s, 1 - p, p);
@@ -1565,6 +1620,12 @@ static size_t pipe_lds(const DevState& s, const PlayArgs& a, int gpw, int* wave_
 // The pipelined numpy-MT rollout: per launch of <= 10 env-steps, k_play (on
 // the caller's stream) draws from words k_mt_ahead twisted during the
 // previous launch, while the next k_mt_ahead runs on the side stream.
+// Hand-off (SN_OPT_PIPE_FLAGS = 1, the default): no packet between two play
+// launches on the caller's stream -- each play lane polls its game's pgen
+// word (pipe_wait), and the side stream's CP waits on the pdone block count
+// (hipStreamWaitValue64) before each twist; 0: HIP events both ways (a wait
+// and a record on the caller's stream between play launches, ~10 us per
+// launch on gfx950: tools/queue_gap.hip).
 static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     DevState& s = e->s;
     int wave;
@@ -1574,18 +1635,34 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     a.ring_lds = kPipeSlot;
     a.vec_out = ((((uintptr_t)a.rewards) & 15) == 0) && ((((uintptr_t)a.actions_out) & 3) == 0);
     const dim3 pg((unsigned)((s.B + kBlock / 64 - 1) / (kBlock / 64)));
+    const bool fl = e->pflags && e->pdone;
+    auto next_gen = [&]() -> uint32_t {
+        if (++e->pgen_cur == 0u) e->pgen_cur = 1u;  // 0 = no wait
+        return e->pgen_cur;
+    };
     if (!e->pvalid) {  // start the pipeline from mt_pos: twist kPipeLead ahead, synchronously
         const int p = (int)(e->pcount & 1u);
-        hipLaunchKernelGGL(k_mt_ahead<true>, pg, dim3(kBlock), 0, st, s, AheadArgs{1 - p, 0, p, e->pipe_lead, e->perr_host_dev});
+        const uint32_t gen = fl ? next_gen() : 0u;
+        hipLaunchKernelGGL(k_mt_ahead<true>, pg, dim3(kBlock), 0, st, s,
+                           AheadArgs{1 - p, 0, p, e->pipe_lead, e->perr_host_dev, gen});
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(e->ev_prep, st));
+        if (fl) HIP_TRY(hipStreamWaitEvent(e->side, e->ev_prep, 0));  // the side's twists continue this state
         e->pvalid = 1;
+        e->pstream = st;
+    }
+    if (st != e->pstream) {  // another caller stream: order behind the last play launch
+        HIP_TRY(hipEventRecord(e->ev_play, e->pstream));
+        HIP_TRY(hipStreamWaitEvent(st, e->ev_play, 0));
+        e->pstream = st;
     }
     const int64_t B = s.B, N = s.N;
     // a tournament game adds its seat draw (<= K - 1 + 1 draws): 10-step
     // launches keep the pair tail < 1e-26 up to K = 8 agents at N <= 4
     // (tools/pipe_tail.py), beyond that 5-step launches
     const int chunk = min(e->chunk_steps, (s.lg_K > 8) ? 5 : pipe_max_chunk(s.N));
+    const unsigned nblk = (gpw == 32) ? (unsigned)((s.B + 32 * (kBlock / 64) - 1) / (32 * (kBlock / 64)))
+                                      : (unsigned)grid_for(s.B);
     for (int t0 = 0; t0 < a.steps; t0 += chunk) {
         PlayArgs c = a;
         c.steps = min(chunk, a.steps - t0);
@@ -1596,40 +1673,50 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         if (a.obs) c.obs = a.obs + (int64_t)t0 * B * N * a.obs_stride;
         const int p = (int)(e->pcount & 1u);
         c.pipe_cin = 1 - p, c.pipe_cout = p, c.pipe_t = p;
-        HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));  // this launch's words are twisted
-        HIP_TRY(hipEventRecord(e->ev_main, st));         // the previous launch's consumption is final
+        c.pgen_want = fl ? e->pgen_cur : 0u;  // the twist-ahead launched last holds this launch's words
+        c.pdone = fl ? e->pdone : nullptr;
+        if (!fl) {
+            HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));  // this launch's words are twisted
+            HIP_TRY(hipEventRecord(e->ev_main, st));         // the previous launch's consumption is final
+        }
         hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
         if (tv) HIP_TRY(hipEventRecord(tv[0], st));
         SN_DISPATCH_N(s.N, {
             if (gpw == 32) {
                 HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_PIPE, 32>,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
-                hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_PIPE, 32>), dim3((unsigned)((s.B + 32 * (kBlock / 64) - 1) / (32 * (kBlock / 64)))),
-                                   dim3(kBlock), shmem, st, s, c);
+                hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_PIPE, 32>), dim3(nblk), dim3(kBlock), shmem, st, s, c);
             } else if (s.lg_K) {
                 if constexpr (NN >= 2 && NN <= kLeagueMaxPlayers) {
                     HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_PIPE, 64, true>,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
-                    hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_PIPE, 64, true>), dim3(grid_for(s.B)), dim3(kBlock), shmem, st, s, c);
+                    hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_PIPE, 64, true>), dim3(nblk), dim3(kBlock), shmem, st, s, c);
                 }
             } else {
                 HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_PIPE>,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
-                hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_PIPE>), dim3(grid_for(s.B)), dim3(kBlock), shmem, st, s, c);
+                hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_PIPE>), dim3(nblk), dim3(kBlock), shmem, st, s, c);
             }
         });
         HIP_TRY(hipGetLastError());
         if (tv) HIP_TRY(hipEventRecord(tv[1], st));
         // the next launch's twist, beside this one: leads the consumer of the launch before
-        HIP_TRY(hipStreamWaitEvent(e->side, e->ev_main, 0));
+        uint32_t gen = 0u;
+        if (fl) {  // every block of the play launches before this one has counted itself
+            HIP_TRY(hipStreamWaitValue64(e->side, e->pdone, (uint64_t)e->pdone_launched, hipStreamWaitValueGte, ~0ull));
+            e->pdone_launched += nblk;
+            gen = next_gen();
+        } else {
+            HIP_TRY(hipStreamWaitEvent(e->side, e->ev_main, 0));
+        }
         if (tv) HIP_TRY(hipEventRecord(tv[2], e->side));
-        hipLaunchKernelGGL(k_mt_ahead<false>, pg, dim3(kBlock), 0, e->side, s, AheadArgs{1 - p, p, 1 - p, e->pipe_lead, e->perr_host_dev});
+        hipLaunchKernelGGL(k_mt_ahead<false>, pg, dim3(kBlock), 0, e->side, s,
+                           AheadArgs{1 - p, p, 1 - p, e->pipe_lead, e->perr_host_dev, gen});
         HIP_TRY(hipGetLastError());
         if (tv) HIP_TRY(hipEventRecord(tv[3], e->side));
-        HIP_TRY(hipEventRecord(e->ev_prep, e->side));
+        if (!fl) HIP_TRY(hipEventRecord(e->ev_prep, e->side));
         e->pcount++;
     }
-    HIP_TRY(hipEventRecord(e->ev_play, st));  // sn_pipe_sync orders behind the last k_play
     return SN_OK;
 }
 

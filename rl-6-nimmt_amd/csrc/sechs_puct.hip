@@ -243,11 +243,13 @@ __device__ __forceinline__ float round_to<__hip_bfloat16>(float v) { return __bf
 
 // seat column i = [0 (the card slot), obs (47)] normalised, 1 (bias), 0 pad
 // to ks features; cards[(i * n_cur) + k] = candidate k's normalised card
+// seat_major: column i is row i of a [S][ks] matrix instead (sn_puct_seat_rows)
 template <typename T>
-__global__ void k_puct_seat_cols(PuctArgs a, int N, int n_cur, T* cols, int ks, float* cards) {
+__global__ void k_puct_seat_cols(PuctArgs a, int N, int n_cur, T* cols, int ks, float* cards, int seat_major) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t S = a.D * N;
-    if (i >= S) return;
+    const int64_t S0 = a.D * N;
+    if (i >= S0) return;
+    const int64_t S = seat_major ? 1 : S0;  // stride between features
     const int64_t d = i / N;
     const int q = (int)(i - d * N);
     const int32_t* ro = a.ro + d * kRoWords;
@@ -258,7 +260,7 @@ __global__ void k_puct_seat_cols(PuctArgs a, int N, int n_cur, T* cols, int ks, 
         dec_to_gp(a, d, g, p);
         kp = players_of(a, g);
     }
-    T* c = cols + i;
+    T* c = cols + (seat_major ? i * ks : i);
     if (q >= kp) {  // an absent seat of a smaller tournament game (its logits are never read)
         for (int f = 0; f < ks; f++) c[f * S] = to_out<T>(f == kRowLen ? 1.f : 0.f);
         for (int k = 0; k < n_cur; k++) cards[i * n_cur + k] = 0.f;
@@ -341,6 +343,121 @@ __global__ __launch_bounds__(256) void k_puct_h1_cols(uint32_t R, uint32_t S, in
         } else {
             o[0] = to_out<T>(v0);
             if (two) o[1] = to_out<T>(v1);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- fused rollout MLP
+// The rollout policy net MultiHeadedMLP(48, (H, H2), (1,)) (utils/nets.py:100-132)
+// per candidate row r = [card, obs of its seat]:
+//   h1  = relu(W1 [card, obs] + b1)                 (layer 1)
+//   h2  = relu(W2 h1 + b2)                          (layer 2)
+//   out = wh . h2 + bh                              (head: the policy logit)
+// The obs part of layer 1 is shared by a seat's candidates: base[seat] =
+// W1[:, 1:] obs + b1 comes from one PyTorch GEMM over the seats
+// (sn_puct_seat_rows + torch.mm), and k_puct_mlp does the rest for a tile of
+// 64 rows per wave in registers: h1[k][r] = relu(base[seat(r)][k] + card(r) *
+// w1c[k]) built straight into the B fragments of v_mfma_f32_32x32x16_bf16
+// (bf16, as k_puct_h1_cols rounds it), layer 2 as 4 x 7 MFMA tiles per 32
+// rows against W2 staged in LDS (bias b2 = the column against the ones
+// feature h1[H] = 1), ReLU + bf16 rounding (the layer's output dtype in the
+// PyTorch path), then the head as a dot with wh over each lane's 16
+// accumulator rows and one cross-half lane swap.  The [features][rows]
+// activations of both layers never reach HBM: per row 4 B of card in, 4 B of
+// f32 logit out, plus the seat's base row (224 B, shared by its n_cur rows).
+// Shapes: K = 112 (7 k-steps of 16: H <= 111 features + the ones feature),
+// M = 128 (4 tiles of 32: H2 <= 127 outputs + the ones pass-through row).
+constexpr int kMlpK = 112;           // layer-2 inputs (padded)
+constexpr int kMlpM = 128;           // layer-2 outputs (padded)
+constexpr int kMlpLdsK = kMlpK + 8;  // LDS row stride of W2 (240 B: 60 dwords, lanes o spread over the banks)
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+__device__ __forceinline__ float bf16_bits_to_f32(uint32_t b) { return __uint_as_float(b << 16); }
+__device__ __forceinline__ uint32_t f32_to_bf16_rne(float v) {  // __float2bfloat16 (finite values)
+    const uint32_t u = __float_as_uint(v);
+    return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+
+__global__ __launch_bounds__(256) void k_puct_mlp(uint32_t R, int n_cur, const uint16_t* base, int ldb,
+                                                 const float* w1c, const float* cards, const uint16_t* w2,
+                                                 const float* head, float* logits) {
+    __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kMlpLdsK];
+    __shared__ __attribute__((aligned(16))) float sC[kMlpK];
+    __shared__ __attribute__((aligned(16))) float sH[kMlpM];
+    for (int i = threadIdx.x; i < kMlpM * (kMlpK / 8); i += blockDim.x) {  // W2: 16-B pieces
+        const int o = i / (kMlpK / 8), c = i - o * (kMlpK / 8);
+        *(uint4*)&sW[o * kMlpLdsK + 8 * c] = *(const uint4*)&w2[o * kMlpK + 8 * c];
+    }
+    for (int i = threadIdx.x; i < kMlpK; i += blockDim.x) sC[i] = w1c[i];
+    for (int i = threadIdx.x; i < kMlpM; i += blockDim.x) sH[i] = head[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, col = lane & 31, half = lane >> 5;
+    const uint32_t tiles = (R + 63u) / 64u;
+    const uint32_t wstep = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t tile = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); tile < tiles; tile += wstep) {
+        uint32_t rr[2];
+        float x[2];
+        const uint16_t* brow[2];
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++) {
+            rr[nt] = tile * 64u + 32u * nt + (uint32_t)col;
+            const uint32_t rc = rr[nt] < R ? rr[nt] : R - 1u;  // a short last tile: clamp the loads, skip the store
+            x[nt] = cards[rc];
+            brow[nt] = base + (size_t)(rc / (uint32_t)n_cur) * ldb;
+        }
+        f32x16_t acc[4][2];
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+            for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+                for (int i = 0; i < 16; i++) acc[mt][nt][i] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < kMlpK / 16; ks++) {
+            const int k0 = 16 * ks + 8 * half;  // this lane's 8 features of the k-step
+            const float4 wa = *(const float4*)&sC[k0], wb = *(const float4*)&sC[k0 + 4];
+            const float w[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+            bf16x8_t bfr[2];
+#pragma unroll
+            for (int nt = 0; nt < 2; nt++) {
+                const uint4 bv = *(const uint4*)(brow[nt] + k0);
+                const uint32_t bw[4] = {bv.x, bv.y, bv.z, bv.w};
+                uint32_t hb[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const float lo = fmaxf(bf16_bits_to_f32(bw[j] & 0xFFFFu) + x[nt] * w[2 * j], 0.f);
+                    const float hi = fmaxf(bf16_bits_to_f32(bw[j] >> 16) + x[nt] * w[2 * j + 1], 0.f);
+                    hb[j] = f32_to_bf16_rne(lo) | (f32_to_bf16_rne(hi) << 16);
+                }
+                bfr[nt] = __builtin_bit_cast(bf16x8_t, make_uint4(hb[0], hb[1], hb[2], hb[3]));
+            }
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++) {
+                const bf16x8_t a = __builtin_bit_cast(bf16x8_t, *(const uint4*)&sW[(32 * mt + col) * kMlpLdsK + k0]);
+                acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr[0], acc[mt][0], 0, 0, 0);
+                acc[mt][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr[1], acc[mt][1], 0, 0, 0);
+            }
+        }
+        // epilogue: relu, bf16 rounding, head dot over this lane's rows o, then the other half's
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++) {
+            float sum = 0.f;
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const float4 hv = *(const float4*)&sH[32 * mt + 8 * g + 4 * half];
+                    const float hw[4] = {hv.x, hv.y, hv.z, hv.w};
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const float v = bf16_bits_to_f32(f32_to_bf16_rne(fmaxf(acc[mt][nt][4 * g + i], 0.f)));
+                        sum = fmaf(v, hw[i], sum);
+                    }
+                }
+            sum += __shfl_xor(sum, 32);
+            if (half == 0 && rr[nt] < R) logits[rr[nt]] = sum;
         }
     }
 }
@@ -721,10 +838,44 @@ sn_status sn_puct_seat_cols(sn_env* e, const sn_puct* q, int n_cur, void* cols, 
     hipStream_t s = (hipStream_t)stream;
     if (bf16)
         hipLaunchKernelGGL(k_puct_seat_cols<__hip_bfloat16>, dim3(grid_for(total)), dim3(kBlock), 0, s, a, e->s.N, n_cur,
-                           (__hip_bfloat16*)cols, ks, cards);
+                           (__hip_bfloat16*)cols, ks, cards, 0);
     else
         hipLaunchKernelGGL(k_puct_seat_cols<float>, dim3(grid_for(total)), dim3(kBlock), 0, s, a, e->s.N, n_cur,
-                           (float*)cols, ks, cards);
+                           (float*)cols, ks, cards, 0);
+    HIP_TRY(hipGetLastError());
+    return SN_OK;
+}
+
+sn_status sn_puct_seat_rows(sn_env* e, const sn_puct* q, int n_cur, void* rows, int ks, float* cards, void* stream) {
+    PuctArgs a{};
+    sn_status st = puct_args(e, q, a);
+    if (st != SN_OK) return st;
+    if (n_cur < 1 || n_cur > a.n) return set_error(SN_EINVAL, "n_cur out of range");
+    if (!rows || !cards) return set_error(SN_EINVAL, "NULL argument");
+    if (ks <= kRowLen || ks > 256) return set_error(SN_EINVAL, "ks must be in 49..256 (48 features + the bias feature)");
+    const int64_t total = a.D * e->s.N;
+    hipLaunchKernelGGL(k_puct_seat_cols<__hip_bfloat16>, dim3(grid_for(total)), dim3(kBlock), 0, (hipStream_t)stream, a,
+                       e->s.N, n_cur, (__hip_bfloat16*)rows, ks, cards, 1);
+    HIP_TRY(hipGetLastError());
+    return SN_OK;
+}
+
+sn_status sn_puct_mlp(sn_env* e, const sn_puct* q, int n_cur, const void* base, int ldb, const float* w1c,
+                      const float* cards, const void* w2, const float* head, float* logits, void* stream) {
+    PuctArgs a{};
+    sn_status st = puct_args(e, q, a);
+    if (st != SN_OK) return st;
+    if (n_cur < 1 || n_cur > a.n) return set_error(SN_EINVAL, "n_cur out of range");
+    if (!base || !w1c || !cards || !w2 || !head || !logits) return set_error(SN_EINVAL, "NULL argument");
+    if (ldb < kMlpK || (ldb & 7)) return set_error(SN_EINVAL, "ldb must be >= 112 and a multiple of 8");
+    if ((((uintptr_t)base) | ((uintptr_t)w2) | ((uintptr_t)w1c) | ((uintptr_t)head)) & 15)
+        return set_error(SN_EINVAL, "base / w2 / w1c / head must be 16-B aligned");
+    const int64_t R = a.D * e->s.N * n_cur;
+    if (R >= (1ll << 31)) return set_error(SN_EINVAL, "too many rows");
+    const int64_t tiles = (R + 63) / 64;
+    const int64_t blocks = std::min<int64_t>((tiles + 3) / 4, 256 * 4);  // waves loop over the tiles beyond
+    hipLaunchKernelGGL(k_puct_mlp, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream, (uint32_t)R, n_cur,
+                       (const uint16_t*)base, ldb, w1c, cards, (const uint16_t*)w2, head, logits);
     HIP_TRY(hipGetLastError());
     return SN_OK;
 }

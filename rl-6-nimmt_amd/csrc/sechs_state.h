@@ -48,6 +48,12 @@ struct DevState {
     uint32_t* ptend; // [2][B] end of the twisted words after a prep launch (by launch parity)
     uint32_t* ptp;   // [B] twist pointer (MtGen's pos field), owned by k_mt_ahead
     uint32_t* perr;  // [1] play lanes that ran past the twisted words (must stay 0)
+    // device-flag hand-off of the pipeline (SN_OPT_PIPE_FLAGS): k_mt_ahead
+    // stores its ring bytes and twisted end write-through (sc1), drains them
+    // and then stores the launch generation in pgen[g]; a k_play lane polls
+    // its game's word before reading them (sc1 loads) -- no cross-queue event
+    // between consecutive play launches
+    uint32_t* pgen;  // [B] generation of the twist-ahead whose words the ring holds
     // batched tournament (sn_league_config): per game the current game's
     // player count k and seat agents, k | agent(seat p) << (4 + 4p)
     uint32_t* lgs;   // [B]
@@ -225,6 +231,25 @@ struct RingGen {
     __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf); }  // cnt == 0: always succeeds
 };
 
+// ---------------------------------------------------------------- sc1 accesses
+// The pipeline's cross-queue hand-off (MI355X_MICROARCH.md, hand-off forms
+// with sc1 loads): the producer (k_mt_ahead, side stream) stores every
+// handed-off byte with sc1 (write-through) stores, waits for them
+// (vmcnt(0)) and only then stores its flag with sc1; the consumer (k_play)
+// polls the flag with sc1 loads and reads every handed-off byte with sc1
+// loads (they bypass L1; no L1 line of the CU can be stale).
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// 16 B at byte offset `off` of a wave-uniform base, buffer_load_dwordx4 ... sc1
+__device__ __forceinline__ u32x4 ld16_sc1(const void* base, uint32_t off) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0xFFFFFFFFu, 0x00020000);
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16 /* sc1 */));
+}
+
 // numpy-MT words for k_play from the pipelined ring: k_mt_ahead twisted the
 // stream up to `tend` (593..600 words past the consumer position of the
 // launch before) while the previous k_play ran.  The first kPipeWin of those
@@ -249,7 +274,9 @@ static __device__ __noinline__ PipeSlow pipe_slow(const uint8_t* ring, int64_t B
     r.k = min(8u, left);
     for (uint32_t i = 0; i < r.k; i++) {
         const uint32_t ri = (pos + i) & (uint32_t)(kPipeRing - 1);
-        r.bytes |= (uint64_t)ring[((int64_t)(ri >> 4) * B + g) * 16 + (ri & 15u)] << (8u * i);
+        const int64_t at = ((int64_t)(ri >> 4) * B + g) * 16 + (ri & 15u);
+        const uint32_t w = ld_sc1((const uint32_t*)(ring + (at & ~3ll)));  // sc1: a handed-off byte
+        r.bytes |= (uint64_t)((w >> (8u * (uint32_t)(at & 3))) & 0xFFu) << (8u * i);
     }
     if (r.k == 0u) {
         atomicAdd(err, 1u);
@@ -270,7 +297,7 @@ struct RingPipe {
         c0 = s.pabsc[(int64_t)cin * B + g];
         // signed: a consumer past the twisted end (an earlier overrun) must
         // not read as a huge window of stale ring bytes
-        const int32_t av = (int32_t)(s.ptend[(int64_t)tpar * B + g] - c0);
+        const int32_t av = (int32_t)(ld_sc1(&s.ptend[(int64_t)tpar * B + g]) - c0);
         if (av < 0) atomicAdd(s.perr, 1u);
         avail = (av < 0) ? 0u : (uint32_t)av;
         win = min(avail, (uint32_t)kPipeWin);
@@ -282,7 +309,7 @@ struct RingPipe {
         const uint32_t q0 = (c0 & (uint32_t)(kPipeRing - 1)) >> 4;
         const uint32_t nch = (off + win + 15u) >> 4;
         for (uint32_t i = 0; i < nch; i++) {
-            const u32x4 c = s.pring[(int64_t)((q0 + i) & (uint32_t)(kPipeRing / 16 - 1)) * B + g];
+            const u32x4 c = ld16_sc1(s.pring, (uint32_t)((((q0 + i) & (uint32_t)(kPipeRing / 16 - 1)) * B + g) * 16));
             *(uint64_t*)(lds_slot + 16u * i) = (uint64_t)c.x | ((uint64_t)c.y << 32);
             *(uint64_t*)(lds_slot + 16u * i + 8u) = (uint64_t)c.z | ((uint64_t)c.w << 32);
         }
@@ -835,6 +862,15 @@ struct sn_env {
     uint64_t pcount;    // play launches so far (parity selects the pabsc / ptend buffers)
     hipStream_t side;
     hipEvent_t ev_prep, ev_main, ev_play;  // ev_play: after the last pipelined k_play (caller's stream)
+    // SN_OPT_PIPE_FLAGS: consecutive play launches with no cross-queue packet
+    // between them; each k_play lane waits for its game's pgen word, each
+    // k_mt_ahead waits (CP-side, hipStreamWaitValue64) for the play launch
+    // before the running one to have counted all its blocks into pdone
+    int pflags;               // SN_OPT_PIPE_FLAGS
+    uint32_t pgen_cur;        // generation of the last twist-ahead launched
+    unsigned long long* pdone;  // signal memory: k_play blocks finished (monotonic)
+    unsigned long long pdone_launched;  // k_play blocks launched so far
+    hipStream_t pstream;      // stream of the last pipelined k_play
     uint32_t* perr_host;                    // pinned, device-mapped mirror of s.perr (PlayArgs::perr_mirror)
     uint32_t* perr_host_dev;
     uint32_t* hbuf;      // one-game fast path (sn_step1 / sn_reset1): pinned, device-mapped exchange words

@@ -53,16 +53,46 @@ def default_capacity(rollout_len=10, minibatch=5, warmup=100):
     return max(4, -(-need // chunks) + 1)
 
 
+def replay_bytes(capacity, decisions):
+    """device bytes of a replay of `capacity` episodes x 10 steps x
+    `decisions` deciders: fp32 candidate rows [10][48], chosen slot (int64),
+    behaviour log pi [10] and reward (fp32)"""
+    return int(capacity) * T_STEPS * int(decisions) * (10 * ROW * 4 + 8 + 10 * 4 + 4)
+
+
+MAX_REPLAY_BYTES = 128 << 30  # default cap on one engine's replay (and at most 80 % of the free device memory)
+
+
 def make_actor_critic(hidden_sizes=(100, 100), activation=None):
     """the reference's net (actor_critic.py:44-46): MultiHeadedMLP(48, (100, 100), (1, 1)) -- policy logit, q"""
     return MultiHeadedMLP(ROW, hidden_sizes=hidden_sizes, head_sizes=(1, 1), activation=activation or nn.ReLU(),
                           head_activations=(None, None))
 
 
+def distinct_picks(S, rows, k, gen, dev):
+    """[rows, k] indices into range(S), each row k DISTINCT uniform picks
+    (random.sample per row, as the reference draws its off-policy batch):
+    rows with a repeated index are redrawn whole, which leaves every row
+    uniform over the ordered k-tuples of distinct indices"""
+    if k > S:
+        raise ValueError(f"sample of {k} distinct sequences from {S}")
+    if S <= 4 * k:  # few candidates: a permutation per row
+        return torch.rand((rows, S), generator=gen, device=dev).argsort(dim=1)[:, :k]
+    pick = torch.randint(0, S, (rows, k), generator=gen, device=dev)
+    for _ in range(64):
+        srt = pick.sort(dim=1).values
+        dup = (srt[:, 1:] == srt[:, :-1]).any(dim=1)
+        n = int(dup.sum())
+        if n == 0:
+            return pick
+        pick[dup] = torch.randint(0, S, (n, k), generator=gen, device=dev)
+    raise RuntimeError("distinct_picks: no distinct draw after 64 rounds")
+
+
 class BatchedACER(BatchedPUCT):
     def __init__(self, env, actor=None, seats_mask=None, net_dtype=torch.bfloat16, seed=0, gamma=0.99, rollout_len=10,
                  minibatch=5, truncate=1.0, warmup=100, r_factor=0.1, critic_weight=1.0, capacity=None,
-                 log_epsilon=-20.0, max_decisions=None):
+                 log_epsilon=-20.0, max_decisions=None, max_replay_bytes=None):
         super().__init__(env, actor if actor is not None else make_actor_critic(), seed=seed, seats_mask=seats_mask,
                          puct_root=False, net_dtype=net_dtype, max_decisions=max_decisions)
         self.gamma, self.truncate, self.r_factor = float(gamma), float(truncate), float(r_factor)
@@ -75,6 +105,19 @@ class BatchedACER(BatchedPUCT):
                           f"sequences per decider, so learn() never passes warmup {max(self.warmup, self.minibatch)} "
                           f"(capacity >= {default_capacity(rollout_len, minibatch, warmup)} learns)")
         D, dev = self.D_max, env.device
+        # the replay grows with capacity x deciders: refuse a size that would
+        # not fit instead of failing inside the allocator (the default
+        # capacity reaches warmup = 100 sequences: ~102 episodes)
+        need = replay_bytes(self.capacity, D)
+        cap = MAX_REPLAY_BYTES if max_replay_bytes is None else int(max_replay_bytes)
+        if dev.type == "cuda":
+            free, _ = torch.cuda.mem_get_info(dev)
+            cap = min(cap, int(0.8 * free))
+        if need > cap:
+            raise ValueError(f"BatchedACER: a replay of {self.capacity} episodes x {D} deciders needs {need / 2**30:.1f} "
+                             f"GiB (limit {cap / 2**30:.1f} GiB): pass a smaller capacity (each episode holds "
+                             f"{len(self.chunks())} sequences per decider; learn() starts past max(warmup, minibatch) = "
+                             f"{max(self.warmup, self.minibatch)} stored sequences) or fewer games")
         self.log_prob = torch.zeros((D,), dtype=torch.float32, device=dev)
         self.entropy = torch.zeros((D,), dtype=torch.float32, device=dev)
         C = self.capacity
@@ -276,8 +319,10 @@ class BatchedACER(BatchedPUCT):
     def league_batches(self, chunk):
         """(slots, chunk ids, decider indices) of the on-policy batch (every
         seat of the newest episode: its sequence `chunk`) and the off-policy
-        batch (`minibatch` stored sequences per seat, uniform over every
-        stored (slot, chunk, seat) of this agent)"""
+        batch (`minibatch` distinct stored sequences per seat, uniform over
+        every stored (slot, chunk, seat) of this agent -- the reference's
+        random.sample over its whole history, here over the replay's last
+        `capacity` rounds)"""
         dev = self.env.device
         s_new = (self.episodes - 1) % self.capacity
         Dn = self.rep_nd[s_new]
@@ -289,7 +334,7 @@ class BatchedACER(BatchedPUCT):
             nd = self.rep_nd[sl]
             tab.append(torch.stack((torch.full((nd,), sl), torch.full((nd,), c), torch.arange(nd)), dim=1))
         tab = torch.cat(tab, dim=0).to(dev)
-        pick = torch.randint(0, tab.shape[0], (Dn, self.minibatch), generator=self._gen, device=dev)
+        pick = distinct_picks(tab.shape[0], Dn, self.minibatch, self._gen, dev)
         off = (tab[pick, 0], tab[pick, 1], tab[pick, 2])
         return on, off
 

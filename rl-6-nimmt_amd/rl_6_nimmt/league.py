@@ -118,7 +118,8 @@ class BatchedTournament:
     (one rank's shard: global slot ids game_offset .. game_offset + num_slots - 1)."""
 
     def __init__(self, num_slots, min_players=2, max_players=4, seed=0, game_offset=0, rng="numpy", device=None,
-                 elo_initial=1600, elo_k=32, net_dtype=torch.bfloat16, train=False, fused=True, distributed=False):
+                 elo_initial=1600, elo_k=32, net_dtype=torch.bfloat16, train=False, fused=True, distributed=False,
+                 baseline_agents=None, baseline_num_games=1, baseline_condition=10):
         """distributed=True: this handle is one rank's shard of ONE tournament
         over the initialised process group (every rank constructs it with the
         same roster and calls the same methods): the tallies and Elo that
@@ -133,6 +134,14 @@ class BatchedTournament:
         self.elo_initial, self.elo_k = float(elo_initial), float(elo_k)
         self.net_dtype, self.train, self.fused = net_dtype, bool(train), bool(fused)
         self.distributed = bool(distributed)
+        # baseline evaluations (tournament.py:13-24,147-155,182-195): each time an
+        # agent's played-game count reaches a multiple of baseline_condition, one
+        # GameSession(agent, *baseline_agents) of baseline_num_games games;
+        # played here as batched sessions on their own handle (see _baselines)
+        self.baseline_agents = list(baseline_agents) if baseline_agents is not None else None
+        self.baseline_num_games, self.baseline_condition = int(baseline_num_games), int(baseline_condition)
+        self.baseline_scores, self.baseline_positions, self.baseline_wins = {}, {}, {}
+        self._baseline_calls = 0
         # the roster, in the reference's dict order (tournament.py:25-35)
         self.names, self.agents, self.active, self.descendants, self.kinds = [], {}, {}, {}, {}
         self.env = None
@@ -168,6 +177,7 @@ class BatchedTournament:
         self.stats = np.concatenate((self.stats, np.zeros((1, 4))), axis=0)
         self.elos = np.concatenate((self.elos, [self.elo_initial]))
         self.positions[name] = []
+        self.baseline_scores[name], self.baseline_positions[name], self.baseline_wins[name] = [], [], []
         if self.env is not None:
             self._configure()
 
@@ -190,6 +200,8 @@ class BatchedTournament:
         self.stats = np.concatenate((self.stats, self.stats[i: i + 1]), axis=0)
         self.elos = np.concatenate((self.elos, self.elos[i: i + 1]))
         self.positions[new_name] = list(self.positions[old_name])
+        for d in (self.baseline_scores, self.baseline_positions, self.baseline_wins):
+            d[new_name] = list(d[old_name])
 
     def remove_player(self, name, full_delete=False):
         """tournament.py:62-76"""
@@ -197,7 +209,8 @@ class BatchedTournament:
         if full_delete:
             i = self.names.index(name)
             self.names.pop(i)
-            for d in (self.agents, self.kinds, self.active, self.descendants, self.positions):
+            for d in (self.agents, self.kinds, self.active, self.descendants, self.positions, self.baseline_scores,
+                      self.baseline_positions, self.baseline_wins):
                 del d[name]
             self.stats = np.delete(self.stats, i, axis=0)
             self.elos = np.delete(self.elos, i)
@@ -328,10 +341,18 @@ class BatchedTournament:
             return BatchedReinforce(env, agent.actor, net_dtype=self.net_dtype, seed=seed, gamma=agent.gamma,
                                     r_factor=agent.r_factor, actor_weight=agent.actor_weight,
                                     entropy_weight=agent.entropy_weight, max_decisions=B)
+        # replay rounds: enough that the stored sequences (every seat of the
+        # agent in each kept round, ceil(10 / rollout_len) per seat) pass
+        # max(warmup, minibatch), from the expected seats per round
+        K = max(1, len(self.active_agents()))
+        seats = B * (self.min_players + self.max_players) / 2.0 / K
+        chunks = -(-T_STEPS // int(agent.rollout_len))
+        need = max(int(agent.warmup), int(agent.batchsize)) + 1
+        capacity = max(2, int(-(-need // max(1.0, seats * chunks))) + 1)
         return BatchedACER(env, agent.actor_critic, net_dtype=self.net_dtype, seed=seed, gamma=agent.gamma,
                            rollout_len=agent.rollout_len, minibatch=agent.batchsize, truncate=agent.truncate,
                            warmup=agent.warmup, r_factor=agent.r_factor, critic_weight=agent.critic_weight,
-                           capacity=2, log_epsilon=agent.log_epsilon, max_decisions=B)
+                           capacity=capacity, log_epsilon=agent.log_epsilon, max_decisions=B)
 
     # ------------------------------------------------------------ games (tournament.py:132-138)
     def play_games(self, games=1, rewards=False):
@@ -446,7 +467,14 @@ class BatchedTournament:
                 rec = gather_league_records(rec)
             K = int(ids.numel())
             s = league_agent_stats(rec, K, self.max_players).cpu().numpy()
+            played_before = self.stats[ids.numpy(), STAT_GAMES].copy()
             np.add.at(self.stats, ids.numpy(), s)
+            if self.baseline_agents is not None:
+                c = self.baseline_condition
+                evals = (self.stats[ids.numpy(), STAT_GAMES] // c - played_before // c).astype(np.int64)
+                for name, k in zip(self.record_names[self._seen], evals):
+                    if k > 0:
+                        self._baselines(name, int(k))
             for name, pos in zip(self.record_names[self._seen], league_positions32(rec, K, self.max_players)):
                 self.positions[name].append(pos)
             sub = replay_league_elo(rec, K, self.max_players, 0.0, self.elo_k, initial=self.elos[ids.numpy()])
@@ -466,6 +494,45 @@ class BatchedTournament:
             raise ValueError("the records span a roster change (seat ids index each round's active list): use "
                              "records_by_roster()")
         return torch.cat([r for r, _ in self.records], dim=0)
+
+    def _baselines(self, name, evals):
+        """`evals` baseline evaluations of agent `name` (tournament.py:182-195):
+        each one GameSession(agent, *baseline_agents).play_game() x
+        baseline_num_games; scores = the per-seat mean over those games,
+        relative positions and the win flag in that seat order (the agent
+        first).  Batched: one slot per evaluation on a tournament handle of
+        its own whose every game seats all 1 + len(baseline_agents) agents; a
+        slot's seat order is a drawn permutation and the per-seat means are
+        taken back into the agent-first order, so the evaluation is the
+        reference's in law (the game treats seats alike), and its games draw
+        from their own streams -- the reference's draw from the tournament's
+        global stream, so with baseline agents a slot's later games are no
+        longer the seeded reference tournament's draw for draw."""
+        from .tournament import Tournament
+
+        K = 1 + len(self.baseline_agents)
+        self._baseline_calls += 1
+        off = (0x40000000 + self._baseline_calls * 0x10000 + self.game_offset) & 0x7FFFFFFF
+        bt = BatchedTournament(evals, K, K, seed=self.seed, game_offset=off, rng="numpy", device=self.device,
+                               net_dtype=self.net_dtype, train=False)
+        seated = [self.agents[name]] + self.baseline_agents
+        names = [getattr(a, "__name__", None) for a in seated]
+        for j, a in enumerate(seated):
+            bt.add_player("agent" if j == 0 else f"baseline{j - 1}", a)
+        rec = bt.play_games(self.baseline_num_games)
+        bt.close()
+        for a, n in zip(seated, names):  # add_player renamed them (tournament.py:40); the evaluation does not
+            if n is not None:
+                a.__name__ = n
+        k, ids = decode_seats(rec[..., 0], K)
+        res = rec[..., 1:].to(torch.float64)  # [games, evals, seat]
+        by_agent = torch.zeros_like(res).scatter_(-1, ids.clamp(min=0), res)  # seat -> agent order
+        means = by_agent.mean(dim=0).cpu().numpy()  # np.mean over the session's results, per agent
+        for sc in means:
+            rel = Tournament._compute_relative_positions(sc)
+            self.baseline_scores[name].append(sc[0])
+            self.baseline_positions[name].append(rel[0])
+            self.baseline_wins[name].append(float(np.argmax(sc) == 0))
 
     def clear_records(self):
         """fold the records so far into the tallies, then drop them (the

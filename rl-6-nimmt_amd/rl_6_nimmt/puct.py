@@ -14,6 +14,7 @@ plays the step and, at the end, backs up.  Rollouts of one decision stay a
 sequential chain, exactly as in the reference.
 """
 import math
+import os
 
 import torch
 from torch import nn
@@ -79,6 +80,9 @@ class FusedMLP:
                 if hasattr(self, "_split"):
                     for old, new in zip(self._split_tensors(), fresh._split_tensors()):
                         old.copy_(new)
+                if getattr(self, "_fused", None) is not None:
+                    for old, new in zip(self._fused, fresh.fused()):
+                        old.copy_(new)
         return True
 
     def _split_tensors(self):
@@ -112,6 +116,38 @@ class FusedMLP:
             ha[:, : hw.shape[1]], ha[:, hw.shape[1]] = hw, hb
             self._split = (w1a, H, pad(H), hidden, ha, w1[:, 0].float().contiguous())
         return self._split
+
+    def fused(self):
+        """the fused rollout form (sn_puct_seat_rows + one GEMM + sn_puct_mlp)
+        for MultiHeadedMLP(48, (H, H2), (1,)) in bf16 with H <= 111, H2 <= 127:
+        W1t [56][112] bf16 (base = seat rows @ W1t: [W1 | b1 | 0] transposed,
+        1 at (48, H) -- the ones feature), w1c [112] f32 (W1[:, 0], then 0),
+        W2 [128][112] bf16 ([W2 | b2 | 0] rows, the ones pass-through row H2),
+        head [128] f32 ([wh | bh | 0]); None for other layouts"""
+        if getattr(self, "_fused", "unset") != "unset":
+            return self._fused
+        self._fused = None
+        sp = self.split()
+        if sp is None or len(self.layers) != 2 or self.head_sizes != [1] or self.layers[0][0].dtype != torch.bfloat16:
+            return None
+        w1a, H, _, _, _, w1c = sp
+        w2, b2 = self.layers[1]
+        H2 = w2.shape[0]
+        if H > 111 or H2 > 127 or w2.shape[1] != H:
+            return None
+        dev = w1a.device
+        w1t = torch.zeros((56, 112), dtype=torch.bfloat16, device=dev)
+        w1t[:, :H] = w1a.t()
+        w1t[ROW, H] = 1.0
+        c = torch.zeros((112,), dtype=torch.float32, device=dev)
+        c[:H] = w1c
+        w2p = torch.zeros((128, 112), dtype=torch.bfloat16, device=dev)
+        w2p[:H2, :H], w2p[:H2, H], w2p[H2, H] = w2, b2, 1.0
+        head = torch.zeros((128,), dtype=torch.float32, device=dev)
+        head[:H2] = self.head_w[:, 0].float()
+        head[H2] = self.head_b[0].float()
+        self._fused = (w1t, c, w2p, head)
+        return self._fused
 
     def __call__(self, rows):
         if self.layers is None:
@@ -176,6 +212,9 @@ class BatchedPUCT:
         self._graphs, self._graphs_seen = {}, {}
         # the rollout rows' layer 1 split (FusedMLP.split): once per seat + the card column
         self.split_l1 = True
+        # the rollout MLP after the per-seat GEMM as one MFMA kernel
+        # (FusedMLP.fused, sn_puct_mlp): bf16 nets of the reference's shape
+        self.fused_mlp = os.environ.get("SECHS_FUSED_MLP", "1") != "0"  # "0": the PyTorch split path (A/B runs)
         self._step_dev = torch.zeros((1,), dtype=torch.int32, device=dev)
 
     # ------------------------------------------------------------ policy net on the device
@@ -195,6 +234,8 @@ class BatchedPUCT:
             sp = self._net.split()  # built here: a graph capture may not allocate
             if sp is not None:
                 self._split_bufs(sp[1], sp[2])
+            if self._net.fused() is not None:
+                self._fused_bufs()
         return self._net
 
     def actor_device(self):
@@ -287,6 +328,29 @@ class BatchedPUCT:
         L, h, st = nat.lib(), self.env._h, self.env._stream()
         bf16 = int(self.net_dtype == torch.bfloat16)
         N = self.env.num_players
+        fz = self._net.fused() if (self.split_l1 and self.fused_mlp) else None
+        if fz is not None:
+            # per rollout step: the seats' [0, obs, 1] rows, base = rows @ W1t
+            # (PyTorch-ROCm GEMM over the D*N seats), then layer 1's card
+            # column + ReLU, layer 2 + ReLU and the head in one MFMA kernel
+            # (f32 logits, packed) -- no activation tensor in HBM
+            w1t, w1c, w2p, head = fz
+            S = self.D * N
+            rows, cards, base, logits = self._fused_bufs()
+            rv, bv = rows[:S], base[:S]
+            for r in range(self.n_mc(n)):
+                q.rollout = r
+                nat.check(L.sn_puct_deal(h, ctypes_ref(q), st), "sn_puct_deal")
+                for t in range(n):
+                    m = n - t
+                    nat.check(L.sn_puct_seat_rows(h, ctypes_ref(q), m, nat.ptr(rv), 56, nat.ptr(cards), st),
+                              "sn_puct_seat_rows")
+                    torch.mm(rv, w1t, out=bv)
+                    nat.check(L.sn_puct_mlp(h, ctypes_ref(q), m, nat.ptr(bv), 112, nat.ptr(w1c), nat.ptr(cards),
+                                            nat.ptr(w2p), nat.ptr(head), nat.ptr(logits), st), "sn_puct_mlp")
+                    self.rows_evaluated += S * m
+                    nat.check(L.sn_puct_step(h, ctypes_ref(q), nat.ptr(logits), t, m, st), "sn_puct_step")
+            return
         sp = self._net.split() if self.split_l1 else None
         if sp is not None:
             # layer 1 once per rollout seat + the card column per candidate
@@ -341,6 +405,18 @@ class BatchedPUCT:
                            torch.empty((kp * S * 10,), dtype=self.net_dtype, device=dev),
                            torch.zeros((S * 10,), dtype=self.net_dtype, device=dev))
         return self._sbufs
+
+    def _fused_bufs(self):
+        """seat rows [D_max*N][56] bf16, cards [D_max*N*10] f32, base
+        [D_max*N][112] bf16, logits [D_max*N*10] f32"""
+        S = self.D_max * self.env.num_players
+        if getattr(self, "_fbufs", None) is None or self._fbufs[0].shape[0] != S:
+            dev = self.env.device
+            self._fbufs = (torch.empty((S, 56), dtype=torch.bfloat16, device=dev),
+                           torch.empty((S * 10,), dtype=torch.float32, device=dev),
+                           torch.empty((S, 112), dtype=torch.bfloat16, device=dev),
+                           torch.empty((S * 10,), dtype=torch.float32, device=dev))
+        return self._fbufs
 
     def _bufs(self, n):
         N = self.env.num_players

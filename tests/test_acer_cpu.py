@@ -253,3 +253,32 @@ def test_batched_acer_default_capacity_reaches_warmup():
     assert any(not torch.equal(a, b) for a, b in zip(eng.actor.parameters(), before))
     with pytest.warns(UserWarning):
         BatchedACER(_HostEnv(2, 2), net_dtype=torch.float32, capacity=4)
+
+
+def test_replay_size_is_checked_before_allocating():
+    """a replay is capacity x 10 x deciders x 19.7 KB; a size above
+    the limit raises a clear error instead of failing in the allocator"""
+    from rl_6_nimmt.acer import BatchedACER, replay_bytes
+
+    assert replay_bytes(102, 8192 * 4) > 60 << 30  # the old INTEGRATION example: ~66 GB
+    with pytest.raises(ValueError, match="capacity"):
+        BatchedACER(_HostEnv(2, 2), net_dtype=torch.float32, capacity=10, max_replay_bytes=replay_bytes(10, 4) - 1)
+    BatchedACER(_HostEnv(2, 2), net_dtype=torch.float32, capacity=10, max_replay_bytes=replay_bytes(10, 4))
+
+
+def test_distinct_off_policy_picks():
+    """the tournament ACER's off-policy batch draws distinct sequences per
+    seat (random.sample in the reference), uniformly"""
+    from rl_6_nimmt.acer import distinct_picks
+
+    g = torch.Generator().manual_seed(0)
+    for S, k in ((5, 5), (12, 5), (1000, 10)):
+        p = distinct_picks(S, 4000, k, g, torch.device("cpu"))
+        assert p.shape == (4000, k) and int(p.min()) >= 0 and int(p.max()) < S
+        srt = p.sort(dim=1).values
+        assert not (srt[:, 1:] == srt[:, :-1]).any()
+        counts = torch.bincount(p.reshape(-1), minlength=S).double()
+        exp = 4000 * k / S
+        assert float(((counts - exp).abs() / exp ** 0.5).max()) < 5.0
+    with pytest.raises(ValueError):
+        distinct_picks(3, 2, 4, g, torch.device("cpu"))

@@ -479,3 +479,31 @@ def test_league_seats_a_reinforce_agent_and_trains_it():
     assert any(not torch.equal(a.detach().cpu(), b.cpu()) for a, b in zip(t.agents["REINFORCE"].parameters(), before))
     assert t.env.pipe_errors() == 0
     t.close()
+
+
+def test_batched_baseline_evaluations():
+    """Tournament(baseline_agents=...) (tournament.py:147-155,182-195): every
+    time an agent's game count reaches a multiple of baseline_condition it
+    gets one evaluation -- GameSession(agent, *baseline_agents) x
+    baseline_num_games, per-seat mean scores, the agent's relative position
+    and win flag -- here batched on a handle of its own"""
+    from rl_6_nimmt.agents import DrunkHamster, MCSAgent
+
+    from rl_6_nimmt.league import BatchedTournament
+
+    base = [DrunkHamster(), DrunkHamster()]
+    t = BatchedTournament(16, 2, 3, seed=4, fused=False, baseline_agents=base, baseline_num_games=2, baseline_condition=3)
+    for i in range(3):
+        t.add_player(f"R{i}", DrunkHamster())
+    t.add_player("M", MCSAgent(mc_max=20))
+    t.play_games(2)
+    st = t.agent_stats().numpy()
+    for i, n in enumerate(t.names):
+        k = int(st[i, 0]) // 3
+        assert len(t.baseline_scores[n]) == k and len(t.baseline_positions[n]) == k and len(t.baseline_wins[n]) == k, n
+        assert all(-171 <= v <= 0 for v in t.baseline_scores[n])
+        assert all(0.0 <= v <= 1.0 for v in t.baseline_positions[n])
+        assert set(t.baseline_wins[n]) <= {0.0, 1.0}
+        assert t.agents[n].__name__ == n
+    assert sum(len(v) for v in t.baseline_scores.values()) > 0
+    t.close()

@@ -530,3 +530,78 @@ def test_batched_customed_learning_step_changes_weights():
     opt.step()
     assert torch.isfinite(loss)
     assert any(not torch.equal(a.cpu(), b.cpu()) for a, b in zip(eng.actor.parameters(), before))
+
+
+@pytest.mark.parametrize("B,n", [(64, 7), (37, 10), (256, 4)])
+def test_fused_mlp_equals_module_forward(B, n):
+    """sn_puct_seat_rows + the per-seat GEMM + sn_puct_mlp (layer 1's card
+    column + ReLU, layer 2 + ReLU and the head in one MFMA kernel) give every
+    rollout candidate's policy logit: equal to the split PyTorch path's
+    logits computed in f32 from the same bf16 activations (to f32 summation
+    order), and to the module's own bf16 forward on the full rows (to the
+    bf16 tolerance of test_layer1_split_equals_full_rows).  Ragged row counts
+    (a short last 64-row tile) included."""
+    import ctypes
+
+    from rl_6_nimmt import _native as nat
+
+    env, eng = _engine(B=B, dtype=torch.bfloat16, mc_max=4, mc_per_card=2, seed=29)
+    N = env.num_players
+    for t in range(10 - n):
+        env.step(eng.decide(10 - t))
+    net = eng.sync_net()
+    w1t, w1c, w2p, head = net.fused()
+    w1a, H, kp, hidden, ha, w1c_s = net.split()
+    q = eng._params(n)
+    L, h, st = nat.lib(), env._h, env._stream()
+    eng.memorize()
+    nat.check(L.sn_puct_deal(h, ctypes.byref(q), st), "deal")
+    tol = 2 ** -6
+    for m in (n, 3, 1):
+        S, R = eng.D * N, eng.D * N * m
+        rows = torch.empty((R, 48), dtype=torch.bfloat16, device=env.device)
+        nat.check(L.sn_puct_rows(h, ctypes.byref(q), m, nat.ptr(rows), 1, st), "rows")
+        srows = torch.empty((S, 56), dtype=torch.bfloat16, device=env.device)
+        cards = torch.empty((R,), dtype=torch.float32, device=env.device)
+        nat.check(L.sn_puct_seat_rows(h, ctypes.byref(q), m, nat.ptr(srows), 56, nat.ptr(cards), st), "seat_rows")
+        cols = torch.empty((56, S), dtype=torch.bfloat16, device=env.device)
+        cards2 = torch.empty((R,), dtype=torch.float32, device=env.device)
+        nat.check(L.sn_puct_seat_cols(h, ctypes.byref(q), m, nat.ptr(cols), 56, nat.ptr(cards2), 1, st), "seat_cols")
+        assert torch.equal(srows, cols.t()) and torch.equal(cards, cards2)  # the same features, seat-major
+        base = torch.mm(srows, w1t)
+        logits = torch.empty((R,), dtype=torch.float32, device=env.device)
+        nat.check(L.sn_puct_mlp(h, ctypes.byref(q), m, nat.ptr(base), 112, nat.ptr(w1c), nat.ptr(cards), nat.ptr(w2p),
+                                nat.ptr(head), nat.ptr(logits), st), "mlp")
+        torch.cuda.synchronize()
+        # the split path's activations (bf16 GEMM outputs), its head in f32
+        h1 = torch.relu(base[:, :H].float().repeat_interleave(m, dim=0) + cards[:, None] * w1c[None, :H])
+        h1 = torch.cat((h1.to(torch.bfloat16), torch.ones((R, 1), dtype=torch.bfloat16, device=env.device)), dim=1)
+        w2, b2 = net.layers[1]
+        x2 = torch.relu(h1[:, :H].float() @ w2.float().t() + b2.float()).to(torch.bfloat16).float()
+        ref = x2 @ net.head_w[:, 0].float() + net.head_b[0].float()
+        assert torch.allclose(logits, ref, rtol=1e-3, atol=1e-3), (logits - ref).abs().max()
+        with torch.no_grad():
+            (want,) = net.module(rows)
+        assert torch.allclose(logits, want[:, 0].float(), rtol=4 * tol, atol=4 * tol), (logits - want[:, 0].float()).abs().max()
+
+
+def test_fused_and_split_rollouts_agree_in_law():
+    """a whole PUCT search with the fused MLP and with the PyTorch split path
+    (same weights, same Philox streams): the f32 vs bf16 logits may flip a
+    sample now and then, so the searches agree in law -- mean root visit
+    counts and chosen moves match closely over 2 048 decisions"""
+    res = {}
+    for fused in (True, False):
+        env, eng = _engine(B=512, dtype=torch.bfloat16, mc_max=20, mc_per_card=10, seed=41)
+        eng.fused_mlp = fused
+        acts = eng.decide(10)
+        torch.cuda.synchronize()
+        res[fused] = (acts.clone(), eng.stats.clone(), eng.rows_evaluated)
+    a1, s1, r1 = res[True]
+    a2, s2, r2 = res[False]
+    assert r1 == r2
+    assert torch.equal(s1[:, 10:20].sum(dim=1), s2[:, 10:20].sum(dim=1))  # every rollout backed up
+    agree = float((a1 == a2).float().mean())
+    assert agree > 0.6, agree
+    m1, m2 = s1[:, :10].double().sum() / s1[:, 10:20].double().sum(), s2[:, :10].double().sum() / s2[:, 10:20].double().sum()
+    assert abs(float(m1 - m2)) < 0.5, (float(m1), float(m2))

@@ -1,0 +1,26 @@
+#!/bin/bash
+# r04: device-flag pipeline + fused PUCT MLP -- parity tests, then A/Bs
+set -o pipefail
+export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/${1:-r04_flags}
+mkdir -p $OUT
+fatal() { [ "$1" -ge 124 ] && { echo "fatal rc=$1 in $2"; exit $1; }; return 0; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_env.py -x -q --timeout 300 --timeout-method thread > $OUT/tests_env.log 2>&1
+rc=$?; tail -4 $OUT/tests_env.log; fatal $rc pytest_env
+[ $rc -ne 0 ] && exit 1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_puct.py -x -q --timeout 300 --timeout-method thread > $OUT/tests_puct.log 2>&1
+rc=$?; tail -4 $OUT/tests_puct.log; fatal $rc pytest_puct
+for rep in 1 2; do
+  for f in 1 0; do
+    SECHS_PIPE_FLAGS=$f timeout -k 10 200 python bench.py --no-cpu --no-mcs --no-puct --no-scalar --no-league --no-mixed-league --no-dropin --no-philox > $OUT/head_f${f}_$rep.json 2> $OUT/head_f${f}_$rep.err
+    rc=$?; fatal $rc head
+    python -c "import json,sys; r=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('flags',sys.argv[2],'rep',sys.argv[3],round(r['value']/1e9,3),'G ms',round(r['ms_per_step'],4),'k_play',round(r['roofline']['kernel_ms']*1e3,1),'ahead',round(r['roofline']['concurrent']['kernel_ms']*1e3,1))" $OUT/head_f${f}_$rep.json $f $rep
+  done
+done
+for f in 1 0; do
+  SECHS_FUSED_MLP=$f timeout -k 10 300 python bench.py --only puct > $OUT/puct_f$f.json 2> $OUT/puct_f$f.err
+  rc=$?; fatal $rc puct
+  python -c "import json,sys; r=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])['extra_config4_puct']; print('fused',sys.argv[2],round(r['value']/1e6,1),'M playout env-steps/s wall',round(r['wall_s'],3))" $OUT/puct_f$f.json $f
+done
+echo done
