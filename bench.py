@@ -542,8 +542,20 @@ def bench_league_mixed(world, rank, slots, mc_max=200, rounds=1, warmup=1):
     barrier(world)
     wall = time.perf_counter() - t0
     rows = {n: e.rows_evaluated for n, e in t.engines.items()}  # the timed rounds only: a fresh league
-    tg = time.perf_counter()
     recs = torch.cat([r for r, _ in t.records[rec0:]], dim=0)
+    # one more round with HIP events around its phases (outside the timed
+    # region: where a round's time goes)
+    t.phase_timing = True
+    tp = time.perf_counter()
+    t.play_games(1)
+    torch.cuda.synchronize()
+    phase_round_s = time.perf_counter() - tp
+    phases = {"gpu_ms": {k: round(v, 2) for k, v in t.phase_ms.items()},
+              "host_enqueue_ms": {k: round(v, 2) for k, v in t.phase_host_ms.items()},
+              "round_wall_s": phase_round_s,
+              "note": "a second, instrumented round: HIP events per phase on the stream (GPU ms) and the host's "
+                      "enqueue time per phase; phases run back to back, so GPU ms sum to about the round"}
+    tg = time.perf_counter()
     K = len(specs)
     from rl_6_nimmt.league import league_agent_stats
 
@@ -573,6 +585,7 @@ def bench_league_mixed(world, rank, slots, mc_max=200, rounds=1, warmup=1):
             "reference_s_per_game": [21.47, 46.95],
             "reference_source": "experiments/simple_tournament.ipynb:158-410 tqdm logs (CPU, one game at a time)",
             "policy_rows_per_round": {n: r / rounds for n, r in rows.items()},
+            "phases": phases,
             "score_gather_ms": gather_ms,
             "score_gather": f"RCCL all_reduce of [{K}, 4] per-agent sums + all_gather of {games} game records"
                             if world > 1 else "single rank (no collective)",

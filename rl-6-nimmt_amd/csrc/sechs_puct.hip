@@ -626,6 +626,78 @@ __global__ void k_puct_step(DevState s, PuctArgs a, const void* logits, int ls, 
     }
 }
 
+// The same step with one lane per SEAT (L lanes per decision, L = N rounded
+// up to a power of two, L <= 8): each lane loads its seat's hand and logits,
+// draws its card (the same Philox uniform, counter = seat, as k_puct_step)
+// and stores its hand back; the decision's first lane gathers the cards
+// (lane shuffles), resolves, and writes the board / outcome / backup.  L
+// times the lanes of k_puct_step (D = 8192 x 4 decisions: 2 waves per SIMD
+// instead of half a wave), the per-decision latency chain split over them.
+template <int N, int L, bool LB>
+__global__ void k_puct_step_seats(DevState s, PuctArgs a, const void* logits, int ls, int t, int n_cur) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t d = i / L;
+    const int q = (int)(i & (L - 1));
+    const bool live = d < a.D;
+    const int64_t dd = live ? d : a.D - 1;  // lanes past the last decision follow along (shuffles), write nothing
+    int64_t g;
+    int p;
+    dec_to_gp(a, dd, g, p);
+    int32_t* ro = a.ro + dd * kRoWords;
+    const int kp = players_of(a, g);
+    const bool seat = q < N && q < kp;
+    uint32_t card = 0xFFu;
+    int idx = 0;
+    if (seat) {
+        float lg[kHand];
+#pragma unroll
+        for (int k = 0; k < kHand; k++) lg[k] = (k < n_cur) ? logit_at<LB>(logits, (dd * N + q) * n_cur + k, ls) : 0.f;
+        Hand h = ro_hand(ro, q);
+        if (t == 0 && q == 0 && (a.flags & 1)) {
+            idx = puct_choose(a.stats + dd * kStatWords, a.hist + dd * kHistBins, a.root_probs + dd * kHand, n_cur,
+                              a.c_puct, nullptr);
+        } else {
+            const uint64_t gid = s.game_offset + (uint64_t)g;
+            const uint64_t stream =
+                ((uint64_t)(uint32_t)gid << 32) | ((uint64_t)p << 28) | ((uint64_t)a.rollout << 8) | (uint64_t)(1 + t);
+            idx = sample_row(lg, n_cur, philox_uniform(a.seed_lo ^ puct_step_of(a), a.seed_hi, stream, (uint32_t)q));
+        }
+        card = hand_get(h, (uint32_t)idx);
+        hand_del(h, (uint32_t)idx);
+        if (n_cur > 1 && live) {
+            ro[8 + 3 * q] = (int32_t)(uint32_t)h.lo;
+            ro[9 + 3 * q] = (int32_t)(uint32_t)(h.lo >> 32);
+            ro[10 + 3 * q] = (int32_t)h.hi;
+        }
+    }
+    // the decision's cards to its first lane (absent seats: 0xFF, resolve skips them)
+    const int lead = (int)(threadIdx.x & 63) & ~(L - 1);
+    uint32_t cards[N];
+#pragma unroll
+    for (int r = 0; r < N; r++) cards[r] = (uint32_t)__shfl((int)card, lead + r);
+    const int first_idx = __shfl(idx, lead);
+    if (q != 0 || !live) return;
+    Board b = ro_board(ro);
+    uint32_t pen[N];
+    resolve<N, true>(b, cards, pen);
+    const int first = (t == 0) ? first_idx : ro[41];
+    const int32_t outcome = ro[40] - (int32_t)pen[0];
+    if (n_cur == 1) {
+        int32_t* st = a.stats + dd * kStatWords;
+        st[first] += outcome;
+        st[10 + first] += 1;
+        st[20] += 1;
+        st[21] = (st[20] == 1) ? outcome : min(st[21], outcome);
+        st[22] = (st[20] == 1) ? outcome : max(st[22], outcome);
+        a.hist[dd * kHistBins + (outcome + 171)] += 1;
+    } else {
+        ro[0] = b.lo.x, ro[1] = b.lo.y, ro[2] = b.lo.z, ro[3] = b.lo.w;
+        ro[4] = b.hi.x, ro[5] = b.hi.y, ro[6] = b.hi.z, ro[7] = b.hi.w;
+        ro[40] = outcome;
+        ro[41] = first;
+    }
+}
+
 // _choose_action_from_outcomes (mcts.py:156-165, temperature None): best mean
 // over moves with playouts, strict '>'; one-card hands play it directly
 __global__ void k_puct_choose(DevState s, PuctArgs a, int32_t* actions, int32_t* best_index) {
@@ -815,7 +887,36 @@ sn_status sn_puct_step(sn_env* e, const sn_puct* q, const float* logits, int t, 
     if (n_cur < 1 || n_cur > a.n || t < 0 || t + n_cur != a.n) return set_error(SN_EINVAL, "t / n_cur inconsistent");
     hipStream_t s = (hipStream_t)stream;
     const int ls = q->logit_stride > 1 ? q->logit_stride : 1;
+    const char* sv = getenv("SECHS_PUCT_STEP_SEATS");  // "0": the one-lane-per-decision kernel (A/B, tests)
+    const int seat_lanes = (sv && sv[0] == '0') ? 0 : 1;
+    if (seat_lanes && e->s.N <= 8) {  // one lane per seat (k_puct_step_seats)
+        const int Lw = e->s.N <= 2 ? 2 : e->s.N <= 4 ? 4 : 8;
+        const int64_t lanes = a.D * Lw;
+#define SN_STEP_SEATS(NN_, L_)                                                                                   \
+    do {                                                                                                        \
+        if (q->logit_bf16)                                                                                      \
+            hipLaunchKernelGGL((k_puct_step_seats<NN_, L_, true>), dim3(grid_for(lanes)), dim3(kBlock), 0, s,  \
+                               e->s, a, (const void*)logits, ls, t, n_cur);                                     \
+        else                                                                                                    \
+            hipLaunchKernelGGL((k_puct_step_seats<NN_, L_, false>), dim3(grid_for(lanes)), dim3(kBlock), 0, s, \
+                               e->s, a, (const void*)logits, ls, t, n_cur);                                     \
+    } while (0)
+        switch (e->s.N) {
+            case 1: SN_STEP_SEATS(1, 2); break;
+            case 2: SN_STEP_SEATS(2, 2); break;
+            case 3: SN_STEP_SEATS(3, 4); break;
+            case 4: SN_STEP_SEATS(4, 4); break;
+            case 5: SN_STEP_SEATS(5, 8); break;
+            case 6: SN_STEP_SEATS(6, 8); break;
+            case 7: SN_STEP_SEATS(7, 8); break;
+            default: SN_STEP_SEATS(8, 8); break;
+        }
+#undef SN_STEP_SEATS
+        HIP_TRY(hipGetLastError());
+        return SN_OK;
+    }
     if (q->logit_bf16) {
+
         SN_DISPATCH_N(e->s.N, hipLaunchKernelGGL((k_puct_step<NN, true>), dim3(grid_for(a.D)), dim3(kBlock), 0, s, e->s, a,
                                                  (const void*)logits, ls, t, n_cur));
     } else {

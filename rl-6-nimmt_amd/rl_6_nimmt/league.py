@@ -142,6 +142,11 @@ class BatchedTournament:
         self.baseline_num_games, self.baseline_condition = int(baseline_num_games), int(baseline_condition)
         self.baseline_scores, self.baseline_positions, self.baseline_wins = {}, {}, {}
         self._baseline_calls = 0
+        # phase_timing = True: _round records HIP events around its phases on
+        # the stream (no synchronisation in between) and sums them, with the
+        # host's enqueue time of each phase, into phase_ms / phase_host_ms
+        self.phase_timing = False
+        self.phase_ms, self.phase_host_ms = {}, {}
         # the roster, in the reference's dict order (tournament.py:25-35)
         self.names, self.agents, self.active, self.descendants, self.kinds = [], {}, {}, {}, {}
         self.env = None
@@ -382,19 +387,45 @@ class BatchedTournament:
         self.total_games += int(games) * self.num_slots
         return (rec, rew) if rewards else rec
 
+    def _phase(self, name):
+        """context of one timed phase of _round (no-op unless phase_timing)"""
+        import contextlib
+        import time
+
+        if not self.phase_timing:
+            return contextlib.nullcontext()
+        t = self
+
+        class _P:
+            def __enter__(self):
+                self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                self.ev[0].record()
+                self.h = time.perf_counter()
+
+            def __exit__(self, *exc):
+                self.ev[1].record()
+                t._phase_events.append((name, self.ev))
+                t.phase_host_ms[name] = t.phase_host_ms.get(name, 0.0) + (time.perf_counter() - self.h) * 1e3
+                return False
+
+        return _P()
+
+    def _phase_collect(self):
+        if self.phase_timing and getattr(self, "_phase_events", None):
+            torch.cuda.synchronize(self.env.device)
+            for name, (a, b) in self._phase_events:
+                self.phase_ms[name] = self.phase_ms.get(name, 0.0) + a.elapsed_time(b)
+        self._phase_events = []
+
     def _round(self):
         """one game per slot: sn_reset (seat draw + deal), then 10 x [net
         agents' engines on their seats -> sn_league_step]"""
         env, L, st = self.env, nat.lib(), self.env._stream()
         B, N, dev = self.num_slots, self.max_players, env.device
-        nat.check(L.sn_reset(env._h, None, st), "sn_reset")  # Tournament.play_game: seats, then the deal
-        if self.engines:
-            k, ids = self.seats()
-            flat = ids.reshape(-1)
-            act = self.active_agents()
-            for name, eng in self.engines.items():
-                eng.use_decisions(torch.nonzero(flat == act.index(name)).flatten())
-                eng.decisions = []
+        self._phase_events = []
+        with self._phase("reset (seat draw + deal) + decision lists"):
+            nat.check(L.sn_reset(env._h, None, st), "sn_reset")  # Tournament.play_game: seats, then the deal
+            self._use_decisions()
         acts = torch.zeros((B, N), dtype=torch.int32, device=dev)
         per_step = torch.zeros((T_STEPS, B, N), dtype=torch.int32, device=dev)
         rec = torch.zeros((B, 1 + N), dtype=torch.int32, device=dev)
@@ -406,12 +437,14 @@ class BatchedTournament:
             for name, eng in self.engines.items():
                 if eng.D == 0:
                     continue
-                a = eng.decide(n, record=self.train)
-                idx = eng.dec.long()
-                flat_acts[idx] = a.reshape(-1)[idx]
-            nat.check(L.sn_league_step(env._h, nat.ptr(acts), nat.ptr(per_step[t]), None,
-                                       nat.ptr(rec) if t == T_STEPS - 1 else None, nat.ptr(invalid[t]),
-                                       nat.ptr(status), st), "sn_league_step")
+                with self._phase(f"decide {name}"):
+                    a = eng.decide(n, record=self.train)
+                    idx = eng.dec.long()
+                    flat_acts[idx] = a.reshape(-1)[idx]
+            with self._phase("league step (MCS + DrunkHamster seats, resolution)"):
+                nat.check(L.sn_league_step(env._h, nat.ptr(acts), nat.ptr(per_step[t]), None,
+                                           nat.ptr(rec) if t == T_STEPS - 1 else None, nat.ptr(invalid[t]),
+                                           nat.ptr(status), st), "sn_league_step")
         bad = int((invalid >= 0).sum())
         if bad:
             raise RuntimeError(f"sn_league_step: {bad} illegal moves of the net agents' engines")
@@ -421,7 +454,17 @@ class BatchedTournament:
             logger.warning("MCS: a legal move got no playout (the reference raises IndexError here, quirk Q6)")
         if self.train:
             self._learn(per_step)
+        self._phase_collect()
         return rec, per_step
+
+    def _use_decisions(self):
+        if self.engines:
+            k, ids = self.seats()
+            flat = ids.reshape(-1)
+            act = self.active_agents()
+            for name, eng in self.engines.items():
+                eng.use_decisions(torch.nonzero(flat == act.index(name)).flatten())
+                eng.decisions = []
 
     def _learn(self, per_step):
         """one Adam step per net agent on its loss over the round's games"""
@@ -433,21 +476,22 @@ class BatchedTournament:
             agent = self.agents[name]
             if agent.optimizer is None:
                 agent.train()
-            if isinstance(eng, BatchedACER):
-                if eng.D:
-                    eng.record_rewards(per_step)
-                    eng.learn(agent.optimizer)
-                continue
-            if eng.D == 0 or not eng.decisions:
-                continue
-            if isinstance(eng, (BatchedPUCTCustomed, BatchedReinforce)):
-                loss = eng.loss(per_step)
-            else:
-                loss = eng.policy_loss()
-            agent.optimizer.zero_grad()
-            loss.backward()
-            agent.optimizer.step()
-            eng.decisions = []
+            with self._phase(f"learn {name}"):
+                if isinstance(eng, BatchedACER):
+                    if eng.D:
+                        eng.record_rewards(per_step)
+                        eng.learn(agent.optimizer)
+                    continue
+                if eng.D == 0 or not eng.decisions:
+                    continue
+                if isinstance(eng, (BatchedPUCTCustomed, BatchedReinforce)):
+                    loss = eng.loss(per_step)
+                else:
+                    loss = eng.policy_loss()
+                agent.optimizer.zero_grad()
+                loss.backward()
+                agent.optimizer.step()
+                eng.decisions = []
 
     def seats(self):
         """(k [slots], active agent index [slots, max_players]) of every slot's current game"""

@@ -605,3 +605,21 @@ def test_fused_and_split_rollouts_agree_in_law():
     assert agree > 0.6, agree
     m1, m2 = s1[:, :10].double().sum() / s1[:, 10:20].double().sum(), s2[:, :10].double().sum() / s2[:, 10:20].double().sum()
     assert abs(float(m1 - m2)) < 0.5, (float(m1), float(m2))
+
+
+def test_seat_parallel_step_equals_one_lane_step(monkeypatch):
+    """k_puct_step_seats (one lane per seat) and k_puct_step (one lane per
+    decision) draw the same Philox uniforms and resolve the same cards: a
+    whole PUCT search gives identical statistics and moves, incl. a
+    tournament-style decision list with 2..4-player games"""
+    res = {}
+    for lanes in ("1", "0"):
+        monkeypatch.setenv("SECHS_PUCT_STEP_SEATS", lanes)
+        env, eng = _engine(B=300, dtype=torch.float32, mc_max=12, mc_per_card=3, seed=17)
+        acts = [eng.decide(10).clone()]
+        env.step(acts[-1])
+        acts.append(eng.decide(9).clone())
+        torch.cuda.synchronize()
+        res[lanes] = (acts, eng.stats.clone(), eng.hist.clone())
+    assert all(torch.equal(a, b) for a, b in zip(res["1"][0], res["0"][0]))
+    assert torch.equal(res["1"][1], res["0"][1]) and torch.equal(res["1"][2], res["0"][2])

@@ -1,5 +1,5 @@
 #!/bin/bash
-# r04: device-flag pipeline + fused PUCT MLP -- parity tests, then A/Bs
+# r04: device-flag pipeline + fused PUCT MLP + seat-parallel PUCT step -- parity tests, then A/Bs
 set -o pipefail
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -18,9 +18,12 @@ for rep in 1 2; do
     python -c "import json,sys; r=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('flags',sys.argv[2],'rep',sys.argv[3],round(r['value']/1e9,3),'G ms',round(r['ms_per_step'],4),'k_play',round(r['roofline']['kernel_ms']*1e3,1),'ahead',round(r['roofline']['concurrent']['kernel_ms']*1e3,1))" $OUT/head_f${f}_$rep.json $f $rep
   done
 done
-for f in 1 0; do
-  SECHS_FUSED_MLP=$f timeout -k 10 300 python bench.py --only puct > $OUT/puct_f$f.json 2> $OUT/puct_f$f.err
+for cfg in "1 1" "1 0" "0 1" "0 0"; do
+  set -- $cfg
+  SECHS_FUSED_MLP=$1 SECHS_PUCT_STEP_SEATS=$2 timeout -k 10 300 python bench.py --only puct > $OUT/puct_$1$2.json 2> $OUT/puct_$1$2.err
   rc=$?; fatal $rc puct
-  python -c "import json,sys; r=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])['extra_config4_puct']; print('fused',sys.argv[2],round(r['value']/1e6,1),'M playout env-steps/s wall',round(r['wall_s'],3))" $OUT/puct_f$f.json $f
+  python -c "import json,sys; r=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])['extra_config4_puct']; print('fused',sys.argv[2],'seats',sys.argv[3],round(r['value']/1e6,1),'M playout env-steps/s wall',round(r['wall_s'],3))" $OUT/puct_$1$2.json $1 $2
 done
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_puct -o run -- python3 $R/bench.py --only puct > $OUT/prof_puct.log 2>&1
+rc=$?; echo "rocprof rc=$rc"; fatal $rc rocprof
 echo done
