@@ -390,26 +390,39 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
     wall = time.perf_counter() - t0
     steps = sum(eng.n_mc(n) * n for n in range(2, 11)) * N_PLAYERS * games
     rows_s = eng.rows_evaluated / wall
-    # the MLP dominates: three hipBLASLt GEMMs per candidate-row batch
-    # (48->100 +ReLU, 100->100 +ReLU, 100->16-padded head).  Skinny K: HBM
-    # bound on its bf16 intermediates -- per row 96 B in, 2 x (200 B out +
-    # 200 B back in), 32 B head out = 928 B; 29 800 FLOP
-    row_bytes = 96 + 2 * (200 + 200) + 32
+    fused = eng.fused_mlp and eng._net is not None and eng._net.fused() is not None
+    tflops = eng.rows_evaluated * 29800 / wall / 1e12
+    if fused:
+        # the rollout MLP runs as sn_puct_mlp (one MFMA kernel after a
+        # per-seat PyTorch GEMM): no activation tensor in HBM; priced as the
+        # reference's 29 800 FLOP per candidate row against the dense bf16
+        # MFMA peak, over the whole game's wall time (every kernel included)
+        roof = {"bound": "mfma", "achieved": tflops, "peak": 2500.0, "unit": "TFLOP/s", "frac": tflops / 2500.0,
+                "traffic": None, "algo_flop_per_row": 29800,
+                "kernel": "rollout step = sn_puct_seat_rows + PyTorch GEMM (layer 1, per seat) + sn_puct_mlp (MFMA: "
+                          "card column, layer 2, head) + k_puct_step_seats; whole-game wall time"}
+    else:
+        # the split PyTorch path: hipBLASLt GEMMs per candidate-row batch,
+        # HBM-bound on their bf16 intermediates -- per row 96 B in, 2 x (200 B
+        # out + 200 B back in), 32 B head out = 928 B
+        row_bytes = 96 + 2 * (200 + 200) + 32
+        roof = {"bound": "hbm", "achieved": rows_s * row_bytes / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": rows_s * row_bytes / 1e9 / HBM_PEAK_GBS, "traffic": None, "algo_bytes_per_row": row_bytes,
+                "mfma_frac": tflops / 2500.0,
+                "kernel": "policy MLP (PyTorch-ROCm hipBLASLt bf16, ReLU fused in the GEMM epilogue), whole game "
+                          "wall time incl. the k_puct_* kernels"}
     return {
         "workload": f"config4: {games} x 4-player games, all seats PUCT (mc_max={mc_max}, mc_per_card={mc_per_card}, "
-                    f"c_puct=2), bf16 policy MLP 48-100-100-1 via PyTorch-ROCm, 1 game; each decision's rollout "
+                    f"c_puct=2), bf16 policy MLP 48-100-100-1 (layer 1's per-seat part a PyTorch-ROCm GEMM, the "
+                    f"rest one MFMA kernel), 1 game; each decision's rollout "
                     f"chain replayed from a captured hipGraph",
         "value": steps / wall,
         "unit": "playout env-steps/s",
         "decisions_per_s": 9 * N_PLAYERS * games / wall,
         "policy_rows_per_s": rows_s,
-        "policy_tflops": eng.rows_evaluated * 29800 / wall / 1e12,
-        "roofline": {"bound": "hbm", "achieved": rows_s * row_bytes / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": rows_s * row_bytes / 1e9 / HBM_PEAK_GBS, "traffic": None,
-                     "algo_bytes_per_row": row_bytes,
-                     "mfma_frac": eng.rows_evaluated * 29800 / wall / 1e12 / 2500.0,
-                     "kernel": "policy MLP (PyTorch-ROCm hipBLASLt bf16, ReLU fused in the GEMM epilogue), whole "
-                               "game wall time incl. the k_puct_* kernels"},
+        "policy_tflops": tflops,
+        "mlp": "fused (sn_puct_mlp)" if fused else "split (PyTorch GEMMs)",
+        "roofline": roof,
         "wall_s": wall,
         "mean_score_per_seat": total.double().mean(dim=0).tolist(),
     }

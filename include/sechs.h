@@ -256,9 +256,13 @@ sn_status sn_league_agents(sn_env* env, const int32_t* kinds_host, const int32_t
    slots' next games start with sn_reset (seat draw, then deal:
    tournament.py:132-138), after any roster change.  Outputs (each may
    be NULL): rewards [B][N], played [B][N] (cards, -1 past k), invalid [B]
-   (first seat whose external card is illegal -- that slot is left untouched --
-   or -1), status [B] |= 1 where an MCSAgent move got no playout (the
-   reference raises IndexError there, quirk Q6). */
+   (first seat whose external card is illegal, or -1: that slot's board,
+   hands and scores are left as they were, but its RANDOM / MCS seats have
+   already drawn this step from the slot's stream and an MCS seat's card
+   memory has moved on -- the slot no longer follows the reference's stream
+   and the caller must treat it as failed; the batched tournament raises right
+   after such a step), status [B] |= 1 where an MCSAgent move got no playout
+   (the reference raises IndexError there, quirk Q6). */
 sn_status sn_league_step(sn_env* env, const int32_t* actions, int32_t* rewards, int32_t* played, int32_t* records,
                          int32_t* invalid, int32_t* status, void* stream);
 /* Sequential multiplayer Elo over game records in the given order (host
@@ -399,6 +403,14 @@ sn_status sn_puct_h1_cols(sn_env* env, const sn_puct* q, int n_cur, const void* 
 sn_status sn_puct_seat_rows(sn_env* env, const sn_puct* q, int n_cur, void* rows, int ks, float* cards, void* stream);
 sn_status sn_puct_mlp(sn_env* env, const sn_puct* q, int n_cur, const void* base, int ldb, const float* w1c,
                       const float* cards, const void* w2, const float* head, float* logits, void* stream);
+/* The same logits with layer 1's per-seat part inside too: one workgroup per
+   64 rollout seats builds their [0, obs, 1] rows in LDS, multiplies them by
+   w1s [128][64] bf16 (the [W1 | b1 | 0] rows, the ones feature's row H) on
+   MFMA, then runs sn_puct_mlp's tile loop over the seats' candidate rows --
+   one launch per rollout step instead of sn_puct_seat_rows + a GEMM +
+   sn_puct_mlp. */
+sn_status sn_puct_mlp_seats(sn_env* env, const sn_puct* q, int n_cur, const void* w1s, const float* w1c, const void* w2,
+                            const float* head, float* logits, void* stream);
 /* best_index [D] (optional): index of the chosen card in the root legal list */
 sn_status sn_puct_choose(sn_env* env, const sn_puct* q, int32_t* actions, int32_t* best_index, void* stream);
 /* PUCTCustomedAgent (agents/mcts.py:325-451, replaces _mcts /

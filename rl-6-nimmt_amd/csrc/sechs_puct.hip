@@ -462,6 +462,171 @@ __global__ __launch_bounds__(256) void k_puct_mlp(uint32_t R, int n_cur, const u
     }
 }
 
+// ---- the whole rollout MLP in one kernel (sn_puct_mlp_seats) -------------
+// A workgroup owns 64 consecutive rollout seats and all their rows (64 x
+// n_cur): phase 1 builds the seats' [0, obs, 1] rows in LDS (write_row: the
+// normalisation of sn_puct_seat_cols) and the candidates' card features,
+// phase 2 computes base = W1s . rows for the 64 seats with MFMA (layer 1's
+// obs part, K = 64) into LDS (bf16, as the PyTorch GEMM rounds it), phase 3
+// runs k_puct_mlp's tile loop over the seats' rows reading base and the
+// cards from LDS.  Replaces sn_puct_seat_rows + the per-seat GEMM +
+// sn_puct_mlp (two launches and the [S][56] / [S][112] HBM round trips).
+constexpr int kSeatBlock = 64;
+constexpr int kSeatRowK = 64;               // seat-row features (48 + the ones feature, zero-padded)
+constexpr int kSeatRowLds = kSeatRowK + 8;  // LDS stride (144 B)
+constexpr int kBaseLds = kMlpK + 8;         // 120 bf16 (240 B) per seat of base in LDS
+
+__global__ __launch_bounds__(256) void k_puct_mlp_seats(PuctArgs a, int N, int n_cur, const uint16_t* w1s,
+                                                       const float* w1c, const uint16_t* w2, const float* head,
+                                                       float* logits) {
+    __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kMlpLdsK];          // W2 [128][120]
+    __shared__ __attribute__((aligned(16))) uint16_t sW1[kMlpM * kSeatRowLds];      // W1s [128][72]
+    __shared__ __attribute__((aligned(16))) uint16_t sRow[kSeatBlock * kSeatRowLds];  // seat rows [64][72]
+    __shared__ __attribute__((aligned(16))) uint16_t sBase[kSeatBlock * kBaseLds];    // base [64][120]
+    __shared__ __attribute__((aligned(16))) float sCard[kSeatBlock * kHand];
+    __shared__ __attribute__((aligned(16))) float sC[kMlpK];
+    __shared__ __attribute__((aligned(16))) float sH[kMlpM];
+    const int tid = threadIdx.x;
+    const int64_t S = a.D * N;
+    const int64_t s0 = (int64_t)blockIdx.x * kSeatBlock;
+    const int nseat = (int)min<int64_t>(kSeatBlock, S - s0);
+    for (int i = tid; i < kMlpM * (kMlpK / 8); i += blockDim.x) {
+        const int o = i / (kMlpK / 8), c = i - o * (kMlpK / 8);
+        *(uint4*)&sW[o * kMlpLdsK + 8 * c] = *(const uint4*)&w2[o * kMlpK + 8 * c];
+    }
+    for (int i = tid; i < kMlpM * (kSeatRowK / 8); i += blockDim.x) {
+        const int o = i / (kSeatRowK / 8), c = i - o * (kSeatRowK / 8);
+        *(uint4*)&sW1[o * kSeatRowLds + 8 * c] = *(const uint4*)&w1s[o * kSeatRowK + 8 * c];
+    }
+    for (int i = tid; i < kMlpK; i += blockDim.x) sC[i] = w1c[i];
+    for (int i = tid; i < kMlpM; i += blockDim.x) sH[i] = head[i];
+    // phase 1: the seats' rows (k_puct_seat_cols' features) and card features
+    if (tid < kSeatBlock) {
+        uint16_t* row = sRow + tid * kSeatRowLds;
+        float* cd = sCard + tid * kHand;
+        const int64_t i = s0 + min(tid, max(nseat - 1, 0));
+        const int64_t d = i / N;
+        const int q = (int)(i - d * N);
+        const int32_t* ro = a.ro + d * kRoWords;
+        int kp = N;
+        if (a.lgs) {
+            int64_t g;
+            int p;
+            dec_to_gp(a, d, g, p);
+            kp = players_of(a, g);
+        }
+        __hip_bfloat16* rb = (__hip_bfloat16*)row;
+        if (q >= kp) {
+            for (int f = 0; f < kSeatRowK; f++) rb[f] = to_out<__hip_bfloat16>(f == kRowLen ? 1.f : 0.f);
+            for (int k = 0; k < kHand; k++) cd[k] = 0.f;
+        } else {
+            const Hand h = ro_hand(ro, q);
+            write_row<__hip_bfloat16>(rb, 0u, h, kp, ro_board(ro), 1);
+            rb[0] = to_out<__hip_bfloat16>(0.f);
+            rb[kRowLen] = to_out<__hip_bfloat16>(1.f);
+            for (int f = kRowLen + 1; f < kSeatRowK; f++) rb[f] = to_out<__hip_bfloat16>(0.f);
+            for (int k = 0; k < kHand; k++)
+                cd[k] = (k < n_cur) ? round_to<__hip_bfloat16>(nrm((float)hand_get(h, (uint32_t)k), 0.f, 103.f)) : 0.f;
+        }
+    }
+    __syncthreads();
+    const int wave = tid >> 6, lane = tid & 63, col = lane & 31, half = lane >> 5;
+    // phase 2: base[seat][j] = sum_k W1s[j][k] rows[seat][k]; wave w: outputs j in [32w, 32w + 32)
+    {
+        f32x16_t acc[2];
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+            for (int i = 0; i < 16; i++) acc[nt][i] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < kSeatRowK / 16; ks++) {
+            const int k0 = 16 * ks + 8 * half;
+            const bf16x8_t af = __builtin_bit_cast(bf16x8_t, *(const uint4*)&sW1[(32 * wave + col) * kSeatRowLds + k0]);
+#pragma unroll
+            for (int nt = 0; nt < 2; nt++) {
+                const bf16x8_t bfr = __builtin_bit_cast(bf16x8_t, *(const uint4*)&sRow[(32 * nt + col) * kSeatRowLds + k0]);
+                acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[nt], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int j = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * half;
+                if (j < kMlpK) sBase[(32 * nt + col) * kBaseLds + j] = (uint16_t)f32_to_bf16_rne(acc[nt][r]);
+            }
+    }
+    __syncthreads();
+    // phase 3: k_puct_mlp's tile loop over this block's rows
+    const uint32_t rows = (uint32_t)nseat * (uint32_t)n_cur;
+    const uint32_t tiles = (rows + 63u) / 64u;
+    const uint32_t rbase = (uint32_t)s0 * (uint32_t)n_cur;
+    for (uint32_t tile = wave; tile < tiles; tile += blockDim.x >> 6) {
+        uint32_t rr[2];
+        float x[2];
+        const uint16_t* brow[2];
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++) {
+            rr[nt] = tile * 64u + 32u * nt + (uint32_t)col;  // block-local row
+            const uint32_t rc = rr[nt] < rows ? rr[nt] : rows - 1u;
+            const uint32_t sl = rc / (uint32_t)n_cur;
+            x[nt] = sCard[sl * kHand + (rc - sl * (uint32_t)n_cur)];
+            brow[nt] = sBase + sl * kBaseLds;
+        }
+        f32x16_t acc[4][2];
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+            for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+                for (int i = 0; i < 16; i++) acc[mt][nt][i] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < kMlpK / 16; ks++) {
+            const int k0 = 16 * ks + 8 * half;
+            const float4 wa = *(const float4*)&sC[k0], wb = *(const float4*)&sC[k0 + 4];
+            const float w[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+            bf16x8_t bfr[2];
+#pragma unroll
+            for (int nt = 0; nt < 2; nt++) {
+                const uint4 bv = *(const uint4*)(brow[nt] + k0);
+                const uint32_t bw[4] = {bv.x, bv.y, bv.z, bv.w};
+                uint32_t hb[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const float lo = fmaxf(bf16_bits_to_f32(bw[j] & 0xFFFFu) + x[nt] * w[2 * j], 0.f);
+                    const float hi = fmaxf(bf16_bits_to_f32(bw[j] >> 16) + x[nt] * w[2 * j + 1], 0.f);
+                    hb[j] = f32_to_bf16_rne(lo) | (f32_to_bf16_rne(hi) << 16);
+                }
+                bfr[nt] = __builtin_bit_cast(bf16x8_t, make_uint4(hb[0], hb[1], hb[2], hb[3]));
+            }
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++) {
+                const bf16x8_t af = __builtin_bit_cast(bf16x8_t, *(const uint4*)&sW[(32 * mt + col) * kMlpLdsK + k0]);
+                acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[0], acc[mt][0], 0, 0, 0);
+                acc[mt][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[1], acc[mt][1], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++) {
+            float sum = 0.f;
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const float4 hv = *(const float4*)&sH[32 * mt + 8 * g + 4 * half];
+                    const float hw[4] = {hv.x, hv.y, hv.z, hv.w};
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const float v = bf16_bits_to_f32(f32_to_bf16_rne(fmaxf(acc[mt][nt][4 * g + i], 0.f)));
+                        sum = fmaf(v, hw[i], sum);
+                    }
+                }
+            sum += __shfl_xor(sum, 32);
+            if (half == 0 && rr[nt] < rows) logits[rbase + rr[nt]] = sum;
+        }
+    }
+}
+
 // np.median of all outcomes so far, from the histogram (kth smallest)
 __device__ double hist_median(const int32_t* hist, int32_t total) {
     const int32_t k0 = (total - 1) / 2, k1 = total / 2;
@@ -957,6 +1122,24 @@ sn_status sn_puct_seat_rows(sn_env* e, const sn_puct* q, int n_cur, void* rows, 
     const int64_t total = a.D * e->s.N;
     hipLaunchKernelGGL(k_puct_seat_cols<__hip_bfloat16>, dim3(grid_for(total)), dim3(kBlock), 0, (hipStream_t)stream, a,
                        e->s.N, n_cur, (__hip_bfloat16*)rows, ks, cards, 1);
+    HIP_TRY(hipGetLastError());
+    return SN_OK;
+}
+
+sn_status sn_puct_mlp_seats(sn_env* e, const sn_puct* q, int n_cur, const void* w1s, const float* w1c, const void* w2,
+                            const float* head, float* logits, void* stream) {
+    PuctArgs a{};
+    sn_status st = puct_args(e, q, a);
+    if (st != SN_OK) return st;
+    if (n_cur < 1 || n_cur > a.n) return set_error(SN_EINVAL, "n_cur out of range");
+    if (!w1s || !w1c || !w2 || !head || !logits) return set_error(SN_EINVAL, "NULL argument");
+    if ((((uintptr_t)w1s) | ((uintptr_t)w2) | ((uintptr_t)w1c) | ((uintptr_t)head)) & 15)
+        return set_error(SN_EINVAL, "w1s / w2 / w1c / head must be 16-B aligned");
+    const int64_t S = a.D * e->s.N;
+    if (S * n_cur >= (1ll << 31)) return set_error(SN_EINVAL, "too many rows");
+    hipLaunchKernelGGL(k_puct_mlp_seats, dim3((unsigned)((S + kSeatBlock - 1) / kSeatBlock)), dim3(kBlock), 0,
+                       (hipStream_t)stream, a, e->s.N, n_cur, (const uint16_t*)w1s, w1c, (const uint16_t*)w2, head,
+                       logits);
     HIP_TRY(hipGetLastError());
     return SN_OK;
 }

@@ -146,7 +146,10 @@ class FusedMLP:
         head = torch.zeros((128,), dtype=torch.float32, device=dev)
         head[:H2] = self.head_w[:, 0].float()
         head[H2] = self.head_b[0].float()
-        self._fused = (w1t, c, w2p, head)
+        w1s = torch.zeros((128, 64), dtype=torch.bfloat16, device=dev)  # sn_puct_mlp_seats: [W1 | b1 | 0] rows
+        w1s[:H, :56] = w1a
+        w1s[H, ROW] = 1.0
+        self._fused = (w1t, c, w2p, head, w1s)
         return self._fused
 
     def __call__(self, rows):
@@ -215,6 +218,9 @@ class BatchedPUCT:
         # the rollout MLP after the per-seat GEMM as one MFMA kernel
         # (FusedMLP.fused, sn_puct_mlp): bf16 nets of the reference's shape
         self.fused_mlp = os.environ.get("SECHS_FUSED_MLP", "1") != "0"  # "0": the PyTorch split path (A/B runs)
+        # "seats": layer 1's per-seat part inside the MLP kernel too (sn_puct_mlp_seats, one launch per step);
+        # "gemm": per-seat rows + a PyTorch GEMM + sn_puct_mlp
+        self.mlp_layer1 = os.environ.get("SECHS_MLP_LAYER1", "gemm")
         self._step_dev = torch.zeros((1,), dtype=torch.int32, device=dev)
 
     # ------------------------------------------------------------ policy net on the device
@@ -334,7 +340,7 @@ class BatchedPUCT:
             # (PyTorch-ROCm GEMM over the D*N seats), then layer 1's card
             # column + ReLU, layer 2 + ReLU and the head in one MFMA kernel
             # (f32 logits, packed) -- no activation tensor in HBM
-            w1t, w1c, w2p, head = fz
+            w1t, w1c, w2p, head, w1s = fz
             S = self.D * N
             rows, cards, base, logits = self._fused_bufs()
             rv, bv = rows[:S], base[:S]
@@ -343,6 +349,12 @@ class BatchedPUCT:
                 nat.check(L.sn_puct_deal(h, ctypes_ref(q), st), "sn_puct_deal")
                 for t in range(n):
                     m = n - t
+                    if self.mlp_layer1 == "seats":
+                        nat.check(L.sn_puct_mlp_seats(h, ctypes_ref(q), m, nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p),
+                                                      nat.ptr(head), nat.ptr(logits), st), "sn_puct_mlp_seats")
+                        self.rows_evaluated += S * m
+                        nat.check(L.sn_puct_step(h, ctypes_ref(q), nat.ptr(logits), t, m, st), "sn_puct_step")
+                        continue
                     nat.check(L.sn_puct_seat_rows(h, ctypes_ref(q), m, nat.ptr(rv), 56, nat.ptr(cards), st),
                               "sn_puct_seat_rows")
                     torch.mm(rv, w1t, out=bv)

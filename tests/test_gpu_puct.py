@@ -550,7 +550,7 @@ def test_fused_mlp_equals_module_forward(B, n):
     for t in range(10 - n):
         env.step(eng.decide(10 - t))
     net = eng.sync_net()
-    w1t, w1c, w2p, head = net.fused()
+    w1t, w1c, w2p, head, w1s = net.fused()
     w1a, H, kp, hidden, ha, w1c_s = net.split()
     q = eng._params(n)
     L, h, st = nat.lib(), env._h, env._stream()
@@ -583,6 +583,15 @@ def test_fused_mlp_equals_module_forward(B, n):
         with torch.no_grad():
             (want,) = net.module(rows)
         assert torch.allclose(logits, want[:, 0].float(), rtol=4 * tol, atol=4 * tol), (logits - want[:, 0].float()).abs().max()
+        # layer 1's per-seat part inside the kernel too (sn_puct_mlp_seats): its base is the MFMA product
+        # rounded to bf16 like the GEMM's, in another summation order (a bf16 ulp here and there)
+        lg2 = torch.full((R,), float("nan"), dtype=torch.float32, device=env.device)
+        nat.check(L.sn_puct_mlp_seats(h, ctypes.byref(q), m, nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p), nat.ptr(head),
+                                      nat.ptr(lg2), st), "mlp_seats")
+        torch.cuda.synchronize()
+        assert not torch.isnan(lg2).any()
+        assert torch.allclose(lg2, logits, rtol=2 * tol, atol=2 * tol), (lg2 - logits).abs().max()
+        assert torch.allclose(lg2, want[:, 0].float(), rtol=4 * tol, atol=4 * tol)
 
 
 def test_fused_and_split_rollouts_agree_in_law():
@@ -594,6 +603,7 @@ def test_fused_and_split_rollouts_agree_in_law():
     for fused in (True, False):
         env, eng = _engine(B=512, dtype=torch.bfloat16, mc_max=20, mc_per_card=10, seed=41)
         eng.fused_mlp = fused
+        eng.mlp_layer1 = "seats"  # the one-launch form (the GEMM form: the statistics test and the bench)
         acts = eng.decide(10)
         torch.cuda.synchronize()
         res[fused] = (acts.clone(), eng.stats.clone(), eng.rows_evaluated)

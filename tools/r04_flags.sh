@@ -24,6 +24,11 @@ for cfg in "1 1" "1 0" "0 1" "0 0"; do
   rc=$?; fatal $rc puct
   python -c "import json,sys; r=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])['extra_config4_puct']; print('fused',sys.argv[2],'seats',sys.argv[3],round(r['value']/1e6,1),'M playout env-steps/s wall',round(r['wall_s'],3))" $OUT/puct_$1$2.json $1 $2
 done
+SECHS_MLP_LAYER1=seats timeout -k 10 300 python bench.py --only puct > $OUT/puct_seats.json 2> $OUT/puct_seats.err
+rc=$?; fatal $rc puct_seats
+python -c "import json,sys; r=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])['extra_config4_puct']; print('layer1 in kernel',round(r['value']/1e6,1),'M playout env-steps/s wall',round(r['wall_s'],3))" $OUT/puct_seats.json
+cd /tmp && SECHS_MLP_LAYER1=seats timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_puct_seats -o run -- python3 $R/bench.py --only puct > $OUT/prof_puct_seats.log 2>&1
+rc=$?; echo "rocprof seats rc=$rc"; fatal $rc rocprof_seats
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_puct -o run -- python3 $R/bench.py --only puct > $OUT/prof_puct.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; fatal $rc rocprof
 echo done
