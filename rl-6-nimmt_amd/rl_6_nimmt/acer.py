@@ -128,6 +128,7 @@ class BatchedACER(BatchedPUCT):
         self.episodes = 0  # episodes written (slot = episodes % capacity)
         self.rep_nd = [0] * C  # deciders stored in each slot (tournament mode: the round's seats of this agent)
         self._t = 0
+        self.decider_chunk = 4096  # deciders per backward pass of an update (learn)
         self._gen = torch.Generator(device=dev)
         self._gen.manual_seed(self.seed ^ 0xACE5)
         self.last_losses = []
@@ -354,10 +355,20 @@ class BatchedACER(BatchedPUCT):
                 continue
             batches = self.league_batches(c) if self.dec is not None else (self.on_policy_batch(c), self.off_policy_batch(c))
             for batch in batches:
-                total, actor, corr, critic = self.loss(*batch)
+                # the loss is a sum over deciders: its gradient accumulates over
+                # decider chunks (bounded activation memory: a 65 536-slot
+                # league's off-policy batch is ~4e7 candidate rows), then one step
                 optimizer.zero_grad()
-                total.backward()
+                D = batch[0].shape[0]
+                if len(batch) == 2:  # explicit decider indices: a chunk's row d is decider d0 + d
+                    batch = (*batch, torch.arange(D, device=batch[0].device)[:, None].expand_as(batch[0]))
+                tot = [0.0, 0.0, 0.0]
+                for d0 in range(0, D, self.decider_chunk):
+                    part = tuple(x[d0: d0 + self.decider_chunk] for x in batch)
+                    total, actor, corr, critic = self.loss(*part)
+                    total.backward()
+                    tot = [tot[0] + float(actor), tot[1] + float(corr), tot[2] + float(critic)]
                 optimizer.step()
-                done_updates.append((float(actor), float(corr), float(critic)))
+                done_updates.append(tuple(tot))
         self.last_losses += done_updates
         return done_updates

@@ -282,3 +282,26 @@ def test_distinct_off_policy_picks():
         assert float(((counts - exp).abs() / exp ** 0.5).max()) < 5.0
     with pytest.raises(ValueError):
         distinct_picks(3, 2, 4, g, torch.device("cpu"))
+
+
+def test_decider_chunked_update_equals_one_batch():
+    """learn() accumulates the gradient of the decider-summed loss over
+    decider chunks (bounded activation memory) before its one Adam step:
+    the same update as one batch over every decider"""
+    import copy
+
+    from rl_6_nimmt.acer import BatchedACER
+
+    torch.manual_seed(0)
+    eng = BatchedACER(_HostEnv(5, 2), net_dtype=torch.float32, rollout_len=10, capacity=3, minibatch=2, warmup=2)
+    _fill_replay(eng, 3, np.random.default_rng(7))
+    eng2 = copy.deepcopy(eng)
+    eng.decider_chunk, eng2.decider_chunk = 3, 10 ** 6
+    eng._gen.manual_seed(11)
+    eng2._gen.manual_seed(11)  # the same off-policy picks
+    o1, o2 = torch.optim.SGD(eng.actor.parameters(), lr=0.1), torch.optim.SGD(eng2.actor.parameters(), lr=0.1)
+    u1, u2 = eng.learn(o1), eng2.learn(o2)
+    assert len(u1) == len(u2) == 2
+    assert np.allclose(np.array(u1), np.array(u2), rtol=1e-5, atol=1e-6)
+    for a, b in zip(eng.actor.parameters(), eng2.actor.parameters()):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6)
