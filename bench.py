@@ -530,20 +530,19 @@ def bench_league_mixed(world, rank, slots, mc_max=200, rounds=1, warmup=1):
     from rl_6_nimmt.distributed import gather_league_records, max_over_ranks, reduce_agent_stats
     from rl_6_nimmt.league import BatchedTournament, replay_league_elo
 
-    # warm-up on a small league of the same agents (kernels, GEMM heuristics,
-    # optimizer state): a round at full size costs as much as the timed one
-    specs = run_py_league(mc_max)
-    w = BatchedTournament(min(slots, 1024), 2, 4, seed=0, game_offset=(1 << 30) + rank * slots, rng="numpy", train=True)
-    for name, agent in specs:
-        w.add_player(name, agent)
-    for _ in range(warmup):
-        w.play_games(1)
-    w.agent_stats()
-    w.close()
+    # warm-up: `warmup` untimed rounds of the SAME league at full size, so
+    # the timed round finds the handle, the engines, their buffers, the ACER
+    # replay and every GEMM shape allocated and selected already (a fresh
+    # league in the timed region measured 3.9-5.9 s per round, r03)
     specs = run_py_league(mc_max)
     t = BatchedTournament(slots, 2, 4, seed=0, game_offset=rank * slots, rng="numpy", train=True)
     for name, agent in specs:
         t.add_player(name, agent)
+    for _ in range(warmup):
+        t.play_games(1)
+    t.agent_stats()
+    for e in t.engines.values():
+        e.rows_evaluated = 0
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
@@ -554,7 +553,7 @@ def bench_league_mixed(world, rank, slots, mc_max=200, rounds=1, warmup=1):
     torch.cuda.synchronize()
     barrier(world)
     wall = time.perf_counter() - t0
-    rows = {n: e.rows_evaluated for n, e in t.engines.items()}  # the timed rounds only: a fresh league
+    rows = {n: e.rows_evaluated for n, e in t.engines.items()}  # the timed rounds only (reset after the warm-up)
     recs = torch.cat([r for r, _ in t.records[rec0:]], dim=0)
     # one more round with HIP events around its phases (outside the timed
     # region: where a round's time goes)
@@ -589,7 +588,8 @@ def bench_league_mixed(world, rank, slots, mc_max=200, rounds=1, warmup=1):
             "workload": f"config5 (run.py league): tournament.py self-play, {world} x {slots} concurrent game slots, "
                         f"agents ACER(minibatch=10), MCS, Alpha0.5 (PUCT), Alpha0.5_customed at mc_max={mc_max} + "
                         f"Random, 2..4 players drawn per game, training on (one batched Adam step per net agent per "
-                        f"round); numpy-MT slot streams (slot g = np.random.seed(g)); {rounds} timed round(s)",
+                        f"round); numpy-MT slot streams (slot g = np.random.seed(g)); {warmup} untimed round(s) of "
+                        f"the same league, then {rounds} timed round(s)",
             "value": games * STEPS_PER_LAUNCH / wall,
             "unit": "env-steps/s",
             "games_per_s": games / wall,
