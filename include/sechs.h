@@ -164,7 +164,11 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          device flags -- a play lane polls its game's
                          generation word, the side stream's CP waits on a
                          block count -- so consecutive play launches have no
-                         packet between them; 0: HIP events both ways. */
+                         packet between them; 0: HIP events both ways.
+                         Either way the handle records its ordering events on
+                         the stream of the last pipelined rollout when later
+                         work needs them: that stream must outlive the
+                         handle's next call (torch's streams always do). */
 enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3, SN_OPT_TIMING = 4, SN_OPT_PIPE_GPW = 5,
        SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7, SN_OPT_PIPE_FLAGS = 8 };
 sn_status sn_set_option(sn_env* env, int option, int value);

@@ -31,4 +31,9 @@ cd /tmp && SECHS_MLP_LAYER1=seats timeout -k 10 300 rocprofv3 --kernel-trace --s
 rc=$?; echo "rocprof seats rc=$rc"; fatal $rc rocprof_seats
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_puct -o run -- python3 $R/bench.py --only puct > $OUT/prof_puct.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; fatal $rc rocprof
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread --deselect tests/test_gpu_env.py --deselect tests/test_gpu_puct.py > $OUT/tests_rest.log 2>&1
+rc=$?; tail -4 $OUT/tests_rest.log; fatal $rc pytest_rest
+timeout -k 10 400 python bench.py --only mixed > $OUT/mixed.json 2> $OUT/mixed.err
+rc=$?; fatal $rc mixed
+python -c "import json,sys; r=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])['extra_config5_run_py_league']; print('run.py league s/round',round(r['s_per_round'],3)); print(json.dumps(r['phases']))" $OUT/mixed.json
 echo done
