@@ -391,6 +391,7 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
     steps = sum(eng.n_mc(n) * n for n in range(2, 11)) * N_PLAYERS * games
     rows_s = eng.rows_evaluated / wall
     fused = eng.fused_mlp and eng._net is not None and eng._net.fused() is not None
+    seats = fused and eng.mlp_layer1 == "seats"
     tflops = eng.rows_evaluated * 29800 / wall / 1e12
     if fused:
         # the rollout MLP runs as sn_puct_mlp (one MFMA kernel after a
@@ -399,8 +400,10 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
         # MFMA peak, over the whole game's wall time (every kernel included)
         roof = {"bound": "mfma", "achieved": tflops, "peak": 2500.0, "unit": "TFLOP/s", "frac": tflops / 2500.0,
                 "traffic": None, "algo_flop_per_row": 29800,
-                "kernel": "rollout step = sn_puct_seat_rows + PyTorch GEMM (layer 1, per seat) + sn_puct_mlp (MFMA: "
-                          "card column, layer 2, head) + k_puct_step_seats; whole-game wall time"}
+                "kernel": ("rollout step = sn_puct_mlp_seats (MFMA: seat rows, layer 1 per seat, card column, "
+                           "layer 2, head in one persistent kernel) + k_puct_step_seats; whole-game wall time") if seats
+                else ("rollout step = sn_puct_seat_rows + PyTorch GEMM (layer 1, per seat) + sn_puct_mlp (MFMA: "
+                      "card column, layer 2, head) + k_puct_step_seats; whole-game wall time")}
     else:
         # the split PyTorch path: hipBLASLt GEMMs per candidate-row batch,
         # HBM-bound on their bf16 intermediates -- per row 96 B in, 2 x (200 B
@@ -413,15 +416,18 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
                           "wall time incl. the k_puct_* kernels"}
     return {
         "workload": f"config4: {games} x 4-player games, all seats PUCT (mc_max={mc_max}, mc_per_card={mc_per_card}, "
-                    f"c_puct=2), bf16 policy MLP 48-100-100-1 (layer 1's per-seat part a PyTorch-ROCm GEMM, the "
-                    f"rest one MFMA kernel), 1 game; each decision's rollout "
+                    f"c_puct=2), bf16 policy MLP 48-100-100-1 ("
+                    + ("one MFMA kernel per rollout step" if seats else
+                       "layer 1's per-seat part a PyTorch-ROCm GEMM, the rest one MFMA kernel")
+                    + f"), 1 game; each decision's rollout "
                     f"chain replayed from a captured hipGraph",
         "value": steps / wall,
         "unit": "playout env-steps/s",
         "decisions_per_s": 9 * N_PLAYERS * games / wall,
         "policy_rows_per_s": rows_s,
         "policy_tflops": tflops,
-        "mlp": "fused (sn_puct_mlp)" if fused else "split (PyTorch GEMMs)",
+        "mlp": "fused, one kernel (sn_puct_mlp_seats)" if seats else "fused (sn_puct_mlp)" if fused
+        else "split (PyTorch GEMMs)",
         "roofline": roof,
         "wall_s": wall,
         "mean_score_per_seat": total.double().mean(dim=0).tolist(),

@@ -160,11 +160,15 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          always use the pipelined one-wave k_play.
      SN_OPT_PIPE_FLAGS   hand-off between the pipelined play launches (caller's
                          stream) and the twist-ahead launches (side stream):
-                         1 (default where hipStreamWaitValue64 is supported):
-                         device flags -- a play lane polls its game's
-                         generation word, the side stream's CP waits on a
-                         block count -- so consecutive play launches have no
-                         packet between them; 0: HIP events both ways.
+                         0 (default; SECHS_PIPE_FLAGS=0/1/2 sets it at
+                         creation): HIP events both ways.  1: device flags --
+                         a play lane polls its game's generation word, the
+                         side stream's CP waits on a block count
+                         (hipStreamWaitValue64) -- no packet between play
+                         launches.  2: play lanes poll, the side stream waits
+                         on an event recorded after each play launch.  Set it
+                         before the pipeline starts (after creation, or after
+                         sn_pipe_sync); SN_EINVAL otherwise.
                          Either way the handle records its ordering events on
                          the stream of the last pipelined rollout when later
                          work needs them: that stream must outlive the

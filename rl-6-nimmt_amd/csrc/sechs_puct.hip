@@ -374,24 +374,100 @@ constexpr int kMlpLdsK = kMlpK + 8;  // LDS row stride of W2 (240 B: 60 dwords, 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 
-__device__ __forceinline__ float bf16_bits_to_f32(uint32_t b) { return __uint_as_float(b << 16); }
-__device__ __forceinline__ uint32_t f32_to_bf16_rne(float v) {  // __float2bfloat16 (finite values)
-    const uint32_t u = __float_as_uint(v);
-    return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+
+// two f32 -> one bf16 pair, round to nearest even (v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
+    const bf16x2_t v = {(__bf16)lo, (__bf16)hi};
+    return __builtin_bit_cast(uint32_t, v);
 }
 
-__global__ __launch_bounds__(256) void k_puct_mlp(uint32_t R, int n_cur, const uint16_t* base, int ldb,
-                                                 const float* w1c, const float* cards, const uint16_t* w2,
-                                                 const float* head, float* logits) {
+// One 64-row tile of the rollout MLP for a wave: rows col (nt = 0) and
+// 32 + col (nt = 1) of the tile, their layer-1 base rows (bf16 [112]) and
+// card features x.  Layer 1's card column + ReLU builds the MFMA B fragments
+// (f32 fma, bf16 rounding as the GEMM's output), layer 2 runs as 4 x 7
+// v_mfma_f32_32x32x16_bf16 against W2 in LDS, its ReLU'd bf16 outputs are
+// dotted with the head (bf16 pairs, v_dot2 in f32) and the two halves of
+// the wave summed.  sH2: the head as bf16 pairs, o = 2i, 2i + 1.
+__device__ __forceinline__ void mlp_tile(const uint16_t* brow0, const uint16_t* brow1, float x0, float x1,
+                                         const uint16_t* sW, const float* sC, const uint32_t* sH2, int col, int half,
+                                         float (&out)[2]) {
+    const uint16_t* brow[2] = {brow0, brow1};
+    const float x[2] = {x0, x1};
+    f32x16_t acc[4][2];
+#pragma unroll
+    for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+            for (int i = 0; i < 16; i++) acc[mt][nt][i] = 0.f;
+#pragma unroll 1
+    for (int ks = 0; ks < kMlpK / 16; ks++) {
+        const int k0 = 16 * ks + 8 * half;  // this lane's 8 features of the k-step
+        const float4 wa = *(const float4*)&sC[k0], wb = *(const float4*)&sC[k0 + 4];
+        const float w[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+        bf16x8_t bfr[2];
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++) {
+            const uint4 bv = *(const uint4*)(brow[nt] + k0);
+            const uint32_t bw[4] = {bv.x, bv.y, bv.z, bv.w};
+            uint32_t hb[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const f32x2_t b2 = {__uint_as_float(bw[j] << 16), __uint_as_float(bw[j] & 0xFFFF0000u)};
+                const f32x2_t w2 = {w[2 * j], w[2 * j + 1]};
+                const f32x2_t xx = {x[nt], x[nt]};
+                const f32x2_t v = __builtin_elementwise_fma(xx, w2, b2);
+                hb[j] = pack_bf16(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f));
+            }
+            bfr[nt] = __builtin_bit_cast(bf16x8_t, make_uint4(hb[0], hb[1], hb[2], hb[3]));
+        }
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++) {
+            const bf16x8_t a = __builtin_bit_cast(bf16x8_t, *(const uint4*)&sW[(32 * mt + col) * kMlpLdsK + k0]);
+            acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr[0], acc[mt][0], 0, 0, 0);
+            acc[mt][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr[1], acc[mt][1], 0, 0, 0);
+        }
+    }
+    // epilogue: ReLU, bf16 rounding, head dot over this lane's outputs o
+    // (C layout: o = 32 mt + 8 g + 4 half + i, i = 0..3), then the other half's
+#pragma unroll
+    for (int nt = 0; nt < 2; nt++) {
+        float sum = 0.f;
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const uint2 hw = *(const uint2*)&sH2[(32 * mt + 8 * g + 4 * half) / 2];
+                const uint32_t p0 = pack_bf16(fmaxf(acc[mt][nt][4 * g], 0.f), fmaxf(acc[mt][nt][4 * g + 1], 0.f));
+                const uint32_t p1 = pack_bf16(fmaxf(acc[mt][nt][4 * g + 2], 0.f), fmaxf(acc[mt][nt][4 * g + 3], 0.f));
+                sum = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, p0),
+                                                      __builtin_bit_cast(bf16x2_t, hw.x), sum, false);
+                sum = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, p1),
+                                                      __builtin_bit_cast(bf16x2_t, hw.y), sum, false);
+            }
+        out[nt] = sum + __shfl_xor(sum, 32);
+    }
+}
+
+// the head as bf16 pairs in LDS (its values are bf16 weights: exact)
+__device__ __forceinline__ void load_head_pairs(const float* head, uint32_t* sH2) {
+    for (int i = threadIdx.x; i < kMlpM / 2; i += blockDim.x) sH2[i] = pack_bf16(head[2 * i], head[2 * i + 1]);
+}
+
+__global__ __launch_bounds__(256, 2) void k_puct_mlp(uint32_t R, int n_cur, const uint16_t* base, int ldb,
+                                                    const float* w1c, const float* cards, const uint16_t* w2,
+                                                    const float* head, float* logits) {
     __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kMlpLdsK];
     __shared__ __attribute__((aligned(16))) float sC[kMlpK];
-    __shared__ __attribute__((aligned(16))) float sH[kMlpM];
+    __shared__ __attribute__((aligned(16))) uint32_t sH2[kMlpM / 2];
     for (int i = threadIdx.x; i < kMlpM * (kMlpK / 8); i += blockDim.x) {  // W2: 16-B pieces
         const int o = i / (kMlpK / 8), c = i - o * (kMlpK / 8);
         *(uint4*)&sW[o * kMlpLdsK + 8 * c] = *(const uint4*)&w2[o * kMlpK + 8 * c];
     }
     for (int i = threadIdx.x; i < kMlpK; i += blockDim.x) sC[i] = w1c[i];
-    for (int i = threadIdx.x; i < kMlpM; i += blockDim.x) sH[i] = head[i];
+    load_head_pairs(head, sH2);
     __syncthreads();
     const int lane = threadIdx.x & 63, col = lane & 31, half = lane >> 5;
     const uint32_t tiles = (R + 63u) / 64u;
@@ -407,89 +483,92 @@ __global__ __launch_bounds__(256) void k_puct_mlp(uint32_t R, int n_cur, const u
             x[nt] = cards[rc];
             brow[nt] = base + (size_t)(rc / (uint32_t)n_cur) * ldb;
         }
-        f32x16_t acc[4][2];
+        float out[2];
+        mlp_tile(brow[0], brow[1], x[0], x[1], sW, sC, sH2, col, half, out);
 #pragma unroll
-        for (int mt = 0; mt < 4; mt++)
-#pragma unroll
-            for (int nt = 0; nt < 2; nt++)
-#pragma unroll
-                for (int i = 0; i < 16; i++) acc[mt][nt][i] = 0.f;
-#pragma unroll
-        for (int ks = 0; ks < kMlpK / 16; ks++) {
-            const int k0 = 16 * ks + 8 * half;  // this lane's 8 features of the k-step
-            const float4 wa = *(const float4*)&sC[k0], wb = *(const float4*)&sC[k0 + 4];
-            const float w[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
-            bf16x8_t bfr[2];
-#pragma unroll
-            for (int nt = 0; nt < 2; nt++) {
-                const uint4 bv = *(const uint4*)(brow[nt] + k0);
-                const uint32_t bw[4] = {bv.x, bv.y, bv.z, bv.w};
-                uint32_t hb[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const float lo = fmaxf(bf16_bits_to_f32(bw[j] & 0xFFFFu) + x[nt] * w[2 * j], 0.f);
-                    const float hi = fmaxf(bf16_bits_to_f32(bw[j] >> 16) + x[nt] * w[2 * j + 1], 0.f);
-                    hb[j] = f32_to_bf16_rne(lo) | (f32_to_bf16_rne(hi) << 16);
-                }
-                bfr[nt] = __builtin_bit_cast(bf16x8_t, make_uint4(hb[0], hb[1], hb[2], hb[3]));
-            }
-#pragma unroll
-            for (int mt = 0; mt < 4; mt++) {
-                const bf16x8_t a = __builtin_bit_cast(bf16x8_t, *(const uint4*)&sW[(32 * mt + col) * kMlpLdsK + k0]);
-                acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr[0], acc[mt][0], 0, 0, 0);
-                acc[mt][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr[1], acc[mt][1], 0, 0, 0);
-            }
-        }
-        // epilogue: relu, bf16 rounding, head dot over this lane's rows o, then the other half's
-#pragma unroll
-        for (int nt = 0; nt < 2; nt++) {
-            float sum = 0.f;
-#pragma unroll
-            for (int mt = 0; mt < 4; mt++)
-#pragma unroll
-                for (int g = 0; g < 4; g++) {
-                    const float4 hv = *(const float4*)&sH[32 * mt + 8 * g + 4 * half];
-                    const float hw[4] = {hv.x, hv.y, hv.z, hv.w};
-#pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        const float v = bf16_bits_to_f32(f32_to_bf16_rne(fmaxf(acc[mt][nt][4 * g + i], 0.f)));
-                        sum = fmaf(v, hw[i], sum);
-                    }
-                }
-            sum += __shfl_xor(sum, 32);
-            if (half == 0 && rr[nt] < R) logits[rr[nt]] = sum;
-        }
+        for (int nt = 0; nt < 2; nt++)
+            if (half == 0 && rr[nt] < R) logits[rr[nt]] = out[nt];
     }
 }
 
 // ---- the whole rollout MLP in one kernel (sn_puct_mlp_seats) -------------
-// A workgroup owns 64 consecutive rollout seats and all their rows (64 x
-// n_cur): phase 1 builds the seats' [0, obs, 1] rows in LDS (write_row: the
-// normalisation of sn_puct_seat_cols) and the candidates' card features,
-// phase 2 computes base = W1s . rows for the 64 seats with MFMA (layer 1's
-// obs part, K = 64) into LDS (bf16, as the PyTorch GEMM rounds it), phase 3
-// runs k_puct_mlp's tile loop over the seats' rows reading base and the
-// cards from LDS.  Replaces sn_puct_seat_rows + the per-seat GEMM +
-// sn_puct_mlp (two launches and the [S][56] / [S][112] HBM round trips).
+// A workgroup loads W1s / W2 into LDS once and then loops over groups of 64
+// consecutive rollout seats (persistent grid: two workgroups per CU, the
+// occupancy the 64-row MFMA tiles' registers allow).  Per group: phase 1
+// builds the seats' [0, obs, 1] rows in LDS (the features of write_row /
+// sn_puct_seat_cols, four lanes per seat) and the candidates' card
+// features, phase 2 computes base = W1s . rows for the 64 seats with MFMA
+// (layer 1's obs part, K = 64) into LDS (bf16, as the PyTorch GEMM rounds
+// it), phase 3 runs k_puct_mlp's tile loop over the group's rows reading
+// base and the cards from LDS.  Replaces sn_puct_seat_rows + the per-seat
+// GEMM + sn_puct_mlp (two launches and the [S][56] / [S][112] HBM round trips).
 constexpr int kSeatBlock = 64;
 constexpr int kSeatRowK = 64;               // seat-row features (48 + the ones feature, zero-padded)
 constexpr int kSeatRowLds = kSeatRowK + 8;  // LDS stride (144 B)
 constexpr int kBaseLds = kMlpK + 8;         // 120 bf16 (240 B) per seat of base in LDS
 
-__global__ __launch_bounds__(256) void k_puct_mlp_seats(PuctArgs a, int N, int n_cur, const uint16_t* w1s,
-                                                       const float* w1c, const uint16_t* w2, const float* head,
-                                                       float* logits) {
+__device__ __forceinline__ uint16_t bf16_bits(float v) { return __builtin_bit_cast(uint16_t, __float2bfloat16(v)); }
+
+// phase 1, lane `part` (0..3) of seat `sl`: hand features / cards k = part,
+// part + 4, part + 8, board row `part`, a quarter of the zero padding, and
+// one of the constant features (write_row's values, feature 0 = the card
+// slot left 0: the candidates' cards enter through w1c)
+__device__ __forceinline__ void seat_row_part(const PuctArgs& a, int N, int n_cur, int64_t i, int part, uint16_t* row,
+                                              float* cd) {
+    const int64_t d = i / N;
+    const int q = (int)(i - d * N);
+    const int32_t* ro = a.ro + d * kRoWords;
+    int kp = N;
+    if (a.lgs) {
+        int64_t g;
+        int p;
+        dec_to_gp(a, d, g, p);
+        kp = players_of(a, g);
+    }
+    const bool live = q < kp;
+    const Hand h = ro_hand(ro, live ? q : 0);
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const int k = part + 4 * j;
+        if (k < kHand) {
+            const uint32_t c = hand_get(h, (uint32_t)k);
+            row[1 + k] = live ? bf16_bits(nrm(c == 0xFFu ? -1.f : (float)c, 0.f, 103.f)) : (uint16_t)0;
+            cd[k] = (live && k < n_cur) ? round_to<__hip_bfloat16>(nrm((float)c, 0.f, 103.f)) : 0.f;
+        }
+    }
+    const uint32_t lo = (uint32_t)ro[part], hi = (uint32_t)ro[4 + part];  // board row `part` (ro_board)
+    const uint32_t len = len_of(hi);
+    row[12 + part] = live ? bf16_bits(nrm((float)len, 1.f, 5.f)) : (uint16_t)0;
+    row[16 + part] = live ? bf16_bits(nrm((float)end_of(hi), 0.f, 103.f)) : (uint16_t)0;
+    row[20 + part] = live ? bf16_bits(nrm((float)heads_in(hi), 1.f, 10.f)) : (uint16_t)0;
+#pragma unroll
+    for (int c = 0; c < kThreshold; c++) {
+        const float v = (c < 5 && (uint32_t)c < len) ? (float)card_at(lo, hi, c < 5 ? c : 0) : -1.f;
+        row[24 + part * kThreshold + c] = live ? bf16_bits(nrm(v, 0.f, 103.f)) : (uint16_t)0;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int f = kRowLen + 1 + part + 4 * j;
+        if (f < kSeatRowK) row[f] = 0;
+    }
+    if (part == 0) row[0] = 0;
+    if (part == 1) row[11] = live ? bf16_bits(nrm((float)kp, 0.f, 6.f)) : (uint16_t)0;
+    if (part == 2) row[kRowLen] = bf16_bits(1.f);
+}
+
+__global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(PuctArgs a, int N, int n_cur, const uint16_t* w1s,
+                                                          const float* w1c, const uint16_t* w2, const float* head,
+                                                          float* logits) {
     __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kMlpLdsK];          // W2 [128][120]
     __shared__ __attribute__((aligned(16))) uint16_t sW1[kMlpM * kSeatRowLds];      // W1s [128][72]
     __shared__ __attribute__((aligned(16))) uint16_t sRow[kSeatBlock * kSeatRowLds];  // seat rows [64][72]
     __shared__ __attribute__((aligned(16))) uint16_t sBase[kSeatBlock * kBaseLds];    // base [64][120]
     __shared__ __attribute__((aligned(16))) float sCard[kSeatBlock * kHand];
     __shared__ __attribute__((aligned(16))) float sC[kMlpK];
-    __shared__ __attribute__((aligned(16))) float sH[kMlpM];
+    __shared__ __attribute__((aligned(16))) uint32_t sH2[kMlpM / 2];
     const int tid = threadIdx.x;
     const int64_t S = a.D * N;
-    const int64_t s0 = (int64_t)blockIdx.x * kSeatBlock;
-    const int nseat = (int)min<int64_t>(kSeatBlock, S - s0);
+    const int64_t groups = (S + kSeatBlock - 1) / kSeatBlock;
     for (int i = tid; i < kMlpM * (kMlpK / 8); i += blockDim.x) {
         const int o = i / (kMlpK / 8), c = i - o * (kMlpK / 8);
         *(uint4*)&sW[o * kMlpLdsK + 8 * c] = *(const uint4*)&w2[o * kMlpK + 8 * c];
@@ -499,35 +578,15 @@ __global__ __launch_bounds__(256) void k_puct_mlp_seats(PuctArgs a, int N, int n
         *(uint4*)&sW1[o * kSeatRowLds + 8 * c] = *(const uint4*)&w1s[o * kSeatRowK + 8 * c];
     }
     for (int i = tid; i < kMlpK; i += blockDim.x) sC[i] = w1c[i];
-    for (int i = tid; i < kMlpM; i += blockDim.x) sH[i] = head[i];
-    // phase 1: the seats' rows (k_puct_seat_cols' features) and card features
-    if (tid < kSeatBlock) {
-        uint16_t* row = sRow + tid * kSeatRowLds;
-        float* cd = sCard + tid * kHand;
-        const int64_t i = s0 + min(tid, max(nseat - 1, 0));
-        const int64_t d = i / N;
-        const int q = (int)(i - d * N);
-        const int32_t* ro = a.ro + d * kRoWords;
-        int kp = N;
-        if (a.lgs) {
-            int64_t g;
-            int p;
-            dec_to_gp(a, d, g, p);
-            kp = players_of(a, g);
-        }
-        __hip_bfloat16* rb = (__hip_bfloat16*)row;
-        if (q >= kp) {
-            for (int f = 0; f < kSeatRowK; f++) rb[f] = to_out<__hip_bfloat16>(f == kRowLen ? 1.f : 0.f);
-            for (int k = 0; k < kHand; k++) cd[k] = 0.f;
-        } else {
-            const Hand h = ro_hand(ro, q);
-            write_row<__hip_bfloat16>(rb, 0u, h, kp, ro_board(ro), 1);
-            rb[0] = to_out<__hip_bfloat16>(0.f);
-            rb[kRowLen] = to_out<__hip_bfloat16>(1.f);
-            for (int f = kRowLen + 1; f < kSeatRowK; f++) rb[f] = to_out<__hip_bfloat16>(0.f);
-            for (int k = 0; k < kHand; k++)
-                cd[k] = (k < n_cur) ? round_to<__hip_bfloat16>(nrm((float)hand_get(h, (uint32_t)k), 0.f, 103.f)) : 0.f;
-        }
+    load_head_pairs(head, sH2);
+    for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+    const int64_t s0 = grp * kSeatBlock;
+    const int nseat = (int)min<int64_t>(kSeatBlock, S - s0);
+    __syncthreads();  // the previous group's phase 3 is done with sBase / sCard
+    // phase 1: the seats' rows and card features, four lanes per seat
+    {
+        const int sl = tid >> 2;
+        seat_row_part(a, N, n_cur, s0 + min(sl, nseat - 1), tid & 3, sRow + sl * kSeatRowLds, sCard + sl * kHand);
     }
     __syncthreads();
     const int wave = tid >> 6, lane = tid & 63, col = lane & 31, half = lane >> 5;
@@ -553,11 +612,11 @@ __global__ __launch_bounds__(256) void k_puct_mlp_seats(PuctArgs a, int N, int n
 #pragma unroll
             for (int r = 0; r < 16; r++) {
                 const int j = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * half;
-                if (j < kMlpK) sBase[(32 * nt + col) * kBaseLds + j] = (uint16_t)f32_to_bf16_rne(acc[nt][r]);
+                if (j < kMlpK) sBase[(32 * nt + col) * kBaseLds + j] = (uint16_t)pack_bf16(acc[nt][r], 0.f);
             }
     }
     __syncthreads();
-    // phase 3: k_puct_mlp's tile loop over this block's rows
+    // phase 3: k_puct_mlp's tile loop over the group's rows
     const uint32_t rows = (uint32_t)nseat * (uint32_t)n_cur;
     const uint32_t tiles = (rows + 63u) / 64u;
     const uint32_t rbase = (uint32_t)s0 * (uint32_t)n_cur;
@@ -567,63 +626,18 @@ __global__ __launch_bounds__(256) void k_puct_mlp_seats(PuctArgs a, int N, int n
         const uint16_t* brow[2];
 #pragma unroll
         for (int nt = 0; nt < 2; nt++) {
-            rr[nt] = tile * 64u + 32u * nt + (uint32_t)col;  // block-local row
+            rr[nt] = tile * 64u + 32u * nt + (uint32_t)col;  // group-local row
             const uint32_t rc = rr[nt] < rows ? rr[nt] : rows - 1u;
             const uint32_t sl = rc / (uint32_t)n_cur;
             x[nt] = sCard[sl * kHand + (rc - sl * (uint32_t)n_cur)];
             brow[nt] = sBase + sl * kBaseLds;
         }
-        f32x16_t acc[4][2];
+        float out[2];
+        mlp_tile(brow[0], brow[1], x[0], x[1], sW, sC, sH2, col, half, out);
 #pragma unroll
-        for (int mt = 0; mt < 4; mt++)
-#pragma unroll
-            for (int nt = 0; nt < 2; nt++)
-#pragma unroll
-                for (int i = 0; i < 16; i++) acc[mt][nt][i] = 0.f;
-#pragma unroll
-        for (int ks = 0; ks < kMlpK / 16; ks++) {
-            const int k0 = 16 * ks + 8 * half;
-            const float4 wa = *(const float4*)&sC[k0], wb = *(const float4*)&sC[k0 + 4];
-            const float w[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
-            bf16x8_t bfr[2];
-#pragma unroll
-            for (int nt = 0; nt < 2; nt++) {
-                const uint4 bv = *(const uint4*)(brow[nt] + k0);
-                const uint32_t bw[4] = {bv.x, bv.y, bv.z, bv.w};
-                uint32_t hb[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const float lo = fmaxf(bf16_bits_to_f32(bw[j] & 0xFFFFu) + x[nt] * w[2 * j], 0.f);
-                    const float hi = fmaxf(bf16_bits_to_f32(bw[j] >> 16) + x[nt] * w[2 * j + 1], 0.f);
-                    hb[j] = f32_to_bf16_rne(lo) | (f32_to_bf16_rne(hi) << 16);
-                }
-                bfr[nt] = __builtin_bit_cast(bf16x8_t, make_uint4(hb[0], hb[1], hb[2], hb[3]));
-            }
-#pragma unroll
-            for (int mt = 0; mt < 4; mt++) {
-                const bf16x8_t af = __builtin_bit_cast(bf16x8_t, *(const uint4*)&sW[(32 * mt + col) * kMlpLdsK + k0]);
-                acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[0], acc[mt][0], 0, 0, 0);
-                acc[mt][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[1], acc[mt][1], 0, 0, 0);
-            }
-        }
-#pragma unroll
-        for (int nt = 0; nt < 2; nt++) {
-            float sum = 0.f;
-#pragma unroll
-            for (int mt = 0; mt < 4; mt++)
-#pragma unroll
-                for (int g = 0; g < 4; g++) {
-                    const float4 hv = *(const float4*)&sH[32 * mt + 8 * g + 4 * half];
-                    const float hw[4] = {hv.x, hv.y, hv.z, hv.w};
-#pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        const float v = bf16_bits_to_f32(f32_to_bf16_rne(fmaxf(acc[mt][nt][4 * g + i], 0.f)));
-                        sum = fmaf(v, hw[i], sum);
-                    }
-                }
-            sum += __shfl_xor(sum, 32);
-            if (half == 0 && rr[nt] < rows) logits[rbase + rr[nt]] = sum;
-        }
+        for (int nt = 0; nt < 2; nt++)
+            if (half == 0 && rr[nt] < rows) logits[rbase + rr[nt]] = out[nt];
+    }
     }
 }
 
@@ -1137,7 +1151,14 @@ sn_status sn_puct_mlp_seats(sn_env* e, const sn_puct* q, int n_cur, const void* 
         return set_error(SN_EINVAL, "w1s / w2 / w1c / head must be 16-B aligned");
     const int64_t S = a.D * e->s.N;
     if (S * n_cur >= (1ll << 31)) return set_error(SN_EINVAL, "too many rows");
-    hipLaunchKernelGGL(k_puct_mlp_seats, dim3((unsigned)((S + kSeatBlock - 1) / kSeatBlock)), dim3(kBlock), 0,
+    static int cus = 0;  // persistent grid: two workgroups per CU (the kernel's occupancy)
+    if (!cus) {
+        int dev = 0;
+        HIP_TRY(hipGetDevice(&dev));
+        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const int64_t groups = (S + kSeatBlock - 1) / kSeatBlock;
+    hipLaunchKernelGGL(k_puct_mlp_seats, dim3((unsigned)std::min<int64_t>(groups, 2ll * cus)), dim3(kBlock), 0,
                        (hipStream_t)stream, a, e->s.N, n_cur, (const uint16_t*)w1s, w1c, (const uint16_t*)w2, head,
                        logits);
     HIP_TRY(hipGetLastError());

@@ -267,6 +267,10 @@ struct PipeSlow {
     uint32_t k;
 };
 
+// SC1: the device-flag hand-off (SN_OPT_PIPE_FLAGS) -- every handed-off byte
+// read with sc1 loads; the event hand-off reads them plainly (its own
+// instantiation: no runtime branch in the event path)
+template <bool SC1>
 static __device__ __noinline__ PipeSlow pipe_slow(const uint8_t* ring, int64_t B, int64_t g, uint32_t pos, uint32_t left,
                                                   uint32_t* err) {
     PipeSlow r;
@@ -275,8 +279,10 @@ static __device__ __noinline__ PipeSlow pipe_slow(const uint8_t* ring, int64_t B
     for (uint32_t i = 0; i < r.k; i++) {
         const uint32_t ri = (pos + i) & (uint32_t)(kPipeRing - 1);
         const int64_t at = ((int64_t)(ri >> 4) * B + g) * 16 + (ri & 15u);
-        const uint32_t w = ld_sc1((const uint32_t*)(ring + (at & ~3ll)));  // sc1: a handed-off byte
-        r.bytes |= (uint64_t)((w >> (8u * (uint32_t)(at & 3))) & 0xFFu) << (8u * i);
+        uint32_t b;
+        if constexpr (SC1) b = (ld_sc1((const uint32_t*)(ring + (at & ~3ll))) >> (8u * (uint32_t)(at & 3))) & 0xFFu;
+        else b = ring[at];
+        r.bytes |= (uint64_t)b << (8u * i);
     }
     if (r.k == 0u) {
         atomicAdd(err, 1u);
@@ -285,7 +291,9 @@ static __device__ __noinline__ PipeSlow pipe_slow(const uint8_t* ring, int64_t B
     return r;
 }
 
-struct RingPipe {
+template <bool SC1>
+struct RingPipeT {
+    static constexpr bool kSc1 = SC1;
     const uint8_t* slot;  // LDS window: chunk-aligned copy starting at the consumer's chunk
     const uint8_t* ring;
     uint32_t* err;
@@ -297,7 +305,8 @@ struct RingPipe {
         c0 = s.pabsc[(int64_t)cin * B + g];
         // signed: a consumer past the twisted end (an earlier overrun) must
         // not read as a huge window of stale ring bytes
-        const int32_t av = (int32_t)(ld_sc1(&s.ptend[(int64_t)tpar * B + g]) - c0);
+        const uint32_t* te = &s.ptend[(int64_t)tpar * B + g];
+        const int32_t av = (int32_t)((SC1 ? ld_sc1(te) : *te) - c0);
         if (av < 0) atomicAdd(s.perr, 1u);
         avail = (av < 0) ? 0u : (uint32_t)av;
         win = min(avail, (uint32_t)kPipeWin);
@@ -309,7 +318,10 @@ struct RingPipe {
         const uint32_t q0 = (c0 & (uint32_t)(kPipeRing - 1)) >> 4;
         const uint32_t nch = (off + win + 15u) >> 4;
         for (uint32_t i = 0; i < nch; i++) {
-            const u32x4 c = ld16_sc1(s.pring, (uint32_t)((((q0 + i) & (uint32_t)(kPipeRing / 16 - 1)) * B + g) * 16));
+            const int64_t ci = (int64_t)((q0 + i) & (uint32_t)(kPipeRing / 16 - 1)) * B + g;
+            u32x4 c;
+            if constexpr (SC1) c = ld16_sc1(s.pring, (uint32_t)(ci * 16));
+            else c = s.pring[ci];
             *(uint64_t*)(lds_slot + 16u * i) = (uint64_t)c.x | ((uint64_t)c.y << 32);
             *(uint64_t*)(lds_slot + 16u * i + 8u) = (uint64_t)c.z | ((uint64_t)c.w << 32);
         }
@@ -328,7 +340,7 @@ struct RingPipe {
         }
         const uint32_t left = (avail > take) ? avail - take : 0u;
         if (left == 0u && !forced) return false;  // prefetch stops at the twisted end
-        const PipeSlow r = pipe_slow(ring, B, g, c0 + take, left, err);
+        const PipeSlow r = pipe_slow<SC1>(ring, B, g, c0 + take, left, err);
         buf.append(r.bytes, r.k);
         take += r.k;
         return true;
@@ -338,20 +350,23 @@ struct RingPipe {
     }
     __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf, true); }
 };
+using RingPipe = RingPipeT<false>;
 
 // Phase (A) of deck_shuffle2 on the pipelined ring: the words are read
 // straight from the LDS window by stream position (no byte buffer: appending
 // and dropping a variable number of bytes is a long 64-bit shift chain), the
 // next pass's 8 bytes prefetched while this pass decodes.  Same words, same
 // targets as the generic form.
-__device__ __forceinline__ uint64_t pipe_peek8(const RingPipe& r, uint32_t t) {
+template <bool SC1>
+__device__ __forceinline__ uint64_t pipe_peek8(const RingPipeT<SC1>& r, uint32_t t) {
     const uint32_t p = r.off + t, a8 = p & ~7u, sh = 8u * (p & 7u);
     const uint64_t lo = *(const uint64_t*)(r.slot + a8);
     const uint64_t hi = *(const uint64_t*)(r.slot + a8 + 8u);
     return sh ? ((lo >> sh) | (hi << (64u - sh))) : lo;
 }
 
-__device__ __forceinline__ void shuffle_targets(RingPipe& rng, ByteBuf& buf, uint8_t* jslot, int C) {
+template <bool SC1>
+__device__ __forceinline__ void shuffle_targets(RingPipeT<SC1>& rng, ByteBuf& buf, uint8_t* jslot, int C) {
     uint32_t t = rng.take - buf.cnt;  // next unconsumed byte (buffered bytes are re-read from the window)
     buf.clear();
     uint32_t i = (uint32_t)C - 1u;
@@ -361,7 +376,7 @@ __device__ __forceinline__ void shuffle_targets(RingPipe& rng, ByteBuf& buf, uin
         w = pipe_peek8(rng, t);
     } else {
         const uint32_t left = (rng.avail > t) ? rng.avail - t : 0u;
-        const PipeSlow r = pipe_slow(rng.ring, rng.B, rng.g, rng.c0 + t, left, rng.err);
+        const PipeSlow r = pipe_slow<SC1>(rng.ring, rng.B, rng.g, rng.c0 + t, left, rng.err);
         w = r.bytes, valid = r.k;
     }
     while (i >= 1u) {
@@ -388,7 +403,7 @@ __device__ __forceinline__ void shuffle_targets(RingPipe& rng, ByteBuf& buf, uin
                 w = pipe_peek8(rng, t), valid = 8u;
             } else {
                 const uint32_t left = (rng.avail > t) ? rng.avail - t : 0u;
-                const PipeSlow r = pipe_slow(rng.ring, rng.B, rng.g, rng.c0 + t, left, rng.err);
+                const PipeSlow r = pipe_slow<SC1>(rng.ring, rng.B, rng.g, rng.c0 + t, left, rng.err);
                 w = r.bytes, valid = r.k;
             }
         }
@@ -868,6 +883,7 @@ struct sn_env {
     // before the running one to have counted all its blocks into pdone
     int pflags;               // SN_OPT_PIPE_FLAGS
     uint32_t pgen_cur;        // generation of the last twist-ahead launched
+    int pflags_max;           // highest SN_OPT_PIPE_FLAGS mode this handle supports (0: events only)
     unsigned long long* pdone;  // signal memory: k_play blocks finished (monotonic)
     unsigned long long pdone_launched;  // k_play blocks launched so far
     hipStream_t pstream;      // stream of the last pipelined k_play

@@ -218,9 +218,9 @@ class BatchedPUCT:
         # the rollout MLP after the per-seat GEMM as one MFMA kernel
         # (FusedMLP.fused, sn_puct_mlp): bf16 nets of the reference's shape
         self.fused_mlp = os.environ.get("SECHS_FUSED_MLP", "1") != "0"  # "0": the PyTorch split path (A/B runs)
-        # "seats": layer 1's per-seat part inside the MLP kernel too (sn_puct_mlp_seats, one launch per step);
-        # "gemm": per-seat rows + a PyTorch GEMM + sn_puct_mlp
-        self.mlp_layer1 = os.environ.get("SECHS_MLP_LAYER1", "gemm")
+        # "seats" (default): layer 1's per-seat part inside the MLP kernel too (sn_puct_mlp_seats, one
+        # launch per step); "gemm": per-seat rows + a PyTorch GEMM + sn_puct_mlp
+        self.mlp_layer1 = os.environ.get("SECHS_MLP_LAYER1", "seats")
         self._step_dev = torch.zeros((1,), dtype=torch.int32, device=dev)
 
     # ------------------------------------------------------------ policy net on the device

@@ -193,7 +193,7 @@ class VecSechsNimmtEnv:
         if pipe_lead is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPE_LEAD, int(pipe_lead)), "sn_set_option")
         if pipe_flags is not None:
-            nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPE_FLAGS, int(bool(pipe_flags))), "sn_set_option")
+            nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPE_FLAGS, int(pipe_flags)), "sn_set_option")
         if pipe_gpw is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPE_GPW, int(pipe_gpw)), "sn_set_option")
         if play_split is not None:

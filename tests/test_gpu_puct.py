@@ -532,7 +532,7 @@ def test_batched_customed_learning_step_changes_weights():
     assert any(not torch.equal(a.cpu(), b.cpu()) for a, b in zip(eng.actor.parameters(), before))
 
 
-@pytest.mark.parametrize("B,n", [(64, 7), (37, 10), (256, 4)])
+@pytest.mark.parametrize("B,n", [(64, 7), (37, 10), (256, 4), (10000, 8)])
 def test_fused_mlp_equals_module_forward(B, n):
     """sn_puct_seat_rows + the per-seat GEMM + sn_puct_mlp (layer 1's card
     column + ReLU, layer 2 + ReLU and the head in one MFMA kernel) give every
@@ -540,7 +540,8 @@ def test_fused_mlp_equals_module_forward(B, n):
     logits computed in f32 from the same bf16 activations (to f32 summation
     order), and to the module's own bf16 forward on the full rows (to the
     bf16 tolerance of test_layer1_split_equals_full_rows).  Ragged row counts
-    (a short last 64-row tile) included."""
+    (a short last 64-row tile) included; B = 10 000 gives sn_puct_mlp_seats'
+    persistent workgroups several 64-seat groups each."""
     import ctypes
 
     from rl_6_nimmt import _native as nat
@@ -603,7 +604,7 @@ def test_fused_and_split_rollouts_agree_in_law():
     for fused in (True, False):
         env, eng = _engine(B=512, dtype=torch.bfloat16, mc_max=20, mc_per_card=10, seed=41)
         eng.fused_mlp = fused
-        eng.mlp_layer1 = "seats"  # the one-launch form (the GEMM form: the statistics test and the bench)
+        eng.mlp_layer1 = "gemm"  # the GEMM form (the one-launch form, the default: the statistics test and the bench)
         acts = eng.decide(10)
         torch.cuda.synchronize()
         res[fused] = (acts.clone(), eng.stats.clone(), eng.rows_evaluated)
