@@ -158,23 +158,11 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          1 (default) or 0 (never).  Measured (65 536 x 4p):
                          74 -> 59 us per 10 env-steps.  Numpy-compat handles
                          always use the pipelined one-wave k_play.
-     SN_OPT_PIPE_FLAGS   hand-off between the pipelined play launches (caller's
-                         stream) and the twist-ahead launches (side stream):
-                         0 (default; SECHS_PIPE_FLAGS=0/1/2 sets it at
-                         creation): HIP events both ways.  1: device flags --
-                         a play lane polls its game's generation word, the
-                         side stream's CP waits on a block count
-                         (hipStreamWaitValue64) -- no packet between play
-                         launches.  2: play lanes poll, the side stream waits
-                         on an event recorded after each play launch.  Set it
-                         before the pipeline starts (after creation, or after
-                         sn_pipe_sync); SN_EINVAL otherwise.
-                         Either way the handle records its ordering events on
-                         the stream of the last pipelined rollout when later
-                         work needs them: that stream must outlive the
-                         handle's next call (torch's streams always do). */
+   A pipelined (numpy-compat) handle records its ordering events on the
+   stream of the last pipelined rollout when later work needs them: that
+   stream must outlive the handle's next call (torch's streams always do). */
 enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3, SN_OPT_TIMING = 4, SN_OPT_PIPE_GPW = 5,
-       SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7, SN_OPT_PIPE_FLAGS = 8 };
+       SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7 };
 sn_status sn_set_option(sn_env* env, int option, int value);
 /* pipelined rollouts whose draws ran past the twisted words (must be 0; a
    nonzero count means those games' draws are wrong) [sync].  The count is

@@ -263,130 +263,25 @@ struct AheadArgs {
     int tout;  // ptend parity written
     int lead;  // words to keep twisted past the consumer (kPipeLead; smaller only to test the overrun path)
     uint32_t* perr_mirror;  // host-mapped copy of *perr, refreshed at launch start (off the play stream)
-    uint32_t gen;           // != 0: store it to pgen[g] once this game's ring bytes and twisted end are out
 };
 
-// One game's twist-ahead, all 64 lanes of a wave: the words [t0, t0 + n) of
-// the stream (n: up to `lead` past the consumer c, a multiple of 8), their
-// tempered low bytes into the ring.  Phase 1 (words 0 .. min(n, 224)) has
-// all inputs in memory: twist_load issues their loads (so that a wave can
-// keep several games' loads in flight), twist_finish mixes and stores them
-// and runs phase 2 (words 224 .. n, in order: word j reads j - 227).
-struct TwistJob {
-    int64_t g;
-    uint32_t Tp, t0, n, T0;
-    uint32_t A[4], Bv[4], Cv[4], IX[4];
-};
-
-__device__ __forceinline__ void twist_begin(const DevState& s, const AheadArgs& a, TwistJob& J, int64_t g, uint32_t Tp,
-                                            uint32_t t0, uint32_t c, uint32_t lane) {
-    J.g = g, J.Tp = Tp, J.t0 = t0;
-    // signed: a consumer past the twisted end means a play lane overran
-    // (counted there too); twist nothing rather than underflow the lead
-    const int32_t lead = (int32_t)(t0 - c);
-    if (lead < 0 && lane == 0u) atomicAdd(s.perr, 1u);
-    J.n = (lead >= 0 && lead < a.lead) ? (((uint32_t)(a.lead - lead)) & ~7u) : 0u;
-    J.T0 = (Tp == (uint32_t)kMtN) ? 0u : Tp;
-}
-
-__device__ __forceinline__ void twist_load(const DevState& s, TwistJob& J, uint32_t lane) {
+template <bool INIT>
+__global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
     constexpr uint32_t D = kMtN - kMtM;  // 227
     constexpr uint32_t P1 = 224;          // words twisted before any store (all inputs already in memory)
-    const uint32_t* st = s.mt + J.g * kMtN;
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-        const uint32_t j = 64u * b + lane;
-        J.IX[b] = 0xFFFFu;
-        if (j < J.n && j < P1) {
-            const uint32_t idx = (J.T0 + j) % (uint32_t)kMtN;
-            J.IX[b] = idx;
-            J.A[b] = st[idx];
-            J.Bv[b] = st[(idx + 1u == (uint32_t)kMtN) ? 0u : idx + 1u];
-            J.Cv[b] = st[(idx < D) ? idx + kMtM : idx - D];
-        }
-    }
-}
-
-// FL: the device-flag hand-off (sc1 ring / twisted-end stores, then pgen)
-template <bool FL>
-__device__ __forceinline__ void twist_finish(const DevState& s, const AheadArgs& a, const TwistJob& J, uint32_t lane) {
-    constexpr uint32_t D = kMtN - kMtM;
-    constexpr uint32_t P1 = 224;
-    const int64_t B = s.B, g = J.g;
-    uint32_t* st = s.mt + g * kMtN;
-    uint8_t* ring = (uint8_t*)s.pring;
-    const uint32_t n = J.n, t0 = J.t0, T0 = J.T0;
-    auto ring_dword = [&](uint32_t j, uint32_t v) {  // t0 is 8-aligned: lanes 4m..4m+3 share one dword
-        const uint32_t y = mt_temper(v) & 0xFFu;
-        const uint32_t d = y | (__shfl_down(y, 1) << 8) | (__shfl_down(y, 2) << 16) | (__shfl_down(y, 3) << 24);
-        const uint32_t ri = (t0 + j) & (uint32_t)(kPipeRing - 1);
-        // device-flag mode: sc1 (write-through), handed off to the next k_play on the
-        // other queue by the pgen flag; otherwise streaming stores
-        uint32_t* rp = (uint32_t*)(ring + ((int64_t)(ri >> 4) * B + g) * 16 + (ri & 12u));
-        if ((lane & 3u) == 0u && j < n) {
-            if constexpr (FL) st_sc1(rp, d);
-            else st_nt(rp, d, SECHS_NT_MORE);
-        }
-    };
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-        if (64u * b >= min(n, P1)) break;
-        const uint32_t j = 64u * b + lane;
-        uint32_t v = 0u;
-        if (J.IX[b] != 0xFFFFu) {
-            v = mt_mix(J.A[b], J.Bv[b], J.Cv[b]);
-            st_nt(&st[J.IX[b]], v, SECHS_NT_MORE);
-            if (J.IX[b] == 0u) s.mt0[g] = J.A[b];
-        }
-        ring_dword(j, v);
-    }
-    for (uint32_t j0 = P1; j0 < n; j0 += 64u) {
-        const uint32_t j = j0 + lane;
-        uint32_t v = 0u;
-        if (j < n) {
-            const uint32_t idx = (T0 + j) % (uint32_t)kMtN;
-            const uint32_t aa = st[idx];
-            v = mt_mix(aa, st[(idx + 1u == (uint32_t)kMtN) ? 0u : idx + 1u], st[(idx < D) ? idx + kMtM : idx - D]);
-            st[idx] = v;
-            if (idx == 0u) s.mt0[g] = aa;
-        }
-        ring_dword(j, v);
-    }
-    if (lane == 0u) {
-        uint32_t Tn = J.Tp;
-        if (n) {
-            Tn = T0 + n;
-            while (Tn > (uint32_t)kMtN) Tn -= kMtN;
-        }
-        s.ptp[g] = Tn;
-        if constexpr (FL) st_sc1(&s.ptend[(int64_t)a.tout * B + g], t0 + n);
-        else s.ptend[(int64_t)a.tout * B + g] = t0 + n;
-    }
-    if constexpr (FL) {  // every lane's ring / ptend stores drained, then the flag
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0u) st_sc1(&s.pgen[g], a.gen);
-    }
-}
-
-// publish the overrun count so far (every k_play before the running one) to
-// the host without a sync; sn_rollout reads it at entry
-__device__ __forceinline__ void publish_perr(const DevState& s, const AheadArgs& a) {
-    if (a.perr_mirror)
-        __hip_atomic_store(a.perr_mirror, __hip_atomic_load(s.perr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-template <bool INIT, bool FL>
-__global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
     const int64_t g = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     if (g >= s.B) return;  // whole waves
     const uint32_t lane = threadIdx.x & 63u;
     const int64_t B = s.B;
-    if (g == 0 && lane == 0u) publish_perr(s, a);
+    // publish the overrun count so far (every k_play before the running one)
+    // to the host without a sync; sn_rollout reads it at entry
+    if (g == 0 && lane == 0u && a.perr_mirror)
+        __hip_atomic_store(a.perr_mirror, __hip_atomic_load(s.perr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t* st = s.mt + g * kMtN;
+    uint8_t* ring = (uint8_t*)s.pring;
     uint32_t Tp, t0, c;
     if (INIT) {
-        const uint32_t* st = s.mt + g * kMtN;
-        uint8_t* ring = (uint8_t*)s.pring;
         const uint32_t code = s.mt_pos[g];
         Tp = code & 0x7FFu;
         const uint32_t rem = (code >> 16) & kMtCntMask;
@@ -404,43 +299,67 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
     } else {
         Tp = s.ptp[g];
         t0 = s.ptend[(int64_t)a.tin * B + g];
-        const uint32_t* pc = &s.pabsc[(int64_t)a.cin * B + g];
-        c = FL ? ld_sc1(pc) : *pc;  // the play launch before last (other queue)
+        c = s.pabsc[(int64_t)a.cin * B + g];
     }
-    TwistJob J;
-    twist_begin(s, a, J, g, Tp, t0, c, lane);
-    twist_load(s, J, lane);
-    twist_finish<FL>(s, a, J, lane);
-}
-
-// The twist waves of the in-launch pipeline (SN_OPT_PIPE_FLAGS = 3,
-// k_play_tw): a wave twists the next launch's words for the `ng` games of
-// the play wave beside it, kTwistBatch games' phase-1 loads in flight at a
-// time.  It leads the consumer position the play waves start from (pabsc
-// cin), from the twisted end they read up to (ptend tin), and writes the
-// other ptend parity -- the ring bytes it stores lie past every byte the
-// running play waves may read (lead + one launch < kPipeRing).
-constexpr int kTwistBatch = 4;
-__device__ __forceinline__ void twist_role(const DevState& s, const AheadArgs& a, int64_t g0, int ng, uint32_t lane) {
-    const int64_t B = s.B;
-    uint32_t Tp_l = 0u, t0_l = 0u, c_l = 0u;  // lane l: game g0 + l
-    if ((int)lane < ng) {
-        Tp_l = s.ptp[g0 + lane];
-        t0_l = s.ptend[(int64_t)a.tin * B + g0 + lane];
-        c_l = s.pabsc[(int64_t)a.cin * B + g0 + lane];
-    }
-    for (int j0 = 0; j0 < ng; j0 += kTwistBatch) {
-        TwistJob J[kTwistBatch];
+    // signed: a consumer past the twisted end means a play lane overran
+    // (counted there too); twist nothing rather than underflow the lead
+    const int32_t lead = (int32_t)(t0 - c);
+    if (lead < 0 && lane == 0u) atomicAdd(s.perr, 1u);
+    const uint32_t n = (lead >= 0 && lead < a.lead) ? (((uint32_t)(a.lead - lead)) & ~7u) : 0u;
+    const uint32_t T0 = (Tp == (uint32_t)kMtN) ? 0u : Tp;
+    auto ring_dword = [&](uint32_t j, uint32_t v) {  // t0 is 8-aligned: lanes 4m..4m+3 share one dword
+        const uint32_t y = mt_temper(v) & 0xFFu;
+        const uint32_t d = y | (__shfl_down(y, 1) << 8) | (__shfl_down(y, 2) << 16) | (__shfl_down(y, 3) << 24);
+        const uint32_t ri = (t0 + j) & (uint32_t)(kPipeRing - 1);
+        if ((lane & 3u) == 0u && j < n) st_nt((uint32_t*)(ring + ((int64_t)(ri >> 4) * B + g) * 16 + (ri & 12u)), d, SECHS_NT_MORE);
+    };
+    // phase 1: words 0 .. min(n, 224)
+    uint32_t A[4], Bv[4], Cv[4], IX[4];
 #pragma unroll
-        for (int q = 0; q < kTwistBatch; q++) {
-            const int j = min(j0 + q, ng - 1);  // a short last batch repeats its last game's loads (not its stores)
-            twist_begin(s, a, J[q], g0 + j, __builtin_amdgcn_readlane(Tp_l, j), __builtin_amdgcn_readlane(t0_l, j),
-                        __builtin_amdgcn_readlane(c_l, j), (j0 + q < ng) ? lane : 1u);
-            twist_load(s, J[q], lane);
+    for (int b = 0; b < 4; b++) {
+        const uint32_t j = 64u * b + lane;
+        IX[b] = 0xFFFFu;
+        if (j < n && j < P1) {
+            const uint32_t idx = (T0 + j) % (uint32_t)kMtN;
+            IX[b] = idx;
+            A[b] = st[idx];
+            Bv[b] = st[(idx + 1u == (uint32_t)kMtN) ? 0u : idx + 1u];
+            Cv[b] = st[(idx < D) ? idx + kMtM : idx - D];
         }
+    }
 #pragma unroll
-        for (int q = 0; q < kTwistBatch; q++)
-            if (j0 + q < ng) twist_finish<false>(s, a, J[q], lane);
+    for (int b = 0; b < 4; b++) {
+        if (64u * b >= min(n, P1)) break;
+        const uint32_t j = 64u * b + lane;
+        uint32_t v = 0u;
+        if (IX[b] != 0xFFFFu) {
+            v = mt_mix(A[b], Bv[b], Cv[b]);
+            st_nt(&st[IX[b]], v, SECHS_NT_MORE);
+            if (IX[b] == 0u) s.mt0[g] = A[b];
+        }
+        ring_dword(j, v);
+    }
+    // phase 2: words 224 .. n, in order (their inputs include words just twisted)
+    for (uint32_t j0 = P1; j0 < n; j0 += 64u) {
+        const uint32_t j = j0 + lane;
+        uint32_t v = 0u;
+        if (j < n) {
+            const uint32_t idx = (T0 + j) % (uint32_t)kMtN;
+            const uint32_t aa = st[idx];
+            v = mt_mix(aa, st[(idx + 1u == (uint32_t)kMtN) ? 0u : idx + 1u], st[(idx < D) ? idx + kMtM : idx - D]);
+            st[idx] = v;
+            if (idx == 0u) s.mt0[g] = aa;
+        }
+        ring_dword(j, v);
+    }
+    if (lane == 0u) {
+        uint32_t Tn = Tp;
+        if (n) {
+            Tn = T0 + n;
+            while (Tn > (uint32_t)kMtN) Tn -= kMtN;
+        }
+        s.ptp[g] = Tn;
+        s.ptend[(int64_t)a.tout * B + g] = t0 + n;
     }
 }
 
@@ -513,26 +432,7 @@ struct PlayArgs {
     int32_t* league_rec;     // league: [episodes][B][1 + N] per finished game: seats word, results
     int step0;               // league: env-steps of this rollout before this launch (episode index of a record)
     int n0;                  // k_play_split: every game's hand size at the launch's start (aligned handle)
-    uint32_t pgen_want;      // RNG_NUMPY_PIPE, device-flag mode: wait until pgen[g] reaches it (0: no wait)
-    unsigned long long* pdone;  // RNG_NUMPY_PIPE, device-flag mode: each block adds 1 when its stores are out
 };
-
-// device-flag pipeline: this lane's game waits for its twist-ahead words
-// (pgen[g] >= want, sc1 poll, wave-uniform exit).  Bounded: past ~1 s (the
-// wall clock runs at <= 100 MHz) the lane counts an overrun (perr, surfaced
-// as SN_ERNG) and goes on, so a lost hand-off can never hang the GPU.
-__device__ __noinline__ void pipe_wait(const DevState& s, int64_t g, uint32_t want) {
-    const uint64_t t0 = wall_clock64();
-    for (;;) {
-        const bool ok = (int32_t)(ld_sc1(&s.pgen[g]) - want) >= 0;
-        if (__all(ok)) return;
-        if (wall_clock64() - t0 > (1ull << 27)) {
-            if (!ok) atomicAdd(s.perr, 1u);
-            return;
-        }
-        __builtin_amdgcn_s_sleep(2);
-    }
-}
 
 // The env-step loop of one lane (game g).  R supplies the random words
 // (topup/force, sechs_device.h).  Each wave
@@ -767,21 +667,14 @@ __device__ __forceinline__ void play_body(const DevState& s, const PlayArgs& a, 
     load_results<N>(s, g, a.flags, sum_res, episodes);
     uint32_t lg = LG ? s.lgs[g] : 0u;
     ByteBuf buf;
-    if constexpr (MODE == RNG_NUMPY_PIPE || MODE == RNG_NUMPY_PIPE_FL) {
-        constexpr bool FL = MODE == RNG_NUMPY_PIPE_FL;
-        if constexpr (FL) {
-            pipe_wait(s, g, a.pgen_want);
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);  // no ring load above the poll
-        }
-        using Pipe = RingPipeT<FL>;
-        Pipe rng;
+    if constexpr (MODE == RNG_NUMPY_PIPE) {
+        RingPipe rng;
         rng.load(s, g, buf, wave_lds + a.wave_lds - GPW * a.ring_lds + lane * a.ring_lds, a.pipe_cin, a.pipe_t);
         pp.mark(PH_PROLOGUE);
-        StreamSrc<N, Pipe> src{rng, buf, wave_lds + lane * kDealStride};
-        play_steps<N, StreamSrc<N, Pipe>, GPW, LG>(s, a, g, lane, wave_lds, G, src, sum_res, episodes, pp, lg, 0, a.steps);
-        uint32_t* pc = &s.pabsc[(int64_t)a.pipe_cout * s.B + g];
-        if constexpr (FL) st_sc1(pc, rng.consumed(buf));  // read by k_mt_ahead on the other queue
-        else *pc = rng.consumed(buf);
+        StreamSrc<N, RingPipe> src{rng, buf, wave_lds + lane * kDealStride};
+        play_steps<N, StreamSrc<N, RingPipe>, GPW, LG>(s, a, g, lane, wave_lds, G, src, sum_res, episodes, pp, lg, 0,
+                                                       a.steps);
+        s.pabsc[(int64_t)a.pipe_cout * s.B + g] = rng.consumed(buf);  // read by k_mt_ahead on the other queue
     } else {
         typename RngOf<MODE, kPlayPrefetch>::T rng;
         if constexpr (MODE == RNG_NUMPY_RING || MODE == RNG_NUMPY_RING_HBM) {
@@ -807,34 +700,6 @@ template <int N, int MODE, int GPW = 64, bool LG = false>
 __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
     play_body<N, MODE, GPW, LG>(s, a, lds_dyn, (int)threadIdx.x);
-    if constexpr (MODE == RNG_NUMPY_PIPE_FL) {
-        if (a.pdone) {  // device-flag pipeline, mode 1: this block's pabsc stores are out -> count it (CP-polled)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (threadIdx.x == 0) __hip_atomic_fetch_add(a.pdone, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
-}
-
-// The in-launch pipeline (SN_OPT_PIPE_FLAGS = 3): waves 0..3 of a block play
-// as k_play<N, RNG_NUMPY_PIPE> (launch i), waves 4..7 twist launch i + 1's
-// words for the same games (twist_role) -- k_mt_ahead's work beside the game
-// loop on the same SIMDs (one play wave and one twist wave each), with no
-// second queue and no cross-queue packet between launches.
-template <int N, int GPW, bool LG = false>
-__global__ __launch_bounds__(2 * kBlock) void k_play_tw(DevState s, PlayArgs a, AheadArgs t) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
-    const int tid = (int)threadIdx.x;
-    if (tid < kBlock) {
-        play_body<N, RNG_NUMPY_PIPE, GPW, LG>(s, a, lds_dyn, tid);
-        return;
-    }
-    const int w = (tid - kBlock) >> 6;
-    const uint32_t lane = (uint32_t)tid & 63u;
-    const int64_t g0 = ((int64_t)blockIdx.x * (kBlock / 64) + w) * GPW;
-    if (g0 >= s.B) return;
-    if (blockIdx.x == 0 && w == 0 && lane == 0u) publish_perr(s, t);
-    twist_role(s, t, g0, (int)min<int64_t>(GPW, s.B - g0), lane);
 }
 
 // ---- one-game fast path (the scalar drop-in SechsNimmtEnv, B == 1) -------
@@ -1394,7 +1259,7 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
             size_t bytes;
         } pal[] = {{(void**)&s.pring, (size_t)kPipeRing * B}, {(void**)&s.pabsc, sizeof(uint32_t) * 2 * B},
                    {(void**)&s.ptend, sizeof(uint32_t) * 2 * B}, {(void**)&s.ptp, sizeof(uint32_t) * B},
-                   {(void**)&s.perr, sizeof(uint32_t)}, {(void**)&s.pgen, sizeof(uint32_t) * B}};
+                   {(void**)&s.perr, sizeof(uint32_t)}};
         for (auto& a : pal) {
             if (hipMalloc(a.p, a.bytes) != hipSuccess) {
                 sn_destroy(e);
@@ -1420,21 +1285,6 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
             return fail(SN_ENOMEM, "pinned overrun mirror allocation failed");
         }
         *e->perr_host = 0u;
-        // pipeline hand-off modes (SN_OPT_PIPE_FLAGS): the device-flag modes
-        // 1 and 2 need the ring within 32-bit buffer offsets, mode 1 also
-        // CP-side stream waits on memory.  Default: SECHS_PIPE_FLAGS (0..3),
-        // else 0 (events).
-        if ((uint64_t)kPipeRing * (uint64_t)B < (1ull << 32)) {
-            e->pflags_max = 2;
-            int can_wait = 0;
-            (void)hipDeviceGetAttribute(&can_wait, hipDeviceAttributeCanUseStreamWaitValue, device);
-            if (can_wait &&
-                hipExtMallocWithFlags((void**)&e->pdone, sizeof(unsigned long long), hipMallocSignalMemory) == hipSuccess)
-                (void)hipMemset(e->pdone, 0, sizeof(unsigned long long));
-        }
-        const char* pf = getenv("SECHS_PIPE_FLAGS");
-        const int want = (pf && pf[0] >= '0' && pf[0] <= '3') ? pf[0] - '0' : 0;
-        if (want == 3 || (want == 2 && e->pflags_max >= 2) || (want == 1 && e->pdone)) e->pflags = want;
     }
     if (rng_mode == SN_RNG_NUMPY_MT) {
         const sn_status r = sn_set_option(e, SN_OPT_RING_WORDS, N <= 4 ? 256 : 512);
@@ -1465,12 +1315,11 @@ sn_status sn_destroy(sn_env* e) {
     if (e->ev_main) (void)hipEventDestroy(e->ev_main);
     if (e->ev_play) (void)hipEventDestroy(e->ev_play);
     if (e->perr_host) (void)hipHostFree(e->perr_host);
-    if (e->pdone) (void)hipFree(e->pdone);
     if (e->hbuf) (void)hipHostFree(e->hbuf);
     if (e->side) (void)hipStreamDestroy(e->side);
     free_timing(e);
     void* ps[] = {s.hand, s.row_lo, s.row_hi, s.score, s.sum_res, s.episodes, s.mt_pos, s.ctr, s.mt, s.mt0, s.ring,
-                  s.pring, s.pabsc, s.ptend, s.ptp, s.perr, s.pgen, s.lgs, s.lmem};
+                  s.pring, s.pabsc, s.ptend, s.ptp, s.perr, s.lgs, s.lmem};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     delete e;
@@ -1519,15 +1368,6 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
         case SN_OPT_PLAY_SPLIT:
             if (value < 0 || value > 1) return fail(SN_EINVAL, "play split must be 0 or 1");
             e->play_split = value;
-            return SN_OK;
-        case SN_OPT_PIPE_FLAGS:
-            if (value < 0 || value > 3) return fail(SN_EINVAL, "pipe flags must be 0, 1, 2 or 3");
-            if (e->pvalid && value != e->pflags)  // the hand-off state (ev_main, pgen) belongs to the running mode
-                return fail(SN_EINVAL, "pipe flags change only between pipelines (after sn_pipe_sync or a reset)");
-            if ((value == 1 || value == 2) && (value > e->pflags_max || (value == 1 && !e->pdone)))
-                return fail(SN_EUNSUPPORTED, "no device-flag hand-off of this kind on this handle (numpy mode, "
-                                             "B * 1024 < 2^32, mode 1: hipStreamWaitValue64 support)");
-            e->pflags = value;
             return SN_OK;
         case SN_OPT_PIPE_LEAD:
             if (value < 64 || value > kPipeLead) return fail(SN_EINVAL, "pipe lead must be in 64..600");
@@ -1726,44 +1566,23 @@ static size_t pipe_lds(const DevState& s, const PlayArgs& a, int gpw, int* wave_
     return (size_t)wave * (kBlock / 64);
 }
 
-// one pipelined play launch (MODE: RNG_NUMPY_PIPE or, device-flag hand-off, RNG_NUMPY_PIPE_FL)
-extern "C++" template <int GPW>
-static sn_status pipe_play_tw(const DevState& s, const PlayArgs& c, const AheadArgs& t, unsigned nblk, size_t shmem,
-                              hipStream_t st) {
-    SN_DISPATCH_N(s.N, {
-        if (s.lg_K) {
-            if constexpr (NN >= 2 && NN <= kLeagueMaxPlayers) {
-                HIP_TRY(hipFuncSetAttribute((const void*)k_play_tw<NN, GPW, true>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
-                hipLaunchKernelGGL((k_play_tw<NN, GPW, true>), dim3(nblk), dim3(2 * kBlock), shmem, st, s, c, t);
-            }
-        } else {
-            HIP_TRY(hipFuncSetAttribute((const void*)k_play_tw<NN, GPW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)shmem));
-            hipLaunchKernelGGL((k_play_tw<NN, GPW>), dim3(nblk), dim3(2 * kBlock), shmem, st, s, c, t);
-        }
-    });
-    HIP_TRY(hipGetLastError());
-    return SN_OK;
-}
-
-extern "C++" template <int MODE>
+// one pipelined play launch
 static sn_status pipe_play(const DevState& s, const PlayArgs& c, int gpw, unsigned nblk, size_t shmem, hipStream_t st) {
     SN_DISPATCH_N(s.N, {
         if (gpw == 32) {
-            HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, MODE, 32>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)shmem));
-            hipLaunchKernelGGL((k_play<NN, MODE, 32>), dim3(nblk), dim3(kBlock), shmem, st, s, c);
+            HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_PIPE, 32>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
+            hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_PIPE, 32>), dim3(nblk), dim3(kBlock), shmem, st, s, c);
         } else if (s.lg_K) {
             if constexpr (NN >= 2 && NN <= kLeagueMaxPlayers) {
-                HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, MODE, 64, true>,
+                HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_PIPE, 64, true>,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
-                hipLaunchKernelGGL((k_play<NN, MODE, 64, true>), dim3(nblk), dim3(kBlock), shmem, st, s, c);
+                hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_PIPE, 64, true>), dim3(nblk), dim3(kBlock), shmem, st, s, c);
             }
         } else {
-            HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)shmem));
-            hipLaunchKernelGGL((k_play<NN, MODE>), dim3(nblk), dim3(kBlock), shmem, st, s, c);
+            HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_PIPE>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
+            hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_PIPE>), dim3(nblk), dim3(kBlock), shmem, st, s, c);
         }
     });
     HIP_TRY(hipGetLastError());
@@ -1773,14 +1592,9 @@ static sn_status pipe_play(const DevState& s, const PlayArgs& c, int gpw, unsign
 // The pipelined numpy-MT rollout: per launch of <= 10 env-steps, k_play (on
 // the caller's stream) draws from words k_mt_ahead twisted during the
 // previous launch, while the next k_mt_ahead runs on the side stream.
-// Hand-off (SN_OPT_PIPE_FLAGS): 0 (default) HIP events both ways -- a wait
-// and a record on the caller's stream between play launches (~10 us per
-// launch on gfx950: tools/queue_gap.hip); 1: no packet
-// between play launches -- each play lane polls its game's pgen word
-// (pipe_wait) and the side stream's CP waits on the pdone block count
-// (hipStreamWaitValue64) before each twist; 2: play lanes poll pgen, the
-// side stream waits on an event recorded after each play launch (one marker
-// packet between play launches, no wait packet).
+// Hand-off: HIP events both ways -- a wait and a record on the caller's
+// stream between play launches.  (Device-flag and in-launch hand-offs were
+// built and measured slower on gfx950)
 static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     DevState& s = e->s;
     int wave;
@@ -1790,23 +1604,12 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     a.ring_lds = kPipeSlot;
     a.vec_out = ((((uintptr_t)a.rewards) & 15) == 0) && ((((uintptr_t)a.actions_out) & 3) == 0);
     const dim3 pg((unsigned)((s.B + kBlock / 64 - 1) / (kBlock / 64)));
-    const bool tw = e->pflags == 3;                  // in-launch twist waves (k_play_tw): one queue
-    const bool fl = e->pflags == 1 || e->pflags == 2;  // play lanes poll pgen
-    const bool fc = e->pflags == 1 && e->pdone;      // the side's CP waits on the pdone count
-    auto next_gen = [&]() -> uint32_t {
-        if (++e->pgen_cur == 0u) e->pgen_cur = 1u;  // 0 = no wait
-        return e->pgen_cur;
-    };
     if (!e->pvalid) {  // start the pipeline from mt_pos: twist kPipeLead ahead, synchronously
         const int p = (int)(e->pcount & 1u);
-        const uint32_t gen = fl ? next_gen() : 0u;
-        const AheadArgs aa{1 - p, 0, p, e->pipe_lead, e->perr_host_dev, gen};
-        if (fl) hipLaunchKernelGGL((k_mt_ahead<true, true>), pg, dim3(kBlock), 0, st, s, aa);
-        else hipLaunchKernelGGL((k_mt_ahead<true, false>), pg, dim3(kBlock), 0, st, s, aa);
+        hipLaunchKernelGGL(k_mt_ahead<true>, pg, dim3(kBlock), 0, st, s,
+                           AheadArgs{1 - p, 0, p, e->pipe_lead, e->perr_host_dev});
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(e->ev_prep, st));
-        if (fl) HIP_TRY(hipStreamWaitEvent(e->side, e->ev_prep, 0));  // the side's twists continue this state
-        if (fl && !fc) HIP_TRY(hipEventRecord(e->ev_main, st));       // mode 2: the first twist's "previous play"
         e->pvalid = 1;
         e->pstream = st;
     }
@@ -1832,51 +1635,23 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         if (a.obs) c.obs = a.obs + (int64_t)t0 * B * N * a.obs_stride;
         const int p = (int)(e->pcount & 1u);
         c.pipe_cin = 1 - p, c.pipe_cout = p, c.pipe_t = p;
-        c.pgen_want = fl ? e->pgen_cur : 0u;  // the twist-ahead launched last holds this launch's words
-        c.pdone = fc ? e->pdone : nullptr;
+        HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));  // this launch's words are twisted
+        HIP_TRY(hipEventRecord(e->ev_main, st));         // the previous launch's consumption is final
         hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
-        if (tw) {  // play + the next launch's twist in one launch on the caller's stream
-            if (tv) HIP_TRY(hipEventRecord(tv[0], st));
-            const AheadArgs t{1 - p, p, 1 - p, e->pipe_lead, e->perr_host_dev, 0u};
-            const sn_status r = (gpw == 32) ? pipe_play_tw<32>(s, c, t, nblk, shmem, st)
-                                            : pipe_play_tw<64>(s, c, t, nblk, shmem, st);
-            if (r != SN_OK) return r;
-            if (tv) {
-                HIP_TRY(hipEventRecord(tv[1], st));
-                HIP_TRY(hipEventRecord(tv[2], st));  // no separate twist launch: an empty interval
-                HIP_TRY(hipEventRecord(tv[3], st));
-            }
-            e->pcount++;
-            continue;
-        }
-        if (!fl) {
-            HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));  // this launch's words are twisted
-            HIP_TRY(hipEventRecord(e->ev_main, st));         // the previous launch's consumption is final
-        }
         if (tv) HIP_TRY(hipEventRecord(tv[0], st));
         {
-            const sn_status r = fl ? pipe_play<RNG_NUMPY_PIPE_FL>(s, c, gpw, nblk, shmem, st)
-                                   : pipe_play<RNG_NUMPY_PIPE>(s, c, gpw, nblk, shmem, st);
+            const sn_status r = pipe_play(s, c, gpw, nblk, shmem, st);
             if (r != SN_OK) return r;
         }
         if (tv) HIP_TRY(hipEventRecord(tv[1], st));
         // the next launch's twist, beside this one: leads the consumer of the launch before
-        uint32_t gen = 0u;
-        if (fc) {  // every block of the play launches before this one has counted itself
-            HIP_TRY(hipStreamWaitValue64(e->side, e->pdone, (uint64_t)e->pdone_launched, hipStreamWaitValueGte, ~0ull));
-            e->pdone_launched += nblk;
-        } else {  // events / mode 2: ev_main marks the end of the play launch before this one
-            HIP_TRY(hipStreamWaitEvent(e->side, e->ev_main, 0));
-        }
-        if (fl) gen = next_gen();
+        HIP_TRY(hipStreamWaitEvent(e->side, e->ev_main, 0));
         if (tv) HIP_TRY(hipEventRecord(tv[2], e->side));
-        const AheadArgs aa{1 - p, p, 1 - p, e->pipe_lead, e->perr_host_dev, gen};
-        if (fl) hipLaunchKernelGGL((k_mt_ahead<false, true>), pg, dim3(kBlock), 0, e->side, s, aa);
-        else hipLaunchKernelGGL((k_mt_ahead<false, false>), pg, dim3(kBlock), 0, e->side, s, aa);
+        hipLaunchKernelGGL(k_mt_ahead<false>, pg, dim3(kBlock), 0, e->side, s,
+                           AheadArgs{1 - p, p, 1 - p, e->pipe_lead, e->perr_host_dev});
         HIP_TRY(hipGetLastError());
         if (tv) HIP_TRY(hipEventRecord(tv[3], e->side));
-        if (!fl) HIP_TRY(hipEventRecord(e->ev_prep, e->side));
-        if (fl && !fc) HIP_TRY(hipEventRecord(e->ev_main, st));  // mode 2: this play launch's end, for the next twist
+        HIP_TRY(hipEventRecord(e->ev_prep, e->side));
         e->pcount++;
     }
     return SN_OK;

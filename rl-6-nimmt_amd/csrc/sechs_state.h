@@ -48,12 +48,6 @@ struct DevState {
     uint32_t* ptend; // [2][B] end of the twisted words after a prep launch (by launch parity)
     uint32_t* ptp;   // [B] twist pointer (MtGen's pos field), owned by k_mt_ahead
     uint32_t* perr;  // [1] play lanes that ran past the twisted words (must stay 0)
-    // device-flag hand-off of the pipeline (SN_OPT_PIPE_FLAGS): k_mt_ahead
-    // stores its ring bytes and twisted end write-through (sc1), drains them
-    // and then stores the launch generation in pgen[g]; a k_play lane polls
-    // its game's word before reading them (sc1 loads) -- no cross-queue event
-    // between consecutive play launches
-    uint32_t* pgen;  // [B] generation of the twist-ahead whose words the ring holds
     // batched tournament (sn_league_config): per game the current game's
     // player count k and seat agents, k | agent(seat p) << (4 + 4p)
     uint32_t* lgs;   // [B]
@@ -231,25 +225,6 @@ struct RingGen {
     __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf); }  // cnt == 0: always succeeds
 };
 
-// ---------------------------------------------------------------- sc1 accesses
-// The pipeline's cross-queue hand-off (MI355X_MICROARCH.md, hand-off forms
-// with sc1 loads): the producer (k_mt_ahead, side stream) stores every
-// handed-off byte with sc1 (write-through) stores, waits for them
-// (vmcnt(0)) and only then stores its flag with sc1; the consumer (k_play)
-// polls the flag with sc1 loads and reads every handed-off byte with sc1
-// loads (they bypass L1; no L1 line of the CU can be stale).
-__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// 16 B at byte offset `off` of a wave-uniform base, buffer_load_dwordx4 ... sc1
-__device__ __forceinline__ u32x4 ld16_sc1(const void* base, uint32_t off) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0xFFFFFFFFu, 0x00020000);
-    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16 /* sc1 */));
-}
-
 // numpy-MT words for k_play from the pipelined ring: k_mt_ahead twisted the
 // stream up to `tend` (593..600 words past the consumer position of the
 // launch before) while the previous k_play ran.  The first kPipeWin of those
@@ -267,10 +242,6 @@ struct PipeSlow {
     uint32_t k;
 };
 
-// SC1: the device-flag hand-off (SN_OPT_PIPE_FLAGS) -- every handed-off byte
-// read with sc1 loads; the event hand-off reads them plainly (its own
-// instantiation: no runtime branch in the event path)
-template <bool SC1>
 static __device__ __noinline__ PipeSlow pipe_slow(const uint8_t* ring, int64_t B, int64_t g, uint32_t pos, uint32_t left,
                                                   uint32_t* err) {
     PipeSlow r;
@@ -278,11 +249,7 @@ static __device__ __noinline__ PipeSlow pipe_slow(const uint8_t* ring, int64_t B
     r.k = min(8u, left);
     for (uint32_t i = 0; i < r.k; i++) {
         const uint32_t ri = (pos + i) & (uint32_t)(kPipeRing - 1);
-        const int64_t at = ((int64_t)(ri >> 4) * B + g) * 16 + (ri & 15u);
-        uint32_t b;
-        if constexpr (SC1) b = (ld_sc1((const uint32_t*)(ring + (at & ~3ll))) >> (8u * (uint32_t)(at & 3))) & 0xFFu;
-        else b = ring[at];
-        r.bytes |= (uint64_t)b << (8u * i);
+        r.bytes |= (uint64_t)ring[((int64_t)(ri >> 4) * B + g) * 16 + (ri & 15u)] << (8u * i);
     }
     if (r.k == 0u) {
         atomicAdd(err, 1u);
@@ -291,9 +258,7 @@ static __device__ __noinline__ PipeSlow pipe_slow(const uint8_t* ring, int64_t B
     return r;
 }
 
-template <bool SC1>
-struct RingPipeT {
-    static constexpr bool kSc1 = SC1;
+struct RingPipe {
     const uint8_t* slot;  // LDS window: chunk-aligned copy starting at the consumer's chunk
     const uint8_t* ring;
     uint32_t* err;
@@ -305,8 +270,7 @@ struct RingPipeT {
         c0 = s.pabsc[(int64_t)cin * B + g];
         // signed: a consumer past the twisted end (an earlier overrun) must
         // not read as a huge window of stale ring bytes
-        const uint32_t* te = &s.ptend[(int64_t)tpar * B + g];
-        const int32_t av = (int32_t)((SC1 ? ld_sc1(te) : *te) - c0);
+        const int32_t av = (int32_t)(s.ptend[(int64_t)tpar * B + g] - c0);
         if (av < 0) atomicAdd(s.perr, 1u);
         avail = (av < 0) ? 0u : (uint32_t)av;
         win = min(avail, (uint32_t)kPipeWin);
@@ -318,10 +282,7 @@ struct RingPipeT {
         const uint32_t q0 = (c0 & (uint32_t)(kPipeRing - 1)) >> 4;
         const uint32_t nch = (off + win + 15u) >> 4;
         for (uint32_t i = 0; i < nch; i++) {
-            const int64_t ci = (int64_t)((q0 + i) & (uint32_t)(kPipeRing / 16 - 1)) * B + g;
-            u32x4 c;
-            if constexpr (SC1) c = ld16_sc1(s.pring, (uint32_t)(ci * 16));
-            else c = s.pring[ci];
+            const u32x4 c = s.pring[(int64_t)((q0 + i) & (uint32_t)(kPipeRing / 16 - 1)) * B + g];
             *(uint64_t*)(lds_slot + 16u * i) = (uint64_t)c.x | ((uint64_t)c.y << 32);
             *(uint64_t*)(lds_slot + 16u * i + 8u) = (uint64_t)c.z | ((uint64_t)c.w << 32);
         }
@@ -340,7 +301,7 @@ struct RingPipeT {
         }
         const uint32_t left = (avail > take) ? avail - take : 0u;
         if (left == 0u && !forced) return false;  // prefetch stops at the twisted end
-        const PipeSlow r = pipe_slow<SC1>(ring, B, g, c0 + take, left, err);
+        const PipeSlow r = pipe_slow(ring, B, g, c0 + take, left, err);
         buf.append(r.bytes, r.k);
         take += r.k;
         return true;
@@ -350,23 +311,20 @@ struct RingPipeT {
     }
     __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf, true); }
 };
-using RingPipe = RingPipeT<false>;
 
 // Phase (A) of deck_shuffle2 on the pipelined ring: the words are read
 // straight from the LDS window by stream position (no byte buffer: appending
 // and dropping a variable number of bytes is a long 64-bit shift chain), the
 // next pass's 8 bytes prefetched while this pass decodes.  Same words, same
 // targets as the generic form.
-template <bool SC1>
-__device__ __forceinline__ uint64_t pipe_peek8(const RingPipeT<SC1>& r, uint32_t t) {
+__device__ __forceinline__ uint64_t pipe_peek8(const RingPipe& r, uint32_t t) {
     const uint32_t p = r.off + t, a8 = p & ~7u, sh = 8u * (p & 7u);
     const uint64_t lo = *(const uint64_t*)(r.slot + a8);
     const uint64_t hi = *(const uint64_t*)(r.slot + a8 + 8u);
     return sh ? ((lo >> sh) | (hi << (64u - sh))) : lo;
 }
 
-template <bool SC1>
-__device__ __forceinline__ void shuffle_targets(RingPipeT<SC1>& rng, ByteBuf& buf, uint8_t* jslot, int C) {
+__device__ __forceinline__ void shuffle_targets(RingPipe& rng, ByteBuf& buf, uint8_t* jslot, int C) {
     uint32_t t = rng.take - buf.cnt;  // next unconsumed byte (buffered bytes are re-read from the window)
     buf.clear();
     uint32_t i = (uint32_t)C - 1u;
@@ -376,7 +334,7 @@ __device__ __forceinline__ void shuffle_targets(RingPipeT<SC1>& rng, ByteBuf& bu
         w = pipe_peek8(rng, t);
     } else {
         const uint32_t left = (rng.avail > t) ? rng.avail - t : 0u;
-        const PipeSlow r = pipe_slow<SC1>(rng.ring, rng.B, rng.g, rng.c0 + t, left, rng.err);
+        const PipeSlow r = pipe_slow(rng.ring, rng.B, rng.g, rng.c0 + t, left, rng.err);
         w = r.bytes, valid = r.k;
     }
     while (i >= 1u) {
@@ -403,7 +361,7 @@ __device__ __forceinline__ void shuffle_targets(RingPipeT<SC1>& rng, ByteBuf& bu
                 w = pipe_peek8(rng, t), valid = 8u;
             } else {
                 const uint32_t left = (rng.avail > t) ? rng.avail - t : 0u;
-                const PipeSlow r = pipe_slow<SC1>(rng.ring, rng.B, rng.g, rng.c0 + t, left, rng.err);
+                const PipeSlow r = pipe_slow(rng.ring, rng.B, rng.g, rng.c0 + t, left, rng.err);
                 w = r.bytes, valid = r.k;
             }
         }
@@ -877,15 +835,6 @@ struct sn_env {
     uint64_t pcount;    // play launches so far (parity selects the pabsc / ptend buffers)
     hipStream_t side;
     hipEvent_t ev_prep, ev_main, ev_play;  // ev_play: after the last pipelined k_play (caller's stream)
-    // SN_OPT_PIPE_FLAGS: consecutive play launches with no cross-queue packet
-    // between them; each k_play lane waits for its game's pgen word, each
-    // k_mt_ahead waits (CP-side, hipStreamWaitValue64) for the play launch
-    // before the running one to have counted all its blocks into pdone
-    int pflags;               // SN_OPT_PIPE_FLAGS
-    uint32_t pgen_cur;        // generation of the last twist-ahead launched
-    int pflags_max;           // highest SN_OPT_PIPE_FLAGS mode this handle supports (0: events only)
-    unsigned long long* pdone;  // signal memory: k_play blocks finished (monotonic)
-    unsigned long long pdone_launched;  // k_play blocks launched so far
     hipStream_t pstream;      // stream of the last pipelined k_play
     uint32_t* perr_host;                    // pinned, device-mapped mirror of s.perr (PlayArgs::perr_mirror)
     uint32_t* perr_host_dev;

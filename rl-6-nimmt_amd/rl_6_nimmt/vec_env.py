@@ -186,14 +186,12 @@ class VecSechsNimmtEnv:
 
     # ------------------------------------------------------------ numpy RNG bridge
     def set_option(self, ring_words=None, chunk_steps=None, pipeline=None, pipe_gpw=None, pipe_lead=None,
-                   play_split=None, pipe_flags=None):
+                   play_split=None):
         """rollout tuning (include/sechs.h SN_OPT_*; all numpy-compat only except play_split,
         the role-split kernel of philox handles); results never depend on it
         (except pipe_lead < 600, a test knob that makes overruns -- PipeOverrunError -- likely)"""
         if pipe_lead is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPE_LEAD, int(pipe_lead)), "sn_set_option")
-        if pipe_flags is not None:
-            nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPE_FLAGS, int(pipe_flags)), "sn_set_option")
         if pipe_gpw is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPE_GPW, int(pipe_gpw)), "sn_set_option")
         if play_split is not None:

@@ -534,21 +534,13 @@ def test_pipelined_overrun_is_an_error(N, lead):
         env.rollout(10)
 
 
-@pytest.mark.parametrize("flags", [0, 1, 2, 3])
 @pytest.mark.parametrize("plan", [(10, 10, 10, 10), (25, 1, 1, 7, 30), (3, 10, 10)])
-def test_pipe_flag_handoff_matches_oracle(flags, plan):
-    """SN_OPT_PIPE_FLAGS: the twist-ahead hands its ring to the next play
-    launch through per-game generation words (sc1 stores, drained, then the
-    flag; the play lanes poll it) and the side stream waits on the play
-    blocks' count, instead of HIP events both ways -- same words, same
-    draws: actions, rewards, obs and final MT states equal the oracle's for
-    launch plans with several launches per call and 1-step launches.  Mode 2:
-    the play lanes poll the same words, the side stream waits on an event
-    recorded after each play launch.  Mode 3: one launch per chunk, the twist
-    waves of the play kernel twist the next launch's words (no side stream)."""
+def test_pipelined_launch_plans_match_oracle(plan):
+    """several pipelined launches per call and 1-step launches: each launch's
+    twist-ahead hands its ring to the next play launch (events both ways) --
+    actions, rewards, obs and final MT states equal the oracle's"""
     B, N, seed = 300, 4, 31
     env = venv(B, N, seed=seed, rng="numpy")
-    env.set_option(pipe_flags=flags)
     env.reset()
     ref = O.VecOracle(B, N, rng_mode=O.RNG_NUMPY_MT, seed=seed)
     ref.reset()
@@ -567,15 +559,13 @@ def test_pipe_flag_handoff_matches_oracle(flags, plan):
     assert env.pipe_errors() == 0
 
 
-@pytest.mark.parametrize("flags", [0, 1, 2, 3])
-def test_pipe_flag_handoff_full_size_across_streams(flags):
-    """65 536 games, 12 back-to-back episodes of the device-flag pipeline
-    with the caller's stream switching between rollouts (the library orders a
-    new stream behind the last play launch): every episode equals the oracle
-    (checked on 16 sampled games' own oracle streams) and no lane overran or timed out"""
+def test_pipelined_full_size_across_streams():
+    """65 536 games, 12 back-to-back episodes of the pipeline with the
+    caller's stream switching between rollouts (the library orders a new
+    stream behind the last play launch): every episode equals the oracle
+    (checked on 16 sampled games' own oracle streams) and no lane overran"""
     B, N, seed = 65536, 4, 3
     env = venv(B, N, seed=seed, rng="numpy")
-    env.set_option(pipe_flags=flags)
     env.reset()
     idx = np.arange(0, B, 64)
     refs = [O.VecOracle(1, N, rng_mode=O.RNG_NUMPY_MT, seed=seed, game_offset=int(g)) for g in idx[:16]]

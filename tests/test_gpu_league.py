@@ -35,12 +35,8 @@ def _league(B, K, lo, hi, seed, game_offset=0, rng="numpy"):
     return t
 
 
-@pytest.mark.parametrize("pipe", ["0", "3"])
-def test_league_slots_replay_reference_tournaments(pipe, monkeypatch):
-    """(pipe "3": the in-launch pipeline, twist waves inside the league's play kernel)"""
+def test_league_slots_replay_reference_tournaments():
     from rl_6_nimmt.league import decode_seats
-
-    monkeypatch.setenv("SECHS_PIPE_FLAGS", pipe)
 
     groups = {}
     for r in load("tournament_games.json")["league"]:
