@@ -56,7 +56,7 @@ ALGO_BYTES_PER_STEP = (33 * N_PLAYERS + 57) + 47 * N_PLAYERS  # 377 B at N = 4
 # applied by tools/pmc_traffic.py.  PMC counters cannot be read inside a plain
 # run, so the committed summary of the current kernels is reported beside the
 # live timing.
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r03_pmc_traffic_{rng}.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r04_pmc_traffic_{rng}.json")
 
 
 def parse():
@@ -921,27 +921,27 @@ def main():
         },
         "episodes_checksum": {"episodes": int(eps.sum().item()) * world, "mean_score_per_seat": (tot / (eps.sum().item() * world)).tolist()},
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and want("cpu"):
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.rng)
-    if world == 1 and not args.no_mcs:
+    if world == 1 and not args.no_mcs and want("mcs"):
         result["extra_config3_mcs"] = bench_mcs(args.mcs_games, args.mcs_rollouts)
-    if world == 1 and not args.no_puct:
+    if world == 1 and not args.no_puct and want("puct"):
         result["extra_config4_puct"] = bench_puct(args.puct_games)
         result["extra_config4_customed"] = bench_customed(args.puct_games)
         result["extra_acer"] = bench_acer(args.puct_games // 2)
-    if world == 1 and not args.no_scalar:
+    if world == 1 and not args.no_scalar and want("scalar"):
         result["extra_config1_scalar"] = bench_scalar()
-    if not args.no_league:
+    if not args.no_league and want("league"):
         league = bench_league(world, rank, B, args.league_rounds)
         if rank == 0:
             result["extra_config5_tournament"] = league
-    if not args.no_mixed_league:
+    if not args.no_mixed_league and want("mixed"):
         mixed = bench_league_mixed(world, rank, args.mixed_slots, args.mixed_mc_max)
         if rank == 0:
             result["extra_config5_run_py_league"] = mixed
-    if world == 1 and not args.no_dropin:
+    if world == 1 and not args.no_dropin and want("dropin"):
         result["extra_dropin_search"] = bench_dropin()
-    if world == 1 and not args.no_philox and args.rng == "numpy":
+    if world == 1 and not args.no_philox and args.rng == "numpy" and want("philox"):
         # config 2 in the counter-based mode ("philox ... used for
         # throughput"): same games-per-launch, role-split k_play (SN_OPT_PLAY_SPLIT 1)
         env2 = VecSechsNimmtEnv(B, N_PLAYERS, seed=0, rng="philox")

@@ -1,13 +1,25 @@
 #!/usr/bin/env python3
 """Step timeline of the pipelined bench from a rocprofv3 --kernel-trace csv:
 per step, k_play and k_mt_ahead start/end relative to the previous k_play's
-end (shows the cross-stream hand-off gaps).  Usage: trace_gaps.py kernel_trace.csv"""
+end (shows the cross-stream hand-off gaps).  Usage: trace_gaps.py kernel_trace.csv | run_results.db | <dir>"""
 import csv
 import sys
 
-rows = [r for r in csv.DictReader(open(sys.argv[1]))]
-ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows
-      if "k_play" in r["Kernel_Name"] or "k_mt_ahead" in r["Kernel_Name"]]
+def load(path):
+    """(start, end, name) of every kernel: a kernel_trace.csv, or a rocpd
+    database (run_results.db, or the directory holding it)"""
+    if path.endswith(".csv"):
+        return [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in csv.DictReader(open(path))]
+    import os
+    import sqlite3
+
+    db = sqlite3.connect(path if path.endswith(".db") else os.path.join(path, "run_results.db"))
+    cols = [r[1] for r in db.execute("pragma table_info(kernels)")]
+    name = "kernel_name" if "kernel_name" in cols else [c for c in cols if "name" in c.lower()][0]
+    return [(int(a), int(b), n) for a, b, n in db.execute(f"select start, end, {name} from kernels")]
+
+
+ks = [k for k in load(sys.argv[1]) if "k_play" in k[2] or "k_mt_ahead" in k[2]]
 ks.sort()
 plays = [k for k in ks if "k_play" in k[2]]
 aheads = [k for k in ks if "k_mt_ahead<false>" in k[2]]
