@@ -300,12 +300,13 @@ def host_cpu_info():
 # instruction per 2 cycles each (MI355X_MICROARCH.md "Wave scheduling"), at
 # the 2.4 GHz peak engine clock
 VALU_PEAK_GINSTR = 256 * 4 * 2.4 / 2  # 1228.8 G wave-instructions/s
-SQ_EXTRAS = os.path.join(ROOT, "profiles", "r02_sq_extras.json")
+SQ_EXTRAS = os.path.join(ROOT, "profiles", "r04_sq_extras.json")
 
 
 def sq_extras(kernel):
     """SQ counters of the config-3/4 kernels, summed over one run of the legs
-    (tools/sq_extras.sh -> profiles/r02_sq_extras.json)"""
+    (tools/r04_prof2.sh -> profiles/r04_sq_extras.json; config 3 only: the PMC pass over the
+    graph-replayed config-4 leg crashes rocprofv3 on this image)"""
     if not os.path.exists(SQ_EXTRAS):
         return None
     for name, c in json.load(open(SQ_EXTRAS)).items():

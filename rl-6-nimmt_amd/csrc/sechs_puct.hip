@@ -524,20 +524,40 @@ __device__ __forceinline__ uint16_t bf16_bits(float v) { return __builtin_bit_ca
 // part + 4, part + 8, board row `part`, a quarter of the zero padding, and
 // one of the constant features (write_row's values, feature 0 = the card
 // slot left 0: the candidates' cards enter through w1c)
-__device__ __forceinline__ void seat_row_part(const PuctArgs& a, int N, int n_cur, int64_t i, int part, uint16_t* row,
-                                              float* cd) {
+// what lane `part` of seat i reads from the rollout state (global loads,
+// issued one group ahead by k_puct_mlp_seats)
+struct SeatIn {
+    uint32_t h0, h1, h2;  // the seat's hand words (ro_hand)
+    uint32_t lo, hi;      // board row `part` (ro_board)
+    int kp;               // players of the seat's game
+    bool live;            // a seated player (q < kp)
+};
+
+__device__ __forceinline__ SeatIn seat_load(const PuctArgs& a, int N, int64_t i, int part) {
     const int64_t d = i / N;
     const int q = (int)(i - d * N);
     const int32_t* ro = a.ro + d * kRoWords;
-    int kp = N;
+    SeatIn in;
+    in.kp = N;
     if (a.lgs) {
         int64_t g;
         int p;
         dec_to_gp(a, d, g, p);
-        kp = players_of(a, g);
+        in.kp = players_of(a, g);
     }
-    const bool live = q < kp;
-    const Hand h = ro_hand(ro, live ? q : 0);
+    in.live = q < in.kp;
+    const int qq = in.live ? q : 0;
+    in.h0 = (uint32_t)ro[8 + 3 * qq], in.h1 = (uint32_t)ro[9 + 3 * qq], in.h2 = (uint32_t)ro[10 + 3 * qq];
+    in.lo = (uint32_t)ro[part], in.hi = (uint32_t)ro[4 + part];
+    return in;
+}
+
+__device__ __forceinline__ void seat_row_part(const SeatIn& in, int n_cur, int part, uint16_t* row, float* cd) {
+    const bool live = in.live;
+    const int kp = in.kp;
+    Hand h;
+    h.lo = in.h0 | ((uint64_t)in.h1 << 32);
+    h.hi = in.h2;
 #pragma unroll
     for (int j = 0; j < 3; j++) {
         const int k = part + 4 * j;
@@ -547,7 +567,7 @@ __device__ __forceinline__ void seat_row_part(const PuctArgs& a, int N, int n_cu
             cd[k] = (live && k < n_cur) ? round_to<__hip_bfloat16>(nrm((float)c, 0.f, 103.f)) : 0.f;
         }
     }
-    const uint32_t lo = (uint32_t)ro[part], hi = (uint32_t)ro[4 + part];  // board row `part` (ro_board)
+    const uint32_t lo = in.lo, hi = in.hi;
     const uint32_t len = len_of(hi);
     row[12 + part] = live ? bf16_bits(nrm((float)len, 1.f, 5.f)) : (uint16_t)0;
     row[16 + part] = live ? bf16_bits(nrm((float)end_of(hi), 0.f, 103.f)) : (uint16_t)0;
@@ -590,15 +610,19 @@ __global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(PuctArgs a, int N, in
     }
     for (int i = tid; i < kMlpK; i += blockDim.x) sC[i] = w1c[i];
     load_head_pairs(head, sH2);
+    const int sl = tid >> 2, part = tid & 3;  // phase 1: four lanes per seat
+    auto group_load = [&](int64_t grp) {
+        const int64_t s0 = grp * kSeatBlock;
+        return seat_load(a, N, s0 + min<int64_t>(sl, S - s0 - 1), part);
+    };
+    SeatIn nxt = group_load(min<int64_t>(blockIdx.x, groups - 1));
     for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
     const int64_t s0 = grp * kSeatBlock;
     const int nseat = (int)min<int64_t>(kSeatBlock, S - s0);
+    const SeatIn cur = nxt;
     __syncthreads();  // the previous group's phase 3 is done with sBase / sCard
-    // phase 1: the seats' rows and card features, four lanes per seat
-    {
-        const int sl = tid >> 2;
-        seat_row_part(a, N, n_cur, s0 + min(sl, nseat - 1), tid & 3, sRow + sl * kSeatRowLds, sCard + sl * kHand);
-    }
+    // phase 1: the seats' rows and card features
+    seat_row_part(cur, n_cur, part, sRow + sl * kSeatRowLds, sCard + sl * kHand);
     __syncthreads();
     const int wave = tid >> 6, lane = tid & 63, col = lane & 31, half = lane >> 5;
     // phase 2: base[seat][j] = sum_k W1s[j][k] rows[seat][k]; wave w: outputs j in [32w, 32w + 32)
@@ -627,6 +651,8 @@ __global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(PuctArgs a, int N, in
             }
     }
     __syncthreads();
+    // the next group's rollout-state loads fly during phase 3
+    if (grp + gridDim.x < groups) nxt = group_load(grp + gridDim.x);
     // phase 3: k_puct_mlp's tile loop over the group's rows
     const uint32_t rows = (uint32_t)nseat * (uint32_t)n_cur;
     const uint32_t tiles = (rows + 63u) / 64u;
