@@ -502,182 +502,6 @@ __global__ __launch_bounds__(256, 2) void k_puct_mlp(uint32_t R, int n_cur, cons
     }
 }
 
-// ---- the whole rollout MLP in one kernel (sn_puct_mlp_seats) -------------
-// A workgroup loads W1s / W2 into LDS once and then loops over groups of 64
-// consecutive rollout seats (persistent grid: two workgroups per CU, the
-// occupancy the 64-row MFMA tiles' registers allow).  Per group: phase 1
-// builds the seats' [0, obs, 1] rows in LDS (the features of write_row /
-// sn_puct_seat_cols, four lanes per seat) and the candidates' card
-// features, phase 2 computes base = W1s . rows for the 64 seats with MFMA
-// (layer 1's obs part, K = 64) into LDS (bf16, as the PyTorch GEMM rounds
-// it), phase 3 runs k_puct_mlp's tile loop over the group's rows reading
-// base and the cards from LDS.  Replaces sn_puct_seat_rows + the per-seat
-// GEMM + sn_puct_mlp (two launches and the [S][56] / [S][112] HBM round trips).
-constexpr int kSeatBlock = 64;
-constexpr int kSeatRowK = 64;               // seat-row features (48 + the ones feature, zero-padded)
-constexpr int kSeatRowLds = kSeatRowK + 8;  // LDS stride (144 B)
-constexpr int kBaseLds = kMlpK + 8;         // 120 bf16 (240 B) per seat of base in LDS
-
-__device__ __forceinline__ uint16_t bf16_bits(float v) { return __builtin_bit_cast(uint16_t, __float2bfloat16(v)); }
-
-// phase 1, lane `part` (0..3) of seat `sl`: hand features / cards k = part,
-// part + 4, part + 8, board row `part`, a quarter of the zero padding, and
-// one of the constant features (write_row's values, feature 0 = the card
-// slot left 0: the candidates' cards enter through w1c)
-// what lane `part` of seat i reads from the rollout state (global loads,
-// issued one group ahead by k_puct_mlp_seats)
-struct SeatIn {
-    uint32_t h0, h1, h2;  // the seat's hand words (ro_hand)
-    uint32_t lo, hi;      // board row `part` (ro_board)
-    int kp;               // players of the seat's game
-    bool live;            // a seated player (q < kp)
-};
-
-__device__ __forceinline__ SeatIn seat_load(const PuctArgs& a, int N, int64_t i, int part) {
-    const int64_t d = i / N;
-    const int q = (int)(i - d * N);
-    const int32_t* ro = a.ro + d * kRoWords;
-    SeatIn in;
-    in.kp = N;
-    if (a.lgs) {
-        int64_t g;
-        int p;
-        dec_to_gp(a, d, g, p);
-        in.kp = players_of(a, g);
-    }
-    in.live = q < in.kp;
-    const int qq = in.live ? q : 0;
-    in.h0 = (uint32_t)ro[8 + 3 * qq], in.h1 = (uint32_t)ro[9 + 3 * qq], in.h2 = (uint32_t)ro[10 + 3 * qq];
-    in.lo = (uint32_t)ro[part], in.hi = (uint32_t)ro[4 + part];
-    return in;
-}
-
-__device__ __forceinline__ void seat_row_part(const SeatIn& in, int n_cur, int part, uint16_t* row, float* cd) {
-    const bool live = in.live;
-    const int kp = in.kp;
-    Hand h;
-    h.lo = in.h0 | ((uint64_t)in.h1 << 32);
-    h.hi = in.h2;
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-        const int k = part + 4 * j;
-        if (k < kHand) {
-            const uint32_t c = hand_get(h, (uint32_t)k);
-            row[1 + k] = live ? bf16_bits(nrm(c == 0xFFu ? -1.f : (float)c, 0.f, 103.f)) : (uint16_t)0;
-            cd[k] = (live && k < n_cur) ? round_to<__hip_bfloat16>(nrm((float)c, 0.f, 103.f)) : 0.f;
-        }
-    }
-    const uint32_t lo = in.lo, hi = in.hi;
-    const uint32_t len = len_of(hi);
-    row[12 + part] = live ? bf16_bits(nrm((float)len, 1.f, 5.f)) : (uint16_t)0;
-    row[16 + part] = live ? bf16_bits(nrm((float)end_of(hi), 0.f, 103.f)) : (uint16_t)0;
-    row[20 + part] = live ? bf16_bits(nrm((float)heads_in(hi), 1.f, 10.f)) : (uint16_t)0;
-#pragma unroll
-    for (int c = 0; c < kThreshold; c++) {
-        const float v = (c < 5 && (uint32_t)c < len) ? (float)card_at(lo, hi, c < 5 ? c : 0) : -1.f;
-        row[24 + part * kThreshold + c] = live ? bf16_bits(nrm(v, 0.f, 103.f)) : (uint16_t)0;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int f = kRowLen + 1 + part + 4 * j;
-        if (f < kSeatRowK) row[f] = 0;
-    }
-    if (part == 0) row[0] = 0;
-    if (part == 1) row[11] = live ? bf16_bits(nrm((float)kp, 0.f, 6.f)) : (uint16_t)0;
-    if (part == 2) row[kRowLen] = bf16_bits(1.f);
-}
-
-__global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(PuctArgs a, int N, int n_cur, const uint16_t* w1s,
-                                                          const float* w1c, const uint16_t* w2, const float* head,
-                                                          float* logits) {
-    __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kMlpLdsK];          // W2 [128][120]
-    __shared__ __attribute__((aligned(16))) uint16_t sW1[kMlpM * kSeatRowLds];      // W1s [128][72]
-    __shared__ __attribute__((aligned(16))) uint16_t sRow[kSeatBlock * kSeatRowLds];  // seat rows [64][72]
-    __shared__ __attribute__((aligned(16))) uint16_t sBase[kSeatBlock * kBaseLds];    // base [64][120]
-    __shared__ __attribute__((aligned(16))) float sCard[kSeatBlock * kHand];
-    __shared__ __attribute__((aligned(16))) float sC[kMlpK];
-    __shared__ __attribute__((aligned(16))) uint32_t sH2[kMlpM / 2];
-    const int tid = threadIdx.x;
-    const int64_t S = a.D * N;
-    const int64_t groups = (S + kSeatBlock - 1) / kSeatBlock;
-    for (int i = tid; i < kMlpM * (kMlpK / 8); i += blockDim.x) {
-        const int o = i / (kMlpK / 8), c = i - o * (kMlpK / 8);
-        *(uint4*)&sW[o * kMlpLdsK + 8 * c] = *(const uint4*)&w2[o * kMlpK + 8 * c];
-    }
-    for (int i = tid; i < kMlpM * (kSeatRowK / 8); i += blockDim.x) {
-        const int o = i / (kSeatRowK / 8), c = i - o * (kSeatRowK / 8);
-        *(uint4*)&sW1[o * kSeatRowLds + 8 * c] = *(const uint4*)&w1s[o * kSeatRowK + 8 * c];
-    }
-    for (int i = tid; i < kMlpK; i += blockDim.x) sC[i] = w1c[i];
-    load_head_pairs(head, sH2);
-    const int sl = tid >> 2, part = tid & 3;  // phase 1: four lanes per seat
-    auto group_load = [&](int64_t grp) {
-        const int64_t s0 = grp * kSeatBlock;
-        return seat_load(a, N, s0 + min<int64_t>(sl, S - s0 - 1), part);
-    };
-    SeatIn nxt = group_load(min<int64_t>(blockIdx.x, groups - 1));
-    for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
-    const int64_t s0 = grp * kSeatBlock;
-    const int nseat = (int)min<int64_t>(kSeatBlock, S - s0);
-    const SeatIn cur = nxt;
-    __syncthreads();  // the previous group's phase 3 is done with sBase / sCard
-    // phase 1: the seats' rows and card features
-    seat_row_part(cur, n_cur, part, sRow + sl * kSeatRowLds, sCard + sl * kHand);
-    __syncthreads();
-    const int wave = tid >> 6, lane = tid & 63, col = lane & 31, half = lane >> 5;
-    // phase 2: base[seat][j] = sum_k W1s[j][k] rows[seat][k]; wave w: outputs j in [32w, 32w + 32)
-    {
-        f32x16_t acc[2];
-#pragma unroll
-        for (int nt = 0; nt < 2; nt++)
-#pragma unroll
-            for (int i = 0; i < 16; i++) acc[nt][i] = 0.f;
-#pragma unroll
-        for (int ks = 0; ks < kSeatRowK / 16; ks++) {
-            const int k0 = 16 * ks + 8 * half;
-            const bf16x8_t af = __builtin_bit_cast(bf16x8_t, *(const uint4*)&sW1[(32 * wave + col) * kSeatRowLds + k0]);
-#pragma unroll
-            for (int nt = 0; nt < 2; nt++) {
-                const bf16x8_t bfr = __builtin_bit_cast(bf16x8_t, *(const uint4*)&sRow[(32 * nt + col) * kSeatRowLds + k0]);
-                acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[nt], 0, 0, 0);
-            }
-        }
-#pragma unroll
-        for (int nt = 0; nt < 2; nt++)
-#pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const int j = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * half;
-                if (j < kMlpK) sBase[(32 * nt + col) * kBaseLds + j] = (uint16_t)pack_bf16(acc[nt][r], 0.f);
-            }
-    }
-    __syncthreads();
-    // the next group's rollout-state loads fly during phase 3
-    if (grp + gridDim.x < groups) nxt = group_load(grp + gridDim.x);
-    // phase 3: k_puct_mlp's tile loop over the group's rows
-    const uint32_t rows = (uint32_t)nseat * (uint32_t)n_cur;
-    const uint32_t tiles = (rows + 63u) / 64u;
-    const uint32_t rbase = (uint32_t)s0 * (uint32_t)n_cur;
-    for (uint32_t tile = wave; tile < tiles; tile += blockDim.x >> 6) {
-        uint32_t rr[2];
-        float x[2];
-        const uint16_t* brow[2];
-#pragma unroll
-        for (int nt = 0; nt < 2; nt++) {
-            rr[nt] = tile * 64u + 32u * nt + (uint32_t)col;  // group-local row
-            const uint32_t rc = rr[nt] < rows ? rr[nt] : rows - 1u;
-            const uint32_t sl = rc / (uint32_t)n_cur;
-            x[nt] = sCard[sl * kHand + (rc - sl * (uint32_t)n_cur)];
-            brow[nt] = sBase + sl * kBaseLds;
-        }
-        float out[2];
-        mlp_tile(brow[0], brow[1], x[0], x[1], sW, sC, sH2, col, half, out);
-#pragma unroll
-        for (int nt = 0; nt < 2; nt++)
-            if (half == 0 && rr[nt] < rows) logits[rbase + rr[nt]] = out[nt];
-    }
-    }
-}
-
 // np.median of all outcomes so far, from the histogram (kth smallest)
 __device__ double hist_median(const int32_t* hist, int32_t total) {
     const int32_t k0 = (total - 1) / 2, k1 = total / 2;
@@ -849,9 +673,11 @@ __global__ void k_puct_step(DevState s, PuctArgs a, const void* logits, int ls, 
 // (lane shuffles), resolves, and writes the board / outcome / backup.  L
 // times the lanes of k_puct_step (D = 8192 x 4 decisions: 2 waves per SIMD
 // instead of half a wave), the per-decision latency chain split over them.
-template <int N, int L, bool LB>
-__global__ void k_puct_step_seats(DevState s, PuctArgs a, const void* logits, int ls, int t, int n_cur) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// lane i of the step (seat i & (L - 1) of decision i / L); logit(dd, q, k):
+// candidate k's logit of seat q of decision dd
+template <int N, int L, class Logit>
+__device__ __forceinline__ void step_seat(const DevState& s, const PuctArgs& a, Logit logit, int t, int n_cur,
+                                          int64_t i) {
     const int64_t d = i / L;
     const int q = (int)(i & (L - 1));
     const bool live = d < a.D;
@@ -867,7 +693,7 @@ __global__ void k_puct_step_seats(DevState s, PuctArgs a, const void* logits, in
     if (seat) {
         float lg[kHand];
 #pragma unroll
-        for (int k = 0; k < kHand; k++) lg[k] = (k < n_cur) ? logit_at<LB>(logits, (dd * N + q) * n_cur + k, ls) : 0.f;
+        for (int k = 0; k < kHand; k++) lg[k] = (k < n_cur) ? logit(dd, q, k) : 0.f;
         Hand h = ro_hand(ro, q);
         if (t == 0 && q == 0 && (a.flags & 1)) {
             idx = puct_choose(a.stats + dd * kStatWords, a.hist + dd * kHistBins, a.root_probs + dd * kHand, n_cur,
@@ -911,6 +737,210 @@ __global__ void k_puct_step_seats(DevState s, PuctArgs a, const void* logits, in
         ro[4] = b.hi.x, ro[5] = b.hi.y, ro[6] = b.hi.z, ro[7] = b.hi.w;
         ro[40] = outcome;
         ro[41] = first;
+    }
+}
+
+template <int N, int L, bool LB>
+__global__ void k_puct_step_seats(DevState s, PuctArgs a, const void* logits, int ls, int t, int n_cur) {
+    step_seat<N, L>(
+        s, a, [&](int64_t dd, int q, int k) { return logit_at<LB>(logits, (dd * N + q) * n_cur + k, ls); }, t, n_cur,
+        (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// ---- the whole rollout MLP in one kernel (sn_puct_mlp_seats) -------------
+// A workgroup loads W1s / W2 into LDS once and then loops over groups of 64
+// consecutive rollout seats (persistent grid: two workgroups per CU, the
+// occupancy the 64-row MFMA tiles' registers allow).  Per group: phase 1
+// builds the seats' [0, obs, 1] rows in LDS (the features of write_row /
+// sn_puct_seat_cols, four lanes per seat) and the candidates' card
+// features, phase 2 computes base = W1s . rows for the 64 seats with MFMA
+// (layer 1's obs part, K = 64) into LDS (bf16, as the PyTorch GEMM rounds
+// it), phase 3 runs k_puct_mlp's tile loop over the group's rows reading
+// base and the cards from LDS.  Replaces sn_puct_seat_rows + the per-seat
+// GEMM + sn_puct_mlp (two launches and the [S][56] / [S][112] HBM round trips).
+constexpr int kSeatBlock = 64;
+constexpr int kSeatRowK = 64;               // seat-row features (48 + the ones feature, zero-padded)
+constexpr int kSeatRowLds = kSeatRowK + 8;  // LDS stride (144 B)
+constexpr int kBaseLds = kMlpK + 8;         // 120 bf16 (240 B) per seat of base in LDS
+
+__device__ __forceinline__ uint16_t bf16_bits(float v) { return __builtin_bit_cast(uint16_t, __float2bfloat16(v)); }
+
+// phase 1, lane `part` (0..3) of seat `sl`: hand features / cards k = part,
+// part + 4, part + 8, board row `part`, a quarter of the zero padding, and
+// one of the constant features (write_row's values, feature 0 = the card
+// slot left 0: the candidates' cards enter through w1c)
+// what lane `part` of seat i reads from the rollout state (global loads,
+// issued one group ahead by k_puct_mlp_seats)
+struct SeatIn {
+    uint32_t h0, h1, h2;  // the seat's hand words (ro_hand)
+    uint32_t lo, hi;      // board row `part` (ro_board)
+    int kp;               // players of the seat's game
+    bool live;            // a seated player (q < kp)
+};
+
+__device__ __forceinline__ SeatIn seat_load(const PuctArgs& a, int N, int64_t i, int part) {
+    const int64_t d = i / N;
+    const int q = (int)(i - d * N);
+    const int32_t* ro = a.ro + d * kRoWords;
+    SeatIn in;
+    in.kp = N;
+    if (a.lgs) {
+        int64_t g;
+        int p;
+        dec_to_gp(a, d, g, p);
+        in.kp = players_of(a, g);
+    }
+    in.live = q < in.kp;
+    const int qq = in.live ? q : 0;
+    in.h0 = (uint32_t)ro[8 + 3 * qq], in.h1 = (uint32_t)ro[9 + 3 * qq], in.h2 = (uint32_t)ro[10 + 3 * qq];
+    in.lo = (uint32_t)ro[part], in.hi = (uint32_t)ro[4 + part];
+    return in;
+}
+
+__device__ __forceinline__ void seat_row_part(const SeatIn& in, int n_cur, int part, uint16_t* row, float* cd) {
+    const bool live = in.live;
+    const int kp = in.kp;
+    Hand h;
+    h.lo = in.h0 | ((uint64_t)in.h1 << 32);
+    h.hi = in.h2;
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const int k = part + 4 * j;
+        if (k < kHand) {
+            const uint32_t c = hand_get(h, (uint32_t)k);
+            row[1 + k] = live ? bf16_bits(nrm(c == 0xFFu ? -1.f : (float)c, 0.f, 103.f)) : (uint16_t)0;
+            cd[k] = (live && k < n_cur) ? round_to<__hip_bfloat16>(nrm((float)c, 0.f, 103.f)) : 0.f;
+        }
+    }
+    const uint32_t lo = in.lo, hi = in.hi;
+    const uint32_t len = len_of(hi);
+    row[12 + part] = live ? bf16_bits(nrm((float)len, 1.f, 5.f)) : (uint16_t)0;
+    row[16 + part] = live ? bf16_bits(nrm((float)end_of(hi), 0.f, 103.f)) : (uint16_t)0;
+    row[20 + part] = live ? bf16_bits(nrm((float)heads_in(hi), 1.f, 10.f)) : (uint16_t)0;
+#pragma unroll
+    for (int c = 0; c < kThreshold; c++) {
+        const float v = (c < 5 && (uint32_t)c < len) ? (float)card_at(lo, hi, c < 5 ? c : 0) : -1.f;
+        row[24 + part * kThreshold + c] = live ? bf16_bits(nrm(v, 0.f, 103.f)) : (uint16_t)0;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int f = kRowLen + 1 + part + 4 * j;
+        if (f < kSeatRowK) row[f] = 0;
+    }
+    if (part == 0) row[0] = 0;
+    if (part == 1) row[11] = live ? bf16_bits(nrm((float)kp, 0.f, 6.f)) : (uint16_t)0;
+    if (part == 2) row[kRowLen] = bf16_bits(1.f);
+}
+
+// NS > 0 (sn_puct_mlp_step, N = NS, a power of two <= 8): phase 4 runs the
+// rollout step of the group's decisions (step_seat, one lane per seat in
+// wave 0) from the logits the group just produced, kept in LDS -- the step
+// kernel's launch, its logit reads and its latency chain move beside the
+// other workgroup's MFMA work.  Groups of 64 seats hold whole decisions.
+template <int NS>
+__global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(DevState s, PuctArgs a, int N, int n_cur, int t,
+                                                          const uint16_t* w1s, const float* w1c, const uint16_t* w2,
+                                                          const float* head, float* logits) {
+    __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kMlpLdsK];          // W2 [128][120]
+    __shared__ __attribute__((aligned(16))) uint16_t sW1[kMlpM * kSeatRowLds];      // W1s [128][72]
+    __shared__ __attribute__((aligned(16))) uint16_t sRow[kSeatBlock * kSeatRowLds];  // seat rows [64][72]
+    __shared__ __attribute__((aligned(16))) uint16_t sBase[kSeatBlock * kBaseLds];    // base [64][120]
+    __shared__ __attribute__((aligned(16))) float sCard[kSeatBlock * kHand];
+    __shared__ __attribute__((aligned(16))) float sC[kMlpK];
+    __shared__ __attribute__((aligned(16))) uint32_t sH2[kMlpM / 2];
+    __shared__ float sLog[NS ? kSeatBlock * kHand : 1];  // phase 4: the group's logits
+    const int tid = threadIdx.x;
+    const int64_t S = a.D * N;
+    const int64_t groups = (S + kSeatBlock - 1) / kSeatBlock;
+    for (int i = tid; i < kMlpM * (kMlpK / 8); i += blockDim.x) {
+        const int o = i / (kMlpK / 8), c = i - o * (kMlpK / 8);
+        *(uint4*)&sW[o * kMlpLdsK + 8 * c] = *(const uint4*)&w2[o * kMlpK + 8 * c];
+    }
+    for (int i = tid; i < kMlpM * (kSeatRowK / 8); i += blockDim.x) {
+        const int o = i / (kSeatRowK / 8), c = i - o * (kSeatRowK / 8);
+        *(uint4*)&sW1[o * kSeatRowLds + 8 * c] = *(const uint4*)&w1s[o * kSeatRowK + 8 * c];
+    }
+    for (int i = tid; i < kMlpK; i += blockDim.x) sC[i] = w1c[i];
+    load_head_pairs(head, sH2);
+    const int sl = tid >> 2, part = tid & 3;  // phase 1: four lanes per seat
+    auto group_load = [&](int64_t grp) {
+        const int64_t s0 = grp * kSeatBlock;
+        return seat_load(a, N, s0 + min<int64_t>(sl, S - s0 - 1), part);
+    };
+    SeatIn nxt = group_load(min<int64_t>(blockIdx.x, groups - 1));
+    for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+    const int64_t s0 = grp * kSeatBlock;
+    const int nseat = (int)min<int64_t>(kSeatBlock, S - s0);
+    const SeatIn cur = nxt;
+    __syncthreads();  // the previous group's phase 3 is done with sBase / sCard
+    // phase 1: the seats' rows and card features
+    seat_row_part(cur, n_cur, part, sRow + sl * kSeatRowLds, sCard + sl * kHand);
+    __syncthreads();
+    const int wave = tid >> 6, lane = tid & 63, col = lane & 31, half = lane >> 5;
+    // phase 2: base[seat][j] = sum_k W1s[j][k] rows[seat][k]; wave w: outputs j in [32w, 32w + 32)
+    {
+        f32x16_t acc[2];
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+            for (int i = 0; i < 16; i++) acc[nt][i] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < kSeatRowK / 16; ks++) {
+            const int k0 = 16 * ks + 8 * half;
+            const bf16x8_t af = __builtin_bit_cast(bf16x8_t, *(const uint4*)&sW1[(32 * wave + col) * kSeatRowLds + k0]);
+#pragma unroll
+            for (int nt = 0; nt < 2; nt++) {
+                const bf16x8_t bfr = __builtin_bit_cast(bf16x8_t, *(const uint4*)&sRow[(32 * nt + col) * kSeatRowLds + k0]);
+                acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[nt], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int j = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * half;
+                if (j < kMlpK) sBase[(32 * nt + col) * kBaseLds + j] = (uint16_t)pack_bf16(acc[nt][r], 0.f);
+            }
+    }
+    __syncthreads();
+    // the next group's rollout-state loads fly during phase 3
+    if (grp + gridDim.x < groups) nxt = group_load(grp + gridDim.x);
+    // phase 3: k_puct_mlp's tile loop over the group's rows
+    const uint32_t rows = (uint32_t)nseat * (uint32_t)n_cur;
+    const uint32_t tiles = (rows + 63u) / 64u;
+    const uint32_t rbase = (uint32_t)s0 * (uint32_t)n_cur;
+    for (uint32_t tile = wave; tile < tiles; tile += blockDim.x >> 6) {
+        uint32_t rr[2];
+        float x[2];
+        const uint16_t* brow[2];
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++) {
+            rr[nt] = tile * 64u + 32u * nt + (uint32_t)col;  // group-local row
+            const uint32_t rc = rr[nt] < rows ? rr[nt] : rows - 1u;
+            const uint32_t sl = rc / (uint32_t)n_cur;
+            x[nt] = sCard[sl * kHand + (rc - sl * (uint32_t)n_cur)];
+            brow[nt] = sBase + sl * kBaseLds;
+        }
+        float out[2];
+        mlp_tile(brow[0], brow[1], x[0], x[1], sW, sC, sH2, col, half, out);
+#pragma unroll
+        for (int nt = 0; nt < 2; nt++)
+            if (half == 0 && rr[nt] < rows) {
+                if constexpr (NS > 0) sLog[rr[nt]] = out[nt];
+                if (logits) logits[rbase + rr[nt]] = out[nt];
+            }
+    }
+    if constexpr (NS > 0) {  // phase 4: the group's decisions take their rollout step
+        __syncthreads();
+        if (wave == 0)
+            step_seat<NS, NS>(
+                s, a,
+                [&](int64_t dd, int q, int k) {
+                    const int64_t li = min<int64_t>(max<int64_t>(dd * NS + q - s0, 0), kSeatBlock - 1);
+                    return sLog[li * n_cur + k];
+                },
+                t, n_cur, s0 + lane);
+    }
     }
 }
 
@@ -1177,16 +1207,21 @@ sn_status sn_puct_seat_rows(sn_env* e, const sn_puct* q, int n_cur, void* rows, 
     return SN_OK;
 }
 
-sn_status sn_puct_mlp_seats(sn_env* e, const sn_puct* q, int n_cur, const void* w1s, const float* w1c, const void* w2,
-                            const float* head, float* logits, void* stream) {
+// the one-kernel rollout MLP (NS = 0) or MLP + step (NS = N)
+static sn_status launch_mlp_seats(sn_env* e, const sn_puct* q, int t, int n_cur, const void* w1s, const float* w1c,
+                                  const void* w2, const float* head, float* logits, void* stream, bool step) {
     PuctArgs a{};
     sn_status st = puct_args(e, q, a);
     if (st != SN_OK) return st;
     if (n_cur < 1 || n_cur > a.n) return set_error(SN_EINVAL, "n_cur out of range");
-    if (!w1s || !w1c || !w2 || !head || !logits) return set_error(SN_EINVAL, "NULL argument");
+    if (step && (t < 0 || t + n_cur != a.n)) return set_error(SN_EINVAL, "t / n_cur inconsistent");
+    if (!w1s || !w1c || !w2 || !head || (!logits && !step)) return set_error(SN_EINVAL, "NULL argument");
     if ((((uintptr_t)w1s) | ((uintptr_t)w2) | ((uintptr_t)w1c) | ((uintptr_t)head)) & 15)
         return set_error(SN_EINVAL, "w1s / w2 / w1c / head must be 16-B aligned");
-    const int64_t S = a.D * e->s.N;
+    const int N = e->s.N;
+    if (step && N != 2 && N != 4 && N != 8)
+        return set_error(SN_EUNSUPPORTED, "the fused rollout step needs N = 2, 4 or 8 (whole decisions per 64 seats)");
+    const int64_t S = a.D * N;
     if (S * n_cur >= (1ll << 31)) return set_error(SN_EINVAL, "too many rows");
     static int cus = 0;  // persistent grid: two workgroups per CU (the kernel's occupancy)
     if (!cus) {
@@ -1195,11 +1230,29 @@ sn_status sn_puct_mlp_seats(sn_env* e, const sn_puct* q, int n_cur, const void* 
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     }
     const int64_t groups = (S + kSeatBlock - 1) / kSeatBlock;
-    hipLaunchKernelGGL(k_puct_mlp_seats, dim3((unsigned)std::min<int64_t>(groups, 2ll * cus)), dim3(kBlock), 0,
-                       (hipStream_t)stream, a, e->s.N, n_cur, (const uint16_t*)w1s, w1c, (const uint16_t*)w2, head,
-                       logits);
+    const dim3 grid((unsigned)std::min<int64_t>(groups, 2ll * cus));
+    hipStream_t s = (hipStream_t)stream;
+    const uint16_t *w1p = (const uint16_t*)w1s, *w2p = (const uint16_t*)w2;
+    if (!step)
+        hipLaunchKernelGGL(k_puct_mlp_seats<0>, grid, dim3(kBlock), 0, s, e->s, a, N, n_cur, 0, w1p, w1c, w2p, head, logits);
+    else if (N == 2)
+        hipLaunchKernelGGL(k_puct_mlp_seats<2>, grid, dim3(kBlock), 0, s, e->s, a, N, n_cur, t, w1p, w1c, w2p, head, logits);
+    else if (N == 4)
+        hipLaunchKernelGGL(k_puct_mlp_seats<4>, grid, dim3(kBlock), 0, s, e->s, a, N, n_cur, t, w1p, w1c, w2p, head, logits);
+    else
+        hipLaunchKernelGGL(k_puct_mlp_seats<8>, grid, dim3(kBlock), 0, s, e->s, a, N, n_cur, t, w1p, w1c, w2p, head, logits);
     HIP_TRY(hipGetLastError());
     return SN_OK;
+}
+
+sn_status sn_puct_mlp_seats(sn_env* e, const sn_puct* q, int n_cur, const void* w1s, const float* w1c, const void* w2,
+                            const float* head, float* logits, void* stream) {
+    return launch_mlp_seats(e, q, 0, n_cur, w1s, w1c, w2, head, logits, stream, false);
+}
+
+sn_status sn_puct_mlp_step(sn_env* e, const sn_puct* q, int t, int n_cur, const void* w1s, const float* w1c,
+                           const void* w2, const float* head, float* logits, void* stream) {
+    return launch_mlp_seats(e, q, t, n_cur, w1s, w1c, w2, head, logits, stream, true);
 }
 
 sn_status sn_puct_mlp(sn_env* e, const sn_puct* q, int n_cur, const void* base, int ldb, const float* w1c,

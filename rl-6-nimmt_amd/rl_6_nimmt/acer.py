@@ -224,6 +224,16 @@ class BatchedACER(BatchedPUCT):
         L = self.rollout_len
         return [(c, min(T_STEPS, c + L)) for c in range(0, T_STEPS, L)]
 
+    def _chunk_tables(self):
+        """chunks() as device tensors (start, length), built once per rollout_len:
+        a host list copied per loss() call would wait for the stream each time"""
+        key = (self.rollout_len, str(self.env.device))
+        if getattr(self, "_chunk_tab", (None,))[0] != key:
+            ch = torch.tensor([c for c, _ in self.chunks()], device=self.env.device)
+            ln = torch.tensor([e - c for c, e in self.chunks()], device=self.env.device)
+            self._chunk_tab = (key, ch, ln)
+        return self._chunk_tab[1], self._chunk_tab[2]
+
     def stored_sequences(self, upto_chunk=None):
         """(slot, chunk index) of every stored sequence, oldest episode first;
         the newest episode only up to `upto_chunk` (inclusive)"""
@@ -248,8 +258,7 @@ class BatchedACER(BatchedPUCT):
         dev = self.actor_device()
         D, K = slots.shape
         L = self.rollout_len
-        ch = torch.tensor([c for c, _ in self.chunks()], device=self.env.device)
-        ln = torch.tensor([e - c for c, e in self.chunks()], device=self.env.device)
+        ch, ln = self._chunk_tables()
         j = torch.arange(L, device=self.env.device)
         t = ch[chunk_ids][:, :, None] + j  # [D, K, L]
         valid = j < ln[chunk_ids][:, :, None]
@@ -362,13 +371,16 @@ class BatchedACER(BatchedPUCT):
                 D = batch[0].shape[0]
                 if len(batch) == 2:  # explicit decider indices: a chunk's row d is decider d0 + d
                     batch = (*batch, torch.arange(D, device=batch[0].device)[:, None].expand_as(batch[0]))
-                tot = [0.0, 0.0, 0.0]
+                tot = None  # loss components stay on the device: no host sync per decider chunk
                 for d0 in range(0, D, self.decider_chunk):
                     part = tuple(x[d0: d0 + self.decider_chunk] for x in batch)
                     total, actor, corr, critic = self.loss(*part)
                     total.backward()
-                    tot = [tot[0] + float(actor), tot[1] + float(corr), tot[2] + float(critic)]
+                    comp = torch.stack((actor, corr, critic))
+                    tot = comp if tot is None else tot + comp
                 optimizer.step()
-                done_updates.append(tuple(tot))
+                done_updates.append(tot)
+        # one transfer for the whole schedule
+        done_updates = [tuple(float(v) for v in u) for u in torch.stack(done_updates).cpu()] if done_updates else []
         self.last_losses += done_updates
         return done_updates

@@ -221,6 +221,8 @@ class BatchedPUCT:
         # "seats" (default): layer 1's per-seat part inside the MLP kernel too (sn_puct_mlp_seats, one
         # launch per step); "gemm": per-seat rows + a PyTorch GEMM + sn_puct_mlp
         self.mlp_layer1 = os.environ.get("SECHS_MLP_LAYER1", "seats")
+        # with "seats": the rollout step inside the same launch (sn_puct_mlp_step; N = 2, 4, 8)
+        self.mlp_step = os.environ.get("SECHS_MLP_STEP", "1") != "0"
         self._step_dev = torch.zeros((1,), dtype=torch.int32, device=dev)
 
     # ------------------------------------------------------------ policy net on the device
@@ -350,9 +352,13 @@ class BatchedPUCT:
                 for t in range(n):
                     m = n - t
                     if self.mlp_layer1 == "seats":
+                        self.rows_evaluated += S * m
+                        if self.mlp_step and N in (2, 4, 8):
+                            nat.check(L.sn_puct_mlp_step(h, ctypes_ref(q), t, m, nat.ptr(w1s), nat.ptr(w1c),
+                                                         nat.ptr(w2p), nat.ptr(head), None, st), "sn_puct_mlp_step")
+                            continue
                         nat.check(L.sn_puct_mlp_seats(h, ctypes_ref(q), m, nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p),
                                                       nat.ptr(head), nat.ptr(logits), st), "sn_puct_mlp_seats")
-                        self.rows_evaluated += S * m
                         nat.check(L.sn_puct_step(h, ctypes_ref(q), nat.ptr(logits), t, m, st), "sn_puct_step")
                         continue
                     nat.check(L.sn_puct_seat_rows(h, ctypes_ref(q), m, nat.ptr(rv), 56, nat.ptr(cards), st),
