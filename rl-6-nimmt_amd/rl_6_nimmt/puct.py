@@ -346,6 +346,18 @@ class BatchedPUCT:
             S = self.D * N
             rows, cards, base, logits = self._fused_bufs()
             rv, bv = rows[:S], base[:S]
+            if self.mlp_layer1 == "seats" and self.mlp_step and N in (2, 4, 8):
+                # one launch per rollout step; the arguments built once (the
+                # league's engines run this loop eagerly: host time per launch)
+                qr, deal, mlp_step = ctypes_ref(q), L.sn_puct_deal, L.sn_puct_mlp_step
+                wargs = (nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p), nat.ptr(head), None, st)
+                for r in range(self.n_mc(n)):
+                    q.rollout = r
+                    nat.check(deal(h, qr, st), "sn_puct_deal")
+                    for t in range(n):
+                        nat.check(mlp_step(h, qr, t, n - t, *wargs), "sn_puct_mlp_step")
+                self.rows_evaluated += self.n_mc(n) * S * (n * (n + 1) // 2)
+                return
             for r in range(self.n_mc(n)):
                 q.rollout = r
                 nat.check(L.sn_puct_deal(h, ctypes_ref(q), st), "sn_puct_deal")
@@ -353,10 +365,6 @@ class BatchedPUCT:
                     m = n - t
                     if self.mlp_layer1 == "seats":
                         self.rows_evaluated += S * m
-                        if self.mlp_step and N in (2, 4, 8):
-                            nat.check(L.sn_puct_mlp_step(h, ctypes_ref(q), t, m, nat.ptr(w1s), nat.ptr(w1c),
-                                                         nat.ptr(w2p), nat.ptr(head), None, st), "sn_puct_mlp_step")
-                            continue
                         nat.check(L.sn_puct_mlp_seats(h, ctypes_ref(q), m, nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p),
                                                       nat.ptr(head), nat.ptr(logits), st), "sn_puct_mlp_seats")
                         nat.check(L.sn_puct_step(h, ctypes_ref(q), nat.ptr(logits), t, m, st), "sn_puct_step")
