@@ -407,14 +407,6 @@ sn_status sn_puct_mlp(sn_env* env, const sn_puct* q, int n_cur, const void* base
    sn_puct_seat_rows + a GEMM + sn_puct_mlp. */
 sn_status sn_puct_mlp_seats(sn_env* env, const sn_puct* q, int n_cur, const void* w1s, const float* w1c, const void* w2,
                             const float* head, float* logits, void* stream);
-/* sn_puct_mlp_seats + sn_puct_step(t, n_cur) in one launch (mcts.py:209-228
-   the policy, :86-100 the rollout step): each workgroup steps its group's
-   decisions from the logits it just produced (kept in LDS; `logits` may be
-   NULL, else they are stored too).  The same Philox draws and cards as the
-   two launches.  N = 2, 4 or 8 (whole decisions per 64 seats), else
-   SN_EUNSUPPORTED (use the two calls). */
-sn_status sn_puct_mlp_step(sn_env* env, const sn_puct* q, int t, int n_cur, const void* w1s, const float* w1c,
-                           const void* w2, const float* head, float* logits, void* stream);
 /* best_index [D] (optional): index of the chosen card in the root legal list */
 sn_status sn_puct_choose(sn_env* env, const sn_puct* q, int32_t* actions, int32_t* best_index, void* stream);
 /* PUCTCustomedAgent (agents/mcts.py:325-451, replaces _mcts /

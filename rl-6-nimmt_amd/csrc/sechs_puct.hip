@@ -405,20 +405,18 @@ __device__ __forceinline__ uint32_t pack_bf16(float lo, float hi) {
 // v_mfma_f32_32x32x16_bf16 against W2 in LDS, its ReLU'd bf16 outputs are
 // dotted with the head (bf16 pairs, v_dot2 in f32) and the two halves of
 // the wave summed.  sH2: the head as bf16 pairs, o = 2i, 2i + 1.
-__device__ __forceinline__ void mlp_tile(const uint16_t* brow0, const uint16_t* brow1, float x0, float x1,
-                                         const uint16_t* sW, const float* sC, const uint32_t* sH2, int col, int half,
-                                         float (&out)[2]) {
-    const uint16_t* brow[2] = {brow0, brow1};
-    const float x[2] = {x0, x1};
-    f32x16_t acc[4][2];
+template <int NT>
+__device__ __forceinline__ void mlp_tile(const uint16_t* const (&brow)[NT], const float (&x)[NT], const uint16_t* sW,
+                                         const float* sC, const uint32_t* sH2, int col, int half, float (&out)[NT]) {
+    f32x16_t acc[4][NT];
     // one k-step: the B fragments (16 features of the two 32-row halves), then 4 x 2 MFMAs
     auto kstep = [&](int ks, bool first) {
         const int k0 = 16 * ks + 8 * half;  // this lane's 8 features of the k-step
         const float4 wa = *(const float4*)&sC[k0], wb = *(const float4*)&sC[k0 + 4];
         const float w[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
-        bf16x8_t bfr[2];
+        bf16x8_t bfr[NT];
 #pragma unroll
-        for (int nt = 0; nt < 2; nt++) {
+        for (int nt = 0; nt < NT; nt++) {
             const uint4 bv = *(const uint4*)(brow[nt] + k0);
             const uint32_t bw[4] = {bv.x, bv.y, bv.z, bv.w};
             uint32_t hb[4];
@@ -434,8 +432,9 @@ __device__ __forceinline__ void mlp_tile(const uint16_t* brow0, const uint16_t* 
         for (int mt = 0; mt < 4; mt++) {
             const bf16x8_t a = __builtin_bit_cast(bf16x8_t, *(const uint4*)&sW[(32 * mt + col) * kMlpLdsK + k0]);
             const f32x16_t zero = {};
-            acc[mt][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr[0], first ? zero : acc[mt][0], 0, 0, 0);
-            acc[mt][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr[1], first ? zero : acc[mt][1], 0, 0, 0);
+#pragma unroll
+            for (int nt = 0; nt < NT; nt++)
+                acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr[nt], first ? zero : acc[mt][nt], 0, 0, 0);
         }
     };
     kstep(0, true);  // the accumulators start from the first k-step's products (no zeroing pass)
@@ -444,7 +443,7 @@ __device__ __forceinline__ void mlp_tile(const uint16_t* brow0, const uint16_t* 
     // epilogue: ReLU, bf16 rounding, head dot over this lane's outputs o
     // (C layout: o = 32 mt + 8 g + 4 half + i, i = 0..3), then the other half's
 #pragma unroll
-    for (int nt = 0; nt < 2; nt++) {
+    for (int nt = 0; nt < NT; nt++) {
         float sum = 0.f;
 #pragma unroll
         for (int mt = 0; mt < 4; mt++)
@@ -495,7 +494,7 @@ __global__ __launch_bounds__(256, 2) void k_puct_mlp(uint32_t R, int n_cur, cons
             brow[nt] = base + (size_t)(rc / (uint32_t)n_cur) * ldb;
         }
         float out[2];
-        mlp_tile(brow[0], brow[1], x[0], x[1], sW, sC, sH2, col, half, out);
+        mlp_tile<2>(brow, x, sW, sC, sH2, col, half, out);
 #pragma unroll
         for (int nt = 0; nt < 2; nt++)
             if (half == 0 && rr[nt] < R) logits[rr[nt]] = out[nt];
@@ -832,15 +831,10 @@ __device__ __forceinline__ void seat_row_part(const SeatIn& in, int n_cur, int p
     if (part == 2) row[kRowLen] = bf16_bits(1.f);
 }
 
-// NS > 0 (sn_puct_mlp_step, N = NS, a power of two <= 8): phase 4 runs the
-// rollout step of the group's decisions (step_seat, one lane per seat in
-// wave 0) from the logits the group just produced, kept in LDS -- the step
-// kernel's launch, its logit reads and its latency chain move beside the
-// other workgroup's MFMA work.  Groups of 64 seats hold whole decisions.
-template <int NS>
-__global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(DevState s, PuctArgs a, int N, int n_cur, int t,
-                                                          const uint16_t* w1s, const float* w1c, const uint16_t* w2,
-                                                          const float* head, float* logits) {
+__global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(PuctArgs a, int N, int n_cur, const uint16_t* w1s,
+                                                          const float* w1c, const uint16_t* w2, const float* head,
+                                                          float* logits) {
+    constexpr int TNT = 2;  // 32-row halves per phase-3 tile (32-row tiles measured slower)
     __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kMlpLdsK];          // W2 [128][120]
     __shared__ __attribute__((aligned(16))) uint16_t sW1[kMlpM * kSeatRowLds];      // W1s [128][72]
     __shared__ __attribute__((aligned(16))) uint16_t sRow[kSeatBlock * kSeatRowLds];  // seat rows [64][72]
@@ -848,7 +842,6 @@ __global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(DevState s, PuctArgs 
     __shared__ __attribute__((aligned(16))) float sCard[kSeatBlock * kHand];
     __shared__ __attribute__((aligned(16))) float sC[kMlpK];
     __shared__ __attribute__((aligned(16))) uint32_t sH2[kMlpM / 2];
-    __shared__ float sLog[NS ? kSeatBlock * kHand : 1];  // phase 4: the group's logits
     const int tid = threadIdx.x;
     const int64_t S = a.D * N;
     const int64_t groups = (S + kSeatBlock - 1) / kSeatBlock;
@@ -897,9 +890,10 @@ __global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(DevState s, PuctArgs 
 #pragma unroll
         for (int nt = 0; nt < 2; nt++)
 #pragma unroll
-            for (int r = 0; r < 16; r++) {
+            for (int r = 0; r < 16; r += 2) {  // C rows j, j + 1 (r & 3 in {0, 1} or {2, 3}): one b32 store
                 const int j = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * half;
-                if (j < kMlpK) sBase[(32 * nt + col) * kBaseLds + j] = (uint16_t)pack_bf16(acc[nt][r], 0.f);
+                if (j < kMlpK)
+                    *(uint32_t*)&sBase[(32 * nt + col) * kBaseLds + j] = pack_bf16(acc[nt][r], acc[nt][r + 1]);
             }
     }
     __syncthreads();
@@ -907,39 +901,25 @@ __global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(DevState s, PuctArgs 
     if (grp + gridDim.x < groups) nxt = group_load(grp + gridDim.x);
     // phase 3: k_puct_mlp's tile loop over the group's rows
     const uint32_t rows = (uint32_t)nseat * (uint32_t)n_cur;
-    const uint32_t tiles = (rows + 63u) / 64u;
+    const uint32_t tiles = (rows + 32u * TNT - 1u) / (32u * TNT);
     const uint32_t rbase = (uint32_t)s0 * (uint32_t)n_cur;
     for (uint32_t tile = wave; tile < tiles; tile += blockDim.x >> 6) {
-        uint32_t rr[2];
-        float x[2];
-        const uint16_t* brow[2];
+        uint32_t rr[TNT];
+        float x[TNT];
+        const uint16_t* brow[TNT];
 #pragma unroll
-        for (int nt = 0; nt < 2; nt++) {
-            rr[nt] = tile * 64u + 32u * nt + (uint32_t)col;  // group-local row
+        for (int nt = 0; nt < TNT; nt++) {
+            rr[nt] = tile * 32u * TNT + 32u * nt + (uint32_t)col;  // group-local row
             const uint32_t rc = rr[nt] < rows ? rr[nt] : rows - 1u;
             const uint32_t sl = rc / (uint32_t)n_cur;
             x[nt] = sCard[sl * kHand + (rc - sl * (uint32_t)n_cur)];
             brow[nt] = sBase + sl * kBaseLds;
         }
-        float out[2];
-        mlp_tile(brow[0], brow[1], x[0], x[1], sW, sC, sH2, col, half, out);
+        float out[TNT];
+        mlp_tile<TNT>(brow, x, sW, sC, sH2, col, half, out);
 #pragma unroll
-        for (int nt = 0; nt < 2; nt++)
-            if (half == 0 && rr[nt] < rows) {
-                if constexpr (NS > 0) sLog[rr[nt]] = out[nt];
-                if (logits) logits[rbase + rr[nt]] = out[nt];
-            }
-    }
-    if constexpr (NS > 0) {  // phase 4: the group's decisions take their rollout step
-        __syncthreads();
-        if (wave == 0)
-            step_seat<NS, NS>(
-                s, a,
-                [&](int64_t dd, int q, int k) {
-                    const int64_t li = min<int64_t>(max<int64_t>(dd * NS + q - s0, 0), kSeatBlock - 1);
-                    return sLog[li * n_cur + k];
-                },
-                t, n_cur, s0 + lane);
+        for (int nt = 0; nt < TNT; nt++)
+            if (half == 0 && rr[nt] < rows) logits[rbase + rr[nt]] = out[nt];
     }
     }
 }
@@ -1207,21 +1187,16 @@ sn_status sn_puct_seat_rows(sn_env* e, const sn_puct* q, int n_cur, void* rows, 
     return SN_OK;
 }
 
-// the one-kernel rollout MLP (NS = 0) or MLP + step (NS = N)
-static sn_status launch_mlp_seats(sn_env* e, const sn_puct* q, int t, int n_cur, const void* w1s, const float* w1c,
-                                  const void* w2, const float* head, float* logits, void* stream, bool step) {
+sn_status sn_puct_mlp_seats(sn_env* e, const sn_puct* q, int n_cur, const void* w1s, const float* w1c, const void* w2,
+                            const float* head, float* logits, void* stream) {
     PuctArgs a{};
     sn_status st = puct_args(e, q, a);
     if (st != SN_OK) return st;
     if (n_cur < 1 || n_cur > a.n) return set_error(SN_EINVAL, "n_cur out of range");
-    if (step && (t < 0 || t + n_cur != a.n)) return set_error(SN_EINVAL, "t / n_cur inconsistent");
-    if (!w1s || !w1c || !w2 || !head || (!logits && !step)) return set_error(SN_EINVAL, "NULL argument");
+    if (!w1s || !w1c || !w2 || !head || !logits) return set_error(SN_EINVAL, "NULL argument");
     if ((((uintptr_t)w1s) | ((uintptr_t)w2) | ((uintptr_t)w1c) | ((uintptr_t)head)) & 15)
         return set_error(SN_EINVAL, "w1s / w2 / w1c / head must be 16-B aligned");
-    const int N = e->s.N;
-    if (step && N != 2 && N != 4 && N != 8)
-        return set_error(SN_EUNSUPPORTED, "the fused rollout step needs N = 2, 4 or 8 (whole decisions per 64 seats)");
-    const int64_t S = a.D * N;
+    const int64_t S = a.D * e->s.N;
     if (S * n_cur >= (1ll << 31)) return set_error(SN_EINVAL, "too many rows");
     static int cus = 0;  // persistent grid: two workgroups per CU (the kernel's occupancy)
     if (!cus) {
@@ -1230,29 +1205,11 @@ static sn_status launch_mlp_seats(sn_env* e, const sn_puct* q, int t, int n_cur,
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     }
     const int64_t groups = (S + kSeatBlock - 1) / kSeatBlock;
-    const dim3 grid((unsigned)std::min<int64_t>(groups, 2ll * cus));
-    hipStream_t s = (hipStream_t)stream;
-    const uint16_t *w1p = (const uint16_t*)w1s, *w2p = (const uint16_t*)w2;
-    if (!step)
-        hipLaunchKernelGGL(k_puct_mlp_seats<0>, grid, dim3(kBlock), 0, s, e->s, a, N, n_cur, 0, w1p, w1c, w2p, head, logits);
-    else if (N == 2)
-        hipLaunchKernelGGL(k_puct_mlp_seats<2>, grid, dim3(kBlock), 0, s, e->s, a, N, n_cur, t, w1p, w1c, w2p, head, logits);
-    else if (N == 4)
-        hipLaunchKernelGGL(k_puct_mlp_seats<4>, grid, dim3(kBlock), 0, s, e->s, a, N, n_cur, t, w1p, w1c, w2p, head, logits);
-    else
-        hipLaunchKernelGGL(k_puct_mlp_seats<8>, grid, dim3(kBlock), 0, s, e->s, a, N, n_cur, t, w1p, w1c, w2p, head, logits);
+    hipLaunchKernelGGL(k_puct_mlp_seats, dim3((unsigned)std::min<int64_t>(groups, 2ll * cus)), dim3(kBlock), 0,
+                       (hipStream_t)stream, a, e->s.N, n_cur, (const uint16_t*)w1s, w1c, (const uint16_t*)w2, head,
+                       logits);
     HIP_TRY(hipGetLastError());
     return SN_OK;
-}
-
-sn_status sn_puct_mlp_seats(sn_env* e, const sn_puct* q, int n_cur, const void* w1s, const float* w1c, const void* w2,
-                            const float* head, float* logits, void* stream) {
-    return launch_mlp_seats(e, q, 0, n_cur, w1s, w1c, w2, head, logits, stream, false);
-}
-
-sn_status sn_puct_mlp_step(sn_env* e, const sn_puct* q, int t, int n_cur, const void* w1s, const float* w1c,
-                           const void* w2, const float* head, float* logits, void* stream) {
-    return launch_mlp_seats(e, q, t, n_cur, w1s, w1c, w2, head, logits, stream, true);
 }
 
 sn_status sn_puct_mlp(sn_env* e, const sn_puct* q, int n_cur, const void* base, int ldb, const float* w1c,

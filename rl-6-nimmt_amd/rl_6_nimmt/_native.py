@@ -100,7 +100,6 @@ SIGNATURES = {
     "sn_puct_seat_rows": ([_P, _P, _I, _P, _I, _P, _P], _I),
     "sn_puct_mlp": ([_P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P], _I),
     "sn_puct_mlp_seats": ([_P, _P, _I, _P, _P, _P, _P, _P, _P], _I),
-    "sn_puct_mlp_step": ([_P, _P, _I, _I, _P, _P, _P, _P, _P, _P], _I),
     "sn_puct_choose": ([_P, _P, _P, _P, _P], _I),
     "sn_pcv_choose": ([_P, _P, _P, _P, _P, _P, _P, _P], _I),
     "sn_policy_sample": ([_P, _P, _P, _P, _P, _P, _P, _P], _I),

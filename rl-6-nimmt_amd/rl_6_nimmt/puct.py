@@ -221,8 +221,6 @@ class BatchedPUCT:
         # "seats" (default): layer 1's per-seat part inside the MLP kernel too (sn_puct_mlp_seats, one
         # launch per step); "gemm": per-seat rows + a PyTorch GEMM + sn_puct_mlp
         self.mlp_layer1 = os.environ.get("SECHS_MLP_LAYER1", "seats")
-        # with "seats": the rollout step inside the same launch (sn_puct_mlp_step; N = 2, 4, 8)
-        self.mlp_step = os.environ.get("SECHS_MLP_STEP", "1") != "0"
         self._step_dev = torch.zeros((1,), dtype=torch.int32, device=dev)
 
     # ------------------------------------------------------------ policy net on the device
@@ -346,16 +344,18 @@ class BatchedPUCT:
             S = self.D * N
             rows, cards, base, logits = self._fused_bufs()
             rv, bv = rows[:S], base[:S]
-            if self.mlp_layer1 == "seats" and self.mlp_step and N in (2, 4, 8):
-                # one launch per rollout step; the arguments built once (the
+            if self.mlp_layer1 == "seats":
+                # two launches per rollout step, the arguments built once (the
                 # league's engines run this loop eagerly: host time per launch)
-                qr, deal, mlp_step = ctypes_ref(q), L.sn_puct_deal, L.sn_puct_mlp_step
-                wargs = (nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p), nat.ptr(head), None, st)
+                qr, deal, mlp, step = ctypes_ref(q), L.sn_puct_deal, L.sn_puct_mlp_seats, L.sn_puct_step
+                wargs = (nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p), nat.ptr(head), nat.ptr(logits), st)
+                lp = nat.ptr(logits)
                 for r in range(self.n_mc(n)):
                     q.rollout = r
                     nat.check(deal(h, qr, st), "sn_puct_deal")
                     for t in range(n):
-                        nat.check(mlp_step(h, qr, t, n - t, *wargs), "sn_puct_mlp_step")
+                        nat.check(mlp(h, qr, n - t, *wargs), "sn_puct_mlp_seats")
+                        nat.check(step(h, qr, lp, t, n - t, st), "sn_puct_step")
                 self.rows_evaluated += self.n_mc(n) * S * (n * (n + 1) // 2)
                 return
             for r in range(self.n_mc(n)):

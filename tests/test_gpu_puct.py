@@ -634,23 +634,3 @@ def test_seat_parallel_step_equals_one_lane_step(monkeypatch):
         res[lanes] = (acts, eng.stats.clone(), eng.hist.clone())
     assert all(torch.equal(a, b) for a, b in zip(res["1"][0], res["0"][0]))
     assert torch.equal(res["1"][1], res["0"][1]) and torch.equal(res["1"][2], res["0"][2])
-
-
-@pytest.mark.parametrize("mask", [None, 0b0101])
-def test_fused_mlp_step_equals_two_launches(mask):
-    """sn_puct_mlp_step (the rollout step inside the MLP launch, from the
-    logits in LDS) and sn_puct_mlp_seats + sn_puct_step: the same logits, the
-    same Philox draws -- identical search statistics and moves over two
-    decisions, every seat deciding or two of four"""
-    res = {}
-    for fused in (True, False):
-        env, eng = _engine(B=300, mask=mask, dtype=torch.bfloat16, mc_max=12, mc_per_card=3, seed=23)
-        eng.mlp_layer1, eng.mlp_step = "seats", fused
-        acts = [eng.decide(10).clone()]
-        env.step(acts[-1])
-        acts.append(eng.decide(9).clone())
-        torch.cuda.synchronize()
-        res[fused] = (acts, eng.stats.clone(), eng.hist.clone(), eng.rows_evaluated)
-    assert all(torch.equal(a, b) for a, b in zip(res[True][0], res[False][0]))
-    assert torch.equal(res[True][1], res[False][1]) and torch.equal(res[True][2], res[False][2])
-    assert res[True][3] == res[False][3]
