@@ -31,6 +31,7 @@ than max(warmup, minibatch) sequences are stored, one on-policy update (the
 newest sequence of every decider) and one off-policy update (`minibatch`
 stored sequences per decider, drawn without replacement on the device).
 """
+import os
 import warnings
 
 import torch
@@ -128,7 +129,16 @@ class BatchedACER(BatchedPUCT):
         self.episodes = 0  # episodes written (slot = episodes % capacity)
         self.rep_nd = [0] * C  # deciders stored in each slot (tournament mode: the round's seats of this agent)
         self._t = 0
-        self.decider_chunk = 4096  # deciders per backward pass of an update (learn)
+        # deciders per backward pass of an update (learn): bounds the activations
+        # (~1.6 KB per candidate row of the fp32 forward + backward).  Larger
+        # chunks run fewer, larger fp32 GEMMs: the run.py league's ACER update
+        # took 406 / 320 / 286 ms per round at 4096 / 16384 / 65536 deciders
+        # (profiles/r04_handoff_and_mlp_ab.txt); a quarter of the free memory
+        # at construction caps it
+        per_decider = max(self.minibatch, 1) * self.rollout_len * 10 * 1600
+        budget = (torch.cuda.mem_get_info(dev)[0] // 4) if dev.type == "cuda" else (8 << 30)
+        self.decider_chunk = int(os.environ.get("SECHS_ACER_DECIDER_CHUNK",
+                                                max(1024, min(65536, budget // per_decider))))
         self._gen = torch.Generator(device=dev)
         self._gen.manual_seed(self.seed ^ 0xACE5)
         self.last_losses = []
