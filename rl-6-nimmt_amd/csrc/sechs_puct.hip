@@ -386,6 +386,14 @@ __device__ __forceinline__ float relu_f32(float v) {
     asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(v));
     return r;
 }
+// ReLU of a bf16 pair after rounding (the same as rounding after the ReLU:
+// rounding keeps the sign): a signed 16-bit max with 0 per half, one
+// v_pk_max_i16 for two values (-0.0 = 0x8000 becomes +0)
+__device__ __forceinline__ uint32_t relu_bf16x2(uint32_t p) {
+    uint32_t r;
+    asm("v_pk_max_i16 %0, %1, 0" : "=v"(r) : "v"(p));
+    return r;
+}
 __device__ __forceinline__ float fma_f32(float a, float b, float c) {
     float r;
     asm("v_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -424,7 +432,7 @@ __device__ __forceinline__ void mlp_tile(const uint16_t* const (&brow)[NT], cons
             for (int j = 0; j < 4; j++) {
                 const float lo = fma_f32(x[nt], w[2 * j], __uint_as_float(bw[j] << 16));
                 const float hi = fma_f32(x[nt], w[2 * j + 1], __uint_as_float(bw[j] & 0xFFFF0000u));
-                hb[j] = pack_bf16(relu_f32(lo), relu_f32(hi));
+                hb[j] = relu_bf16x2(pack_bf16(lo, hi));
             }
             bfr[nt] = __builtin_bit_cast(bf16x8_t, make_uint4(hb[0], hb[1], hb[2], hb[3]));
         }
@@ -450,8 +458,8 @@ __device__ __forceinline__ void mlp_tile(const uint16_t* const (&brow)[NT], cons
 #pragma unroll
             for (int g = 0; g < 4; g++) {
                 const uint2 hw = *(const uint2*)&sH2[(32 * mt + 8 * g + 4 * half) / 2];
-                const uint32_t p0 = pack_bf16(relu_f32(acc[mt][nt][4 * g]), relu_f32(acc[mt][nt][4 * g + 1]));
-                const uint32_t p1 = pack_bf16(relu_f32(acc[mt][nt][4 * g + 2]), relu_f32(acc[mt][nt][4 * g + 3]));
+                const uint32_t p0 = relu_bf16x2(pack_bf16(acc[mt][nt][4 * g], acc[mt][nt][4 * g + 1]));
+                const uint32_t p1 = relu_bf16x2(pack_bf16(acc[mt][nt][4 * g + 2], acc[mt][nt][4 * g + 3]));
                 sum = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, p0),
                                                       __builtin_bit_cast(bf16x2_t, hw.x), sum, false);
                 sum = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, p1),
