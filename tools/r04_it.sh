@@ -17,6 +17,7 @@ done
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_puct -o run -- python3 $R/bench.py --only puct > $OUT/prof_puct.log 2>&1)
 rc=$?; echo "rocprof puct rc=$rc"; fatal $rc rocprof_puct
 python3 tools/db_kstats.py $OUT/prof_puct $OUT/puct_kernel_stats.csv
+python3 tools/step_by_t.py $OUT/prof_puct > $OUT/puct_by_t.txt; cat $OUT/puct_by_t.txt
 find $R/gpurun_out -name "*.db" -size +1M -delete
 timeout -k 10 400 python bench.py --only mixed > $OUT/mixed.json 2> $OUT/mixed.err
 rc=$?; fatal $rc mixed
