@@ -851,56 +851,78 @@ __global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(PuctArgs a, int N, in
                                                           const float* w1c, const uint16_t* w2, const float* head,
                                                           float* logits) {
     constexpr int TNT = 2;  // 32-row halves per phase-3 tile (32-row tiles measured slower)
-    __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kMlpLdsK];          // W2 [128][120]
-    __shared__ __attribute__((aligned(16))) uint16_t sW1[kMlpM * kSeatRowLds];      // W1s [128][72]
+    constexpr int kWaves = kBlock / 64;
+    __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kMlpLdsK];            // W2 [128][120]
     __shared__ __attribute__((aligned(16))) uint16_t sRow[kSeatBlock * kSeatRowLds];  // seat rows [64][72]
-    __shared__ __attribute__((aligned(16))) uint16_t sBase[kSeatBlock * kBaseLds];    // base [64][120]
-    __shared__ __attribute__((aligned(16))) float sCard[kSeatBlock * kHand];
+    __shared__ __attribute__((aligned(16))) uint16_t sBase[2][kSeatBlock * kBaseLds];  // base [64][120], 2 groups
+    __shared__ __attribute__((aligned(16))) float sCard[2][kSeatBlock * kHand];
     __shared__ __attribute__((aligned(16))) float sC[kMlpK];
     __shared__ __attribute__((aligned(16))) uint32_t sH2[kMlpM / 2];
     const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63, col = lane & 31, half = lane >> 5;
     const int64_t S = a.D * N;
     const int64_t groups = (S + kSeatBlock - 1) / kSeatBlock;
     for (int i = tid; i < kMlpM * (kMlpK / 8); i += blockDim.x) {
         const int o = i / (kMlpK / 8), c = i - o * (kMlpK / 8);
         *(uint4*)&sW[o * kMlpLdsK + 8 * c] = *(const uint4*)&w2[o * kMlpK + 8 * c];
     }
-    for (int i = tid; i < kMlpM * (kSeatRowK / 8); i += blockDim.x) {
-        const int o = i / (kSeatRowK / 8), c = i - o * (kSeatRowK / 8);
-        *(uint4*)&sW1[o * kSeatRowLds + 8 * c] = *(const uint4*)&w1s[o * kSeatRowK + 8 * c];
-    }
     for (int i = tid; i < kMlpK; i += blockDim.x) sC[i] = w1c[i];
     load_head_pairs(head, sH2);
+    // phase 2's A fragments (W1s rows 32 wave + col, the four k-steps) stay in registers
+    bf16x8_t w1f[kSeatRowK / 16];
+#pragma unroll
+    for (int ks = 0; ks < kSeatRowK / 16; ks++)
+        w1f[ks] = __builtin_bit_cast(bf16x8_t, *(const uint4*)&w1s[(32 * wave + col) * kSeatRowK + 16 * ks + 8 * half]);
     const int sl = tid >> 2, part = tid & 3;  // phase 1: four lanes per seat
     auto group_load = [&](int64_t grp) {
         const int64_t s0 = grp * kSeatBlock;
         return seat_load(a, N, s0 + min<int64_t>(sl, S - s0 - 1), part);
     };
+    // one 64-row phase-3 tile of a group held in buffer `buf`
+    auto run_tile = [&](int buf, uint32_t tile, uint32_t rows, uint32_t rbase) {
+        uint32_t rr[TNT];
+        float x[TNT];
+        const uint16_t* brow[TNT];
+#pragma unroll
+        for (int nt = 0; nt < TNT; nt++) {
+            rr[nt] = tile * 32u * TNT + 32u * nt + (uint32_t)col;  // group-local row
+            const uint32_t rc = rr[nt] < rows ? rr[nt] : rows - 1u;
+            const uint32_t q = rc / (uint32_t)n_cur;
+            x[nt] = sCard[buf][q * kHand + (rc - q * (uint32_t)n_cur)];
+            brow[nt] = sBase[buf] + q * kBaseLds;
+        }
+        float out[TNT];
+        mlp_tile<TNT>(brow, x, sW, sC, sH2, col, half, out);
+#pragma unroll
+        for (int nt = 0; nt < TNT; nt++)
+            if (half == 0 && rr[nt] < rows) logits[rbase + rr[nt]] = out[nt];
+    };
+    // tiles of the previous group left for this iteration (the waves share a
+    // tile list of those + this group's tiles; up to 3 of this group's are
+    // carried to the next iteration so that every wave gets the same count)
+    uint32_t pend_first = 0u, pend_cnt = 0u, pend_rows = 0u, pend_rbase = 0u;
     SeatIn nxt = group_load(min<int64_t>(blockIdx.x, groups - 1));
-    for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+    int it = 0;
+    for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x, it++) {
+    const int buf = it & 1;
     const int64_t s0 = grp * kSeatBlock;
     const int nseat = (int)min<int64_t>(kSeatBlock, S - s0);
     const SeatIn cur = nxt;
-    __syncthreads();  // the previous group's phase 3 is done with sBase / sCard
+    __syncthreads();  // the last iteration's tiles are done with this buffer, phase 2 with sRow
     // phase 1: the seats' rows and card features
-    seat_row_part(cur, n_cur, part, sRow + sl * kSeatRowLds, sCard + sl * kHand);
+    seat_row_part(cur, n_cur, part, sRow + sl * kSeatRowLds, sCard[buf] + sl * kHand);
     __syncthreads();
-    const int wave = tid >> 6, lane = tid & 63, col = lane & 31, half = lane >> 5;
     // phase 2: base[seat][j] = sum_k W1s[j][k] rows[seat][k]; wave w: outputs j in [32w, 32w + 32)
     {
         f32x16_t acc[2];
 #pragma unroll
-        for (int nt = 0; nt < 2; nt++)
-#pragma unroll
-            for (int i = 0; i < 16; i++) acc[nt][i] = 0.f;
-#pragma unroll
         for (int ks = 0; ks < kSeatRowK / 16; ks++) {
             const int k0 = 16 * ks + 8 * half;
-            const bf16x8_t af = __builtin_bit_cast(bf16x8_t, *(const uint4*)&sW1[(32 * wave + col) * kSeatRowLds + k0]);
 #pragma unroll
             for (int nt = 0; nt < 2; nt++) {
                 const bf16x8_t bfr = __builtin_bit_cast(bf16x8_t, *(const uint4*)&sRow[(32 * nt + col) * kSeatRowLds + k0]);
-                acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[nt], 0, 0, 0);
+                const f32x16_t zero = {};
+                acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1f[ks], bfr, ks ? acc[nt] : zero, 0, 0, 0);
             }
         }
 #pragma unroll
@@ -909,34 +931,25 @@ __global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(PuctArgs a, int N, in
             for (int r = 0; r < 16; r += 2) {  // C rows j, j + 1 (r & 3 in {0, 1} or {2, 3}): one b32 store
                 const int j = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * half;
                 if (j < kMlpK)
-                    *(uint32_t*)&sBase[(32 * nt + col) * kBaseLds + j] = pack_bf16(acc[nt][r], acc[nt][r + 1]);
+                    *(uint32_t*)&sBase[buf][(32 * nt + col) * kBaseLds + j] = pack_bf16(acc[nt][r], acc[nt][r + 1]);
             }
     }
     __syncthreads();
+    const bool more = grp + gridDim.x < groups;
     // the next group's rollout-state loads fly during phase 3
-    if (grp + gridDim.x < groups) nxt = group_load(grp + gridDim.x);
-    // phase 3: k_puct_mlp's tile loop over the group's rows
+    if (more) nxt = group_load(grp + gridDim.x);
+    // phase 3: the shared tile list
     const uint32_t rows = (uint32_t)nseat * (uint32_t)n_cur;
     const uint32_t tiles = (rows + 32u * TNT - 1u) / (32u * TNT);
     const uint32_t rbase = (uint32_t)s0 * (uint32_t)n_cur;
-    for (uint32_t tile = wave; tile < tiles; tile += blockDim.x >> 6) {
-        uint32_t rr[TNT];
-        float x[TNT];
-        const uint16_t* brow[TNT];
-#pragma unroll
-        for (int nt = 0; nt < TNT; nt++) {
-            rr[nt] = tile * 32u * TNT + 32u * nt + (uint32_t)col;  // group-local row
-            const uint32_t rc = rr[nt] < rows ? rr[nt] : rows - 1u;
-            const uint32_t sl = rc / (uint32_t)n_cur;
-            x[nt] = sCard[sl * kHand + (rc - sl * (uint32_t)n_cur)];
-            brow[nt] = sBase + sl * kBaseLds;
-        }
-        float out[TNT];
-        mlp_tile<TNT>(brow, x, sW, sC, sH2, col, half, out);
-#pragma unroll
-        for (int nt = 0; nt < TNT; nt++)
-            if (half == 0 && rr[nt] < rows) logits[rbase + rr[nt]] = out[nt];
+    const uint32_t total = pend_cnt + tiles;
+    uint32_t defer = more ? total % kWaves : 0u;
+    if (defer > tiles) defer = 0u;  // only this group's tiles can wait
+    for (uint32_t i = (uint32_t)wave; i < total - defer; i += kWaves) {
+        if (i < pend_cnt) run_tile(buf ^ 1, pend_first + i, pend_rows, pend_rbase);
+        else run_tile(buf, i - pend_cnt, rows, rbase);
     }
+    pend_first = tiles - defer, pend_cnt = defer, pend_rows = rows, pend_rbase = rbase;
     }
 }
 
