@@ -812,30 +812,48 @@ __device__ __forceinline__ SeatIn seat_load(const PuctArgs& a, int N, int64_t i,
     return in;
 }
 
-__device__ __forceinline__ void seat_row_part(const SeatIn& in, int n_cur, int part, uint16_t* row, float* cd) {
+// the row features as bf16 bits by value (write_row's nrm + rounding, looked
+// up instead of a correctly rounded f32 division per feature): card / hand
+// slot c in -1..103 at [c + 1], row length, bull heads and player count after
+constexpr int kLutCard = 0, kLutLen = 105, kLutHeads = 113, kLutN = 177, kLutSize = 193;
+__device__ __forceinline__ void build_row_lut(uint16_t* lut) {
+    for (int i = threadIdx.x; i < kLutSize; i += blockDim.x) {
+        float v;
+        if (i < kLutLen) v = nrm((float)(i - 1), 0.f, 103.f);
+        else if (i < kLutHeads) v = nrm((float)(i - kLutLen), 1.f, 5.f);
+        else if (i < kLutN) v = nrm((float)(i - kLutHeads), 1.f, 10.f);
+        else v = nrm((float)(i - kLutN), 0.f, 6.f);
+        lut[i] = bf16_bits(v);
+    }
+}
+
+__device__ __forceinline__ void seat_row_part(const SeatIn& in, int n_cur, int part, uint16_t* row, float* cd,
+                                              const uint16_t* lut) {
     const bool live = in.live;
     const int kp = in.kp;
     Hand h;
     h.lo = in.h0 | ((uint64_t)in.h1 << 32);
     h.hi = in.h2;
+    auto card_bits = [&](uint32_t c) { return lut[kLutCard + (c == 0xFFu ? 0u : min(c, 103u) + 1u)]; };  // 0xFF: -1
 #pragma unroll
     for (int j = 0; j < 3; j++) {
         const int k = part + 4 * j;
         if (k < kHand) {
             const uint32_t c = hand_get(h, (uint32_t)k);
-            row[1 + k] = live ? bf16_bits(nrm(c == 0xFFu ? -1.f : (float)c, 0.f, 103.f)) : (uint16_t)0;
-            cd[k] = (live && k < n_cur) ? round_to<__hip_bfloat16>(nrm((float)c, 0.f, 103.f)) : 0.f;
+            const uint16_t b = card_bits(c);
+            row[1 + k] = live ? b : (uint16_t)0;
+            cd[k] = (live && k < n_cur) ? __uint_as_float((uint32_t)b << 16) : 0.f;
         }
     }
     const uint32_t lo = in.lo, hi = in.hi;
     const uint32_t len = len_of(hi);
-    row[12 + part] = live ? bf16_bits(nrm((float)len, 1.f, 5.f)) : (uint16_t)0;
-    row[16 + part] = live ? bf16_bits(nrm((float)end_of(hi), 0.f, 103.f)) : (uint16_t)0;
-    row[20 + part] = live ? bf16_bits(nrm((float)heads_in(hi), 1.f, 10.f)) : (uint16_t)0;
+    row[12 + part] = live ? lut[kLutLen + min(len, 7u)] : (uint16_t)0;
+    row[16 + part] = live ? card_bits(end_of(hi)) : (uint16_t)0;
+    row[20 + part] = live ? lut[kLutHeads + min(heads_in(hi), 63u)] : (uint16_t)0;  // <= 35 in a game
 #pragma unroll
     for (int c = 0; c < kThreshold; c++) {
-        const float v = (c < 5 && (uint32_t)c < len) ? (float)card_at(lo, hi, c < 5 ? c : 0) : -1.f;
-        row[24 + part * kThreshold + c] = live ? bf16_bits(nrm(v, 0.f, 103.f)) : (uint16_t)0;
+        const uint32_t v = (c < 5 && (uint32_t)c < len) ? card_at(lo, hi, c < 5 ? c : 0) : 0xFFu;
+        row[24 + part * kThreshold + c] = live ? card_bits(v) : (uint16_t)0;
     }
 #pragma unroll
     for (int j = 0; j < 4; j++) {
@@ -843,7 +861,7 @@ __device__ __forceinline__ void seat_row_part(const SeatIn& in, int n_cur, int p
         if (f < kSeatRowK) row[f] = 0;
     }
     if (part == 0) row[0] = 0;
-    if (part == 1) row[11] = live ? bf16_bits(nrm((float)kp, 0.f, 6.f)) : (uint16_t)0;
+    if (part == 1) row[11] = live ? lut[kLutN + min(kp, 15)] : (uint16_t)0;
     if (part == 2) row[kRowLen] = bf16_bits(1.f);
 }
 
@@ -858,8 +876,10 @@ __global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(PuctArgs a, int N, in
     __shared__ __attribute__((aligned(16))) float sCard[2][kSeatBlock * kHand];
     __shared__ __attribute__((aligned(16))) float sC[kMlpK];
     __shared__ __attribute__((aligned(16))) uint32_t sH2[kMlpM / 2];
+    __shared__ uint16_t sLut[kLutSize];
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63, col = lane & 31, half = lane >> 5;
+    build_row_lut(sLut);
     const int64_t S = a.D * N;
     const int64_t groups = (S + kSeatBlock - 1) / kSeatBlock;
     for (int i = tid; i < kMlpM * (kMlpK / 8); i += blockDim.x) {
@@ -910,7 +930,7 @@ __global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(PuctArgs a, int N, in
     const SeatIn cur = nxt;
     __syncthreads();  // the last iteration's tiles are done with this buffer, phase 2 with sRow
     // phase 1: the seats' rows and card features
-    seat_row_part(cur, n_cur, part, sRow + sl * kSeatRowLds, sCard[buf] + sl * kHand);
+    seat_row_part(cur, n_cur, part, sRow + sl * kSeatRowLds, sCard[buf] + sl * kHand, sLut);
     __syncthreads();
     // phase 2: base[seat][j] = sum_k W1s[j][k] rows[seat][k]; wave w: outputs j in [32w, 32w + 32)
     {
