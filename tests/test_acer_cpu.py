@@ -305,3 +305,28 @@ def test_decider_chunked_update_equals_one_batch():
     assert np.allclose(np.array(u1), np.array(u2), rtol=1e-5, atol=1e-6)
     for a, b in zip(eng.actor.parameters(), eng2.actor.parameters()):
         assert torch.allclose(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_splitk_training_forward_equals_module():
+    """train_forward (SplitKLinear: the weight gradient as batched partial
+    products over row chunks) gives the module's outputs and, to float64
+    rounding, its gradients -- over enough rows for the chunked path"""
+    import torch
+
+    from rl_6_nimmt.acer import make_actor_critic, train_forward
+
+    torch.manual_seed(0)
+    x = torch.randn(300_000, 48, dtype=torch.float64, requires_grad=True)
+    net = make_actor_critic().double()
+    grads = []
+    for fwd in (lambda r: train_forward(net, r), net):
+        out = fwd(x)
+        loss = (out[0] ** 2).sum() + (3 * out[1]).sum()
+        net.zero_grad()
+        x.grad = None
+        loss.backward()
+        grads.append(([p.grad.clone() for p in net.parameters()], x.grad.clone(), [o.detach() for o in out]))
+    (g1, x1, o1), (g2, x2, o2) = grads
+    assert all(torch.equal(a, b) for a, b in zip(o1, o2))
+    assert torch.equal(x1, x2)
+    assert all(torch.allclose(a, b, rtol=1e-12, atol=1e-12 * float(b.abs().max())) for a, b in zip(g1, g2))
