@@ -1,5 +1,7 @@
 #!/bin/bash
 # r04: pipe hand-off modes A/B (0 events, 1 CP wait on a block count, 2 poll + event marker),
+# (historical A/B: the SN_OPT_PIPE_FLAGS modes it selects were measured slower and removed from the
+#  library -- DESIGN.md §4; SECHS_PIPE_FLAGS is ignored by the current build)
 # persistent one-kernel PUCT MLP vs the GEMM form, rest of the GPU suite, league phases
 set -o pipefail
 export TMPDIR=/tmp

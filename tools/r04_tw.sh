@@ -1,5 +1,7 @@
 #!/bin/bash
 # r04: the in-launch pipeline (SN_OPT_PIPE_FLAGS = 3, k_play_tw) -- parity, then headline A/B vs events (0)
+# (historical A/B: the SN_OPT_PIPE_FLAGS modes it selects were measured slower and removed from the
+#  library -- DESIGN.md §4; SECHS_PIPE_FLAGS is ignored by the current build)
 set -o pipefail
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
