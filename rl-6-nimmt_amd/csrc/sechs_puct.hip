@@ -703,6 +703,18 @@ __device__ __forceinline__ void step_seat(const DevState& s, const PuctArgs& a, 
     int32_t* ro = a.ro + dd * kRoWords;
     const int kp = players_of(a, g);
     const bool seat = q < N && q < kp;
+    // the resolving lane's words, loaded with the seat's (no second round trip after the shuffles;
+    // nothing below writes them before the resolve)
+    Board b{};
+    int32_t r40 = 0, r41 = 0, s20 = 0, s21 = 0, s22 = 0;
+    if (q == 0) {
+        b = ro_board(ro);
+        r40 = ro[40], r41 = ro[41];
+        if (n_cur == 1) {
+            const int32_t* st = a.stats + dd * kStatWords;
+            s20 = st[20], s21 = st[21], s22 = st[22];
+        }
+    }
     uint32_t card = 0xFFu;
     int idx = 0;
     if (seat) {
@@ -734,18 +746,18 @@ __device__ __forceinline__ void step_seat(const DevState& s, const PuctArgs& a, 
     for (int r = 0; r < N; r++) cards[r] = (uint32_t)__shfl((int)card, lead + r);
     const int first_idx = __shfl(idx, lead);
     if (q != 0 || !live) return;
-    Board b = ro_board(ro);
     uint32_t pen[N];
     resolve<N, true>(b, cards, pen);
-    const int first = (t == 0) ? first_idx : ro[41];
-    const int32_t outcome = ro[40] - (int32_t)pen[0];
+    const int first = (t == 0) ? first_idx : r41;
+    const int32_t outcome = r40 - (int32_t)pen[0];
     if (n_cur == 1) {
         int32_t* st = a.stats + dd * kStatWords;
         st[first] += outcome;
         st[10 + first] += 1;
-        st[20] += 1;
-        st[21] = (st[20] == 1) ? outcome : min(st[21], outcome);
-        st[22] = (st[20] == 1) ? outcome : max(st[22], outcome);
+        const int32_t total = s20 + 1;
+        st[20] = total;
+        st[21] = (total == 1) ? outcome : min(s21, outcome);
+        st[22] = (total == 1) ? outcome : max(s22, outcome);
         a.hist[dd * kHistBins + (outcome + 171)] += 1;
     } else {
         ro[0] = b.lo.x, ro[1] = b.lo.y, ro[2] = b.lo.z, ro[3] = b.lo.w;
