@@ -20,6 +20,7 @@ import torch
 from torch import nn
 
 from . import _native as nat
+from .splitk import train_forward
 from .utils.nets import MultiHeadedMLP
 
 ROW = 48
@@ -501,7 +502,7 @@ class BatchedPUCT:
         dev = self.actor_device()
         loss = torch.zeros((), device=dev)
         for rows, n, best in self.decisions:
-            (logits,) = self.actor(rows.to(dev))
+            (logits,) = train_forward(self.actor, rows.to(dev))
             logp = torch.log_softmax(logits.reshape(-1, n), dim=1)
             loss = loss - logp.gather(1, best.to(dev).long()[:, None]).sum()
         return loss
@@ -590,7 +591,7 @@ class BatchedPUCTCustomed(BatchedPUCT):
         target = self._decider_rewards(per_step)[:-1].sum(dim=0).float().to(dev)  # [D]
         logps, values = [], []
         for rows, n, best in self.decisions:
-            (out,) = self.actor(rows.to(dev))
+            (out,) = train_forward(self.actor, rows.to(dev))
             out = out.reshape(-1, n, 2)
             best = best.to(dev).long()[:, None]
             logp = torch.log_softmax(out[:, :, 0], dim=1)

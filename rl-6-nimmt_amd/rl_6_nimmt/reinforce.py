@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 from . import _native as nat
+from .splitk import train_forward
 from .puct import ROW, BatchedPUCT, ctypes_ref, make_actor
 
 
@@ -94,7 +95,7 @@ class BatchedReinforce(BatchedPUCT):
         dev = self.actor_device()
         logps, ents = [], []
         for rows, n, idx in self.decisions:
-            (logits,) = self.actor(rows.to(dev))
+            (logits,) = train_forward(self.actor, rows.to(dev))
             logp = torch.log_softmax(logits.reshape(-1, n), dim=1)
             logps.append(logp.gather(1, idx.to(dev).long()[:, None])[:, 0])
             ents.append(-(logp.exp() * logp).sum(dim=1))
