@@ -173,26 +173,29 @@ __global__ __launch_bounds__(64) void k_league_mcs(DevState s, LeagueStepArgs a)
     wmt_load(m, s.mt + g * kMtN, s.mt_pos[g], lane);
     int32_t q6s = 0;
     for (uint32_t p = 0; p < k; p++) {  // GameSession.play_game: agents in seat order (play.py:38-41)
+        Hand hp = G.hand[0];  // seat p's hand by a select chain (a runtime index would keep G in scratch)
+#pragma unroll
+        for (int j = 1; j < N; j++) hp = (p == (uint32_t)j) ? G.hand[j] : hp;
         const uint32_t agent = (lg >> (4 + 4 * p)) & 15u;
         const uint32_t kind = (uint32_t)((a.kinds >> (4 * agent)) & 15u);
         uint32_t card = 0xFFu;
         if (kind == SN_AGENT_RANDOM) {
             const uint32_t mx = G.n - 1u;
             wmt_draws(m, 1u, [&](uint32_t) -> uint32_t { return mx; }, L.dr, lane);
-            card = hand_get(G.hand[p], L.dr[0]);
+            card = hand_get(hp, L.dr[0]);
         } else if (kind == SN_AGENT_MCS) {
             const int64_t dn = g * N + p;
             u32x4 mem = {s.lmem[dn], s.lmem[DN + dn], s.lmem[2 * DN + dn], s.lmem[3 * DN + dn]};
-            mem = memorize(mem, G.n, (uint32_t)kMaxCards, G.hand[p], G.b);  // mcts.py:47-49, 62-73
+            mem = memorize(mem, G.n, (uint32_t)kMaxCards, hp, G.b);  // mcts.py:47-49, 62-73
             if (lane == 0u) s.lmem[dn] = mem.x, s.lmem[DN + dn] = mem.y, s.lmem[2 * DN + dn] = mem.z, s.lmem[3 * DN + dn] = mem.w;
             bool q6 = false;
             const int mpc = a.mpc[agent], mmax = a.mmax[agent];
             switch (k) {  // the playouts seat the game's k players (mcts.py:62-64)
-                case 2: card = wmcs_decide<2>(m, L, G.b, G.hand[p], G.n, mem, mpc, mmax, &q6, lane); break;
-                case 3: card = wmcs_decide<3>(m, L, G.b, G.hand[p], G.n, mem, mpc, mmax, &q6, lane); break;
-                case 4: card = wmcs_decide<4>(m, L, G.b, G.hand[p], G.n, mem, mpc, mmax, &q6, lane); break;
-                case 5: card = wmcs_decide<5>(m, L, G.b, G.hand[p], G.n, mem, mpc, mmax, &q6, lane); break;
-                default: card = wmcs_decide<6>(m, L, G.b, G.hand[p], G.n, mem, mpc, mmax, &q6, lane); break;
+                case 2: card = wmcs_decide_inl<2>(m, L, G.b, hp, G.n, mem, mpc, mmax, &q6, lane); break;
+                case 3: card = wmcs_decide_inl<3>(m, L, G.b, hp, G.n, mem, mpc, mmax, &q6, lane); break;
+                case 4: card = wmcs_decide_inl<4>(m, L, G.b, hp, G.n, mem, mpc, mmax, &q6, lane); break;
+                case 5: card = wmcs_decide_inl<5>(m, L, G.b, hp, G.n, mem, mpc, mmax, &q6, lane); break;
+                default: card = wmcs_decide_inl<6>(m, L, G.b, hp, G.n, mem, mpc, mmax, &q6, lane); break;
             }
             q6s |= q6 ? 1 : 0;
         }

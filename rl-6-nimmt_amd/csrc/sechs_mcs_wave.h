@@ -208,10 +208,14 @@ struct WmcsLds {
 // MCSAgent._mcts + _choose_action_from_outcomes (mcts.py:91-106, 156-172) for
 // a game of K players, on the wave's stream: the chosen card; *q6 when some
 // legal move got no playout (the reference raises IndexError, quirk Q6)
+// (inlined into the league step kernel: there the stream cursor, the card
+// memory and the hands then stay in registers -- 225 -> 138 VGPRs, league MCS
+// step 164 -> 106 ms per run.py round; the one-decision drop-in kernel keeps
+// the out-of-line form, wmcs_decide below)
 template <int K>
-__device__ uint32_t wmcs_decide(WaveMt& m, WmcsLds& L, const Board& root, const Hand& me, uint32_t n, u32x4 avail,
-                                int mc_per_card, int mc_max, bool* q6, uint32_t lane, int32_t* sums_out = nullptr,
-                                int32_t* counts_out = nullptr) {
+__device__ __forceinline__ uint32_t wmcs_decide_inl(WaveMt& m, WmcsLds& L, const Board& root, const Hand& me, uint32_t n,
+                                                    u32x4 avail, int mc_per_card, int mc_max, bool* q6, uint32_t lane,
+                                                    int32_t* sums_out = nullptr, int32_t* counts_out = nullptr) {
     int64_t fact = 1;
     for (uint32_t i = 2; i <= n; i++) fact *= i;
     const uint32_t n_mc = (uint32_t)min((int64_t)mc_max, (int64_t)mc_per_card * fact);
@@ -277,6 +281,13 @@ __device__ uint32_t wmcs_decide(WaveMt& m, WmcsLds& L, const Board& root, const 
     }
     *q6 = missing;
     return hand_get(me, best);
+}
+
+template <int K>
+__device__ uint32_t wmcs_decide(WaveMt& m, WmcsLds& L, const Board& root, const Hand& me, uint32_t n, u32x4 avail,
+                                int mc_per_card, int mc_max, bool* q6, uint32_t lane, int32_t* sums_out = nullptr,
+                                int32_t* counts_out = nullptr) {
+    return wmcs_decide_inl<K>(m, L, root, me, n, avail, mc_per_card, mc_max, q6, lane, sums_out, counts_out);
 }
 
 }  // namespace sechs
