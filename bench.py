@@ -394,13 +394,21 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
     fused = eng.fused_mlp and eng._net is not None and eng._net.fused() is not None
     seats = fused and eng.mlp_layer1 == "seats"
     tflops = eng.rows_evaluated * 29800 / wall / 1e12
+    sq4 = None  # SQ counters of the rollout MLP kernel (tools/r04_puct_pmc.sh, eager launches)
+    try:
+        c = json.load(open(os.path.join(ROOT, "profiles", "r04_sq_config4_kernels.json")))["k_puct_mlp_seats"]
+        sq4 = {"mfma_busy_cycles_per_launch": c["SQ_VALU_MFMA_BUSY_CYCLES"] / c["dispatches_per_pass"],
+               "valu_per_wave": c["SQ_INSTS_VALU_per_wave"], "mfma_per_wave": c["SQ_INSTS_MFMA"] / c["SQ_WAVES"],
+               "source": "profiles/r04_sq_config4_kernels.json"}
+    except (OSError, KeyError, ValueError, ZeroDivisionError):
+        pass
     if fused:
         # the rollout MLP runs as sn_puct_mlp (one MFMA kernel after a
         # per-seat PyTorch GEMM): no activation tensor in HBM; priced as the
         # reference's 29 800 FLOP per candidate row against the dense bf16
         # MFMA peak, over the whole game's wall time (every kernel included)
         roof = {"bound": "mfma", "achieved": tflops, "peak": 2500.0, "unit": "TFLOP/s", "frac": tflops / 2500.0,
-                "traffic": None, "algo_flop_per_row": 29800,
+                "traffic": None, "algo_flop_per_row": 29800, "sq": sq4,
                 "kernel": ("rollout step = sn_puct_mlp_seats (MFMA: seat rows, layer 1 per seat, card column, "
                            "layer 2, head in one persistent kernel) + k_puct_step_seats; whole-game wall time") if seats
                 else ("rollout step = sn_puct_seat_rows + PyTorch GEMM (layer 1, per seat) + sn_puct_mlp (MFMA: "
