@@ -72,6 +72,8 @@ def parse():
     ap.add_argument("--pipe-gpw", type=int, default=64, choices=[32, 64], help="games per k_play wave (pipelined path)")
     ap.add_argument("--play-split", type=int, default=None, choices=[0, 1],
                     help="SN_OPT_PLAY_SPLIT (default: the library's)")
+    ap.add_argument("--play-quad", type=int, default=None, choices=[0, 1],
+                    help="SN_OPT_PLAY_QUAD: four lanes per game, k_play_quad (default: the library's, 0)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-philox", action="store_true", help="skip the philox-mode leg of config 2")
@@ -452,7 +454,7 @@ def bench_league(world, rank, slots, rounds, warmup=2, K=5, lo=2, hi=4):
     rank.  Then the RCCL score gather: all_reduce of the per-agent sums and
     all_gather of every game's record, Elo replayed on rank 0 (host C++) in
     canonical order -- timed separately."""
-    from rl_6_nimmt.distributed import gather_league_records, max_over_ranks, reduce_agent_stats
+    from rl_6_nimmt.distributed import backend_label, gather_league_records, max_over_ranks, reduce_agent_stats
     from rl_6_nimmt.league import BatchedTournament, replay_league_elo
 
     t = BatchedTournament(slots, lo, hi, seed=0, game_offset=rank * slots, rng="numpy")
@@ -479,7 +481,7 @@ def bench_league(world, rank, slots, rounds, warmup=2, K=5, lo=2, hi=4):
 
     timed = t.all_records()  # the timed rounds only
     stats = reduce_agent_stats(league_agent_stats(timed, K, hi))
-    allrec = gather_league_records(timed)
+    allrec = gather_league_records(timed, dst=0)  # the Elo replay runs on rank 0 only
     torch.cuda.synchronize()
     gather_ms = (time.perf_counter() - tg) * 1e3
     if world > 1:
@@ -502,8 +504,8 @@ def bench_league(world, rank, slots, rounds, warmup=2, K=5, lo=2, hi=4):
             "wall_s": wall,
             "ms_per_round": wall / rounds * 1e3,
             "score_gather_ms": gather_ms,
-            "score_gather": f"RCCL all_reduce of [{K}, 4] per-agent sums + all_gather of {games} game records "
-                            f"({allrec.numel() * 4 / 1e6:.1f} MB)" if world > 1 else "single rank (no collective)",
+            "score_gather": f"{backend_label()} all_reduce of [{K}, 4] per-agent sums + gather to rank 0 of {games} "
+                            f"game records ({allrec.numel() * 4 / 1e6:.1f} MB)" if world > 1 else "single rank (no collective)",
             "elo_replay_ms": elo_ms,
             "agents": {f"DrunkHamster_{i}": {"games": int(s[i, 0]), "mean_score": s[i, 1] / s[i, 0],
                                               "mean_position": s[i, 2] / s[i, 0], "win_fraction": s[i, 3] / s[i, 0],
@@ -542,7 +544,7 @@ def bench_league_mixed(world, rank, slots, mc_max=200, rounds=1, warmup=1):
     whole game, then every net agent's batched update), then the RCCL
     gather of the per-agent sums and every game record + the rank-0 Elo
     replay."""
-    from rl_6_nimmt.distributed import gather_league_records, max_over_ranks, reduce_agent_stats
+    from rl_6_nimmt.distributed import backend_label, gather_league_records, max_over_ranks, reduce_agent_stats
     from rl_6_nimmt.league import BatchedTournament, replay_league_elo
 
     # warm-up: `warmup` untimed rounds of the SAME league at full size, so
@@ -587,7 +589,7 @@ def bench_league_mixed(world, rank, slots, mc_max=200, rounds=1, warmup=1):
     from rl_6_nimmt.league import league_agent_stats
 
     stats = reduce_agent_stats(league_agent_stats(recs, K, 4))
-    allrec = gather_league_records(recs)
+    allrec = gather_league_records(recs, dst=0)  # the Elo replay runs on rank 0 only
     torch.cuda.synchronize()
     gather_ms = (time.perf_counter() - tg) * 1e3
     if world > 1:
@@ -615,8 +617,8 @@ def bench_league_mixed(world, rank, slots, mc_max=200, rounds=1, warmup=1):
             "policy_rows_per_round": {n: r / rounds for n, r in rows.items()},
             "phases": phases,
             "score_gather_ms": gather_ms,
-            "score_gather": f"RCCL all_reduce of [{K}, 4] per-agent sums + all_gather of {games} game records"
-                            if world > 1 else "single rank (no collective)",
+            "score_gather": f"{backend_label()} all_reduce of [{K}, 4] per-agent sums + gather to rank 0 of {games} "
+                            f"game records" if world > 1 else "single rank (no collective)",
             "elo_replay_ms": elo_ms,
             "agents": {n: {"games": int(s[i, 0]), "mean_score": s[i, 1] / max(1, s[i, 0]),
                            "win_fraction": s[i, 3] / max(1, s[i, 0]), "elo": float(elos[i])}
@@ -842,7 +844,7 @@ def main():
     B = args.games
     env = VecSechsNimmtEnv(B, N_PLAYERS, seed=0, game_offset=rank * B, rng=args.rng)
     if args.rng == "numpy":
-        env.set_option(pipe_gpw=args.pipe_gpw, play_split=args.play_split)
+        env.set_option(pipe_gpw=args.pipe_gpw, play_split=args.play_split, play_quad=args.play_quad)
     env.reset()
     out = make_out(env, B, not args.no_obs)
     wall, kern_ms, kt = time_rollouts(env, out, args.steps, args.warmup, world)

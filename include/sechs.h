@@ -158,11 +158,16 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          1 (default) or 0 (never).  Measured (65 536 x 4p):
                          74 -> 59 us per 10 env-steps.  Numpy-compat handles
                          always use the pipelined one-wave k_play.
-   A pipelined (numpy-compat) handle records its ordering events on the
-   stream of the last pipelined rollout when later work needs them: that
-   stream must outlive the handle's next call (torch's streams always do). */
+     SN_OPT_PLAY_QUAD    1: pipelined numpy-compat DrunkHamster rollouts of
+                         a 4-player handle (no tournament, obs rows of 48
+                         bytes or none) run k_play_quad, four lanes per game;
+                         0 (default): the one-lane k_play.  Same words, same
+                         outputs (the GPU tests run both).
+   A pipelined (numpy-compat) rollout records its ordering event on the
+   caller's stream before it returns; later calls only wait on that event,
+   so the caller may destroy the stream after the call. */
 enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3, SN_OPT_TIMING = 4, SN_OPT_PIPE_GPW = 5,
-       SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7 };
+       SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7, SN_OPT_PLAY_QUAD = 8 };
 sn_status sn_set_option(sn_env* env, int option, int value);
 /* pipelined rollouts whose draws ran past the twisted words (must be 0; a
    nonzero count means those games' draws are wrong) [sync].  The count is
@@ -188,10 +193,13 @@ sn_status sn_debug_phases(uint64_t* out, int n);
 /* ---- One-game fast path (the scalar drop-in SechsNimmtEnv) ------------
    For a handle of B == 1: one kernel launch and one stream sync per call
    (host-memory arguments and results; pinned, device-mapped buffer inside
-   the handle).  out_host: int32 [2 + 2N + 12N] = first illegal seat or -1
+   the handle).  out_host: int32 [2 + 15N] = first illegal seat or -1
    (env.py:114-118; nothing changes then), done, rewards [N] (env.py:64-77),
    scores [N] (penalties so far), then the N observation rows as int8 bytes,
-   48 per seat (47 used, env.py:174-212). [sync] */
+   48 per seat (47 used, env.py:174-212), then per seat the placement of its
+   card for the debug trace (env.py:128,145,165): target row | undercut
+   (_pick_row_to_replace) << 2 | scored (_score_row) << 3 | penalty << 8
+   (all 0 after an illegal step or a reset). [sync] */
 sn_status sn_step1(sn_env* env, const int32_t* actions_host, int32_t* out_host, int flags);
 /* env.py:43-51 reset() drawing from the numpy legacy state (key, pos) given
    -- np.random.get_state() -- and returning the advanced state for

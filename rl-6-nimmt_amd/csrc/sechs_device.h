@@ -154,8 +154,9 @@ __device__ __forceinline__ uint32_t card_at(uint32_t lo, uint32_t hi, int i) {
 }
 
 // place card c on the board (env.py:127-134 for one card); returns the
-// bull heads its player takes
-__device__ __forceinline__ uint32_t place_card(Board& b, uint32_t c) {
+// bull heads its player takes.  info (the drop-in env's debug trace,
+// env.py:128,145,165): target row | undercut << 2 | scored << 3
+__device__ __forceinline__ uint32_t place_card(Board& b, uint32_t c, uint32_t* info = nullptr) {
     const uint32_t h[4] = {b.hi.x, b.hi.y, b.hi.z, b.hi.w};
     // _find_row: the row whose last card is the largest one below c
     int best = -1;
@@ -185,6 +186,7 @@ __device__ __forceinline__ uint32_t place_card(Board& b, uint32_t c) {
     const uint32_t len = len_of(hi_t);
     const bool take = under || len == (uint32_t)(kThreshold - 1);  // 6th card, env.py:133
     const uint32_t penalty = take ? heads_in(hi_t) : 0u;           // _score_row: the whole old row
+    if (info) *info = (uint32_t)tr | (under ? 4u : 0u) | (take ? 8u : 0u);
     const uint32_t lo_new = take ? c : (lo_t | (len < 4u ? (c << (8u * len)) : 0u));
     const uint32_t hi_new = take ? ((1u << 8) | (hc << 16) | (c << 24))
                                  : ((len == 4u ? c : (hi_t & 0xFFu)) | ((len + 1u) << 8) |
@@ -205,7 +207,8 @@ __device__ __forceinline__ uint32_t place_card(Board& b, uint32_t c) {
 // SKIP: seats whose card is 0xFF (absent: a tournament game with fewer
 // players than the handle's seats) play nothing.
 template <int N, bool SKIP = false>
-__device__ __forceinline__ void resolve(Board& b, const uint32_t (&card)[N], uint32_t (&pen)[N]) {
+__device__ __forceinline__ void resolve(Board& b, const uint32_t (&card)[N], uint32_t (&pen)[N],
+                                        uint32_t* trace = nullptr) {
     uint32_t key[N];
 #pragma unroll
     for (int p = 0; p < N; p++) key[p] = (card[p] << 4) | (uint32_t)p;
@@ -221,8 +224,10 @@ __device__ __forceinline__ void resolve(Board& b, const uint32_t (&card)[N], uin
 #pragma unroll
     for (int k = 0; k < N; k++) {
         if (SKIP && (key[k] >> 4) >= 0xFFu) break;  // absent seats sort last
-        const uint32_t penalty = place_card(b, key[k] >> 4);
+        uint32_t info = 0u;
+        const uint32_t penalty = place_card(b, key[k] >> 4, trace ? &info : nullptr);
         const uint32_t p = key[k] & 15u;
+        if (trace) trace[p] = info | (penalty << 8);  // per seat: its card's row, flags, penalty
 #pragma unroll
         for (int q = 0; q < N; q++) pen[q] += (p == (uint32_t)q) ? penalty : 0u;
     }

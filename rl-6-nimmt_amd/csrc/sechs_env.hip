@@ -702,6 +702,8 @@ __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
     play_body<N, MODE, GPW, LG>(s, a, lds_dyn, (int)threadIdx.x);
 }
 
+#include "sechs_quad.h"
+
 // ---- one-game fast path (the scalar drop-in SechsNimmtEnv, B == 1) -------
 // One launch per env.step / env.reset: the actions arrive as kernel
 // arguments, the results (invalid seat, done, rewards, scores, int8 obs rows)
@@ -709,7 +711,9 @@ __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
 // device-mapped host words, so a call is one launch + one stream sync
 // instead of a chain of blocking copies.  Words of hbuf:
 constexpr int kH1In = 0;      // [624] key, [624] numpy pos        (sn_reset1 in)
-constexpr int kH1Out = 1024;  // [0] invalid, [1] done, [2, 2+N) rewards, [2+N, 2+2N) scores, obs bytes N x 48
+constexpr int kH1Out = 1024;  // [0] invalid, [1] done, [2, 2+N) rewards, [2+N, 2+2N) scores, obs bytes N x 48,
+                              // [kH1Trace, +N) per seat: row | undercut << 2 | scored << 3 | penalty << 8 (sn_step1)
+constexpr int kH1Trace = 160;  // words into the out block (past 2 + 14 N for N <= 10)
 constexpr int kH1Mt = 2048;   // [624] key, [624] code, [625] mt0  (sn_reset1 out)
 constexpr int kH1Words = 4096;
 
@@ -755,11 +759,14 @@ __global__ void k_step1(DevState s, Acts1 acts, uint32_t* hb, int summ) {
     if (bad < 0) {
 #pragma unroll
         for (int p = 0; p < N; p++) hand_del(G.hand[p], idx[p]);
-        resolve<N>(G.b, card, pen);
+        uint32_t trace[N];
+        resolve<N>(G.b, card, pen, trace);
 #pragma unroll
         for (int p = 0; p < N; p++) G.score[p] += (int32_t)pen[p];
         G.n -= 1u;
         store_game<N>(s, 0, G);
+#pragma unroll
+        for (int p = 0; p < N; p++) out[kH1Trace + p] = trace[p];
     }
     out[0] = (uint32_t)bad;
     out[1] = (G.n == 0u) ? 1u : 0u;
@@ -1223,6 +1230,10 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
     sn_env* e = new (std::nothrow) sn_env();
     if (!e) return fail(SN_ENOMEM, "host allocation failed");
     e->device = device;
+    if (hipDeviceGetAttribute(&e->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || e->cus < 1) {
+        delete e;
+        return fail(SN_EHIP, "cannot query the device's CU count");
+    }
     DevState& s = e->s;
     s.B = num_games, s.N = num_players, s.C = num_cards, s.rng_mode = rng_mode;
     s.seed = seed, s.game_offset = game_offset;
@@ -1251,6 +1262,11 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
     e->pipe_lead = kPipeLead;
     e->phase = -1;
     e->play_split = 1;
+    e->play_quad = 0;  // measured: k_play_quad alone is no faster and slows the concurrent twist
+    {
+        const char* ps = getenv("SECHS_PIPE_SERIAL");
+        e->pipe_serial = (ps && ps[0] == '1') ? 1 : 0;
+    }
     e->pvalid = 0;
     e->pcount = 0;
     if (rng_mode == SN_RNG_NUMPY_MT) {
@@ -1368,6 +1384,10 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
         case SN_OPT_PLAY_SPLIT:
             if (value < 0 || value > 1) return fail(SN_EINVAL, "play split must be 0 or 1");
             e->play_split = value;
+            return SN_OK;
+        case SN_OPT_PLAY_QUAD:
+            if (value < 0 || value > 1) return fail(SN_EINVAL, "play quad must be 0 or 1");
+            e->play_quad = value;
             return SN_OK;
         case SN_OPT_PIPE_LEAD:
             if (value < 64 || value > kPipeLead) return fail(SN_EINVAL, "pipe lead must be in 64..600");
@@ -1533,9 +1553,10 @@ sn_status sn_pipe_sync(sn_env* e, hipStream_t st) {
     // k_pipe_code reads the last k_play's consumer position (pabsc) and the
     // last k_mt_ahead's twisted end: wait for both, whatever stream `st` is
     // (the null stream does not order behind a non-blocking caller stream).
-    // The events are recorded here, behind everything enqueued so far on
-    // the play stream and the side stream, not once per launch.
-    HIP_TRY(hipEventRecord(e->ev_play, e->pstream));
+    // ev_play was recorded behind the last pipelined k_play when its rollout
+    // was enqueued (launch_pipe), on the caller's stream of that call -- so no
+    // stream of an earlier call is touched here; ev_prep is recorded now,
+    // behind everything enqueued so far on the side stream.
     HIP_TRY(hipStreamWaitEvent(st, e->ev_play, 0));
     HIP_TRY(hipEventRecord(e->ev_prep, e->side));
     HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));
@@ -1611,12 +1632,8 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(e->ev_prep, st));
         e->pvalid = 1;
-        e->pstream = st;
-    }
-    if (st != e->pstream) {  // another caller stream: order behind the last play launch
-        HIP_TRY(hipEventRecord(e->ev_play, e->pstream));
+    } else if (st != e->play_st) {  // another caller stream: order behind the last pipelined k_play
         HIP_TRY(hipStreamWaitEvent(st, e->ev_play, 0));
-        e->pstream = st;
     }
     const int64_t B = s.B, N = s.N;
     // a tournament game adds its seat draw (<= K - 1 + 1 draws): 10-step
@@ -1625,6 +1642,13 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     const int chunk = min(e->chunk_steps, (s.lg_K > 8) ? 5 : pipe_max_chunk(s.N));
     const unsigned nblk = (gpw == 32) ? (unsigned)((s.B + 32 * (kBlock / 64) - 1) / (32 * (kBlock / 64)))
                                       : (unsigned)grid_for(s.B);
+    // four lanes per game (k_play_quad): N = 4 DrunkHamster seats, 48-byte
+    // 16-B aligned obs rows (or none); anything else keeps k_play
+    const bool quad = e->play_quad && gpw == 64 && N == 4 && !s.lg_K && !a.actions && !a.invalid &&
+                      (!a.obs || (a.obs_stride == 48 && (((uintptr_t)a.obs) & 15) == 0));
+    const size_t qshmem = (size_t)kQuadWave * (kBlock / 64);
+    const unsigned qblk = (unsigned)((s.B + kQuadGames * (kBlock / 64) - 1) / (kQuadGames * (kBlock / 64)));
+    if (quad) HIP_TRY(hipFuncSetAttribute((const void*)k_play_quad, hipFuncAttributeMaxDynamicSharedMemorySize, (int)qshmem));
     for (int t0 = 0; t0 < a.steps; t0 += chunk) {
         PlayArgs c = a;
         c.steps = min(chunk, a.steps - t0);
@@ -1639,12 +1663,17 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         HIP_TRY(hipEventRecord(e->ev_main, st));         // the previous launch's consumption is final
         hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
         if (tv) HIP_TRY(hipEventRecord(tv[0], st));
-        {
+        if (quad) {
+            hipLaunchKernelGGL(k_play_quad, dim3(qblk), dim3(kBlock), qshmem, st, s, c);
+            HIP_TRY(hipGetLastError());
+        } else {
             const sn_status r = pipe_play(s, c, gpw, nblk, shmem, st);
             if (r != SN_OK) return r;
         }
         if (tv) HIP_TRY(hipEventRecord(tv[1], st));
-        // the next launch's twist, beside this one: leads the consumer of the launch before
+        // the next launch's twist, beside this one: leads the consumer of the launch before.
+        // SECHS_PIPE_SERIAL=1 (diagnostics: solo kernel times) orders it after this launch instead
+        if (e->pipe_serial) HIP_TRY(hipEventRecord(e->ev_main, st));
         HIP_TRY(hipStreamWaitEvent(e->side, e->ev_main, 0));
         if (tv) HIP_TRY(hipEventRecord(tv[2], e->side));
         hipLaunchKernelGGL(k_mt_ahead<false>, pg, dim3(kBlock), 0, e->side, s,
@@ -1654,6 +1683,11 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         HIP_TRY(hipEventRecord(e->ev_prep, e->side));
         e->pcount++;
     }
+    // behind this rollout's last k_play, on the caller's stream of THIS call:
+    // the next call (or sn_pipe_sync) orders behind it without touching a
+    // stream the caller may have destroyed since (one record per rollout)
+    HIP_TRY(hipEventRecord(e->ev_play, st));
+    e->play_st = st;
     return SN_OK;
 }
 
@@ -1969,9 +2003,12 @@ static sn_status h1_ready(sn_env* e) {
     return SN_OK;
 }
 
-static void h1_copy_out(const sn_env* e, int32_t* out) {
+// out_host: the 2 + 14 N result words, then N trace words (sn_step1; zeros for a reset)
+static void h1_copy_out(const sn_env* e, int32_t* out, bool trace) {
     const int N = e->s.N;
     std::memcpy(out, e->hbuf + kH1Out, sizeof(uint32_t) * (2 + 2 * N + 12 * N));
+    if (trace) std::memcpy(out + 2 + 14 * N, e->hbuf + kH1Out + kH1Trace, sizeof(uint32_t) * N);
+    else std::memset(out + 2 + 14 * N, 0, sizeof(uint32_t) * N);
 }
 
 sn_status sn_step1(sn_env* e, const int32_t* actions_host, int32_t* out_host, int flags) {
@@ -1986,7 +2023,7 @@ sn_status sn_step1(sn_env* e, const int32_t* actions_host, int32_t* out_host, in
     SN_DISPATCH_N(e->s.N, hipLaunchKernelGGL((k_step1<NN>), dim3(1), dim3(64), 0, 0, e->s, a, e->hbuf_dev, summ));
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(0));
-    h1_copy_out(e, out_host);
+    h1_copy_out(e, out_host, true);
     return SN_OK;
 }
 
@@ -2006,7 +2043,7 @@ sn_status sn_reset1(sn_env* e, const uint32_t* key_host, int32_t pos, uint32_t* 
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(0));
     e->phase = 0;  // one game, just dealt
-    h1_copy_out(e, out_host);
+    h1_copy_out(e, out_host, false);
     // the advanced state in numpy's (key, pos) form, as sn_mt_get
     std::memcpy(key_out_host, e->hbuf + kH1Mt, sizeof(uint32_t) * kMtN);
     const uint32_t code = e->hbuf[kH1Mt + kMtN];

@@ -1259,12 +1259,7 @@ sn_status sn_puct_mlp_seats(sn_env* e, const sn_puct* q, int n_cur, const void* 
         return set_error(SN_EINVAL, "w1s / w2 / w1c / head must be 16-B aligned");
     const int64_t S = a.D * e->s.N;
     if (S * n_cur >= (1ll << 31)) return set_error(SN_EINVAL, "too many rows");
-    static int cus = 0;  // persistent grid: two workgroups per CU (the kernel's occupancy)
-    if (!cus) {
-        int dev = 0;
-        HIP_TRY(hipGetDevice(&dev));
-        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    }
+    const int cus = e->cus;  // persistent grid: two workgroups per CU (the kernel's occupancy) of the handle's device
     const int64_t groups = (S + kSeatBlock - 1) / kSeatBlock;
     hipLaunchKernelGGL(k_puct_mlp_seats, dim3((unsigned)std::min<int64_t>(groups, 2ll * cus)), dim3(kBlock), 0,
                        (hipStream_t)stream, a, e->s.N, n_cur, (const uint16_t*)w1s, w1c, (const uint16_t*)w2, head,

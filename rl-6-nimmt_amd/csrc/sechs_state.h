@@ -819,6 +819,7 @@ inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBloc
 
 struct sn_env {
     int device;
+    int cus;          // compute units of `device` (persistent grids size by it)
     int chunk_steps;  // SN_OPT_CHUNK_STEPS
     int pipe;         // SN_OPT_PIPELINE
     int pipe_gpw;     // SN_OPT_PIPE_GPW: games per k_play wave on the pipelined path (32 or 64)
@@ -828,14 +829,16 @@ struct sn_env {
     int lg_mpc[16], lg_mmax[16];  // MCSAgent agents: mc_per_card, mc_max
     int phase;        // every game's env-steps since its deal, mod 10, when they are in lockstep; -1 unknown
     int play_split;   // SN_OPT_PLAY_SPLIT: role-split k_play for lockstep DrunkHamster rollouts
+    int play_quad;    // SN_OPT_PLAY_QUAD: four lanes per game (k_play_quad) on the pipelined N = 4 path
+    int pipe_serial;  // SECHS_PIPE_SERIAL=1 (diagnostics): each twist waits for the play launch before it (no overlap)
     sechs::DevState s;
     // pipelined twist-ahead (sechs_env.hip launch_pipe): a k_mt_ahead for the
     // next play launch may be in flight on `side` (ev_prep) after a rollout
     int pvalid;         // ring + ptend/pabsc/ptp are the live RNG state (mt_pos is stale)
     uint64_t pcount;    // play launches so far (parity selects the pabsc / ptend buffers)
     hipStream_t side;
-    hipEvent_t ev_prep, ev_main, ev_play;  // ev_play: after the last pipelined k_play (caller's stream)
-    hipStream_t pstream;      // stream of the last pipelined k_play
+    hipEvent_t ev_prep, ev_main, ev_play;  // ev_play: after the last pipelined k_play (recorded on that call's stream)
+    hipStream_t play_st;  // that stream's handle VALUE, compared only (never used: the caller may destroy it)
     uint32_t* perr_host;                    // pinned, device-mapped mirror of s.perr (PlayArgs::perr_mirror)
     uint32_t* perr_host_dev;
     uint32_t* hbuf;      // one-game fast path (sn_step1 / sn_reset1): pinned, device-mapped exchange words

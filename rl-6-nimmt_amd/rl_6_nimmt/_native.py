@@ -22,6 +22,7 @@ SN_I8, SN_I16, SN_I32, SN_I64, SN_F32 = 1, 2, 3, 4, 5
 SN_AUTO_RESET, SN_NO_SUMMARIES = 1, 2
 SN_OPT_RING_WORDS, SN_OPT_CHUNK_STEPS, SN_OPT_PIPELINE, SN_OPT_TIMING, SN_OPT_PIPE_GPW, SN_OPT_PIPE_LEAD = 1, 2, 3, 4, 5, 6
 SN_OPT_PLAY_SPLIT = 7
+SN_OPT_PLAY_QUAD = 8
 SN_AGENT_RANDOM, SN_AGENT_MCS, SN_AGENT_EXTERNAL = 0, 1, 2
 
 class SnPuct(ctypes.Structure):

@@ -10,6 +10,9 @@ data path).  After a block of games:
     (tournament.py:157-164) in global game-id order;
   * `gather_league_records`: the same for the batched tournament's records
     (league.py), which carry no id column: rank order is global slot order.
+    With `dst` the records go to that rank only (dist.gather): the bench's
+    Elo replay runs on rank 0 alone; a distributed BatchedTournament keeps
+    the all_gather, since every rank ranks the same roster for `evolve`.
 Works with any torch.distributed backend (nccl = RCCL on the GPUs, gloo on
 CPU): every helper hands the collective a tensor on the device the process
 group's backend takes (`collective_device`: RCCL takes device tensors only,
@@ -74,6 +77,28 @@ def all_gather_cat(t, dim=0):
     return torch.cat(parts, dim=dim).to(t.device)
 
 
+def gather_cat_to(t, dst=0, dim=0):
+    """every rank's `t` (same shape on every rank) concatenated along `dim`
+    in rank order on rank `dst` (on t's device); None on the other ranks"""
+    if not group_active():
+        return t
+    c = _on(t.contiguous(), collective_device())
+    if dist.get_rank() == dst:
+        parts = [torch.empty_like(c) for _ in range(dist.get_world_size())]
+        dist.gather(c, parts, dst=dst)
+        return torch.cat(parts, dim=dim).to(t.device)
+    dist.gather(c, None, dst=dst)
+    return None
+
+
+def backend_label():
+    """the collective library the process group runs on, for result lines"""
+    if not group_active():
+        return "single process (no collective)"
+    b = str(dist.get_backend())
+    return "RCCL" if b == "nccl" else b
+
+
 def gather_game_records(records):
     """records: int32 tensor [G, 1 + 2*N] rows (global game id, seat agent ids, seat scores),
     same G on every rank.  Returns all ranks' rows sorted by global game id."""
@@ -82,12 +107,16 @@ def gather_game_records(records):
     return records[order]
 
 
-def gather_league_records(records):
+def gather_league_records(records, dst=None):
     """Batched-tournament records of this rank, int32 [games, slots, 1 + N]
-    (rank r owns global slots [r*slots, (r+1)*slots)), all_gather'ed (RCCL on
-    the GPUs) into [games, world*slots, 1 + N]: round major, then global slot
-    id -- the canonical order of the Elo replay (league.replay_league_elo)."""
-    return all_gather_cat(records, dim=1)
+    (rank r owns global slots [r*slots, (r+1)*slots)), gathered (RCCL on the
+    GPUs) into [games, world*slots, 1 + N]: round major, then global slot id
+    -- the canonical order of the Elo replay (league.replay_league_elo).
+    dst=None: on every rank (all_gather); dst=r: on rank r only, None on the
+    others (dist.gather -- the Elo replay needs them on one rank)."""
+    if dst is None:
+        return all_gather_cat(records, dim=1)
+    return gather_cat_to(records, dst=dst, dim=1)
 
 
 def max_over_ranks(values, device=None):

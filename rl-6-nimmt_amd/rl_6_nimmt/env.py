@@ -78,7 +78,7 @@ class SechsNimmtEnv:
         self._vec = VecSechsNimmtEnv(1, num_players, num_cards, seed=0, rng="numpy", include_summaries=include_summaries)
         # one-game fast path (sn_step1 / sn_reset1): host-side argument and
         # result buffers, one kernel launch + one sync per call
-        self._out = np.zeros(2 + 2 * num_players + 12 * num_players, dtype=np.int32)
+        self._out = np.zeros(2 + 15 * num_players, dtype=np.int32)  # sn_step1's words (include/sechs.h)
         self._acts = np.zeros(num_players, dtype=np.int32)
         self._key = np.zeros(624, dtype=np.uint32)
         self._pos = ctypes.c_int32()
@@ -139,9 +139,15 @@ class SechsNimmtEnv:
         rewards = self._out[2: 2 + N].copy()
         done = bool(self._out[1])
         self._unpack()
-        if self.verbose:
+        if self.verbose:  # _play_cards' debug lines, cards ascending (env.py:128,145,165)
+            trace = self._out[2 + 14 * N: 2 + 15 * N]
             for card, p in sorted((int(c), p) for p, c in enumerate(acts)):
                 logger.debug(f"{self._player_name(p)} plays card {card + 1}")
+                w = int(trace[p])
+                if w & 4:
+                    logger.debug(f"  ...chooses to replace row {(w & 3) + 1}")
+                if w & 8:
+                    logger.debug(f"  ...and gains {w >> 8} Hornochsen")
         return self._create_states(), rewards, done, dict()
 
     def render(self, mode="human"):
@@ -205,7 +211,7 @@ class SechsNimmtEnv:
         """Python mirrors from the packed fast-path result (scores, obs rows)."""
         N = self._num_players
         self._scores = self._out[2 + N: 2 + 2 * N].copy()
-        rows = self._out[2 + 2 * N:].view(np.int8).reshape(N, 48)
+        rows = self._out[2 + 2 * N: 2 + 14 * N].view(np.int8).reshape(N, 48)
         obs = rows[:, : obs_length(self._include_summaries)].astype(np.int64)
         self._obs = obs
         self._hands = [[int(c) for c in obs[p, :HAND] if c >= 0] for p in range(N)]

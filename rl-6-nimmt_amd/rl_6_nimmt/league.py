@@ -119,16 +119,36 @@ class BatchedTournament:
 
     def __init__(self, num_slots, min_players=2, max_players=4, seed=0, game_offset=0, rng="numpy", device=None,
                  elo_initial=1600, elo_k=32, net_dtype=torch.bfloat16, train=False, fused=True, distributed=False,
-                 baseline_agents=None, baseline_num_games=1, baseline_condition=10):
+                 baseline_agents=None, baseline_num_games=1, baseline_condition=10, updates_per_round=1):
         """distributed=True: this handle is one rank's shard of ONE tournament
         over the initialised process group (every rank constructs it with the
         same roster and calls the same methods): the tallies and Elo that
         evolve / agent_stats / replay_elo use are folded from every rank's
         records (all_gather, canonical order), so every rank keeps the same
-        roster.  False: the tallies are this rank's own (reduce them with
+        roster.  Every accessor that folds records -- evolve, agent_stats,
+        replay_elo, winner, table / __str__, copy_player, remove_player,
+        clear_records -- is then a COLLECTIVE: all ranks must call it, in the
+        same order (one rank alone blocks in the all_gather).  total_games
+        counts every rank's games, and baseline evaluations draw from
+        rank-independent streams, so the ranks' baseline lists agree.
+        False: the tallies are this rank's own (reduce them with
         distributed.reduce_agent_stats), and evolve refuses to run on more
-        than one rank."""
+        than one rank.
+
+        updates_per_round (train=True): Adam steps each PUCT / PUCTCustomed /
+        REINFORCE agent takes per round.  The reference steps once per GAME
+        the agent played (learn() at episode end, play.py:52-67,
+        mcts.py:230-261); a round plays every slot's game at once, so its
+        games' losses are split into k contiguous chunks (by slot) with one
+        step each: 1 (default) = one step on the whole round's loss, "games"
+        = one step per game played (the reference's count; every game's
+        search still used the round's starting weights).  ACER keeps its own
+        update schedule (acer.py).  optimizer_steps[name] counts the steps."""
         assert 0 < min_players <= max_players
+        if updates_per_round != "games" and not (isinstance(updates_per_round, int) and updates_per_round >= 1):
+            raise ValueError('updates_per_round must be an int >= 1 or "games"')
+        self.updates_per_round = updates_per_round
+        self.optimizer_steps = {}
         self.num_slots, self.min_players, self.max_players = int(num_slots), int(min_players), int(max_players)
         self.seed, self.game_offset, self.rng, self.device = int(seed), int(game_offset), rng, device
         self.elo_initial, self.elo_k = float(elo_initial), float(elo_k)
@@ -384,7 +404,12 @@ class BatchedTournament:
             rew = torch.cat(rews, dim=0) if rewards else None
         self.records.append((rec, self._ids.clone()))
         self.record_names.append(tuple(self.active_agents()))
-        self.total_games += int(games) * self.num_slots
+        world = 1
+        if self.distributed:
+            from .distributed import world_size
+
+            world = world_size()  # every rank plays the same number of slots per round
+        self.total_games += int(games) * self.num_slots * world
         return (rec, rew) if rewards else rec
 
     def _phase(self, name):
@@ -485,13 +510,20 @@ class BatchedTournament:
                     continue
                 if eng.D == 0 or not eng.decisions:
                     continue
-                if isinstance(eng, (BatchedPUCTCustomed, BatchedReinforce)):
-                    loss = eng.loss(per_step)
-                else:
-                    loss = eng.policy_loss()
-                agent.optimizer.zero_grad()
-                loss.backward()
-                agent.optimizer.step()
+                # one decider per game of this agent (a game seats distinct agents):
+                # k contiguous decider ranges = k chunks of games
+                D = int(eng.D)
+                k = D if self.updates_per_round == "games" else min(int(self.updates_per_round), D)
+                bounds = [D * c // k for c in range(k + 1)]
+                for d0, d1 in zip(bounds[:-1], bounds[1:]):
+                    if isinstance(eng, (BatchedPUCTCustomed, BatchedReinforce)):
+                        loss = eng.loss(per_step, d0, d1) if k > 1 else eng.loss(per_step)
+                    else:
+                        loss = eng.policy_loss(d0, d1) if k > 1 else eng.policy_loss()
+                    agent.optimizer.zero_grad()
+                    loss.backward()
+                    agent.optimizer.step()
+                    self.optimizer_steps[name] = self.optimizer_steps.get(name, 0) + 1
                 eng.decisions = []
 
     def seats(self):
@@ -557,7 +589,11 @@ class BatchedTournament:
 
         K = 1 + len(self.baseline_agents)
         self._baseline_calls += 1
-        off = (0x40000000 + self._baseline_calls * 0x10000 + self.game_offset) & 0x7FFFFFFF
+        # a distributed tournament folds the same records on every rank and so
+        # runs the same evaluations there: their streams must not depend on
+        # the rank's slot offset, or the ranks' baseline lists would diverge
+        shard_off = 0 if self.distributed else self.game_offset
+        off = (0x40000000 + self._baseline_calls * 0x10000 + shard_off) & 0x7FFFFFFF
         bt = BatchedTournament(evals, K, K, seed=self.seed, game_offset=off, rng="numpy", device=self.device,
                                net_dtype=self.net_dtype, train=False)
         seated = [self.agents[name]] + self.baseline_agents

@@ -493,18 +493,21 @@ class BatchedPUCT:
         return hands.gather(2, k[..., None])[..., 0].to(torch.int32)
 
     # ------------------------------------------------------------ training (mcts.py:230-261)
-    def policy_loss(self):
+    def policy_loss(self, d0=0, d1=None):
         """-sum over recorded decisions of log pi(chosen root move) under the
         current weights (the reference stores log(probs[best]) from the
         rollout that first chose it -- same weights during an episode, so the
         same value).  n == 1 decisions play without search and add log 1 = 0
-        (mcts.py:50-51), so they are not recorded."""
+        (mcts.py:50-51), so they are not recorded.  [d0, d1): the deciders
+        (games) whose terms are summed -- one decider's term is the
+        reference's per-episode loss (mcts.py:244-255)."""
         dev = self.actor_device()
         loss = torch.zeros((), device=dev)
         for rows, n, best in self.decisions:
-            (logits,) = train_forward(self.actor, rows.to(dev))
+            e = best.shape[0] if d1 is None else d1
+            (logits,) = train_forward(self.actor, rows[d0 * n: e * n].to(dev))
             logp = torch.log_softmax(logits.reshape(-1, n), dim=1)
-            loss = loss - logp.gather(1, best.to(dev).long()[:, None]).sum()
+            loss = loss - logp.gather(1, best[d0:e].to(dev).long()[:, None]).sum()
         return loss
 
 
@@ -584,16 +587,19 @@ class BatchedPUCTCustomed(BatchedPUCT):
         seats = [p for p in range(self.env.num_players) if (self.seats_mask >> p) & 1]
         return per_step[:, :, seats].reshape(per_step.shape[0], -1)  # [10, D] in decision order
 
-    def loss(self, per_step=None):
-        """reference loss of the recorded episode (mcts.py:431-451), summed over games"""
+    def loss(self, per_step=None, d0=0, d1=None):
+        """reference loss of the recorded episode (mcts.py:431-451), summed over
+        the games of deciders [d0, d1) (all by default)"""
         per_step = self.episode_rewards if per_step is None else per_step
         dev = self.actor_device()
         target = self._decider_rewards(per_step)[:-1].sum(dim=0).float().to(dev)  # [D]
+        target = target[d0:d1]
         logps, values = [], []
         for rows, n, best in self.decisions:
-            (out,) = train_forward(self.actor, rows.to(dev))
+            e = best.shape[0] if d1 is None else d1
+            (out,) = train_forward(self.actor, rows[d0 * n: e * n].to(dev))
             out = out.reshape(-1, n, 2)
-            best = best.to(dev).long()[:, None]
+            best = best[d0:e].to(dev).long()[:, None]
             logp = torch.log_softmax(out[:, :, 0], dim=1)
             logps.append(logp.gather(1, best)[:, 0])
             values.append(out[:, :, 1].gather(1, best)[:, 0])

@@ -89,19 +89,21 @@ class BatchedReinforce(BatchedPUCT):
             G[:, t] = acc
         return G.float()
 
-    def loss(self, per_step=None):
-        """policy.py:174-196 summed over games, on the recorded rows"""
+    def loss(self, per_step=None, d0=0, d1=None):
+        """policy.py:174-196 summed over the games of deciders [d0, d1) (all by
+        default), on the recorded rows"""
         per_step = self.episode_rewards if per_step is None else per_step
         dev = self.actor_device()
         logps, ents = [], []
         for rows, n, idx in self.decisions:
-            (logits,) = train_forward(self.actor, rows.to(dev))
+            e = idx.shape[0] if d1 is None else d1
+            (logits,) = train_forward(self.actor, rows[d0 * n: e * n].to(dev))
             logp = torch.log_softmax(logits.reshape(-1, n), dim=1)
-            logps.append(logp.gather(1, idx.to(dev).long()[:, None])[:, 0])
+            logps.append(logp.gather(1, idx[d0:e].to(dev).long()[:, None])[:, 0])
             ents.append(-(logp.exp() * logp).sum(dim=1))
         logps, ents = torch.stack(logps, dim=1), torch.stack(ents, dim=1)  # [D, T]
         T = logps.shape[1]
-        G = self.returns(per_step)[:, :T].to(dev)
+        G = self.returns(per_step)[d0:d1, :T].to(dev)
         disc = torch.exp(np.log(self.gamma) * torch.linspace(0, T - 1, T)).to(dev)
         actor_loss = -(disc[None, :] * G * logps).sum()
         entropy_loss = -ents.sum()

@@ -118,6 +118,29 @@ def test_notebook_games_through_dropin_env():
         assert (-env._scores).tolist() == G["final_scores"]
 
 
+def test_notebook_debug_trace_through_dropin_env(caplog):
+    """the drop-in env's verbose log is the reference's -- per
+    step, cards ascending: "<name> (player p) plays card c" (env.py:128), on
+    an undercut "  ...chooses to replace row r" (env.py:145), on a scored row
+    "  ...and gains h Hornochsen" (env.py:165) -- line for line against the
+    notebook's rendered DEBUG output (F1 `trace`)."""
+    import logging
+
+    from rl_6_nimmt import SechsNimmtEnv
+
+    games = load("notebook_games.json")["games"]
+    assert sum(any("chooses" in x for x in G["trace"]) for G in games) >= 3
+    for G in games:
+        env = SechsNimmtEnv(len(G["names"]), player_names=G["names"], verbose=True)
+        env.reset_to([list(r) for r in G["board"]], [list(h) for h in G["hands"]])
+        caplog.clear()
+        with caplog.at_level(logging.DEBUG, logger="rl_6_nimmt.env"):
+            for acts in G["actions"]:
+                env.step(acts)
+        got = [r.getMessage() for r in caplog.records if r.name == "rl_6_nimmt.env" and r.levelno == logging.DEBUG]
+        assert got == G["trace"]
+
+
 def test_tournament_dropin_plays_games():
     from rl_6_nimmt import Tournament
     from rl_6_nimmt.agents import DrunkHamster, MCSAgent

@@ -582,3 +582,38 @@ def test_pipelined_full_size_across_streams():
             assert np.array_equal(acts[:, idx[j]], ra[:, 0]), (e, j)
     torch.cuda.synchronize()
     assert env.pipe_errors() == 0
+
+
+@pytest.mark.parametrize("B,summ", [(65536, True), (1000, True), (4104, False)])
+def test_quad_kernel_equals_one_lane_kernel(B, summ):
+    """k_play_quad (four lanes per game: seat / row lanes, DPP quad
+    reductions, SN_OPT_PLAY_QUAD) and the one-lane k_play consume the same
+    numpy-MT words and emit identical rewards, actions, done and int8 obs --
+    launch patterns 10 / 1 / 7 / 23 steps (episodes cross launches), with
+    and without obs; then hands, scores, results and the exported numpy
+    states agree, and a 1-game reference session check via the oracle."""
+    outs = {}
+    for quad in (1, 0):
+        env = venv(B, 4, seed=77, rng="numpy", include_summaries=summ)
+        env.set_option(play_quad=quad)
+        env.reset()
+        got = []
+        for T, obs in ((10, True), (1, True), (7, False), (23, True)):
+            o = env.rollout(T, want_actions=True, want_obs=obs, check=True)
+            got.append({k: v.cpu().numpy() for k, v in o.items()})
+        s, e = env.results()
+        got.append({"hands": env.hands().cpu().numpy(), "scores": env.scores().cpu().numpy(),
+                    "sums": s.cpu().numpy(), "eps": e.cpu().numpy()})
+        got.append({f"mt{g}": np.append(*env.get_mt_state(g)) for g in (0, B // 3, B - 1)})
+        assert env.pipe_errors() == 0
+        outs[quad] = got
+        env.close()
+    for a, b in zip(outs[1], outs[0]):
+        assert a.keys() == b.keys()
+        for k in a:
+            assert np.array_equal(a[k], b[k]), k
+    ref = O.VecOracle(min(B, 256), 4, rng_mode=O.RNG_NUMPY_MT, seed=77)
+    ref.reset()
+    rr, rd, ra, ro = ref.rollout(10, include_summaries=summ, want_obs=True)
+    assert np.array_equal(outs[1][0]["rewards"][:, : min(B, 256)], rr)
+    assert np.array_equal(outs[1][0]["obs"][:, : min(B, 256), :, : O.obs_len(summ)], ro)

@@ -507,3 +507,110 @@ def test_batched_baseline_evaluations():
         assert t.agents[n].__name__ == n
     assert sum(len(v) for v in t.baseline_scores.values()) > 0
     t.close()
+
+
+def _dist_tournament(B, seed, game_offset, distributed, condition=128):
+    from rl_6_nimmt.agents import DrunkHamster, MCSAgent
+    from rl_6_nimmt.league import BatchedTournament
+
+    t = BatchedTournament(B, 2, 4, seed=seed, game_offset=game_offset, rng="numpy", fused=False,
+                          distributed=distributed, baseline_agents=[DrunkHamster(), DrunkHamster()],
+                          baseline_condition=condition)
+    for i in range(4):
+        t.add_player(f"a{i}")
+    t.add_player("mcs", MCSAgent(mc_max=10))
+    t.play_games(2)
+    t.evolve(copies=(2,), max_players=5)
+    t.play_games(1)
+    w = t.winner()
+    out = {"names": list(t.names), "active": dict(t.active), "stats": t.agent_stats().numpy(),
+           "elos": t.replay_elo(), "total": t.total_games, "table": str(t),
+           "positions": {n: np.concatenate(p) if p else np.zeros(0) for n, p in t.positions.items()},
+           "baseline": {n: list(v) for n, v in t.baseline_scores.items()},
+           "winner": getattr(w, "__name__", None), "errs": t.env.pipe_errors()}
+    t.close()
+    return out
+
+
+def _rank_dist_tournament(rank, world, port, q, B):
+    """one rank of a distributed=True tournament on cuda:0 (gloo: two ranks
+    cannot share one GPU under RCCL): play, evolve, play, then every
+    accessor -- each a collective on every rank"""
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = _dist_tournament(B, 5, rank * B, True)
+    got = [None] * world
+    dist.all_gather_object(got, out)
+    if rank == 0:
+        q.put(got)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_distributed_tournament_keeps_one_roster_on_every_rank():
+    """BatchedTournament(distributed=True) on 2 ranks -- play,
+    evolve, play -- leaves the SAME roster, tallies, Elo, positions, baseline
+    evaluations, winner and table on both ranks, equal to one process holding
+    every slot; total_games counts the whole world"""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    B = 256
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_dist_tournament, args=(r, 2, port, q, B)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = _dist_tournament(2 * B, 5, 0, False)
+    for r in got:
+        assert r["errs"] == 0
+        assert r["names"] == ref["names"] and r["active"] == ref["active"]
+        assert np.array_equal(r["stats"], ref["stats"])
+        assert np.allclose(r["elos"], ref["elos"], rtol=0, atol=1e-9)
+        assert r["total"] == ref["total"] == 3 * 2 * B
+        assert r["table"] == ref["table"]
+        assert r["winner"] == ref["winner"]
+        assert r["baseline"] == ref["baseline"] and any(len(v) for v in ref["baseline"].values())
+        for n in ref["positions"]:
+            assert np.array_equal(r["positions"][n], ref["positions"][n])
+
+
+@pytest.mark.parametrize("k", [1, 3, "games"])
+def test_updates_per_round_takes_k_adam_steps(k):
+    """BatchedTournament(updates_per_round=k): each trained PUCT /
+    PUCTCustomed / REINFORCE agent takes k Adam steps per round (k chunks of
+    its games); "games" takes one per game it played -- the reference's count
+    (learn() at every episode end, play.py:52-67, mcts.py:230-261)"""
+    from rl_6_nimmt.agents import BatchedReinforceAgent, PUCTAgent, PUCTCustomedAgent
+    from rl_6_nimmt.league import BatchedTournament, decode_seats
+
+    torch.manual_seed(0)
+    t = BatchedTournament(48, 2, 4, seed=1, rng="numpy", fused=False, train=True, updates_per_round=k)
+    nets = {"p": PUCTAgent(mc_max=6), "c": PUCTCustomedAgent(mc_max=6), "r": BatchedReinforceAgent()}
+    for n, a in nets.items():
+        a.train()
+        t.add_player(n, a)
+    t.add_player("x0")
+    before = {n: [q.detach().clone() for q in a.parameters()] for n, a in nets.items()}
+    rec = t.play_games(1)
+    kk, ids = decode_seats(rec[0, :, 0], 4)
+    act = t.active_agents()
+    for n in nets:
+        j = act.index(n)
+        games = int(((ids == j) & (torch.arange(4, device=ids.device)[None, :] < kk[:, None])).any(dim=1).sum())
+        want = games if k == "games" else min(k, games)
+        assert games > 3 and t.optimizer_steps.get(n, 0) == want, (n, games, t.optimizer_steps)
+        assert any(not torch.equal(a.cpu(), b.detach().cpu()) for a, b in zip(before[n], nets[n].parameters()))
+    t.close()

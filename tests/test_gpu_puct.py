@@ -211,6 +211,22 @@ def test_policy_loss_matches_reference_training_loss():
     rgrads = torch.autograd.grad(ref, list(eng.actor.parameters()))
     ref = ref.detach()
     assert abs(float(loss) - float(ref)) <= 1e-5 * abs(float(ref)), (float(loss), float(ref))
+    # one decider's term alone is the reference's per-episode loss (what a
+    # BatchedTournament(updates_per_round="games") steps on), and the chunks
+    # of any split sum to the whole
+    with torch.no_grad():
+        for d in (0, 5, eng.D - 1):
+            g, p = divmod(d, N)
+            one = torch.zeros(())
+            for obs, hands, n, best in seen:
+                x = torch.cat((hands[g, p, :n].float()[:, None], obs[g, p][None, :].expand(n, -1)), dim=1)
+                (logits,) = eng.actor(norm(x))
+                one = one - torch.log(torch.softmax(logits, dim=0).flatten()[int(best[d])])
+            got = float(eng.policy_loss(d, d + 1))
+            assert abs(got - float(one)) <= 1e-5 * max(1.0, abs(float(one))), (d, got, float(one))
+        bounds = [0, 7, 40, 41, eng.D]
+        parts = sum(float(eng.policy_loss(a, b)) for a, b in zip(bounds[:-1], bounds[1:]))
+        assert abs(parts - float(loss)) <= 1e-5 * abs(float(loss)), (parts, float(loss))
     # (the head bias's gradient is a sum of softmax residuals that is 0 in
     # exact arithmetic: compare at an absolute floor of 1e-4)
     for a, r in zip(grads, rgrads):
