@@ -74,6 +74,8 @@ def parse():
                     help="SN_OPT_PLAY_SPLIT (default: the library's)")
     ap.add_argument("--play-quad", type=int, default=None, choices=[0, 1],
                     help="SN_OPT_PLAY_QUAD: four lanes per game, k_play_quad (default: the library's, 0)")
+    ap.add_argument("--twist-round", type=int, default=None, choices=[0, 1],
+                    help="SN_OPT_TWIST_ROUND: whole-round MT19937 twists in k_mt_ahead (default: the library's, 1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-philox", action="store_true", help="skip the philox-mode leg of config 2")
@@ -844,7 +846,8 @@ def main():
     B = args.games
     env = VecSechsNimmtEnv(B, N_PLAYERS, seed=0, game_offset=rank * B, rng=args.rng)
     if args.rng == "numpy":
-        env.set_option(pipe_gpw=args.pipe_gpw, play_split=args.play_split, play_quad=args.play_quad)
+        env.set_option(pipe_gpw=args.pipe_gpw, play_split=args.play_split, play_quad=args.play_quad,
+                       twist_round=args.twist_round)
     env.reset()
     out = make_out(env, B, not args.no_obs)
     wall, kern_ms, kt = time_rollouts(env, out, args.steps, args.warmup, world)

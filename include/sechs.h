@@ -163,11 +163,16 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          bytes or none) run k_play_quad, four lanes per game;
                          0 (default): the one-lane k_play.  Same words, same
                          outputs (the GPU tests run both).
+     SN_OPT_TWIST_ROUND  1 (default): the pipelined twist-ahead k_mt_ahead
+                         twists whole MT19937 rounds (each old word read
+                         once, each new word written once: 8 instead of 12
+                         B of MT-state traffic per word); 0: exactly the
+                         words the lead needs.  Same words either way.
    A pipelined (numpy-compat) rollout records its ordering event on the
    caller's stream before it returns; later calls only wait on that event,
    so the caller may destroy the stream after the call. */
 enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3, SN_OPT_TIMING = 4, SN_OPT_PIPE_GPW = 5,
-       SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7, SN_OPT_PLAY_QUAD = 8 };
+       SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7, SN_OPT_PLAY_QUAD = 8, SN_OPT_TWIST_ROUND = 9 };
 sn_status sn_set_option(sn_env* env, int option, int value);
 /* pipelined rollouts whose draws ran past the twisted words (must be 0; a
    nonzero count means those games' draws are wrong) [sync].  The count is
@@ -189,6 +194,15 @@ sn_status sn_kernel_times(sn_env* env, float* play_ms, float* ahead_ms, int32_t*
    (-DSECHS_PHASE_PROF) records them; the product build returns
    SN_EUNSUPPORTED [sync]. */
 sn_status sn_debug_phases(uint64_t* out, int n);
+/* Device-side invariant checks (SN_DASSERT in sechs_device.h / sechs_env.hip:
+   a played card is in its seat's hand, the cards of a step are distinct, a
+   card goes to a row ending below it (or undercuts), rows hold 1..5 cards,
+   a deal gives ten distinct cards per hand): violations counted since the
+   last call, *first_line = the smallest source line that failed; the
+   counters are cleared.  selftest != 0 first runs one deliberately failing
+   check.  Only the libsechs_debug.so build (-DSECHS_DEBUG) has them; the
+   product build returns SN_EUNSUPPORTED [sync]. */
+sn_status sn_debug_failures(uint32_t* count, uint32_t* first_line, int selftest);
 
 /* ---- One-game fast path (the scalar drop-in SechsNimmtEnv) ------------
    For a handle of B == 1: one kernel launch and one stream sync per call

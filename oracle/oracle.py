@@ -12,7 +12,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB = os.path.join(_HERE, "liboracle.so")
+# SECHS_ORACLE_LIB: another build of the same sources (liboracle_asan.so, tools/asan_cpu.sh)
+_LIB = os.environ.get("SECHS_ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")
 
 RNG_PHILOX = 0
 RNG_NUMPY_MT = 1
@@ -21,6 +22,8 @@ ROWS, THRESHOLD, HAND, MAX_CARDS = 4, 6, 10, 104
 
 
 def build(force=False):
+    if os.environ.get("SECHS_ORACLE_LIB"):
+        return _LIB  # prebuilt variant (make -C oracle asan)
     src = os.path.join(_HERE, "sechs_oracle.c")
     if force or not os.path.exists(_LIB) or os.path.getmtime(_LIB) < max(
         os.path.getmtime(src), os.path.getmtime(os.path.join(_HERE, "sechs_oracle.h"))

@@ -22,6 +22,24 @@ namespace sechs {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// SECHS_DEBUG (the libsechs_debug.so variant, make libsechs_debug.so):
+// SN_DASSERT counts violated invariants of the game engine in a device word
+// (sn_debug_failures reads and clears it) instead of trapping -- a trap on a
+// shared GPU box can take the queue down.  Active in sechs_env.hip's kernels
+// (SECHS_DEBUG_HERE); a no-op in the product library and in the other files.
+#if defined(SECHS_DEBUG) && defined(SECHS_DEBUG_HERE)
+__device__ unsigned int g_sn_dbg[2] = {0u, 0xFFFFFFFFu};  // failures, first failing line
+#define SN_DASSERT(c)                                                   \
+    do {                                                                \
+        if (!(c)) {                                                     \
+            atomicAdd(&::sechs::g_sn_dbg[0], 1u);                       \
+            atomicMin(&::sechs::g_sn_dbg[1], (unsigned int)__LINE__);   \
+        }                                                               \
+    } while (0)
+#else
+#define SN_DASSERT(c) ((void)0)
+#endif
+
 constexpr int kRows = 4;
 constexpr int kThreshold = 6;
 constexpr int kHand = 10;
@@ -115,6 +133,17 @@ __device__ __forceinline__ uint32_t hand_len(const Hand& h) {
     return z ? (uint32_t)(__builtin_ctzll(z) >> 3) : 8u + (uint32_t)(__builtin_ctz(zy | 0x80000000u) >> 3);
 }
 
+// the listed cards strictly ascend (distinct cards; debug checks only)
+__device__ __forceinline__ bool hand_strict(const Hand& h) {
+    bool ok = true;
+#pragma unroll
+    for (uint32_t k = 0; k + 1 < (uint32_t)kHand; k++) {
+        const uint32_t a = hand_get(h, k), b = hand_get(h, k + 1u);
+        ok = ok && (b == 0xFFu || a < b);
+    }
+    return ok;
+}
+
 // sorted byte list from a card set of at most 10 cards
 __device__ __forceinline__ Hand hand_from_set(u32x4 s) {
     Hand h;
@@ -187,6 +216,8 @@ __device__ __forceinline__ uint32_t place_card(Board& b, uint32_t c, uint32_t* i
     const bool take = under || len == (uint32_t)(kThreshold - 1);  // 6th card, env.py:133
     const uint32_t penalty = take ? heads_in(hi_t) : 0u;           // _score_row: the whole old row
     if (info) *info = (uint32_t)tr | (under ? 4u : 0u) | (take ? 8u : 0u);
+    SN_DASSERT(c < (uint32_t)kMaxCards && len >= 1u && len <= (uint32_t)(kThreshold - 1));  // a legal card; rows hold 1..5
+    SN_DASSERT(under || end_of(hi_t) < c);                                                  // the row ends below the card
     const uint32_t lo_new = take ? c : (lo_t | (len < 4u ? (c << (8u * len)) : 0u));
     const uint32_t hi_new = take ? ((1u << 8) | (hc << 16) | (c << 24))
                                  : ((len == 4u ? c : (hi_t & 0xFFu)) | ((len + 1u) << 8) |
@@ -221,6 +252,8 @@ __device__ __forceinline__ void resolve(Board& b, const uint32_t (&card)[N], uin
         }
 #pragma unroll
     for (int p = 0; p < N; p++) pen[p] = 0u;
+#pragma unroll
+    for (int k = 0; k + 1 < N; k++) SN_DASSERT((key[k] >> 4) < (key[k + 1] >> 4) || (key[k] >> 4) == 0xFFu);  // distinct cards
 #pragma unroll
     for (int k = 0; k < N; k++) {
         if (SKIP && (key[k] >> 4) >= 0xFFu) break;  // absent seats sort last

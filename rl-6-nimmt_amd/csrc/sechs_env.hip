@@ -14,6 +14,7 @@
 #include <string>
 #include <type_traits>
 
+#define SECHS_DEBUG_HERE  // SN_DASSERT is live in this file's kernels (libsechs_debug.so only)
 #include "sechs_state.h"
 
 using namespace sechs;
@@ -265,7 +266,17 @@ struct AheadArgs {
     uint32_t* perr_mirror;  // host-mapped copy of *perr, refreshed at launch start (off the play stream)
 };
 
-template <bool INIT>
+// ROUND (SN_OPT_TWIST_ROUND): twist whole MT rounds instead of exactly the
+// words the lead needs.  A twist that is due first completes the current
+// round (the per-64-word form below), then -- if the lead is still short --
+// twists the next round of 624 words in LDS: the round's old words are read
+// once, every input of numpy's in-place order (mt[i+1], mt[i+397] / the new
+// mt[i-227]) comes from LDS, and each new word is written once: 8 B of MT
+// traffic per word instead of 12 (the X input of a partial twist is a
+// second HBM read).  The lead then ranges up to 600 + 624 words, so the
+// ring holds kPipeRing = 2048 bytes per game; a handle synchronised while
+// the array is a round ahead of its consumer is untwisted (k_pipe_code).
+template <bool INIT, bool ROUND = false>
 __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
     constexpr uint32_t D = kMtN - kMtM;  // 227
     constexpr uint32_t P1 = 224;          // words twisted before any store (all inputs already in memory)
@@ -305,8 +316,10 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
     // (counted there too); twist nothing rather than underflow the lead
     const int32_t lead = (int32_t)(t0 - c);
     if (lead < 0 && lane == 0u) atomicAdd(s.perr, 1u);
-    const uint32_t n = (lead >= 0 && lead < a.lead) ? (((uint32_t)(a.lead - lead)) & ~7u) : 0u;
     const uint32_t T0 = (Tp == (uint32_t)kMtN) ? 0u : Tp;
+    // ROUND: the words completing the current round (none at a round boundary)
+    const uint32_t n = ROUND ? ((lead >= 0 && lead < a.lead && T0 != 0u) ? (uint32_t)kMtN - T0 : 0u)
+                             : ((lead >= 0 && lead < a.lead) ? (((uint32_t)(a.lead - lead)) & ~7u) : 0u);
     auto ring_dword = [&](uint32_t j, uint32_t v) {  // t0 is 8-aligned: lanes 4m..4m+3 share one dword
         const uint32_t y = mt_temper(v) & 0xFFu;
         const uint32_t d = y | (__shfl_down(y, 1) << 8) | (__shfl_down(y, 2) << 16) | (__shfl_down(y, 3) << 24);
@@ -352,25 +365,83 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
         }
         ring_dword(j, v);
     }
-    if (lane == 0u) {
-        uint32_t Tn = Tp;
-        if (n) {
-            Tn = T0 + n;
-            while (Tn > (uint32_t)kMtN) Tn -= kMtN;
+    uint32_t Tn = Tp, te = t0 + n;
+    if (n) {
+        Tn = T0 + n;
+        while (Tn > (uint32_t)kMtN) Tn -= kMtN;
+    }
+    if constexpr (ROUND) {
+        if (lead >= 0 && lead + (int32_t)n < a.lead) {  // one whole round, in LDS
+            __shared__ uint32_t wround[kBlock / 64][kMtN];
+            uint32_t* w = wround[threadIdx.x >> 6];
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the completing words' stores first
+            for (uint32_t i = lane; i < (uint32_t)kMtN; i += 64u) w[i] = st[i];
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (lane == 0u) s.mt0[g] = w[0];  // old mt[0]: the one word the untwist cannot recover
+            for (uint32_t q = 0; q < (uint32_t)(kMtN + 63) / 64u; q++) {
+                const uint32_t i = 64u * q + lane;
+                uint32_t v = 0u;
+                if (i < (uint32_t)kMtN) {
+                    // numpy's in-place order, 64 words at a time: mt[i+1] (old; mt[0] new for i = 623),
+                    // mt[i+397] (old, i < 227) or mt[i-227] (new, twisted >= 3 chunks ago)
+                    v = mt_mix(w[i], w[(i + 1u == (uint32_t)kMtN) ? 0u : i + 1u], w[(i < D) ? i + kMtM : i - D]);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the chunk's reads before its writes
+                if (i < (uint32_t)kMtN) {
+                    w[i] = v;
+                    st_nt(&st[i], v, SECHS_NT_MORE);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                // tempered low bytes, 4 per dword (te is 8-aligned, 624 = 156 dwords)
+                const uint32_t y = mt_temper(v) & 0xFFu;
+                const uint32_t d = y | (__shfl_down(y, 1) << 8) | (__shfl_down(y, 2) << 16) | (__shfl_down(y, 3) << 24);
+                const uint32_t ri = (te + i) & (uint32_t)(kPipeRing - 1);
+                if ((lane & 3u) == 0u && i < (uint32_t)kMtN)
+                    st_nt((uint32_t*)(ring + ((int64_t)(ri >> 4) * B + g) * 16 + (ri & 12u)), d, SECHS_NT_MORE);
+            }
+            te += kMtN;
+            Tn = kMtN;
         }
+    }
+    if (lane == 0u) {
         s.ptp[g] = Tn;
-        s.ptend[(int64_t)a.tout * B + g] = t0 + n;
+        s.ptend[(int64_t)a.tout * B + g] = te;
     }
 }
 
 // state code of a pipelined handle (for MtGen users and sn_mt_get):
 // twist pointer | (twisted end - consumer) << 16
+__device__ __forceinline__ uint32_t mt_untwist_y_dev(uint32_t t) {
+    const uint32_t lsb = t >> 31;  // the twist constant's top bit is set, y >> 1's is not
+    return (((lsb ? (t ^ 0x9908b0dfu) : t)) << 1) | lsb;
+}
+
 __global__ void k_pipe_code(DevState s, int cin, int tin) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= s.B) return;
-    const int32_t rem = (int32_t)(s.ptend[(int64_t)tin * s.B + g] - s.pabsc[(int64_t)cin * s.B + g]);
+    int32_t rem = (int32_t)(s.ptend[(int64_t)tin * s.B + g] - s.pabsc[(int64_t)cin * s.B + g]);
     if (rem < 0) atomicAdd(s.perr, 1u);  // an overrun (already counted): the stream is lost
-    s.mt_pos[g] = s.ptp[g] | ((uint32_t)max(rem, 0) << 16);
+    const uint32_t tp = s.ptp[g];
+    if (rem > kMtN && tp == (uint32_t)kMtN) {
+        // a whole-round twist (SN_OPT_TWIST_ROUND) left the array one round
+        // ahead of the consumer: undo that round in place (new -> old), the
+        // host mt_unstraddle over all 624 words.  Descending j keeps every
+        // input available: y[j] needs new[j] and new[j-227] (j >= 227) or
+        // old[j+397] (j < 227, restored already); old[j] = top(y[j]) |
+        // low(y[j-1]), old[0]'s low half from mt0.
+        constexpr uint32_t D = kMtN - kMtM;
+        uint32_t* a = s.mt + g * kMtN;
+        uint32_t yj = mt_untwist_y_dev(a[kMtN - 1] ^ a[kMtN - 1 - D]);
+        for (int j = kMtN - 1; j >= 1; j--) {
+            const uint32_t jm = (uint32_t)(j - 1);
+            const uint32_t ym = mt_untwist_y_dev(a[jm] ^ a[(jm >= D) ? jm - D : jm + kMtM]);
+            a[j] = (yj & 0x80000000u) | (ym & 0x7fffffffu);
+            yj = ym;
+        }
+        a[0] = (yj & 0x80000000u) | (s.mt0[g] & 0x7fffffffu);
+        rem -= kMtN;
+    }
+    s.mt_pos[g] = tp | ((uint32_t)max(rem, 0) << 16);
 }
 
 // ---- k_play phase profiler (diagnostics; built only with -DSECHS_PHASE_PROF,
@@ -432,6 +503,8 @@ struct PlayArgs {
     int32_t* league_rec;     // league: [episodes][B][1 + N] per finished game: seats word, results
     int step0;               // league: env-steps of this rollout before this launch (episode index of a record)
     int n0;                  // k_play_split: every game's hand size at the launch's start (aligned handle)
+    int dbg;                 // k_play_quad diagnostics (SECHS_QUAD_DBG; 0 in normal use): bit 0 plain stores for
+                             // rewards / actions / done, bit 1 skip them, bit 2 skip the game-state stores
 };
 
 // The env-step loop of one lane (game g).  R supplies the random words
@@ -469,6 +542,8 @@ struct StreamSrc {
         shuffle_apply(deck, deck + kDeckStride, s.C);
         pp.mark(PH_APPLY);
         deal_from_deck<N>(deck, s.C, G);
+#pragma unroll
+        for (int p = 0; p < N; p++) SN_DASSERT(hand_strict(G.hand[p]) && hand_len(G.hand[p]) == (uint32_t)kHand);
     }
 };
 
@@ -550,7 +625,10 @@ __device__ __forceinline__ void play_steps(const DevState& s, const PlayArgs& a,
         } else {
             src.draws(G, t, kp, LG, idx);
 #pragma unroll
-            for (int p = 0; p < N; p++) card[p] = hand_get(G.hand[p], idx[p]);
+            for (int p = 0; p < N; p++) {
+                card[p] = hand_get(G.hand[p], idx[p]);
+                SN_DASSERT((LG && (uint32_t)p >= kp) || (idx[p] < G.n && card[p] < (uint32_t)s.C));  // the hand holds it
+            }
         }
         pp.mark(PH_DRAW);
         if (a.invalid) a.invalid[g] = bad;
@@ -1262,6 +1340,7 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
     e->pipe_lead = kPipeLead;
     e->phase = -1;
     e->play_split = 1;
+    e->twist_round = 1;
     e->play_quad = 0;  // measured: k_play_quad alone is no faster and slows the concurrent twist
     {
         const char* ps = getenv("SECHS_PIPE_SERIAL");
@@ -1384,6 +1463,10 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
         case SN_OPT_PLAY_SPLIT:
             if (value < 0 || value > 1) return fail(SN_EINVAL, "play split must be 0 or 1");
             e->play_split = value;
+            return SN_OK;
+        case SN_OPT_TWIST_ROUND:
+            if (value < 0 || value > 1) return fail(SN_EINVAL, "twist round must be 0 or 1");
+            e->twist_round = value;
             return SN_OK;
         case SN_OPT_PLAY_QUAD:
             if (value < 0 || value > 1) return fail(SN_EINVAL, "play quad must be 0 or 1");
@@ -1627,8 +1710,9 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     const dim3 pg((unsigned)((s.B + kBlock / 64 - 1) / (kBlock / 64)));
     if (!e->pvalid) {  // start the pipeline from mt_pos: twist kPipeLead ahead, synchronously
         const int p = (int)(e->pcount & 1u);
-        hipLaunchKernelGGL(k_mt_ahead<true>, pg, dim3(kBlock), 0, st, s,
-                           AheadArgs{1 - p, 0, p, e->pipe_lead, e->perr_host_dev});
+        const AheadArgs aa{1 - p, 0, p, e->pipe_lead, e->perr_host_dev};
+        if (e->twist_round) hipLaunchKernelGGL((k_mt_ahead<true, true>), pg, dim3(kBlock), 0, st, s, aa);
+        else hipLaunchKernelGGL((k_mt_ahead<true, false>), pg, dim3(kBlock), 0, st, s, aa);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(e->ev_prep, st));
         e->pvalid = 1;
@@ -1644,6 +1728,10 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
                                       : (unsigned)grid_for(s.B);
     // four lanes per game (k_play_quad): N = 4 DrunkHamster seats, 48-byte
     // 16-B aligned obs rows (or none); anything else keeps k_play
+    {
+        const char* qd = getenv("SECHS_QUAD_DBG");  // timing diagnostics only: bits 1, 2 invalidate the results
+        a.dbg = qd ? atoi(qd) : 0;
+    }
     const bool quad = e->play_quad && gpw == 64 && N == 4 && !s.lg_K && !a.actions && !a.invalid &&
                       (!a.obs || (a.obs_stride == 48 && (((uintptr_t)a.obs) & 15) == 0));
     const size_t qshmem = (size_t)kQuadWave * (kBlock / 64);
@@ -1676,8 +1764,9 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         if (e->pipe_serial) HIP_TRY(hipEventRecord(e->ev_main, st));
         HIP_TRY(hipStreamWaitEvent(e->side, e->ev_main, 0));
         if (tv) HIP_TRY(hipEventRecord(tv[2], e->side));
-        hipLaunchKernelGGL(k_mt_ahead<false>, pg, dim3(kBlock), 0, e->side, s,
-                           AheadArgs{1 - p, p, 1 - p, e->pipe_lead, e->perr_host_dev});
+        const AheadArgs aa{1 - p, p, 1 - p, e->pipe_lead, e->perr_host_dev};
+        if (e->twist_round) hipLaunchKernelGGL((k_mt_ahead<false, true>), pg, dim3(kBlock), 0, e->side, s, aa);
+        else hipLaunchKernelGGL((k_mt_ahead<false, false>), pg, dim3(kBlock), 0, e->side, s, aa);
         HIP_TRY(hipGetLastError());
         if (tv) HIP_TRY(hipEventRecord(tv[3], e->side));
         HIP_TRY(hipEventRecord(e->ev_prep, e->side));
@@ -2084,6 +2173,31 @@ sn_status sn_debug_phases(uint64_t* out, int n) {
 #else
     for (int k = 0; k < n; k++) out[k] = 0ull;
     return fail(SN_EUNSUPPORTED, "built without SECHS_PHASE_PROF (make libsechs_prof.so)");
+#endif
+}
+
+#if defined(SECHS_DEBUG)
+__global__ void k_debug_selftest(int fail) { SN_DASSERT(fail == 0); }
+#endif
+
+sn_status sn_debug_failures(uint32_t* count, uint32_t* first_line, int selftest) {
+    if (!count || !first_line) return fail(SN_EINVAL, "NULL argument");
+    *count = 0u, *first_line = 0u;
+#if defined(SECHS_DEBUG)
+    if (selftest) {  // one deliberately violated assertion: proves the counter is live
+        hipLaunchKernelGGL(k_debug_selftest, dim3(1), dim3(1), 0, 0, 1);
+        HIP_TRY(hipGetLastError());
+    }
+    unsigned int h[2];
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_sn_dbg), sizeof(h)));
+    *count = h[0], *first_line = h[1];
+    const unsigned int z[2] = {0u, 0xFFFFFFFFu};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_sn_dbg), z, sizeof(z)));
+    return SN_OK;
+#else
+    (void)selftest;
+    return fail(SN_EUNSUPPORTED, "built without SECHS_DEBUG (make libsechs_debug.so)");
 #endif
 }
 

@@ -168,6 +168,8 @@ __device__ __forceinline__ uint32_t quad_place(uint32_t& rlo, uint32_t& rhi, uin
     const uint32_t tr = under ? (mn & 3u) : ((best >> 12) & 3u);
     const bool take = under || (best & 15u) == (uint32_t)(kThreshold - 1);  // the 6th card
     const uint32_t pen = take ? (under ? (mn >> 2) : ((best >> 4) & 0xFFu)) : 0u;  // _score_row: the old row
+    SN_DASSERT(under || (best >> 16) - 1u < c);                       // the target row ends below the card
+    SN_DASSERT(len >= 1u && len <= (uint32_t)(kThreshold - 1));        // every row holds 1..5 cards
     if ((uint32_t)q == tr) {
         const uint32_t lo_n = take ? c : (rlo | (len < 4u ? (c << (8u * len)) : 0u));
         const uint32_t hi_n = take ? ((1u << 8) | (hc << 16) | (c << 24))
@@ -257,6 +259,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_play_quad(DevState s, PlayArgs a)
         // ---- DrunkHamster: legal[random_interval(n - 1)] for every seat
         const uint32_t idx = quad_draw(P, t, n - 1u, q);
         const uint32_t card = hand_get(h, idx);
+        SN_DASSERT(idx < n && card < (uint32_t)C);  // the hand holds the card
         hand_del(h, idx);
         pp.mark(PH_DRAW);
         // ---- simultaneous placement, cards ascending (env.py:120-136)
@@ -264,6 +267,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_play_quad(DevState s, PlayArgs a)
         uint32_t k1 = qget<1>(k0), k2 = qget<2>(k0), k3 = qget<3>(k0);
         k0 = qget<0>(k0);
         qce(k0, k1), qce(k2, k3), qce(k0, k2), qce(k1, k3), qce(k1, k2);
+        SN_DASSERT((k0 >> 8) < (k1 >> 8) && (k1 >> 8) < (k2 >> 8) && (k2 >> 8) < (k3 >> 8));  // four distinct cards
         uint32_t pen = 0u;
         {
             const uint32_t keys[4] = {k0, k1, k2, k3};
@@ -277,9 +281,12 @@ __global__ __launch_bounds__(kBlock, 4) void k_play_quad(DevState s, PlayArgs a)
         n -= 1u;
         const bool done = n == 0u;  // env.py:246-249
         pp.mark(PH_RESOLVE);
-        if (a.rewards) st_nt(&a.rewards[o], -(int32_t)pen, SECHS_NT_MORE);
-        if (a.actions_out) st_nt(&a.actions_out[o], (uint8_t)card, SECHS_NT_MORE);
-        if (a.done && q == 0) st_nt(&a.done[(int64_t)step * B + g], (uint8_t)(done ? 1 : 0), SECHS_NT_MORE);
+        if (!(a.dbg & 2)) {
+            const bool nt = SECHS_NT_MORE && !(a.dbg & 1);
+            if (a.rewards) st_nt(&a.rewards[o], -(int32_t)pen, nt);
+            if (a.actions_out) st_nt(&a.actions_out[o], (uint8_t)card, nt);
+            if (a.done && q == 0) st_nt(&a.done[(int64_t)step * B + g], (uint8_t)(done ? 1 : 0), nt);
+        }
         pp.mark(PH_STORE);
         if (done && auto_reset) {
             // GameSession.results.append(scores), then the next play_game(): _deal
@@ -321,6 +328,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_play_quad(DevState s, PlayArgs a)
                     v[2 * k + 1] = two >> 8;
                 }
                 h = hand_from_cards(v);
+                SN_DASSERT(hand_strict(h) && hand_len(h) == (uint32_t)kHand);  // ten distinct cards dealt
                 const uint32_t rc = deck[C - 1 - q];
                 rlo = rc;
                 rhi = meta_row(rc);
@@ -332,6 +340,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_play_quad(DevState s, PlayArgs a)
         }
     }
     // ---- store the game back
+    if (a.dbg & 4) return;  // timing diagnostics only
     s.hand[(int64_t)(q * 3 + 0) * B + g] = (uint32_t)h.lo;
     s.hand[(int64_t)(q * 3 + 1) * B + g] = (uint32_t)(h.lo >> 32);
     s.hand[(int64_t)(q * 3 + 2) * B + g] = h.hi;

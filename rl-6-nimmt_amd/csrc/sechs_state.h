@@ -57,7 +57,7 @@ struct DevState {
     int32_t* lpf;    // [B] 1 (| 2: quirk Q6): lpc holds this step's non-external cards
 };
 
-constexpr int kPipeRing = 1024;  // ring bytes per game (>= lead + one launch)
+constexpr int kPipeRing = 2048;  // ring bytes per game (>= lead + one launch; whole-round twists lead by up to 1223)
 constexpr int kPipeLead = 600;   // words k_mt_ahead keeps twisted ahead of the consumer (<= 624)
 constexpr int kPipeWin = 240;    // of them, copied to LDS per lane at a k_play launch: a 4-player
                                   // episode draws 193.5 words, P(> 240) = 7e-6 per game (the rest come
@@ -829,6 +829,7 @@ struct sn_env {
     int lg_mpc[16], lg_mmax[16];  // MCSAgent agents: mc_per_card, mc_max
     int phase;        // every game's env-steps since its deal, mod 10, when they are in lockstep; -1 unknown
     int play_split;   // SN_OPT_PLAY_SPLIT: role-split k_play for lockstep DrunkHamster rollouts
+    int twist_round;  // SN_OPT_TWIST_ROUND: k_mt_ahead twists whole MT rounds (8 instead of 12 B of MT traffic per word)
     int play_quad;    // SN_OPT_PLAY_QUAD: four lanes per game (k_play_quad) on the pipelined N = 4 path
     int pipe_serial;  // SECHS_PIPE_SERIAL=1 (diagnostics): each twist waits for the play launch before it (no overlap)
     sechs::DevState s;

@@ -23,6 +23,7 @@ SN_AUTO_RESET, SN_NO_SUMMARIES = 1, 2
 SN_OPT_RING_WORDS, SN_OPT_CHUNK_STEPS, SN_OPT_PIPELINE, SN_OPT_TIMING, SN_OPT_PIPE_GPW, SN_OPT_PIPE_LEAD = 1, 2, 3, 4, 5, 6
 SN_OPT_PLAY_SPLIT = 7
 SN_OPT_PLAY_QUAD = 8
+SN_OPT_TWIST_ROUND = 9
 SN_AGENT_RANDOM, SN_AGENT_MCS, SN_AGENT_EXTERNAL = 0, 1, 2
 
 class SnPuct(ctypes.Structure):
@@ -77,6 +78,7 @@ SIGNATURES = {
     "sn_pipe_errors": ([_P, _P], _I),
     "sn_kernel_times": ([_P, _P, _P, _P], _I),
     "sn_debug_phases": ([_P, _I], _I),
+    "sn_debug_failures": ([_P, _P, _I], _I),
     "sn_step1": ([_P, _P, _P, _I], _I),
     "sn_reset1": ([_P, _P, ctypes.c_int32, _P, _P, _P, _I], _I),
     "sn_league_config": ([_P, _I, _I, _I], _I),

@@ -650,3 +650,129 @@ def test_seat_parallel_step_equals_one_lane_step(monkeypatch):
         res[lanes] = (acts, eng.stats.clone(), eng.hist.clone())
     assert all(torch.equal(a, b) for a, b in zip(res["1"][0], res["0"][0]))
     assert torch.equal(res["1"][1], res["0"][1]) and torch.equal(res["1"][2], res["0"][2])
+
+
+def _bf16_forward_bound(x, layers, head_w, head_b, u=2.0 ** -8):
+    """first-order bound on |logit(bf16 path) - logit(f64 reference)| for an
+    MLP Linear-ReLU-...-Linear evaluated with every input, weight, bias and
+    hidden activation rounded to bf16 (unit roundoff u = 2^-8) and f32
+    accumulation: e_in = u|x|; per layer |dz| <= |W| e_in + u (|W||x| + |b|)
+    + 2u|z| (the product rounded to bf16 once as the seat base and once
+    after the card column + ReLU: sn_puct_mlp_seats' two roundings of layer 1,
+    one for layer 2); ReLU is 1-Lipschitz; the head adds |w| e + u (|w||h| +
+    |b|).  Returns (reference logits, bound), both float64."""
+    h, e = x, u * x.abs()
+    for i, (w, b) in enumerate(layers):
+        z = h @ w.T + b
+        e = e @ w.abs().T + u * (h.abs() @ w.abs().T + b.abs()) + (2 if i == 0 else 1) * u * z.abs()
+        h = torch.relu(z)
+    logit = h @ head_w + head_b
+    e = e @ head_w.abs() + u * (h.abs() @ head_w.abs() + head_b.abs())
+    return logit, e
+
+
+@pytest.mark.parametrize("n", [10, 6, 3])
+def test_mlp_seats_kernel_matches_fp32_reference_net(n):
+    """VERDICT r04 #2a: sn_puct_mlp_seats -- the MFMA kernel behind every
+    rollout logit of config 4 -- on the reference-recorded F8 weights
+    (torch.manual_seed(0); PUCTAgent(), utils/nets.py:100-132), at every
+    n_cur of rollouts from positions with n cards left, against the f64
+    reference forward of the SAME normalised rows (sn_puct_rows in f32 --
+    exact vs SechsNimmtStateNormalization, test_root_rows_are_normalised_
+    observations): every logit within the derived first-order bf16 bound
+    (x 1.25 for the second-order terms), and every candidate's softmax
+    probability (mcts.py:219-228) within p * (exp(2 * 1.25 * max bound) - 1)."""
+    import ctypes
+
+    from rl_6_nimmt import _native as nat
+
+    z = np.load(os.path.join(GOLDEN, "puct_policy.npz"))
+    weights = {k: torch.from_numpy(z[k]) for k in z.files if "net" in k}
+    env, eng = _engine(B=512, dtype=torch.bfloat16, mc_max=4, mc_per_card=2, seed=31, weights=weights)
+    N = env.num_players
+    for t in range(10 - n):
+        env.step(eng.decide(10 - t))
+    net = eng.sync_net()
+    w1t, w1c, w2p, head, w1s = net.fused()
+    q = eng._params(n)
+    L, h, st = nat.lib(), env._h, env._stream()
+    eng.memorize()
+    nat.check(L.sn_puct_deal(h, ctypes.byref(q), st), "deal")
+    layers = [(weights["latent_net.0.weight"].double(), weights["latent_net.0.bias"].double()),
+              (weights["latent_net.2.weight"].double(), weights["latent_net.2.bias"].double())]
+    hw, hb = weights["head_nets.0.0.weight"][0].double(), weights["head_nets.0.0.bias"][0].double()
+    worst_dp = 0.0
+    for m in range(n, 0, -1):
+        R = eng.D * N * m
+        rows = torch.empty((R, 48), dtype=torch.float32, device=env.device)
+        nat.check(L.sn_puct_rows(h, ctypes.byref(q), m, nat.ptr(rows), 0, st), "rows f32")
+        lg = torch.full((R,), float("nan"), dtype=torch.float32, device=env.device)
+        nat.check(L.sn_puct_mlp_seats(h, ctypes.byref(q), m, nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p), nat.ptr(head),
+                                      nat.ptr(lg), st), "mlp_seats")
+        torch.cuda.synchronize()
+        ref, bound = _bf16_forward_bound(rows.double().cpu(), layers, hw, hb)
+        got = lg.double().cpu()
+        assert not torch.isnan(got).any()
+        err = (got - ref).abs()
+        assert (err <= 1.25 * bound + 1e-6).all(), (m, float((err / bound).max()))
+        p, pr = torch.softmax(got.view(-1, m), dim=1), torch.softmax(ref.view(-1, m), dim=1)
+        lim = pr * (torch.exp(2 * 1.25 * bound.view(-1, m).max(dim=1, keepdim=True).values) - 1) + 1e-7
+        assert ((p - pr).abs() <= lim).all(), m
+        worst_dp = max(worst_dp, float((p - pr).abs().max()))
+    assert worst_dp < 0.02, worst_dp  # the derived bound is loose; the kernel is far inside it
+
+
+def test_puct_search_statistics_match_reference_in_law():
+    """VERDICT r04 #2b, golden F14 (tools/gen_puct_stats.py): G seeded
+    reference games of GameSession(PUCTAgent(mc_max=20) with the F8 weights,
+    DrunkHamster x 3) -- the batched engine replays the SAME initial deals
+    (seat 0 searching with the same weights in bf16, seats 1-3 uniform legal
+    moves) and must agree in law, game-paired, within 4 standard errors of
+    the paired difference: seat 0's final penalty, and at its first decision
+    the PUCT visit distribution (visit-weighted mean hand rank, largest
+    visit share) and the chosen card's hand rank (mcts.py:191-323)."""
+    d = load("puct_search.json")
+    games = d["games"]
+    G = len(games)
+    z = np.load(os.path.join(GOLDEN, "puct_policy.npz"))
+    weights = {k: torch.from_numpy(z[k]) for k in z.files if "net" in k}
+    env, eng = _engine(B=G, N=4, mask=1, dtype=torch.bfloat16, mc_max=d["mc_max"], mc_per_card=d["mc_per_card"],
+                       seed=2024, weights=weights)
+    board = np.full((G, 4, 6), -1, dtype=np.int8)
+    hands = np.full((G, 4, 10), -1, dtype=np.int8)
+    for g, r in enumerate(games):
+        for i, row in enumerate(r["board0"]):
+            board[g, i, : len(row)] = row
+        hands[g] = np.array(r["hands0"], dtype=np.int8)
+    env.reset_to(torch.from_numpy(board), torch.from_numpy(hands))
+    total = torch.zeros((G, 4), dtype=torch.int32, device=env.device)
+    torch.manual_seed(7)
+    for t in range(10):
+        acts = eng.decide(10 - t)
+        if t == 0:
+            visits = eng.stats[:G, 10:20].cpu().numpy().astype(np.float64)
+            chosen = acts[:, 0].cpu().numpy()
+        acts = torch.where(torch.tensor([True, False, False, False], device=env.device)[None, :], acts,
+                           eng._random_moves())
+        rew, done, inv = env.step(acts)
+        assert (inv.cpu() == -1).all()
+        total += rew
+    assert bool(done.all())
+    ours = {"penalty": -total[:, 0].cpu().numpy().astype(np.float64)}
+    ref = {"penalty": np.array([-r["results"][0] for r in games], dtype=np.float64)}
+    rv = np.array([r["visits"] for r in games], dtype=np.float64)
+    k = np.arange(10, dtype=np.float64)
+    assert np.array_equal(visits.sum(axis=1), rv.sum(axis=1))  # 20 playouts per first decision, all backed up
+    ours["visit_rank"] = (visits * k).sum(axis=1) / visits.sum(axis=1)
+    ref["visit_rank"] = (rv * k).sum(axis=1) / rv.sum(axis=1)
+    ours["max_share"] = visits.max(axis=1) / visits.sum(axis=1)
+    ref["max_share"] = rv.max(axis=1) / rv.sum(axis=1)
+    ours["chosen_rank"] = np.array([list(r["hands0"][0]).index(int(c)) for r, c in zip(games, chosen)], dtype=np.float64)
+    ref["chosen_rank"] = np.array([r["legal"].index(r["chosen"]) for r in games], dtype=np.float64)
+    report = {}
+    for name in ours:
+        diff = ours[name] - ref[name]
+        se = diff.std(ddof=1) / np.sqrt(G)
+        report[name] = (float(ours[name].mean()), float(ref[name].mean()), float(se))
+        assert abs(diff.mean()) <= 4 * se, (name, report[name])
+    print("F14 (ours, reference, paired s.e.):", report)
