@@ -76,6 +76,8 @@ def parse():
                     help="SN_OPT_PLAY_QUAD: four lanes per game, k_play_quad (default: the library's, 0)")
     ap.add_argument("--twist-round", type=int, default=None, choices=[0, 1],
                     help="SN_OPT_TWIST_ROUND: whole-round MT19937 twists in k_mt_ahead (default: the library's, 1)")
+    ap.add_argument("--twist-every", type=int, default=None, choices=[1, 2],
+                    help="SN_OPT_TWIST_EVERY: one k_mt_ahead per 1 or 2 play launches (default: the library's)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-philox", action="store_true", help="skip the philox-mode leg of config 2")
@@ -396,7 +398,8 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
     steps = sum(eng.n_mc(n) * n for n in range(2, 11)) * N_PLAYERS * games
     rows_s = eng.rows_evaluated / wall
     fused = eng.fused_mlp and eng._net is not None and eng._net.fused() is not None
-    seats = fused and eng.mlp_layer1 == "seats"
+    seats = fused and eng.mlp_layer1 in ("seats", "mfma")
+    mfma1 = fused and eng.mlp_layer1 == "mfma"  # layer 1 per candidate row on MFMA (sn_puct_mlp_mfma)
     tflops = eng.rows_evaluated * 29800 / wall / 1e12
     sq4 = None  # SQ counters of the rollout MLP kernel (tools/r04_puct_pmc.sh, eager launches)
     try:
@@ -413,8 +416,10 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
         # MFMA peak, over the whole game's wall time (every kernel included)
         roof = {"bound": "mfma", "achieved": tflops, "peak": 2500.0, "unit": "TFLOP/s", "frac": tflops / 2500.0,
                 "traffic": None, "algo_flop_per_row": 29800, "sq": sq4,
-                "kernel": ("rollout step = sn_puct_mlp_seats (MFMA: seat rows, layer 1 per seat, card column, "
-                           "layer 2, head in one persistent kernel) + k_puct_step_seats; whole-game wall time") if seats
+                "kernel": ("rollout step = sn_puct_mlp_mfma (MFMA: seat rows, layer 1 per candidate row, layer 2, "
+                           "head in one persistent kernel) + k_puct_step_seats; whole-game wall time") if mfma1
+                else ("rollout step = sn_puct_mlp_seats (MFMA: seat rows, layer 1 per seat, card column, "
+                      "layer 2, head in one persistent kernel) + k_puct_step_seats; whole-game wall time") if seats
                 else ("rollout step = sn_puct_seat_rows + PyTorch GEMM (layer 1, per seat) + sn_puct_mlp (MFMA: "
                       "card column, layer 2, head) + k_puct_step_seats; whole-game wall time")}
     else:
@@ -439,7 +444,8 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
         "decisions_per_s": 9 * N_PLAYERS * games / wall,
         "policy_rows_per_s": rows_s,
         "policy_tflops": tflops,
-        "mlp": "fused, one kernel (sn_puct_mlp_seats)" if seats else "fused (sn_puct_mlp)" if fused
+        "mlp": "fused, one kernel (sn_puct_mlp_mfma)" if mfma1 else "fused, one kernel (sn_puct_mlp_seats)" if seats
+        else "fused (sn_puct_mlp)" if fused
         else "split (PyTorch GEMMs)",
         "roofline": roof,
         "wall_s": wall,
@@ -847,7 +853,7 @@ def main():
     env = VecSechsNimmtEnv(B, N_PLAYERS, seed=0, game_offset=rank * B, rng=args.rng)
     if args.rng == "numpy":
         env.set_option(pipe_gpw=args.pipe_gpw, play_split=args.play_split, play_quad=args.play_quad,
-                       twist_round=args.twist_round)
+                       twist_round=args.twist_round, twist_every=args.twist_every)
     env.reset()
     out = make_out(env, B, not args.no_obs)
     wall, kern_ms, kt = time_rollouts(env, out, args.steps, args.warmup, world)

@@ -168,11 +168,17 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          once, each new word written once: 8 instead of 12
                          B of MT-state traffic per word); 0: exactly the
                          words the lead needs.  Same words either way.
+     SN_OPT_TWIST_EVERY  K = 1 (default) or 2: one k_mt_ahead per K play
+                         launches, twisting K launches' words at once (the
+                         lead grows by 300 words per extra launch; the ring
+                         holds them); the play launches between two twists
+                         carry no cross-stream wait.
    A pipelined (numpy-compat) rollout records its ordering event on the
    caller's stream before it returns; later calls only wait on that event,
    so the caller may destroy the stream after the call. */
 enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3, SN_OPT_TIMING = 4, SN_OPT_PIPE_GPW = 5,
-       SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7, SN_OPT_PLAY_QUAD = 8, SN_OPT_TWIST_ROUND = 9 };
+       SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7, SN_OPT_PLAY_QUAD = 8, SN_OPT_TWIST_ROUND = 9,
+       SN_OPT_TWIST_EVERY = 10 };
 sn_status sn_set_option(sn_env* env, int option, int value);
 /* pipelined rollouts whose draws ran past the twisted words (must be 0; a
    nonzero count means those games' draws are wrong) [sync].  The count is
@@ -429,6 +435,15 @@ sn_status sn_puct_mlp(sn_env* env, const sn_puct* q, int n_cur, const void* base
    sn_puct_seat_rows + a GEMM + sn_puct_mlp. */
 sn_status sn_puct_mlp_seats(sn_env* env, const sn_puct* q, int n_cur, const void* w1s, const float* w1c, const void* w2,
                             const float* head, float* logits, void* stream);
+/* The same logits with layer 1 per candidate row on the matrix cores too
+   (round 5): [card, obs, 1] x w1s on MFMA, ReLU + bf16 once, layer 2 against
+   w2q [128][128] bf16 = the [W2 | b2 | 0] rows (+ ones pass-through row) with
+   the columns permuted to the MFMA accumulator layout (k = 16 ks + 8 h + j
+   reads layer-1 output 32 (ks >> 1) + 16 (ks & 1) + 8 (j >> 2) + 4 h +
+   (j & 3); FusedMLP.fused builds it), head as sn_puct_mlp.  One launch per
+   rollout step; no VALU layer-1 column.  w1s, w2q, head 16-B aligned. */
+sn_status sn_puct_mlp_mfma(sn_env* env, const sn_puct* q, int n_cur, const void* w1s, const void* w2q, const float* head,
+                           float* logits, void* stream);
 /* best_index [D] (optional): index of the chosen card in the root legal list */
 sn_status sn_puct_choose(sn_env* env, const sn_puct* q, int32_t* actions, int32_t* best_index, void* stream);
 /* PUCTCustomedAgent (agents/mcts.py:325-451, replaces _mcts /

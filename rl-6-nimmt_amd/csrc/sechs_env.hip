@@ -1341,6 +1341,7 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
     e->phase = -1;
     e->play_split = 1;
     e->twist_round = 1;
+    e->twist_every = 1;
     e->play_quad = 0;  // measured: k_play_quad alone is no faster and slows the concurrent twist
     {
         const char* ps = getenv("SECHS_PIPE_SERIAL");
@@ -1425,7 +1426,9 @@ static void free_timing(sn_env* e) {
     for (int i = 0; i < 4 * e->tcap; i++)
         if (e->tev[i]) (void)hipEventDestroy(e->tev[i]);
     delete[] e->tev;
+    delete[] e->tev_tw;
     e->tev = nullptr;
+    e->tev_tw = nullptr;
     e->tcap = e->tn = 0;
 }
 
@@ -1464,6 +1467,10 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
             if (value < 0 || value > 1) return fail(SN_EINVAL, "play split must be 0 or 1");
             e->play_split = value;
             return SN_OK;
+        case SN_OPT_TWIST_EVERY:
+            if (value < 1 || value > 2) return fail(SN_EINVAL, "twist every must be 1 or 2");
+            e->twist_every = value;
+            return SN_OK;
         case SN_OPT_TWIST_ROUND:
             if (value < 0 || value > 1) return fail(SN_EINVAL, "twist round must be 0 or 1");
             e->twist_round = value;
@@ -1483,6 +1490,7 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
             free_timing(e);
             if (value) {
                 e->tev = new hipEvent_t[4 * value]();
+                e->tev_tw = new int[value]();
                 e->tcap = value;
                 for (int i = 0; i < 4 * value; i++) HIP_TRY(hipEventCreate(&e->tev[i]));
             }
@@ -1643,8 +1651,8 @@ sn_status sn_pipe_sync(sn_env* e, hipStream_t st) {
     HIP_TRY(hipStreamWaitEvent(st, e->ev_play, 0));
     HIP_TRY(hipEventRecord(e->ev_prep, e->side));
     HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));
-    const int p = (int)(e->pcount & 1u);
-    hipLaunchKernelGGL(k_pipe_code, dim3(grid_for(e->s.B)), dim3(kBlock), 0, st, e->s, 1 - p, p);
+    const int p = (int)(e->pcount & 1u);  // the last play launch wrote pabsc[1 - p]; the last twist ptend[tw_out]
+    hipLaunchKernelGGL(k_pipe_code, dim3(grid_for(e->s.B)), dim3(kBlock), 0, st, e->s, 1 - p, e->tw_out);
     HIP_TRY(hipGetLastError());
     e->pvalid = 0;
     return SN_OK;
@@ -1708,9 +1716,16 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     a.ring_lds = kPipeSlot;
     a.vec_out = ((((uintptr_t)a.rewards) & 15) == 0) && ((((uintptr_t)a.actions_out) & 3) == 0);
     const dim3 pg((unsigned)((s.B + kBlock / 64 - 1) / (kBlock / 64)));
+    // SN_OPT_TWIST_EVERY = K: a twist-ahead launch beside every K-th play
+    // launch, leading the consumer of the launch before it by K + 1 launches'
+    // draws (600 words per extra launch pair, + 300 per further launch: the
+    // tail bound of §4 with one more launch per step of K)
+    const int K = e->twist_every;
+    const int lead = e->pipe_lead + (K - 1) * 300;
     if (!e->pvalid) {  // start the pipeline from mt_pos: twist kPipeLead ahead, synchronously
         const int p = (int)(e->pcount & 1u);
-        const AheadArgs aa{1 - p, 0, p, e->pipe_lead, e->perr_host_dev};
+        const AheadArgs aa{1 - p, 0, p, lead, e->perr_host_dev};
+        e->tw_out = p, e->pl_tin = p, e->pphase = 0;
         if (e->twist_round) hipLaunchKernelGGL((k_mt_ahead<true, true>), pg, dim3(kBlock), 0, st, s, aa);
         else hipLaunchKernelGGL((k_mt_ahead<true, false>), pg, dim3(kBlock), 0, st, s, aa);
         HIP_TRY(hipGetLastError());
@@ -1746,9 +1761,12 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         if (a.actions_out) c.actions_out = a.actions_out + (int64_t)t0 * B * N;
         if (a.obs) c.obs = a.obs + (int64_t)t0 * B * N * a.obs_stride;
         const int p = (int)(e->pcount & 1u);
-        c.pipe_cin = 1 - p, c.pipe_cout = p, c.pipe_t = p;
-        HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));  // this launch's words are twisted
-        HIP_TRY(hipEventRecord(e->ev_main, st));         // the previous launch's consumption is final
+        const bool twist_now = (e->pphase % K) == 0;           // a twist-ahead launch beside this play launch
+        const bool wait_now = (K == 1) || (e->pphase % K) == 1;  // the first play launch after one
+        c.pipe_cin = 1 - p, c.pipe_cout = p, c.pipe_t = e->pl_tin;
+        if (wait_now) HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));  // this launch's words are twisted
+        if (twist_now) HIP_TRY(hipEventRecord(e->ev_main, st));         // the previous launch's consumption is final
+        if (e->tn < e->tcap) e->tev_tw[e->tn] = twist_now ? 1 : 0;
         hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
         if (tv) HIP_TRY(hipEventRecord(tv[0], st));
         if (quad) {
@@ -1759,18 +1777,23 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
             if (r != SN_OK) return r;
         }
         if (tv) HIP_TRY(hipEventRecord(tv[1], st));
-        // the next launch's twist, beside this one: leads the consumer of the launch before.
-        // SECHS_PIPE_SERIAL=1 (diagnostics: solo kernel times) orders it after this launch instead
-        if (e->pipe_serial) HIP_TRY(hipEventRecord(e->ev_main, st));
-        HIP_TRY(hipStreamWaitEvent(e->side, e->ev_main, 0));
-        if (tv) HIP_TRY(hipEventRecord(tv[2], e->side));
-        const AheadArgs aa{1 - p, p, 1 - p, e->pipe_lead, e->perr_host_dev};
-        if (e->twist_round) hipLaunchKernelGGL((k_mt_ahead<false, true>), pg, dim3(kBlock), 0, e->side, s, aa);
-        else hipLaunchKernelGGL((k_mt_ahead<false, false>), pg, dim3(kBlock), 0, e->side, s, aa);
-        HIP_TRY(hipGetLastError());
-        if (tv) HIP_TRY(hipEventRecord(tv[3], e->side));
-        HIP_TRY(hipEventRecord(e->ev_prep, e->side));
+        if (twist_now) {
+            // the next launches' twist, beside this one: leads the consumer of the launch before.
+            // SECHS_PIPE_SERIAL=1 (diagnostics: solo kernel times) orders it after this launch instead
+            if (e->pipe_serial) HIP_TRY(hipEventRecord(e->ev_main, st));
+            HIP_TRY(hipStreamWaitEvent(e->side, e->ev_main, 0));
+            if (tv) HIP_TRY(hipEventRecord(tv[2], e->side));
+            const AheadArgs aa{1 - p, e->tw_out, 1 - e->tw_out, lead, e->perr_host_dev};
+            if (e->twist_round) hipLaunchKernelGGL((k_mt_ahead<false, true>), pg, dim3(kBlock), 0, e->side, s, aa);
+            else hipLaunchKernelGGL((k_mt_ahead<false, false>), pg, dim3(kBlock), 0, e->side, s, aa);
+            HIP_TRY(hipGetLastError());
+            if (tv) HIP_TRY(hipEventRecord(tv[3], e->side));
+            HIP_TRY(hipEventRecord(e->ev_prep, e->side));
+            e->tw_out = 1 - e->tw_out;
+            e->pl_tin = e->tw_out;  // the play launches from the next one on read this twist's end
+        }
         e->pcount++;
+        e->pphase++;
     }
     // behind this rollout's last k_play, on the caller's stream of THIS call:
     // the next call (or sn_pipe_sync) orders behind it without touching a
@@ -2148,15 +2171,19 @@ sn_status sn_kernel_times(sn_env* e, float* play_ms, float* ahead_ms, int32_t* n
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipDeviceSynchronize());
     double sp = 0.0, sa = 0.0;
+    int na = 0;
     for (int i = 0; i < e->tn; i++) {
         float a = 0.f, b = 0.f;
         HIP_TRY(hipEventElapsedTime(&a, e->tev[4 * i], e->tev[4 * i + 1]));
-        HIP_TRY(hipEventElapsedTime(&b, e->tev[4 * i + 2], e->tev[4 * i + 3]));
-        sp += a, sa += b;
+        sp += a;
+        if (e->tev_tw[i]) {  // a twist ran beside this launch (every launch unless SN_OPT_TWIST_EVERY > 1)
+            HIP_TRY(hipEventElapsedTime(&b, e->tev[4 * i + 2], e->tev[4 * i + 3]));
+            sa += b, na++;
+        }
     }
     *n = e->tn;
     *play_ms = e->tn ? (float)(sp / e->tn) : 0.f;
-    *ahead_ms = e->tn ? (float)(sa / e->tn) : 0.f;
+    *ahead_ms = na ? (float)(sa / na) : 0.f;
     return SN_OK;
 }
 

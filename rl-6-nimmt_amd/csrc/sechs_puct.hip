@@ -985,6 +985,145 @@ __global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(PuctArgs a, int N, in
     }
 }
 
+// ---- layer 1 per candidate on MFMA too (sn_puct_mlp_mfma) ------------------
+// k_puct_mlp_seats factors layer 1 into a per-seat MFMA product (base) plus
+// a per-candidate card column built on the VALU: ~9 VALU per MFMA in the
+// tile loop (the B fragments' unpack / FMA / pack / ReLU), MFMA busy 30 %.
+// Here every candidate row [card, obs, 1] goes through layer 1 on the matrix
+// cores as well: per 32-row sub-tile, 4 k-steps x 4 output tiles of
+// v_mfma_f32_32x32x16_bf16 against W1s (A fragments held in registers; B
+// = the seat's row from LDS with the candidate's card as feature 0), ReLU +
+// bf16 rounding of the accumulators (ONE rounding of W1 row + b1, the
+// reference split path's h1), and the layer-1 C fragments ARE layer 2's B
+// fragments: lane (col, half) holds outputs o = 32 mt + 8 g + 4 half + i,
+// so layer 2's K is ordered to match -- W2 arrives column-permuted (w2q,
+// FusedMLP.fused: k = 16 ks + 8 half + j <-> o = 32 (ks >> 1) + 16 (ks & 1)
+// + 8 (j >> 2) + 4 half + (j & 3)) and no activation moves between lanes.
+// Then 8 k-steps x 4 tiles of layer 2, ReLU + bf16, the head dot.  48 MFMAs
+// and ~170 VALU per 32 rows (3.5 VALU per MFMA).  Same groups of 64 seats,
+// same persistent grid and carried-tile schedule as k_puct_mlp_seats.
+constexpr int kMlp2K = 128;              // layer-2 K: all 128 layer-1 outputs (permuted, w2q)
+constexpr int kMlp2Lds = kMlp2K + 8;     // LDS row stride of w2q (272 B: 16 lanes' b128 reads hit 64 banks)
+
+__device__ __forceinline__ void mlp2_subtile(const bf16x8_t (&w1f)[4][4], const uint16_t* srow, uint32_t card,
+                                             const uint16_t* sW, const uint32_t* sH2, int col, int half, float& out) {
+    f32x16_t acc[4];
+    // layer 1: [card, obs, 1] x W1s^T, K = 64 (4 k-steps)
+#pragma unroll
+    for (int ks = 0; ks < 4; ks++) {
+        uint4 bv = *(const uint4*)(srow + 16 * ks + 8 * half);
+        if (ks == 0 && half == 0) bv.x = (bv.x & 0xFFFF0000u) | card;  // feature 0: this candidate's card
+        const bf16x8_t b = __builtin_bit_cast(bf16x8_t, bv);
+        const f32x16_t zero = {};
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++)
+            acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1f[mt][ks], b, ks ? acc[mt] : zero, 0, 0, 0);
+    }
+    // ReLU + bf16: layer 2's B fragments, in place (pairs i = 0,1 / 2,3 of each g)
+    uint32_t hb[4][4][2];
+#pragma unroll
+    for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            hb[mt][g][0] = relu_bf16x2(pack_bf16(acc[mt][4 * g], acc[mt][4 * g + 1]));
+            hb[mt][g][1] = relu_bf16x2(pack_bf16(acc[mt][4 * g + 2], acc[mt][4 * g + 3]));
+        }
+    // layer 2: K = 128 (8 k-steps), k-step ks takes tile ks >> 1, groups g = 2 (ks & 1), + 1
+#pragma unroll
+    for (int ks = 0; ks < 8; ks++) {
+        const int mt1 = ks >> 1, g0 = 2 * (ks & 1);
+        const bf16x8_t b = __builtin_bit_cast(
+            bf16x8_t, make_uint4(hb[mt1][g0][0], hb[mt1][g0][1], hb[mt1][g0 + 1][0], hb[mt1][g0 + 1][1]));
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++) {
+            const bf16x8_t a = __builtin_bit_cast(bf16x8_t, *(const uint4*)&sW[(32 * mt + col) * kMlp2Lds + 16 * ks + 8 * half]);
+            const f32x16_t zero = {};
+            acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, ks ? acc[mt] : zero, 0, 0, 0);
+        }
+    }
+    // head: ReLU + bf16 of layer 2, dot with the head pairs, both halves summed
+    float sum = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const uint2 hw = *(const uint2*)&sH2[(32 * mt + 8 * g + 4 * half) / 2];
+            const uint32_t p0 = relu_bf16x2(pack_bf16(acc[mt][4 * g], acc[mt][4 * g + 1]));
+            const uint32_t p1 = relu_bf16x2(pack_bf16(acc[mt][4 * g + 2], acc[mt][4 * g + 3]));
+            sum = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, p0), __builtin_bit_cast(bf16x2_t, hw.x),
+                                                  sum, false);
+            sum = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, p1), __builtin_bit_cast(bf16x2_t, hw.y),
+                                                  sum, false);
+        }
+    out = sum + __shfl_xor(sum, 32);
+}
+
+__global__ __launch_bounds__(256, 2) void k_puct_mlp_mfma(PuctArgs a, int N, int n_cur, const uint16_t* w1s,
+                                                         const uint16_t* w2q, const float* head, float* logits) {
+    constexpr int kWaves = kBlock / 64;
+    __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kMlp2Lds];                 // w2q [128][136]
+    __shared__ __attribute__((aligned(16))) uint16_t sRow[2][kSeatBlock * kSeatRowLds];   // seat rows, 2 groups
+    __shared__ __attribute__((aligned(16))) float sCard[2][kSeatBlock * kHand];
+    __shared__ __attribute__((aligned(16))) uint32_t sH2[kMlpM / 2];
+    __shared__ uint16_t sLut[kLutSize];
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63, col = lane & 31, half = lane >> 5;
+    build_row_lut(sLut);
+    const int64_t S = a.D * N;
+    const int64_t groups = (S + kSeatBlock - 1) / kSeatBlock;
+    for (int i = tid; i < kMlpM * (kMlp2K / 8); i += blockDim.x) {
+        const int o = i / (kMlp2K / 8), c = i - o * (kMlp2K / 8);
+        *(uint4*)&sW[o * kMlp2Lds + 8 * c] = *(const uint4*)&w2q[o * kMlp2K + 8 * c];
+    }
+    load_head_pairs(head, sH2);
+    // layer 1's A fragments: W1s rows 32 mt + col, k-steps ks (64 VGPRs for the kernel's lifetime)
+    bf16x8_t w1f[4][4];
+#pragma unroll
+    for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+        for (int ks = 0; ks < 4; ks++)
+            w1f[mt][ks] = __builtin_bit_cast(bf16x8_t, *(const uint4*)&w1s[(32 * mt + col) * kSeatRowK + 16 * ks + 8 * half]);
+    const int sl = tid >> 2, part = tid & 3;  // phase 1: four lanes per seat
+    auto group_load = [&](int64_t grp) {
+        const int64_t s0 = grp * kSeatBlock;
+        return seat_load(a, N, s0 + min<int64_t>(sl, S - s0 - 1), part);
+    };
+    auto run_sub = [&](int buf, uint32_t t, uint32_t rows, uint32_t rbase) {  // 32-row sub-tile t of a group
+        const uint32_t r = 32u * t + (uint32_t)col;
+        const uint32_t rc = r < rows ? r : rows - 1u;
+        const uint32_t q = rc / (uint32_t)n_cur;
+        const uint32_t card = __float_as_uint(sCard[buf][q * kHand + (rc - q * (uint32_t)n_cur)]) >> 16;  // bf16 bits
+        float out;
+        mlp2_subtile(w1f, sRow[buf] + q * kSeatRowLds, card, sW, sH2, col, half, out);
+        if (half == 0 && r < rows) logits[rbase + r] = out;
+    };
+    uint32_t pend_first = 0u, pend_cnt = 0u, pend_rows = 0u, pend_rbase = 0u;
+    SeatIn nxt = group_load(min<int64_t>(blockIdx.x, groups - 1));
+    int it = 0;
+    for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x, it++) {
+        const int buf = it & 1;
+        const int64_t s0 = grp * kSeatBlock;
+        const int nseat = (int)min<int64_t>(kSeatBlock, S - s0);
+        const SeatIn cur = nxt;
+        __syncthreads();  // the tiles of two groups ago are done with this buffer
+        seat_row_part(cur, n_cur, part, sRow[buf] + sl * kSeatRowLds, sCard[buf] + sl * kHand, sLut);
+        __syncthreads();
+        const bool more = grp + gridDim.x < groups;
+        if (more) nxt = group_load(grp + gridDim.x);  // the next group's loads fly during the tiles
+        const uint32_t rows = (uint32_t)nseat * (uint32_t)n_cur;
+        const uint32_t tiles = (rows + 31u) / 32u;
+        const uint32_t rbase = (uint32_t)s0 * (uint32_t)n_cur;
+        const uint32_t total = pend_cnt + tiles;
+        uint32_t defer = more ? total % kWaves : 0u;
+        if (defer > tiles) defer = 0u;  // only this group's tiles can wait
+        for (uint32_t i = (uint32_t)wave; i < total - defer; i += kWaves) {
+            if (i < pend_cnt) run_sub(buf ^ 1, pend_first + i, pend_rows, pend_rbase);
+            else run_sub(buf, i - pend_cnt, rows, rbase);
+        }
+        pend_first = tiles - defer, pend_cnt = defer, pend_rows = rows, pend_rbase = rbase;
+    }
+}
+
 // _choose_action_from_outcomes (mcts.py:156-165, temperature None): best mean
 // over moves with playouts, strict '>'; one-card hands play it directly
 __global__ void k_puct_choose(DevState s, PuctArgs a, int32_t* actions, int32_t* best_index) {
@@ -1264,6 +1403,24 @@ sn_status sn_puct_mlp_seats(sn_env* e, const sn_puct* q, int n_cur, const void* 
     hipLaunchKernelGGL(k_puct_mlp_seats, dim3((unsigned)std::min<int64_t>(groups, 2ll * cus)), dim3(kBlock), 0,
                        (hipStream_t)stream, a, e->s.N, n_cur, (const uint16_t*)w1s, w1c, (const uint16_t*)w2, head,
                        logits);
+    HIP_TRY(hipGetLastError());
+    return SN_OK;
+}
+
+sn_status sn_puct_mlp_mfma(sn_env* e, const sn_puct* q, int n_cur, const void* w1s, const void* w2q, const float* head,
+                           float* logits, void* stream) {
+    PuctArgs a{};
+    sn_status st = puct_args(e, q, a);
+    if (st != SN_OK) return st;
+    if (n_cur < 1 || n_cur > a.n) return set_error(SN_EINVAL, "n_cur out of range");
+    if (!w1s || !w2q || !head || !logits) return set_error(SN_EINVAL, "NULL argument");
+    if ((((uintptr_t)w1s) | ((uintptr_t)w2q) | ((uintptr_t)head)) & 15)
+        return set_error(SN_EINVAL, "w1s / w2q / head must be 16-B aligned");
+    const int64_t S = a.D * e->s.N;
+    if (S * n_cur >= (1ll << 31)) return set_error(SN_EINVAL, "too many rows");
+    const int64_t groups = (S + kSeatBlock - 1) / kSeatBlock;
+    hipLaunchKernelGGL(k_puct_mlp_mfma, dim3((unsigned)std::min<int64_t>(groups, 2ll * e->cus)), dim3(kBlock), 0,
+                       (hipStream_t)stream, a, e->s.N, n_cur, (const uint16_t*)w1s, (const uint16_t*)w2q, head, logits);
     HIP_TRY(hipGetLastError());
     return SN_OK;
 }

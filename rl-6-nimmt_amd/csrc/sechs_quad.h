@@ -29,11 +29,13 @@
 namespace sechs {
 
 constexpr int kQuadGames = 16;   // games per wave
-constexpr int kQuadStage = 192;  // LDS bytes per game: 4 obs rows x 48 (lane-major), reused as the deal's deck
+constexpr int kQuadStage = 192;  // LDS bytes per game: 4 obs rows x 48 (lane-major); the wave's area doubles as decks
+constexpr int kQuadDeck = 108;   // the deal's deck per game inside that area: 27 dwords, an odd stride, so the
+                                 // 16 games' deck[i] (the same i in lockstep) fall in 16 distinct banks
 constexpr int kQuadSlot = 272;   // LDS bytes per game: the RingPipe window (16 chunks + the funnel's 8, 16-aligned)
 constexpr int kQuadWave = kQuadGames * (kQuadStage + kQuadSlot);
 static_assert(kQuadSlot >= ((kPipeWin + 15 + 15) / 16) * 16 + 16, "window + funnel reads");
-static_assert(kQuadStage >= kMaxCards, "deck fits the staging area");
+static_assert(kQuadDeck >= kMaxCards && kQuadGames * kQuadDeck <= kQuadGames * kQuadStage, "decks fit the staging area");
 
 // lane k of this lane's quad (DPP quad_perm, no LDS)
 template <int K>
@@ -170,13 +172,13 @@ __device__ __forceinline__ uint32_t quad_place(uint32_t& rlo, uint32_t& rhi, uin
     const uint32_t pen = take ? (under ? (mn >> 2) : ((best >> 4) & 0xFFu)) : 0u;  // _score_row: the old row
     SN_DASSERT(under || (best >> 16) - 1u < c);                       // the target row ends below the card
     SN_DASSERT(len >= 1u && len <= (uint32_t)(kThreshold - 1));        // every row holds 1..5 cards
-    if ((uint32_t)q == tr) {
-        const uint32_t lo_n = take ? c : (rlo | (len < 4u ? (c << (8u * len)) : 0u));
-        const uint32_t hi_n = take ? ((1u << 8) | (hc << 16) | (c << 24))
-                                   : ((len == 4u ? c : (rhi & 0xFFu)) | ((len + 1u) << 8) | ((hd + hc) << 16) | (c << 24));
-        rlo = lo_n;
-        rhi = hi_n;
-    }
+    // only the target row's lane changes its row (selects, no branch)
+    const uint32_t lo_n = take ? c : (rlo | (len < 4u ? (c << (8u * len)) : 0u));
+    const uint32_t hi_n = take ? ((1u << 8) | (hc << 16) | (c << 24))
+                               : ((len == 4u ? c : (rhi & 0xFFu)) | ((len + 1u) << 8) | ((hd + hc) << 16) | (c << 24));
+    const bool mine = (uint32_t)q == tr;
+    rlo = mine ? lo_n : rlo;
+    rhi = mine ? hi_n : rhi;
     return pen;
 }
 
@@ -197,7 +199,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_play_quad(DevState s, PlayArgs a)
     __builtin_amdgcn_s_setprio(1);  // over co-resident k_mt_ahead waves, as k_play
     uint8_t* wl = lds_dyn + (tid >> 6) * kQuadWave;
     u32x4* stage = (u32x4*)wl;  // the wave's obs rows, lane-major (3 pieces per lane: an odd stride)
-    uint8_t* deck = wl + gl * kQuadStage;
+    uint8_t* deck = wl + gl * kQuadDeck;  // (staging is idle during a deal: same wave, program order)
     PhaseProf pp;
     pp.start();
     // ---- load: seat q's hand / score / results, row q, the stream window

@@ -829,6 +829,8 @@ struct sn_env {
     int lg_mpc[16], lg_mmax[16];  // MCSAgent agents: mc_per_card, mc_max
     int phase;        // every game's env-steps since its deal, mod 10, when they are in lockstep; -1 unknown
     int play_split;   // SN_OPT_PLAY_SPLIT: role-split k_play for lockstep DrunkHamster rollouts
+    int twist_every;  // SN_OPT_TWIST_EVERY: a k_mt_ahead beside every K-th play launch (K = 1, 2)
+    int tw_out, pl_tin, pphase;  // pipeline: ptend buffer of the last twist / the next play reads; launches since start
     int twist_round;  // SN_OPT_TWIST_ROUND: k_mt_ahead twists whole MT rounds (8 instead of 12 B of MT traffic per word)
     int play_quad;    // SN_OPT_PLAY_QUAD: four lanes per game (k_play_quad) on the pipelined N = 4 path
     int pipe_serial;  // SECHS_PIPE_SERIAL=1 (diagnostics): each twist waits for the play launch before it (no overlap)
@@ -847,6 +849,7 @@ struct sn_env {
     // SN_OPT_TIMING: per-launch event pairs (k_play start/end on the launch
     // stream, k_mt_ahead start/end on `side`), tcap pairs, tn recorded
     hipEvent_t* tev;
+    int* tev_tw;  // per recorded launch: 1 if a twist ran beside it (its pair of side events is valid)
     int tcap, tn;
 };
 

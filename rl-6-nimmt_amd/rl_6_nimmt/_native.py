@@ -24,6 +24,7 @@ SN_OPT_RING_WORDS, SN_OPT_CHUNK_STEPS, SN_OPT_PIPELINE, SN_OPT_TIMING, SN_OPT_PI
 SN_OPT_PLAY_SPLIT = 7
 SN_OPT_PLAY_QUAD = 8
 SN_OPT_TWIST_ROUND = 9
+SN_OPT_TWIST_EVERY = 10
 SN_AGENT_RANDOM, SN_AGENT_MCS, SN_AGENT_EXTERNAL = 0, 1, 2
 
 class SnPuct(ctypes.Structure):
@@ -103,6 +104,7 @@ SIGNATURES = {
     "sn_puct_seat_rows": ([_P, _P, _I, _P, _I, _P, _P], _I),
     "sn_puct_mlp": ([_P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P], _I),
     "sn_puct_mlp_seats": ([_P, _P, _I, _P, _P, _P, _P, _P, _P], _I),
+    "sn_puct_mlp_mfma": ([_P, _P, _I, _P, _P, _P, _P, _P], _I),
     "sn_puct_choose": ([_P, _P, _P, _P, _P], _I),
     "sn_pcv_choose": ([_P, _P, _P, _P, _P, _P, _P, _P], _I),
     "sn_policy_sample": ([_P, _P, _P, _P, _P, _P, _P, _P], _I),

@@ -149,6 +149,8 @@ class BatchedTournament:
             raise ValueError('updates_per_round must be an int >= 1 or "games"')
         self.updates_per_round = updates_per_round
         self.optimizer_steps = {}
+        self._inherit = {}  # clone name -> its parent's engine (copy_player), until the clone's engine exists
+        self._dirty = False  # the roster changed since the handle was configured
         self.num_slots, self.min_players, self.max_players = int(num_slots), int(min_players), int(max_players)
         self.seed, self.game_offset, self.rng, self.device = int(seed), int(game_offset), rng, device
         self.elo_initial, self.elo_k = float(elo_initial), float(elo_k)
@@ -206,9 +208,13 @@ class BatchedTournament:
         if self.env is not None:
             self._configure()
 
-    def copy_player(self, old_name, new_name):
-        """tournament.py:54-60: the clone inherits the tallies, Elo and family
-        (the reference round-trips the module through temp_model.pt)"""
+    def copy_player(self, old_name, new_name, _defer=False):
+        """tournament.py:54-60: the clone inherits the tallies, Elo, family and
+        (ACER) replay (the reference round-trips the module through
+        temp_model.pt); it plays from the next game on"""
+        if self.mode == "fused" and not _defer:
+            raise NotImplementedError("the fused all-DrunkHamster league has drawn its next seats already; change the "
+                                      "roster before the first game (or use fused=False)")
         self._fold()
         try:
             clone = copy.deepcopy(self.agents[old_name])
@@ -227,9 +233,15 @@ class BatchedTournament:
         self.positions[new_name] = list(self.positions[old_name])
         for d in (self.baseline_scores, self.baseline_positions, self.baseline_wins):
             d[new_name] = list(d[old_name])
+        if old_name in self.engines:  # the clone's engine (made at the next _configure) inherits its replay
+            self._inherit[new_name] = self.engines[old_name]
+        self._dirty = True  # the handle is reconfigured before the next game
 
-    def remove_player(self, name, full_delete=False):
-        """tournament.py:62-76"""
+    def remove_player(self, name, full_delete=False, _defer=False):
+        """tournament.py:62-76 (from the next game on)"""
+        if self.mode == "fused" and not _defer:
+            raise NotImplementedError("the fused all-DrunkHamster league has drawn its next seats already; change the "
+                                      "roster before the first game (or use fused=False)")
         self._fold()
         if full_delete:
             i = self.names.index(name)
@@ -242,6 +254,7 @@ class BatchedTournament:
             self.engines.pop(name, None)
         else:
             self.active[name] = False
+        self._dirty = True  # the handle is reconfigured before the next game
 
     def active_agents(self):
         return [n for n in self.names if self.active[n]]
@@ -302,8 +315,8 @@ class BatchedTournament:
             else:
                 n_copies = 1
             for c in range(n_copies):
-                self.copy_player(name, f"{name}_{c}")
-            self.remove_player(name, full_delete=n_copies > 0)
+                self.copy_player(name, f"{name}_{c}", _defer=True)
+            self.remove_player(name, full_delete=n_copies > 0, _defer=True)
             kept += n_copies
             per_family[fam] += n_copies
         if self.env is not None:
@@ -339,11 +352,19 @@ class BatchedTournament:
         nat.check(L.sn_league_agents(self.env._h, P(kinds.ctypes.data), P(mpc.ctypes.data), P(mmax.ctypes.data)),
                   "sn_league_agents")
         self._ids = torch.tensor([self.names.index(n) for n in act], dtype=torch.long)
+        self._dirty = False
         keep = {}
         for n in act:
             if self.kinds[n] in NET_KINDS:
-                keep[n] = self.engines.get(n) or self._engine(n)
+                eng = self.engines.get(n)
+                if eng is None:
+                    eng = self._engine(n)
+                    parent = self._inherit.pop(n, None)
+                    if parent is not None:
+                        inherit_replay(eng, parent)
+                keep[n] = eng
         self.engines = keep
+        self._inherit.clear()
 
     def _engine(self, name):
         """the batched engine of one net agent over this handle (decision-list mode)"""
@@ -387,6 +408,8 @@ class BatchedTournament:
         0 past k); with rewards=True also the per-step rewards [10 games, slots, N]."""
         if self.env is None:
             self._start()
+        elif self._dirty:
+            self._configure()  # copy_player / remove_player since the last game (tournament.py:170 asserts here)
         env = self.env
         if self.mode == "fused":
             T = T_STEPS * int(games)
@@ -704,6 +727,31 @@ class BatchedTournament:
         if self.env is not None:
             self.env.close()
             self.env = None
+
+
+def inherit_replay(dst, src):
+    """a clone's ACER engine starts from its parent's replay, as the
+    reference's copy_player carries the agent's history through its
+    torch.save round trip (tournament.py:54-60, the agent's
+    SequentialHistory): the parent's most recent episodes, oldest first, up
+    to the clone's capacity.  Other engines keep nothing across rounds."""
+    from .acer import BatchedACER
+
+    if not (isinstance(dst, BatchedACER) and isinstance(src, BatchedACER)):
+        return
+    if dst.rep_rows.shape[1:] != src.rep_rows.shape[1:]:
+        return
+    n = min(src.episodes, src.capacity, dst.capacity)
+    with torch.no_grad():
+        for k in range(n):
+            e = src.episodes - n + k
+            a, b = e % src.capacity, k % dst.capacity
+            dst.rep_rows[b].copy_(src.rep_rows[a])
+            dst.rep_act[b].copy_(src.rep_act[a])
+            dst.rep_logp[b].copy_(src.rep_logp[a])
+            dst.rep_rew[b].copy_(src.rep_rew[a])
+            dst.rep_nd[b] = src.rep_nd[a]
+    dst.episodes = n
 
 
 def league_agent_stats(records, num_agents, max_players):

@@ -84,6 +84,8 @@ class FusedMLP:
                 if getattr(self, "_fused", None) is not None:
                     for old, new in zip(self._fused, fresh.fused()):
                         old.copy_(new)
+                    if getattr(self, "_w2q", None) is not None:
+                        self._fill_w2q()
         return True
 
     def _split_tensors(self):
@@ -153,6 +155,28 @@ class FusedMLP:
         self._fused = (w1t, c, w2p, head, w1s)
         return self._fused
 
+    def w2q(self):
+        """sn_puct_mlp_mfma's layer-2 weights: the fused form's [128][112] W2
+        rows widened to 128 columns, the columns permuted to the MFMA
+        accumulator layout of layer 1 (column k = 16 ks + 8 h + j holds
+        layer-1 output 32 (ks >> 1) + 16 (ks & 1) + 8 (j >> 2) + 4 h +
+        (j & 3)); None where fused() is None"""
+        fz = self.fused()
+        if fz is None:
+            return None
+        if getattr(self, "_w2q", None) is None:
+            self._w2q = torch.empty((128, 128), dtype=torch.bfloat16, device=fz[2].device)
+            self._w2q_perm = torch.tensor([32 * (k >> 5) + 16 * ((k >> 4) & 1) + 8 * ((k & 7) >> 2) + 4 * ((k >> 3) & 1)
+                                           + (k & 3) for k in range(128)], device=fz[2].device)
+            self._fill_w2q()
+        return self._w2q
+
+    def _fill_w2q(self):
+        w2p = self.fused()[2]
+        wide = torch.zeros((128, 128), dtype=torch.bfloat16, device=w2p.device)
+        wide[:, : w2p.shape[1]] = w2p
+        self._w2q.copy_(wide[:, self._w2q_perm])
+
     def __call__(self, rows):
         if self.layers is None:
             return self.module(rows)
@@ -220,7 +244,8 @@ class BatchedPUCT:
         # (FusedMLP.fused, sn_puct_mlp): bf16 nets of the reference's shape
         self.fused_mlp = os.environ.get("SECHS_FUSED_MLP", "1") != "0"  # "0": the PyTorch split path (A/B runs)
         # "seats" (default): layer 1's per-seat part inside the MLP kernel too (sn_puct_mlp_seats, one
-        # launch per step); "gemm": per-seat rows + a PyTorch GEMM + sn_puct_mlp
+        # launch per step); "mfma": layer 1 per candidate row on the matrix cores as well
+        # (sn_puct_mlp_mfma); "gemm": per-seat rows + a PyTorch GEMM + sn_puct_mlp
         self.mlp_layer1 = os.environ.get("SECHS_MLP_LAYER1", "seats")
         self._step_dev = torch.zeros((1,), dtype=torch.int32, device=dev)
 
@@ -243,6 +268,7 @@ class BatchedPUCT:
                 self._split_bufs(sp[1], sp[2])
             if self._net.fused() is not None:
                 self._fused_bufs()
+                self._net.w2q()
         return self._net
 
     def actor_device(self):
@@ -345,11 +371,16 @@ class BatchedPUCT:
             S = self.D * N
             rows, cards, base, logits = self._fused_bufs()
             rv, bv = rows[:S], base[:S]
-            if self.mlp_layer1 == "seats":
+            if self.mlp_layer1 in ("seats", "mfma"):
                 # two launches per rollout step, the arguments built once (the
                 # league's engines run this loop eagerly: host time per launch)
-                qr, deal, mlp, step = ctypes_ref(q), L.sn_puct_deal, L.sn_puct_mlp_seats, L.sn_puct_step
-                wargs = (nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p), nat.ptr(head), nat.ptr(logits), st)
+                qr, deal, step = ctypes_ref(q), L.sn_puct_deal, L.sn_puct_step
+                if self.mlp_layer1 == "mfma":  # layer 1 per candidate on MFMA too (sn_puct_mlp_mfma)
+                    mlp = L.sn_puct_mlp_mfma
+                    wargs = (nat.ptr(w1s), nat.ptr(self._net.w2q()), nat.ptr(head), nat.ptr(logits), st)
+                else:
+                    mlp = L.sn_puct_mlp_seats
+                    wargs = (nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p), nat.ptr(head), nat.ptr(logits), st)
                 lp = nat.ptr(logits)
                 for r in range(self.n_mc(n)):
                     q.rollout = r

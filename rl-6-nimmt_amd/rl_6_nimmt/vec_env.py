@@ -186,11 +186,12 @@ class VecSechsNimmtEnv:
 
     # ------------------------------------------------------------ numpy RNG bridge
     def set_option(self, ring_words=None, chunk_steps=None, pipeline=None, pipe_gpw=None, pipe_lead=None,
-                   play_split=None, play_quad=None, twist_round=None):
+                   play_split=None, play_quad=None, twist_round=None, twist_every=None):
         """rollout tuning (include/sechs.h SN_OPT_*; all numpy-compat only except play_split,
         the role-split kernel of philox handles; play_quad: four lanes per game on the
         pipelined 4-player path, k_play_quad; twist_round: whole-round MT twists in
-        k_mt_ahead); results never depend on it
+        k_mt_ahead; twist_every: one twist-ahead launch per 1 or 2 play launches); results never
+        depend on it
         (except pipe_lead < 600, a test knob that makes overruns -- PipeOverrunError -- likely)"""
         if pipe_lead is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPE_LEAD, int(pipe_lead)), "sn_set_option")
@@ -198,6 +199,8 @@ class VecSechsNimmtEnv:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPE_GPW, int(pipe_gpw)), "sn_set_option")
         if play_split is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PLAY_SPLIT, int(play_split)), "sn_set_option")
+        if twist_every is not None:
+            nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_TWIST_EVERY, int(twist_every)), "sn_set_option")
         if twist_round is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_TWIST_ROUND, int(twist_round)), "sn_set_option")
         if play_quad is not None:

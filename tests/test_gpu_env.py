@@ -21,7 +21,11 @@ RNG = {"numpy": O.RNG_NUMPY_MT, "philox": O.RNG_PHILOX}
 def venv(*a, **k):
     from rl_6_nimmt.vec_env import VecSechsNimmtEnv
 
-    return VecSechsNimmtEnv(*a, **k)
+    env = VecSechsNimmtEnv(*a, **k)
+    # SECHS_TEST_TWIST_EVERY=2: the same parity tests with one twist-ahead per two play launches
+    if env.rng == "numpy" and os.environ.get("SECHS_TEST_TWIST_EVERY"):
+        env.set_option(twist_every=int(os.environ["SECHS_TEST_TWIST_EVERY"]))
+    return env
 
 
 def load(name):

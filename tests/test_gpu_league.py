@@ -614,3 +614,39 @@ def test_updates_per_round_takes_k_adam_steps(k):
         assert games > 3 and t.optimizer_steps.get(n, 0) == want, (n, games, t.optimizer_steps)
         assert any(not torch.equal(a.cpu(), b.detach().cpu()) for a, b in zip(before[n], nets[n].parameters()))
     t.close()
+
+
+def test_clone_inherits_the_acer_replay_and_plays():
+    """the reference's copy_player round-trips the agent
+    through torch.save, so a clone carries its parent's history
+    (tournament.py:54-60); the clone's batched ACER engine starts from the
+    parent's device replay.  copy_player / remove_player take effect from
+    the next game (the handle is reconfigured lazily): the clone is seated."""
+    from rl_6_nimmt.agents import BatchedACERAgent
+    from rl_6_nimmt.league import BatchedTournament, decode_seats
+
+    torch.manual_seed(0)
+    t = BatchedTournament(256, 2, 4, seed=3, rng="numpy", fused=False, train=True)
+    a = BatchedACERAgent(minibatch=2)
+    a.train()
+    t.add_player("acer", a)
+    for i in range(3):
+        t.add_player(f"r{i}")
+    t.play_games(2)
+    src = t.engines["acer"]
+    assert src.episodes > 0
+    t.copy_player("acer", "acer_c")
+    t.remove_player("r0")
+    t._configure()  # what the next game does first
+    dst = t.engines["acer_c"]
+    n = min(src.episodes, src.capacity, dst.capacity)
+    assert n > 0 and dst.episodes == n
+    for k in range(n):
+        a_, b_ = (src.episodes - n + k) % src.capacity, k % dst.capacity
+        assert torch.equal(dst.rep_rows[b_], src.rep_rows[a_]) and torch.equal(dst.rep_logp[b_], src.rep_logp[a_])
+        assert torch.equal(dst.rep_act[b_], src.rep_act[a_]) and torch.equal(dst.rep_rew[b_], src.rep_rew[a_])
+    rec = t.play_games(1)
+    kk, ids = decode_seats(rec[0, :, 0], 4)
+    seated = (ids == t.active_agents().index("acer_c")) & (torch.arange(4, device=ids.device)[None, :] < kk[:, None])
+    assert bool(seated.any()) and "r0" not in t.active_agents()
+    t.close()

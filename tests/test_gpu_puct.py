@@ -609,6 +609,14 @@ def test_fused_mlp_equals_module_forward(B, n):
         assert not torch.isnan(lg2).any()
         assert torch.allclose(lg2, logits, rtol=2 * tol, atol=2 * tol), (lg2 - logits).abs().max()
         assert torch.allclose(lg2, want[:, 0].float(), rtol=4 * tol, atol=4 * tol)
+        # layer 1 per candidate on MFMA too (sn_puct_mlp_mfma): ONE bf16 rounding of W1 row + b1, as the
+        # module's forward on full rows -- closer to it than the factored kernels
+        lg3 = torch.full((R,), float("nan"), dtype=torch.float32, device=env.device)
+        nat.check(L.sn_puct_mlp_mfma(h, ctypes.byref(q), m, nat.ptr(w1s), nat.ptr(net.w2q()), nat.ptr(head),
+                                     nat.ptr(lg3), st), "mlp_mfma")
+        torch.cuda.synchronize()
+        assert not torch.isnan(lg3).any()
+        assert torch.allclose(lg3, want[:, 0].float(), rtol=2 * tol, atol=2 * tol), (lg3 - want[:, 0].float()).abs().max()
 
 
 def test_fused_and_split_rollouts_agree_in_law():
@@ -652,7 +660,7 @@ def test_seat_parallel_step_equals_one_lane_step(monkeypatch):
     assert torch.equal(res["1"][1], res["0"][1]) and torch.equal(res["1"][2], res["0"][2])
 
 
-def _bf16_forward_bound(x, layers, head_w, head_b, u=2.0 ** -8):
+def _bf16_forward_bound(x, layers, head_w, head_b, u=2.0 ** -8, l1_roundings=2):
     """first-order bound on |logit(bf16 path) - logit(f64 reference)| for an
     MLP Linear-ReLU-...-Linear evaluated with every input, weight, bias and
     hidden activation rounded to bf16 (unit roundoff u = 2^-8) and f32
@@ -664,7 +672,7 @@ def _bf16_forward_bound(x, layers, head_w, head_b, u=2.0 ** -8):
     h, e = x, u * x.abs()
     for i, (w, b) in enumerate(layers):
         z = h @ w.T + b
-        e = e @ w.abs().T + u * (h.abs() @ w.abs().T + b.abs()) + (2 if i == 0 else 1) * u * z.abs()
+        e = e @ w.abs().T + u * (h.abs() @ w.abs().T + b.abs()) + (l1_roundings if i == 0 else 1) * u * z.abs()
         h = torch.relu(z)
     logit = h @ head_w + head_b
     e = e @ head_w.abs() + u * (h.abs() @ head_w.abs() + head_b.abs())
@@ -681,7 +689,9 @@ def test_mlp_seats_kernel_matches_fp32_reference_net(n):
     exact vs SechsNimmtStateNormalization, test_root_rows_are_normalised_
     observations): every logit within the derived first-order bf16 bound
     (x 1.25 for the second-order terms), and every candidate's softmax
-    probability (mcts.py:219-228) within p * (exp(2 * 1.25 * max bound) - 1)."""
+    probability (mcts.py:219-228) within p * (exp(2 * 1.25 * max bound) - 1).
+    Both rollout kernels: sn_puct_mlp_seats (layer 1 factored per seat, two
+    bf16 roundings) and sn_puct_mlp_mfma (layer 1 per candidate, one)."""
     import ctypes
 
     from rl_6_nimmt import _native as nat
@@ -706,19 +716,24 @@ def test_mlp_seats_kernel_matches_fp32_reference_net(n):
         R = eng.D * N * m
         rows = torch.empty((R, 48), dtype=torch.float32, device=env.device)
         nat.check(L.sn_puct_rows(h, ctypes.byref(q), m, nat.ptr(rows), 0, st), "rows f32")
-        lg = torch.full((R,), float("nan"), dtype=torch.float32, device=env.device)
-        nat.check(L.sn_puct_mlp_seats(h, ctypes.byref(q), m, nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p), nat.ptr(head),
-                                      nat.ptr(lg), st), "mlp_seats")
-        torch.cuda.synchronize()
-        ref, bound = _bf16_forward_bound(rows.double().cpu(), layers, hw, hb)
-        got = lg.double().cpu()
-        assert not torch.isnan(got).any()
-        err = (got - ref).abs()
-        assert (err <= 1.25 * bound + 1e-6).all(), (m, float((err / bound).max()))
-        p, pr = torch.softmax(got.view(-1, m), dim=1), torch.softmax(ref.view(-1, m), dim=1)
-        lim = pr * (torch.exp(2 * 1.25 * bound.view(-1, m).max(dim=1, keepdim=True).values) - 1) + 1e-7
-        assert ((p - pr).abs() <= lim).all(), m
-        worst_dp = max(worst_dp, float((p - pr).abs().max()))
+        for kern in ("seats", "mfma"):  # the factored kernel (two layer-1 roundings) and the per-candidate one
+            lg = torch.full((R,), float("nan"), dtype=torch.float32, device=env.device)
+            if kern == "seats":
+                nat.check(L.sn_puct_mlp_seats(h, ctypes.byref(q), m, nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p),
+                                              nat.ptr(head), nat.ptr(lg), st), "mlp_seats")
+            else:
+                nat.check(L.sn_puct_mlp_mfma(h, ctypes.byref(q), m, nat.ptr(w1s), nat.ptr(net.w2q()), nat.ptr(head),
+                                             nat.ptr(lg), st), "mlp_mfma")
+            torch.cuda.synchronize()
+            ref, bound = _bf16_forward_bound(rows.double().cpu(), layers, hw, hb, l1_roundings=2 if kern == "seats" else 1)
+            got = lg.double().cpu()
+            assert not torch.isnan(got).any()
+            err = (got - ref).abs()
+            assert (err <= 1.25 * bound + 1e-6).all(), (kern, m, float((err / bound).max()))
+            p, pr = torch.softmax(got.view(-1, m), dim=1), torch.softmax(ref.view(-1, m), dim=1)
+            lim = pr * (torch.exp(2 * 1.25 * bound.view(-1, m).max(dim=1, keepdim=True).values) - 1) + 1e-7
+            assert ((p - pr).abs() <= lim).all(), (kern, m)
+            worst_dp = max(worst_dp, float((p - pr).abs().max()))
     assert worst_dp < 0.02, worst_dp  # the derived bound is loose; the kernel is far inside it
 
 

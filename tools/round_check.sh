@@ -1,7 +1,8 @@
 #!/bin/bash
-# whole-round twist bring-up: env GPU tests (parity, round boundaries,
-# exports, overruns, quad equality, debug library), the new PUCT / drop-in
-# pins, then an interleaved headline A/B over (twist_round, play_quad).
+# pipeline bring-up: env GPU tests (parity, round boundaries, exports,
+# overruns, quad equality, debug library) under the default options, the env
+# parity tests again with SN_OPT_TWIST_EVERY 2 (SECHS_TEST_TWIST_EVERY), the
+# new PUCT / drop-in pins, then an interleaved headline A/B.
 #   gpurun -- bash tools/round_check.sh <tag>
 set -o pipefail
 export TMPDIR=/tmp
@@ -10,14 +11,20 @@ OUT=$R/gpurun_out/${1:-round}
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_gpu_env.py -x -q --timeout 200 --timeout-method thread > $OUT/pytest_env.log 2>&1
 rc=$?; tail -3 $OUT/pytest_env.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -s tests/test_gpu_puct.py -k "fp32_reference_net or in_law or reference_training_loss" tests/test_gpu_dropin.py -k "trace or fp32_reference_net or in_law or reference_training_loss" > $OUT/pytest_new.log 2>&1
+SECHS_TEST_TWIST_EVERY=2 timeout -k 10 600 python -u -m pytest tests/test_gpu_env.py -x -q --timeout 200 --timeout-method thread -k "pipelined or oracle or round or quad" > $OUT/pytest_env_k2.log 2>&1
+rc=$?; tail -3 $OUT/pytest_env_k2.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -s tests/test_gpu_puct.py tests/test_gpu_dropin.py -k "trace or fp32_reference_net or in_law or reference_training_loss or module_forward" > $OUT/pytest_new.log 2>&1
 rc=$?; grep -E "PASS|FAIL|F14|Error" $OUT/pytest_new.log | tail -12; [ $rc -ge 124 ] && exit $rc
 for rep in 1 2; do
-  for tr in 1 0; do
-    for qd in 0 1; do
-      timeout -k 10 200 python bench.py --only headline --steps 200 --warmup 10 --twist-round $tr --play-quad $qd > $OUT/b_t${tr}_q${qd}_$rep.json 2> $OUT/b_t${tr}_q${qd}_$rep.err || { tail $OUT/b_t${tr}_q${qd}_$rep.err; exit 1; }
-      python -c "import json;d=json.load(open('$OUT/b_t${tr}_q${qd}_$rep.json'));r=d['roofline'];print('twist_round $tr quad $qd: %.3e env-steps/s, ms/step %.4f, play %.4f, ahead %.4f'%(d['value'],d['ms_per_step'],r['kernel_ms'],r['concurrent']['kernel_ms']))"
-    done
+  for cfg in "1 1 0" "1 2 0" "0 1 0" "1 2 1" "1 1 1"; do
+    set -- $cfg
+    nm=b_r$1_k$2_q$3_$rep
+    timeout -k 10 200 python bench.py --only headline --steps 200 --warmup 10 --twist-round $1 --twist-every $2 --play-quad $3 > $OUT/$nm.json 2> $OUT/$nm.err || { tail $OUT/$nm.err; exit 1; }
+    python -c "import json;d=json.load(open('$OUT/$nm.json'));r=d['roofline'];print('round $1 every $2 quad $3: %.3e env-steps/s, ms/step %.4f, play %.4f, ahead %.4f'%(d['value'],d['ms_per_step'],r['kernel_ms'],r['concurrent']['kernel_ms']))"
   done
+done
+for l1 in mfma seats; do
+  SECHS_MLP_LAYER1=$l1 timeout -k 10 300 python bench.py --only puct > $OUT/puct_$l1.json 2> $OUT/puct_$l1.err || { tail $OUT/puct_$l1.err; exit 1; }
+  python -c "import json;d=json.load(open('$OUT/puct_$l1.json'))['extra_config4_puct'];print('config4 $l1: %.3e playout env-steps/s, %.1f TFLOP/s'%(d['value'],d['policy_tflops']))"
 done
 echo done
