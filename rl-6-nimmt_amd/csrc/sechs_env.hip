@@ -326,8 +326,24 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
         const uint32_t ri = (t0 + j) & (uint32_t)(kPipeRing - 1);
         if ((lane & 3u) == 0u && j < n) st_nt((uint32_t*)(ring + ((int64_t)(ri >> 4) * B + g) * 16 + (ri & 12u)), d, SECHS_NT_MORE);
     };
+    // Word-0 crossings of this launch (wave-uniform count): the overwritten
+    // old mt[0] of each.  k_pipe_code's untwist needs one per round the array
+    // runs ahead of the consumer -- two with SN_OPT_TWIST_EVERY = 2 (a lead
+    // of 900 words + a whole round) -- so mt0[g] keeps the newest, mt0[B + g]
+    // the one before; kept in registers here, so no load follows a store of
+    // this launch.
+    uint32_t ncross = 0u, old0a = 0u, old0b = 0u;
+    auto cross = [&](bool hit, uint32_t old) {
+        const uint64_t m = __ballot(hit);
+        if (m) {
+            const uint32_t v = __shfl(old, (int)__builtin_ctzll(m));
+            if (ncross == 0u) old0a = v;
+            else old0b = v;
+            ncross++;
+        }
+    };
     // phase 1: words 0 .. min(n, 224)
-    uint32_t A[4], Bv[4], Cv[4], IX[4];
+    uint32_t A[4] = {0u, 0u, 0u, 0u}, Bv[4], Cv[4], IX[4];
 #pragma unroll
     for (int b = 0; b < 4; b++) {
         const uint32_t j = 64u * b + lane;
@@ -348,21 +364,23 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
         if (IX[b] != 0xFFFFu) {
             v = mt_mix(A[b], Bv[b], Cv[b]);
             st_nt(&st[IX[b]], v, SECHS_NT_MORE);
-            if (IX[b] == 0u) s.mt0[g] = A[b];
         }
+        cross(IX[b] == 0u, A[b]);
         ring_dword(j, v);
     }
     // phase 2: words 224 .. n, in order (their inputs include words just twisted)
     for (uint32_t j0 = P1; j0 < n; j0 += 64u) {
         const uint32_t j = j0 + lane;
-        uint32_t v = 0u;
+        uint32_t v = 0u, aa = 0u;
+        bool at0 = false;
         if (j < n) {
             const uint32_t idx = (T0 + j) % (uint32_t)kMtN;
-            const uint32_t aa = st[idx];
+            aa = st[idx];
             v = mt_mix(aa, st[(idx + 1u == (uint32_t)kMtN) ? 0u : idx + 1u], st[(idx < D) ? idx + kMtM : idx - D]);
             st[idx] = v;
-            if (idx == 0u) s.mt0[g] = aa;
+            at0 = idx == 0u;
         }
+        cross(at0, aa);
         ring_dword(j, v);
     }
     uint32_t Tn = Tp, te = t0 + n;
@@ -377,7 +395,7 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the completing words' stores first
             for (uint32_t i = lane; i < (uint32_t)kMtN; i += 64u) w[i] = st[i];
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            if (lane == 0u) s.mt0[g] = w[0];  // old mt[0]: the one word the untwist cannot recover
+            cross(true, w[0]);  // old mt[0]: the one word the untwist cannot recover
             for (uint32_t q = 0; q < (uint32_t)(kMtN + 63) / 64u; q++) {
                 const uint32_t i = 64u * q + lane;
                 uint32_t v = 0u;
@@ -403,9 +421,17 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
             Tn = kMtN;
         }
     }
+    SN_DASSERT(ncross <= 2u);
     if (lane == 0u) {
         s.ptp[g] = Tn;
         s.ptend[(int64_t)a.tout * B + g] = te;
+        if (ncross == 1u) {
+            s.mt0[B + g] = s.mt0[g];
+            s.mt0[g] = old0a;
+        } else if (ncross >= 2u) {
+            s.mt0[B + g] = old0a;
+            s.mt0[g] = old0b;
+        }
     }
 }
 
@@ -421,26 +447,34 @@ __global__ void k_pipe_code(DevState s, int cin, int tin) {
     if (g >= s.B) return;
     int32_t rem = (int32_t)(s.ptend[(int64_t)tin * s.B + g] - s.pabsc[(int64_t)cin * s.B + g]);
     if (rem < 0) atomicAdd(s.perr, 1u);  // an overrun (already counted): the stream is lost
-    const uint32_t tp = s.ptp[g];
-    if (rem > kMtN && tp == (uint32_t)kMtN) {
-        // a whole-round twist (SN_OPT_TWIST_ROUND) left the array one round
-        // ahead of the consumer: undo that round in place (new -> old), the
-        // host mt_unstraddle over all 624 words.  Descending j keeps every
-        // input available: y[j] needs new[j] and new[j-227] (j >= 227) or
-        // old[j+397] (j < 227, restored already); old[j] = top(y[j]) |
-        // low(y[j-1]), old[0]'s low half from mt0.
+    uint32_t tp = s.ptp[g];
+    // The array ran ahead of the consumer's round (a whole-round twist,
+    // SN_OPT_TWIST_ROUND, or the 900-word lead of SN_OPT_TWIST_EVERY = 2):
+    // undo its newest round's twisted words [0, tp) in place (new -> old),
+    // the host mt_unstraddle, until the unconsumed words fit one array.
+    // Descending j keeps every input available: y[j] needs new[j] and
+    // new[j-227] (j >= 227) or old[j+397] (j < 227: restored already, or
+    // never twisted when j + 397 >= tp); old[j] = top(y[j]) | low(y[j-1]),
+    // old[0]'s low half from mt0 (newest crossing first, then the one before).
+    for (int lvl = 0; rem > kMtN && lvl < 2; lvl++) {
         constexpr uint32_t D = kMtN - kMtM;
+        SN_DASSERT(tp >= 1u && tp <= (uint32_t)kMtN);
+        if (tp < 1u || tp > (uint32_t)kMtN) break;
         uint32_t* a = s.mt + g * kMtN;
-        uint32_t yj = mt_untwist_y_dev(a[kMtN - 1] ^ a[kMtN - 1 - D]);
-        for (int j = kMtN - 1; j >= 1; j--) {
+        auto X = [&](uint32_t j) { return a[(j >= D) ? j - D : j + kMtM]; };
+        uint32_t yj = mt_untwist_y_dev(a[tp - 1] ^ X(tp - 1));
+        for (int j = (int)tp - 1; j >= 1; j--) {
             const uint32_t jm = (uint32_t)(j - 1);
-            const uint32_t ym = mt_untwist_y_dev(a[jm] ^ a[(jm >= D) ? jm - D : jm + kMtM]);
+            const uint32_t ym = mt_untwist_y_dev(a[jm] ^ X(jm));
             a[j] = (yj & 0x80000000u) | (ym & 0x7fffffffu);
             yj = ym;
         }
         a[0] = (yj & 0x80000000u) | (s.mt0[g] & 0x7fffffffu);
-        rem -= kMtN;
+        s.mt0[g] = s.mt0[s.B + g];  // the crossing before is now the newest
+        rem -= (int32_t)tp;
+        tp = kMtN;
     }
+    SN_DASSERT(rem <= kMtN);
     s.mt_pos[g] = tp | ((uint32_t)max(rem, 0) << 16);
 }
 
@@ -1325,7 +1359,7 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
         {(void**)&s.sum_res, sizeof(int32_t) * N * B},     {(void**)&s.episodes, sizeof(int32_t) * B},
         {(void**)&s.mt_pos, sizeof(uint32_t) * B},         {(void**)&s.ctr, sizeof(uint64_t) * B},
         {(void**)&s.mt, rng_mode == SN_RNG_NUMPY_MT ? sizeof(uint32_t) * kMtN * B : 4},
-        {(void**)&s.mt0, sizeof(uint32_t) * B},
+        {(void**)&s.mt0, sizeof(uint32_t) * 2 * B},  // [0]: newest crossing, [1]: the one before (k_mt_ahead)
     };
     for (auto& a : allocs) {
         if (hipMalloc(a.p, a.bytes) != hipSuccess) {

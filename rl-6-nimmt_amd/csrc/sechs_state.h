@@ -38,7 +38,8 @@ struct DevState {
     uint32_t* mt;
     uint32_t* mt_pos;
     uint64_t* ctr;
-    uint32_t* mt0;   // [B] old-round mt[0] saved by k_mt_prep (export of straddling codes)
+    uint32_t* mt0;   // [2][B] old-round mt[0] of the newest word-0 crossing (export of straddling codes),
+                     // then the crossing before it (k_mt_ahead / k_pipe_code untwist, two rounds)
     u32x4* ring;     // [ring_w/16][B] low bytes of the words k_mt_prep twisted ahead
     int ring_w;      // ring words per game (multiple of 64), 0 = no ring
     int pad2_;

@@ -23,8 +23,11 @@ def venv(*a, **k):
 
     env = VecSechsNimmtEnv(*a, **k)
     # SECHS_TEST_TWIST_EVERY=2: the same parity tests with one twist-ahead per two play launches
+    # SECHS_TEST_TWIST_ROUND=0: with exact-lead (partial) twists instead of whole rounds
     if env.rng == "numpy" and os.environ.get("SECHS_TEST_TWIST_EVERY"):
         env.set_option(twist_every=int(os.environ["SECHS_TEST_TWIST_EVERY"]))
+    if env.rng == "numpy" and os.environ.get("SECHS_TEST_TWIST_ROUND"):
+        env.set_option(twist_round=int(os.environ["SECHS_TEST_TWIST_ROUND"]))
     return env
 
 
@@ -529,7 +532,10 @@ def test_pipelined_overrun_is_an_error(N, lead):
     from rl_6_nimmt._native import PipeOverrunError
 
     env = venv(4096, N, seed=1, rng="numpy")
-    env.set_option(pipe_lead=lead)
+    # exact-lead twists beside every launch: whole-round ones (the default) overshoot
+    # a short lead by up to a round, and a twist per two launches adds 300 words to
+    # it, so the first launches would not run dry -- the detection is the same
+    env.set_option(pipe_lead=lead, twist_round=0, twist_every=1)
     env.reset()
     with pytest.raises(PipeOverrunError):
         env.rollout(20, check=True)

@@ -558,14 +558,23 @@ def test_fused_mlp_equals_module_forward(B, n):
     bf16 tolerance of test_layer1_split_equals_full_rows).  Ragged row counts
     (a short last 64-row tile) included; B = 10 000 gives sn_puct_mlp_seats'
     persistent workgroups several 64-seat groups each."""
+    env, eng = _engine(B=B, dtype=torch.bfloat16, mc_max=4, mc_per_card=2, seed=29)
+    for t in range(10 - n):
+        env.step(eng.decide(10 - t))
+    _check_mlp_kernels(env, eng, n)
+
+
+def _check_mlp_kernels(env, eng, n, live=None):
+    """the rollout-logit kernels against the split PyTorch path and the
+    module's forward at n_cur = n, 3, 1 (rows the decision list's rollouts
+    would evaluate); live: bool [D * N] -- seats of the rollouts' games
+    (a tournament game of k < N players has N - k absent seats, whose
+    logits are never read), None = all"""
     import ctypes
 
     from rl_6_nimmt import _native as nat
 
-    env, eng = _engine(B=B, dtype=torch.bfloat16, mc_max=4, mc_per_card=2, seed=29)
     N = env.num_players
-    for t in range(10 - n):
-        env.step(eng.decide(10 - t))
     net = eng.sync_net()
     w1t, w1c, w2p, head, w1s = net.fused()
     w1a, H, kp, hidden, ha, w1c_s = net.split()
@@ -576,6 +585,8 @@ def test_fused_mlp_equals_module_forward(B, n):
     tol = 2 ** -6
     for m in (n, 3, 1):
         S, R = eng.D * N, eng.D * N * m
+        sel = torch.ones((R,), dtype=torch.bool, device=env.device) if live is None else \
+            live.to(env.device).repeat_interleave(m)
         rows = torch.empty((R, 48), dtype=torch.bfloat16, device=env.device)
         nat.check(L.sn_puct_rows(h, ctypes.byref(q), m, nat.ptr(rows), 1, st), "rows")
         srows = torch.empty((S, 56), dtype=torch.bfloat16, device=env.device)
@@ -584,7 +595,9 @@ def test_fused_mlp_equals_module_forward(B, n):
         cols = torch.empty((56, S), dtype=torch.bfloat16, device=env.device)
         cards2 = torch.empty((R,), dtype=torch.float32, device=env.device)
         nat.check(L.sn_puct_seat_cols(h, ctypes.byref(q), m, nat.ptr(cols), 56, nat.ptr(cards2), 1, st), "seat_cols")
-        assert torch.equal(srows, cols.t()) and torch.equal(cards, cards2)  # the same features, seat-major
+        torch.cuda.synchronize()
+        ls = sel.view(S, m)[:, 0]
+        assert torch.equal(srows[ls], cols.t()[ls]) and torch.equal(cards[sel], cards2[sel])  # the same features, seat-major
         base = torch.mm(srows, w1t)
         logits = torch.empty((R,), dtype=torch.float32, device=env.device)
         nat.check(L.sn_puct_mlp(h, ctypes.byref(q), m, nat.ptr(base), 112, nat.ptr(w1c), nat.ptr(cards), nat.ptr(w2p),
@@ -596,27 +609,28 @@ def test_fused_mlp_equals_module_forward(B, n):
         w2, b2 = net.layers[1]
         x2 = torch.relu(h1[:, :H].float() @ w2.float().t() + b2.float()).to(torch.bfloat16).float()
         ref = x2 @ net.head_w[:, 0].float() + net.head_b[0].float()
-        assert torch.allclose(logits, ref, rtol=1e-3, atol=1e-3), (logits - ref).abs().max()
+        assert torch.allclose(logits[sel], ref[sel], rtol=1e-3, atol=1e-3), (logits - ref)[sel].abs().max()
         with torch.no_grad():
             (want,) = net.module(rows)
-        assert torch.allclose(logits, want[:, 0].float(), rtol=4 * tol, atol=4 * tol), (logits - want[:, 0].float()).abs().max()
+        want = want[:, 0].float()
+        assert torch.allclose(logits[sel], want[sel], rtol=4 * tol, atol=4 * tol), (logits - want)[sel].abs().max()
         # layer 1's per-seat part inside the kernel too (sn_puct_mlp_seats): its base is the MFMA product
         # rounded to bf16 like the GEMM's, in another summation order (a bf16 ulp here and there)
         lg2 = torch.full((R,), float("nan"), dtype=torch.float32, device=env.device)
         nat.check(L.sn_puct_mlp_seats(h, ctypes.byref(q), m, nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p), nat.ptr(head),
                                       nat.ptr(lg2), st), "mlp_seats")
         torch.cuda.synchronize()
-        assert not torch.isnan(lg2).any()
-        assert torch.allclose(lg2, logits, rtol=2 * tol, atol=2 * tol), (lg2 - logits).abs().max()
-        assert torch.allclose(lg2, want[:, 0].float(), rtol=4 * tol, atol=4 * tol)
+        assert not torch.isnan(lg2[sel]).any()
+        assert torch.allclose(lg2[sel], logits[sel], rtol=2 * tol, atol=2 * tol), (lg2 - logits)[sel].abs().max()
+        assert torch.allclose(lg2[sel], want[sel], rtol=4 * tol, atol=4 * tol)
         # layer 1 per candidate on MFMA too (sn_puct_mlp_mfma): ONE bf16 rounding of W1 row + b1, as the
         # module's forward on full rows -- closer to it than the factored kernels
         lg3 = torch.full((R,), float("nan"), dtype=torch.float32, device=env.device)
         nat.check(L.sn_puct_mlp_mfma(h, ctypes.byref(q), m, nat.ptr(w1s), nat.ptr(net.w2q()), nat.ptr(head),
                                      nat.ptr(lg3), st), "mlp_mfma")
         torch.cuda.synchronize()
-        assert not torch.isnan(lg3).any()
-        assert torch.allclose(lg3, want[:, 0].float(), rtol=2 * tol, atol=2 * tol), (lg3 - want[:, 0].float()).abs().max()
+        assert not torch.isnan(lg3[sel]).any()
+        assert torch.allclose(lg3[sel], want[sel], rtol=2 * tol, atol=2 * tol), (lg3 - want)[sel].abs().max()
 
 
 def test_fused_and_split_rollouts_agree_in_law():
@@ -645,8 +659,8 @@ def test_fused_and_split_rollouts_agree_in_law():
 def test_seat_parallel_step_equals_one_lane_step(monkeypatch):
     """k_puct_step_seats (one lane per seat) and k_puct_step (one lane per
     decision) draw the same Philox uniforms and resolve the same cards: a
-    whole PUCT search gives identical statistics and moves, incl. a
-    tournament-style decision list with 2..4-player games"""
+    whole PUCT search gives identical statistics and moves (a plain handle;
+    the tournament branches: test_league_puct_kernels_on_tournament_decisions)"""
     res = {}
     for lanes in ("1", "0"):
         monkeypatch.setenv("SECHS_PUCT_STEP_SEATS", lanes)
@@ -658,6 +672,52 @@ def test_seat_parallel_step_equals_one_lane_step(monkeypatch):
         res[lanes] = (acts, eng.stats.clone(), eng.hist.clone())
     assert all(torch.equal(a, b) for a, b in zip(res["1"][0], res["0"][0]))
     assert torch.equal(res["1"][1], res["0"][1]) and torch.equal(res["1"][2], res["0"][2])
+
+
+def test_league_puct_kernels_on_tournament_decisions(monkeypatch):
+    """the tournament branches of the PUCT kernels (players_of,
+    absent seats q >= k of 2- and 3-player games, the live/dead seat lanes)
+    on a BatchedTournament decision list (a PUCT agent among DrunkHamsters,
+    2..4 players): k_puct_step_seats and the one-lane k_puct_step give
+    identical records over whole games (the same Philox uniforms, the same
+    cards), and on the live seats of a fresh deal's decision list the fused
+    rollout-logit kernels equal the split PyTorch path and the module's
+    forward (_check_mlp_kernels)"""
+    from rl_6_nimmt import _native as nat
+    from rl_6_nimmt.agents import DrunkHamster, PUCTAgent
+    from rl_6_nimmt.league import BatchedTournament
+
+    def league():
+        torch.manual_seed(0)
+        t = BatchedTournament(192, 2, 4, seed=13)
+        for name, a in [("P", PUCTAgent(mc_max=12, mc_per_card=3)), ("R0", DrunkHamster()), ("R1", DrunkHamster())]:
+            t.add_player(name, a)
+        return t
+
+    recs = {}
+    for lanes in ("1", "0"):
+        monkeypatch.setenv("SECHS_PUCT_STEP_SEATS", lanes)
+        t = league()
+        recs[lanes] = t.play_games(2).cpu()
+        assert t.mode == "step"
+        t.close()
+    assert torch.equal(recs["1"], recs["0"])
+    k = recs["1"][..., 0] & 15
+    assert int(k.min()) == 2 and int(k.max()) == 4  # absent seats on the lists
+    monkeypatch.delenv("SECHS_PUCT_STEP_SEATS")
+    t = league()
+    t.play_games(1)
+    env = t.env
+    nat.check(nat.lib().sn_reset(env._h, None, env._stream()), "sn_reset")  # a fresh seat draw + deal
+    t._use_decisions()
+    eng = t.engines["P"]
+    kk, _ = t.seats()
+    N = env.num_players
+    g = eng.dec.long() // N
+    live = (torch.arange(N, device=env.device)[None, :] < kk.to(env.device).long()[g][:, None]).reshape(-1)
+    assert eng.D > 0 and not bool(live.all())
+    _check_mlp_kernels(env, eng, 10, live=live)
+    t.close()
 
 
 def _bf16_forward_bound(x, layers, head_w, head_b, u=2.0 ** -8, l1_roundings=2):

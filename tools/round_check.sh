@@ -13,6 +13,8 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_env.py -x -q --timeout 200 
 rc=$?; tail -3 $OUT/pytest_env.log; [ $rc -ne 0 ] && exit $rc
 SECHS_TEST_TWIST_EVERY=2 timeout -k 10 600 python -u -m pytest tests/test_gpu_env.py -x -q --timeout 200 --timeout-method thread -k "pipelined or oracle or round or quad" > $OUT/pytest_env_k2.log 2>&1
 rc=$?; tail -3 $OUT/pytest_env_k2.log; [ $rc -ne 0 ] && exit $rc
+SECHS_TEST_TWIST_EVERY=2 SECHS_TEST_TWIST_ROUND=0 timeout -k 10 600 python -u -m pytest tests/test_gpu_env.py -x -q --timeout 200 --timeout-method thread -k "pipelined or oracle or round or quad" > $OUT/pytest_env_k2r0.log 2>&1
+rc=$?; tail -3 $OUT/pytest_env_k2r0.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -s tests/test_gpu_puct.py tests/test_gpu_dropin.py -k "trace or fp32_reference_net or in_law or reference_training_loss or module_forward" > $OUT/pytest_new.log 2>&1
 rc=$?; grep -E "PASS|FAIL|F14|Error" $OUT/pytest_new.log | tail -12; [ $rc -ge 124 ] && exit $rc
 for rep in 1 2; do
