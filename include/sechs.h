@@ -173,12 +173,25 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          lead grows by 300 words per extra launch; the ring
                          holds them); the play launches between two twists
                          carry no cross-stream wait.
+     SN_OPT_PIPE_FUSED   1: pipelined numpy-compat rollouts that qualify for
+                         k_play_quad (and B a multiple of 16) run it with the
+                         twist folded in: each launch twists one whole round
+                         of every game whose lead is short, for the launches
+                         after it (no side stream, no cross-queue waits);
+                         0 (default): k_mt_ahead beside the play launches.
+                         Same words, same outputs.
+     SN_OPT_PIPE_DEPTH   2: each twist-ahead leads the consumer position of
+                         the play launch two back (by 1 200 words, four
+                         launches) and each play launch waits for the twist
+                         two back, so neither queue waits on a kernel of the
+                         other that has only just finished; 1 (default): the
+                         launch before.  Same words, same outputs.
    A pipelined (numpy-compat) rollout records its ordering event on the
    caller's stream before it returns; later calls only wait on that event,
    so the caller may destroy the stream after the call. */
 enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3, SN_OPT_TIMING = 4, SN_OPT_PIPE_GPW = 5,
        SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7, SN_OPT_PLAY_QUAD = 8, SN_OPT_TWIST_ROUND = 9,
-       SN_OPT_TWIST_EVERY = 10 };
+       SN_OPT_TWIST_EVERY = 10, SN_OPT_PIPE_FUSED = 11, SN_OPT_PIPE_DEPTH = 12 };
 sn_status sn_set_option(sn_env* env, int option, int value);
 /* pipelined rollouts whose draws ran past the twisted words (must be 0; a
    nonzero count means those games' draws are wrong) [sync].  The count is

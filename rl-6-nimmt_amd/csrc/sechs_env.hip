@@ -264,6 +264,7 @@ struct AheadArgs {
     int tout;  // ptend parity written
     int lead;  // words to keep twisted past the consumer (kPipeLead; smaller only to test the overrun path)
     uint32_t* perr_mirror;  // host-mapped copy of *perr, refreshed at launch start (off the play stream)
+    int complete;  // ROUND: always complete a partly twisted round (SN_OPT_PIPE_FUSED's start: whole rounds after)
 };
 
 // ROUND (SN_OPT_TWIST_ROUND): twist whole MT rounds instead of exactly the
@@ -318,7 +319,7 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
     if (lead < 0 && lane == 0u) atomicAdd(s.perr, 1u);
     const uint32_t T0 = (Tp == (uint32_t)kMtN) ? 0u : Tp;
     // ROUND: the words completing the current round (none at a round boundary)
-    const uint32_t n = ROUND ? ((lead >= 0 && lead < a.lead && T0 != 0u) ? (uint32_t)kMtN - T0 : 0u)
+    const uint32_t n = ROUND ? ((lead >= 0 && (a.complete || lead < a.lead) && T0 != 0u) ? (uint32_t)kMtN - T0 : 0u)
                              : ((lead >= 0 && lead < a.lead) ? (((uint32_t)(a.lead - lead)) & ~7u) : 0u);
     auto ring_dword = [&](uint32_t j, uint32_t v) {  // t0 is 8-aligned: lanes 4m..4m+3 share one dword
         const uint32_t y = mt_temper(v) & 0xFFu;
@@ -539,6 +540,10 @@ struct PlayArgs {
     int n0;                  // k_play_split: every game's hand size at the launch's start (aligned handle)
     int dbg;                 // k_play_quad diagnostics (SECHS_QUAD_DBG; 0 in normal use): bit 0 plain stores for
                              // rewards / actions / done, bit 1 skip them, bit 2 skip the game-state stores
+    int fuse_lead;           // k_play_quad, SN_OPT_PIPE_FUSED: > 0 = the launch itself twists one whole round of
+                             // every game whose twisted lead is below this many words (no side stream)
+    int pipe_tout;           // ... and writes the twisted end to this ptend parity
+    uint32_t* perr_mirror;   // ... and publishes *perr to this host-mapped word at its start
 };
 
 // The env-step loop of one lane (game g).  R supplies the random words
@@ -1376,6 +1381,8 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
     e->play_split = 1;
     e->twist_round = 1;
     e->twist_every = 1;
+    e->pipe_fused = 0;
+    e->pipe_depth = 1;
     e->play_quad = 0;  // measured: k_play_quad alone is no faster and slows the concurrent twist
     {
         const char* ps = getenv("SECHS_PIPE_SERIAL");
@@ -1387,8 +1394,8 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
         struct {
             void** p;
             size_t bytes;
-        } pal[] = {{(void**)&s.pring, (size_t)kPipeRing * B}, {(void**)&s.pabsc, sizeof(uint32_t) * 2 * B},
-                   {(void**)&s.ptend, sizeof(uint32_t) * 2 * B}, {(void**)&s.ptp, sizeof(uint32_t) * B},
+        } pal[] = {{(void**)&s.pring, (size_t)kPipeRing * B}, {(void**)&s.pabsc, sizeof(uint32_t) * kPipeSlots * B},
+                   {(void**)&s.ptend, sizeof(uint32_t) * kPipeSlots * B}, {(void**)&s.ptp, sizeof(uint32_t) * B},
                    {(void**)&s.perr, sizeof(uint32_t)}};
         for (auto& a : pal) {
             if (hipMalloc(a.p, a.bytes) != hipSuccess) {
@@ -1409,6 +1416,12 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
             sn_destroy(e);
             return fail(SN_EHIP, "stream/event creation failed");
         }
+        for (int k = 0; k < 4; k++)
+            if (hipEventCreateWithFlags(&e->evp[k], evf) != hipSuccess ||
+                hipEventCreateWithFlags(&e->evt[k], evf) != hipSuccess) {
+                sn_destroy(e);
+                return fail(SN_EHIP, "stream/event creation failed");
+            }
         if (hipHostMalloc((void**)&e->perr_host, sizeof(uint32_t), hipHostMallocMapped) != hipSuccess ||
             hipHostGetDevicePointer((void**)&e->perr_host_dev, e->perr_host, 0) != hipSuccess) {
             sn_destroy(e);
@@ -1444,6 +1457,10 @@ sn_status sn_destroy(sn_env* e) {
     if (e->ev_prep) (void)hipEventDestroy(e->ev_prep);
     if (e->ev_main) (void)hipEventDestroy(e->ev_main);
     if (e->ev_play) (void)hipEventDestroy(e->ev_play);
+    for (int k = 0; k < 4; k++) {
+        if (e->evp[k]) (void)hipEventDestroy(e->evp[k]);
+        if (e->evt[k]) (void)hipEventDestroy(e->evt[k]);
+    }
     if (e->perr_host) (void)hipHostFree(e->perr_host);
     if (e->hbuf) (void)hipHostFree(e->hbuf);
     if (e->side) (void)hipStreamDestroy(e->side);
@@ -1512,6 +1529,14 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
         case SN_OPT_PLAY_QUAD:
             if (value < 0 || value > 1) return fail(SN_EINVAL, "play quad must be 0 or 1");
             e->play_quad = value;
+            return SN_OK;
+        case SN_OPT_PIPE_DEPTH:
+            if (value < 1 || value > 2) return fail(SN_EINVAL, "pipe depth must be 1 or 2");
+            e->pipe_depth = value;
+            return SN_OK;
+        case SN_OPT_PIPE_FUSED:
+            if (value < 0 || value > 1) return fail(SN_EINVAL, "pipe fused must be 0 or 1");
+            e->pipe_fused = value;
             return SN_OK;
         case SN_OPT_PIPE_LEAD:
             if (value < 64 || value > kPipeLead) return fail(SN_EINVAL, "pipe lead must be in 64..600");
@@ -1685,8 +1710,8 @@ sn_status sn_pipe_sync(sn_env* e, hipStream_t st) {
     HIP_TRY(hipStreamWaitEvent(st, e->ev_play, 0));
     HIP_TRY(hipEventRecord(e->ev_prep, e->side));
     HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));
-    const int p = (int)(e->pcount & 1u);  // the last play launch wrote pabsc[1 - p]; the last twist ptend[tw_out]
-    hipLaunchKernelGGL(k_pipe_code, dim3(grid_for(e->s.B)), dim3(kBlock), 0, st, e->s, 1 - p, e->tw_out);
+    // the last play launch wrote pabsc[pl_cout]; the last twist ptend[tw_out]
+    hipLaunchKernelGGL(k_pipe_code, dim3(grid_for(e->s.B)), dim3(kBlock), 0, st, e->s, e->pl_cout, e->tw_out);
     HIP_TRY(hipGetLastError());
     e->pvalid = 0;
     return SN_OK;
@@ -1754,35 +1779,53 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     // launch, leading the consumer of the launch before it by K + 1 launches'
     // draws (600 words per extra launch pair, + 300 per further launch: the
     // tail bound of §4 with one more launch per step of K)
-    const int K = e->twist_every;
-    const int lead = e->pipe_lead + (K - 1) * 300;
+    const int64_t B = s.B, N = s.N;
+    // four lanes per game (k_play_quad): N = 4 DrunkHamster seats, 48-byte
+    // 16-B aligned obs rows (or none); anything else keeps k_play
+    const bool quad_ok = gpw == 64 && N == 4 && !s.lg_K && !a.actions && !a.invalid &&
+                         (!a.obs || (a.obs_stride == 48 && (((uintptr_t)a.obs) & 15) == 0));
+    // SN_OPT_PIPE_FUSED: k_play_quad twists whole rounds itself (whole waves of games)
+    const bool fused = e->pipe_fused && quad_ok && (B % kQuadGames) == 0;
+    const bool quad = fused || (e->play_quad && quad_ok);
+    // SN_OPT_PIPE_DEPTH 2 (not fused): twist i leads the consumer of play i-2
+    // by 4 launches' words (1 200) and play i waits for twist i-2, so neither
+    // queue waits on a kernel of the other that has only just finished
+    const bool deep = !fused && e->pipe_depth == 2;
+    if (e->pvalid && ((e->pfused != 0) != fused || (e->pdeep != 0) != deep)) {  // restart in the other form
+        const sn_status r = sn_pipe_sync(e, st);
+        if (r != SN_OK) return r;
+    }
+    const int K = (fused || deep) ? 1 : e->twist_every;
+    const int lead = e->pipe_lead + (K - 1) * 300 + (deep ? 600 : 0);
     if (!e->pvalid) {  // start the pipeline from mt_pos: twist kPipeLead ahead, synchronously
         const int p = (int)(e->pcount & 1u);
-        const AheadArgs aa{1 - p, 0, p, lead, e->perr_host_dev};
-        e->tw_out = p, e->pl_tin = p, e->pphase = 0;
-        if (e->twist_round) hipLaunchKernelGGL((k_mt_ahead<true, true>), pg, dim3(kBlock), 0, st, s, aa);
+        // fused: complete a partly twisted round, so that the play launches twist whole rounds only
+        const AheadArgs aa{deep ? 3 : 1 - p, 0, deep ? 3 : p, lead, e->perr_host_dev, fused ? 1 : 0};
+        e->tw_out = p, e->pl_tin = p, e->pphase = 0, e->pl_cout = 1 - p;
+        if (deep) e->tw_out = 3, e->pl_cout = 3, e->pi = 0;  // INIT = play -1 and twist -1 (slot 3)
+        if (e->twist_round || fused) hipLaunchKernelGGL((k_mt_ahead<true, true>), pg, dim3(kBlock), 0, st, s, aa);
         else hipLaunchKernelGGL((k_mt_ahead<true, false>), pg, dim3(kBlock), 0, st, s, aa);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(e->ev_prep, st));
+        if (deep) HIP_TRY(hipEventRecord(e->evp[3], st));
         e->pvalid = 1;
+        e->pfused = fused ? 1 : 0;
+        e->pdeep = deep ? 1 : 0;
     } else if (st != e->play_st) {  // another caller stream: order behind the last pipelined k_play
         HIP_TRY(hipStreamWaitEvent(st, e->ev_play, 0));
     }
-    const int64_t B = s.B, N = s.N;
     // a tournament game adds its seat draw (<= K - 1 + 1 draws): 10-step
     // launches keep the pair tail < 1e-26 up to K = 8 agents at N <= 4
     // (tools/pipe_tail.py), beyond that 5-step launches
     const int chunk = min(e->chunk_steps, (s.lg_K > 8) ? 5 : pipe_max_chunk(s.N));
     const unsigned nblk = (gpw == 32) ? (unsigned)((s.B + 32 * (kBlock / 64) - 1) / (32 * (kBlock / 64)))
                                       : (unsigned)grid_for(s.B);
-    // four lanes per game (k_play_quad): N = 4 DrunkHamster seats, 48-byte
-    // 16-B aligned obs rows (or none); anything else keeps k_play
     {
         const char* qd = getenv("SECHS_QUAD_DBG");  // timing diagnostics only: bits 1, 2 invalidate the results
         a.dbg = qd ? atoi(qd) : 0;
     }
-    const bool quad = e->play_quad && gpw == 64 && N == 4 && !s.lg_K && !a.actions && !a.invalid &&
-                      (!a.obs || (a.obs_stride == 48 && (((uintptr_t)a.obs) & 15) == 0));
+    a.fuse_lead = fused ? lead : 0;
+    a.perr_mirror = e->perr_host_dev;
     const size_t qshmem = (size_t)kQuadWave * (kBlock / 64);
     const unsigned qblk = (unsigned)((s.B + kQuadGames * (kBlock / 64) - 1) / (kQuadGames * (kBlock / 64)));
     if (quad) HIP_TRY(hipFuncSetAttribute((const void*)k_play_quad, hipFuncAttributeMaxDynamicSharedMemorySize, (int)qshmem));
@@ -1795,6 +1838,56 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         if (a.actions_out) c.actions_out = a.actions_out + (int64_t)t0 * B * N;
         if (a.obs) c.obs = a.obs + (int64_t)t0 * B * N * a.obs_stride;
         const int p = (int)(e->pcount & 1u);
+        if (fused) {  // one launch on the caller's stream: it twists the rounds its successors read
+            c.pipe_cin = 1 - p, c.pipe_cout = p, c.pipe_t = e->tw_out, c.pipe_tout = 1 - e->tw_out;
+            if (e->tn < e->tcap) e->tev_tw[e->tn] = 0;
+            hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
+            if (tv) HIP_TRY(hipEventRecord(tv[0], st));
+            hipLaunchKernelGGL(k_play_quad, dim3(qblk), dim3(kBlock), qshmem, st, s, c);
+            HIP_TRY(hipGetLastError());
+            if (tv) HIP_TRY(hipEventRecord(tv[1], st));
+            e->tw_out = 1 - e->tw_out;
+            e->pl_tin = e->tw_out;
+            e->pl_cout = p;
+            e->pcount++;
+            e->pphase++;
+            continue;
+        }
+        if (deep) {
+            const uint64_t i = e->pi;
+            const int ti = (int)(i & 3u);
+            const int tsl = (i >= 2u) ? (int)((i - 2u) & 3u) : 3;  // twist i-2 (INIT for the first two)
+            c.pipe_cin = (int)((i + 3u) & 3u), c.pipe_cout = ti, c.pipe_t = tsl;
+            if (i >= 2u) HIP_TRY(hipStreamWaitEvent(st, e->evt[tsl], 0));  // finished a launch ago, as a rule
+            if (e->tn < e->tcap) e->tev_tw[e->tn] = 1;
+            hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
+            if (tv) HIP_TRY(hipEventRecord(tv[0], st));
+            if (quad) {
+                hipLaunchKernelGGL(k_play_quad, dim3(qblk), dim3(kBlock), qshmem, st, s, c);
+                HIP_TRY(hipGetLastError());
+            } else {
+                const sn_status r = pipe_play(s, c, gpw, nblk, shmem, st);
+                if (r != SN_OK) return r;
+            }
+            if (tv) HIP_TRY(hipEventRecord(tv[1], st));
+            HIP_TRY(hipEventRecord(e->evp[ti], st));
+            // twist i, beside play i: leads the consumer of play i-2 (INIT's for the first two);
+            // SECHS_PIPE_SERIAL=1 (diagnostics) orders it after play i instead
+            const int csl = e->pipe_serial ? ti : tsl;
+            HIP_TRY(hipStreamWaitEvent(e->side, e->evp[csl], 0));
+            if (tv) HIP_TRY(hipEventRecord(tv[2], e->side));
+            const AheadArgs aa{csl, (int)((i + 3u) & 3u), ti, lead, e->perr_host_dev};
+            if (e->twist_round) hipLaunchKernelGGL((k_mt_ahead<false, true>), pg, dim3(kBlock), 0, e->side, s, aa);
+            else hipLaunchKernelGGL((k_mt_ahead<false, false>), pg, dim3(kBlock), 0, e->side, s, aa);
+            HIP_TRY(hipGetLastError());
+            if (tv) HIP_TRY(hipEventRecord(tv[3], e->side));
+            HIP_TRY(hipEventRecord(e->evt[ti], e->side));
+            HIP_TRY(hipEventRecord(e->ev_prep, e->side));
+            e->tw_out = ti, e->pl_cout = ti;
+            e->pi++;
+            e->pcount++;
+            continue;
+        }
         const bool twist_now = (e->pphase % K) == 0;           // a twist-ahead launch beside this play launch
         const bool wait_now = (K == 1) || (e->pphase % K) == 1;  // the first play launch after one
         c.pipe_cin = 1 - p, c.pipe_cout = p, c.pipe_t = e->pl_tin;
@@ -1826,6 +1919,7 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
             e->tw_out = 1 - e->tw_out;
             e->pl_tin = e->tw_out;  // the play launches from the next one on read this twist's end
         }
+        e->pl_cout = p;
         e->pcount++;
         e->pphase++;
     }

@@ -33,7 +33,8 @@ constexpr int kQuadStage = 192;  // LDS bytes per game: 4 obs rows x 48 (lane-ma
 constexpr int kQuadDeck = 108;   // the deal's deck per game inside that area: 27 dwords, an odd stride, so the
                                  // 16 games' deck[i] (the same i in lockstep) fall in 16 distinct banks
 constexpr int kQuadSlot = 272;   // LDS bytes per game: the RingPipe window (16 chunks + the funnel's 8, 16-aligned)
-constexpr int kQuadWave = kQuadGames * (kQuadStage + kQuadSlot);
+constexpr int kQuadRound = kMtN * 4;  // SN_OPT_PIPE_FUSED: one MT19937 round (the wave's round buffer, LDS-DMA target)
+constexpr int kQuadWave = kQuadGames * (kQuadStage + kQuadSlot) + kQuadRound;  // 9 920 B: 4 blocks of 4 waves per CU
 static_assert(kQuadSlot >= ((kPipeWin + 15 + 15) / 16) * 16 + 16, "window + funnel reads");
 static_assert(kQuadDeck >= kMaxCards && kQuadGames * kQuadDeck <= kQuadGames * kQuadStage, "decks fit the staging area");
 
@@ -182,6 +183,124 @@ __device__ __forceinline__ uint32_t quad_place(uint32_t& rlo, uint32_t& rhi, uin
     return pen;
 }
 
+// SN_OPT_PIPE_FUSED: one whole MT19937 round of game G, twisted by the
+// whole wave in LDS (w: 624 words of the wave's idle obs staging area), its
+// tempered low bytes to the ring at stream positions te .. te + 623 (te is
+// 8-aligned: rounds are 624 = 78 x 8 words).  numpy's in-place order in
+// three dependency-free phases: words 0..226 read old words only (mt[i+1],
+// mt[i+397]); 227..453 read old mt[i+1] and the new mt[i-227] of phase 1;
+// 454..623 the new mt[i-227] of phase 2 (and mt[623] the new mt[0]).  One
+// HBM read and one write per word (k_mt_ahead's partial twists read the
+// i+397 input a second time).  Returns the old mt[0] (the one word the
+// sync-time untwist cannot recover, mt0).
+// v: the round's old words (word 64k + lane in v[k]), loaded by the caller
+// (a round ahead: quad_round_load)
+__device__ __forceinline__ void quad_round_load(const DevState& s, int64_t G, uint32_t lane, uint32_t (&v)[10]) {
+    const uint32_t* st = s.mt + G * kMtN;
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+        const uint32_t i = 64u * k + lane;
+        v[k] = (i < (uint32_t)kMtN) ? st[i] : 0u;
+    }
+}
+
+__device__ __forceinline__ void quad_round_to_lds(uint32_t lane, uint32_t* w, const uint32_t (&v)[10]) {
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+        const uint32_t i = 64u * k + lane;
+        if (i < (uint32_t)kMtN) w[i] = v[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+// The round's old words by LDS-DMA (global_load_lds_dwordx4, 1 KiB per
+// wave instruction, no VGPRs): three instructions for the 2 496 bytes.
+// Issued as inline asm, so hipcc neither counts them nor makes the step
+// loop's other LDS accesses wait for them (every LDS access of this kernel
+// may alias the one dynamic array); the consumer waits with an explicit
+// `s_waitcnt vmcnt(0)` a whole env-step later.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+__device__ __forceinline__ void quad_round_issue(const DevState& s, int64_t G, uint32_t lane, uint32_t* w) {
+    const uint8_t* src = (const uint8_t*)(s.mt + G * kMtN) + 16u * lane;
+    const uint32_t dst = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)w);  // LDS byte address
+    glds16(src, dst);
+    glds16(src + 1024, dst + 1024u);
+    if (lane < (uint32_t)(kMtN * 4 - 2048) / 16u) glds16(src + 2048, dst + 2048u);
+}
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// w holds the round's old words (quad_round_to_lds / quad_round_issue + vm_drain)
+__device__ __forceinline__ uint32_t quad_twist_round(const DevState& s, int64_t G, uint32_t lane, uint32_t* w,
+                                                     uint32_t te) {
+    constexpr uint32_t D = kMtN - kMtM;  // 227
+    uint32_t* st = s.mt + G * kMtN;
+    const uint32_t old0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)w[0]);
+    uint32_t nv[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {  // phase 1: i < 227
+        const uint32_t i = 64u * k + lane;
+        nv[k] = (i < D) ? mt_mix(w[i], w[i + 1u], w[i + kMtM]) : 0u;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t i = 64u * k + lane;
+        if (i < D) w[i] = nv[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+    for (int k = 0; k < 4; k++) {  // phase 2: 227 <= i < 454
+        const uint32_t i = D + 64u * k + lane;
+        nv[k] = (i < 2u * D) ? mt_mix(w[i], w[i + 1u], w[i - D]) : 0u;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t i = D + 64u * k + lane;
+        if (i < 2u * D) w[i] = nv[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+    for (int k = 0; k < 3; k++) {  // phase 3: 454 <= i < 624
+        const uint32_t i = 2u * D + 64u * k + lane;
+        nv[k] = (i < (uint32_t)kMtN) ? mt_mix(w[i], w[(i + 1u == (uint32_t)kMtN) ? 0u : i + 1u], w[i - D]) : 0u;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const uint32_t i = 2u * D + 64u * k + lane;
+        if (i < (uint32_t)kMtN) w[i] = nv[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // the new round to HBM (state words), its tempered low bytes to the ring
+    // (4 per dword: dword d holds stream positions te + 4d .. te + 4d + 3)
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+        const uint32_t i = 64u * k + lane;
+        if (i < (uint32_t)kMtN) st_nt(&st[i], w[i], SECHS_NT_MORE);
+    }
+    uint8_t* ring = (uint8_t*)s.pring;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const uint32_t d = 64u * k + lane;
+        if (d < (uint32_t)kMtN / 4u) {
+            const u32x4 x = *(const u32x4*)(w + 4u * d);
+            const uint32_t y = (mt_temper(x.x) & 0xFFu) | ((mt_temper(x.y) & 0xFFu) << 8) |
+                               ((mt_temper(x.z) & 0xFFu) << 16) | ((mt_temper(x.w) & 0xFFu) << 24);
+            const uint32_t ri = (te + 4u * d) & (uint32_t)(kPipeRing - 1);
+            st_nt((uint32_t*)(ring + ((int64_t)(ri >> 4) * s.B + G) * 16 + (ri & 12u)), y, SECHS_NT_MORE);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the LDS reads before the area's next use
+    return old0;
+}
+
 // compare-exchange of two sort keys
 __device__ __forceinline__ void qce(uint32_t& a, uint32_t& b) {
     const uint32_t lo = min(a, b), hi = max(a, b);
@@ -224,9 +343,58 @@ __global__ __launch_bounds__(kBlock, 4) void k_play_quad(DevState s, PlayArgs a)
     bool bad_start;
     P.load(s, g, q, wl + kQuadGames * kQuadStage + gl * kQuadSlot, a.pipe_cin, a.pipe_t, bad_start);
     uint32_t t = 0u;
+    // SN_OPT_PIPE_FUSED: the games of this wave whose twisted lead is short get
+    // their next round twisted by this launch, one per env-step: the round's
+    // words are LDS-DMA'd into the wave's round buffer at the step's start and
+    // twisted at its end, so the load's latency hides behind the step (a
+    // register-staged round would hold 10 VGPRs across the step).  Rounds
+    // past the steps (more needy games than steps, rare) run after the loop.
+    // The words are for the NEXT launches -- this one reads below the
+    // twisted end it started with (P.avail) -- and the ring holds lead + 624
+    // < kPipeRing words.
+    const bool fused = a.fuse_lead > 0;
+    uint32_t twisted = 0u;  // this game's round was twisted (quad-uniform)
+    uint32_t te0 = 0u, my_old0 = 0u;
+    uint64_t tw_todo = 0ull;  // needy games (bit 4 gl), not yet issued
+    int tw_fly = -1;          // the bit of the game whose round is in the buffer / in flight
+    uint32_t* rbuf = (uint32_t*)(wl + kQuadGames * (kQuadStage + kQuadSlot));
+    if (fused) {
+        if (blockIdx.x == 0 && tid == 0 && a.perr_mirror)  // overruns so far (earlier launches), as k_mt_ahead does
+            __hip_atomic_store(a.perr_mirror, __hip_atomic_load(s.perr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        te0 = s.ptend[(int64_t)a.pipe_t * B + g];
+        const uint32_t Tp = s.ptp[g];
+        // not round-aligned (the fused start completes rounds, so never): an error, no twist
+        const bool need = q == 0 && !bad_start && P.avail < (uint32_t)a.fuse_lead;
+        if (need && Tp != (uint32_t)kMtN) atomicAdd(s.perr, 1u);
+        tw_todo = __ballot(need && Tp == (uint32_t)kMtN);
+    }
+    // issue the next needy game's round into the buffer (wave-uniform)
+    if (a.dbg & 8) tw_todo = 0ull;  // timing diagnostics only (SECHS_QUAD_DBG bit 3: no twist; overruns follow)
+    auto tw_issue = [&]() {
+        if (tw_fly < 0 && tw_todo) {
+            tw_fly = (int)__builtin_ctzll(tw_todo);
+            tw_todo &= tw_todo - 1ull;
+            quad_round_issue(s, g0 + (tw_fly >> 2), (uint32_t)lane, rbuf);
+        }
+    };
+    // twist the round in the buffer (waits for its DMA and everything before it)
+    auto tw_finish = [&]() {
+        if (tw_fly >= 0) {
+            vm_drain();
+            const int64_t G = g0 + (tw_fly >> 2);
+            const uint32_t teG = (uint32_t)__builtin_amdgcn_readlane((int)te0, tw_fly);
+            // (SECHS_QUAD_DBG bit 4, timing diagnostics only: the DMA and its wait, no twist)
+            const uint32_t old0 = (a.dbg & 16) ? 0u : quad_twist_round(s, G, (uint32_t)lane, rbuf, teG);
+            if (lane == tw_fly) my_old0 = old0;
+            if (gl == (tw_fly >> 2)) twisted = 1u;
+            tw_fly = -1;
+        }
+    };
     pp.mark(PH_PROLOGUE);
     const int C = s.C;
     for (int step = 0; step < a.steps; step++) {
+        if (fused) tw_issue();
         // ---- observation rows (pre-action), env.py:174-212
         if (a.obs) {
             Board b;
@@ -340,6 +508,18 @@ __global__ __launch_bounds__(kBlock, 4) void k_play_quad(DevState s, PlayArgs a)
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             pp.mark(PH_HANDS);
         }
+        if (fused) tw_finish();
+    }
+    if (fused) {  // the round in flight, then any rounds left over (more needy games than steps)
+        tw_finish();
+        while (tw_todo) {
+            tw_issue();
+            tw_finish();
+        }
+        if (q == 0 && twisted) {  // the crossing before becomes mt0[1] (k_pipe_code's second untwist level)
+            s.mt0[B + g] = s.mt0[g];
+            s.mt0[g] = my_old0;
+        }
     }
     // ---- store the game back
     if (a.dbg & 4) return;  // timing diagnostics only
@@ -353,6 +533,10 @@ __global__ __launch_bounds__(kBlock, 4) void k_play_quad(DevState s, PlayArgs a)
     if (q == 0) {
         if (auto_reset) s.episodes[g] = eps;
         s.pabsc[(int64_t)a.pipe_cout * B + g] = P.c0 + t;  // read by k_mt_ahead on the other queue
+        if (fused) {
+            s.ptend[(int64_t)a.pipe_tout * B + g] = te0 + (twisted ? (uint32_t)kMtN : 0u);
+            if (twisted) s.ptp[g] = kMtN;
+        }
         if (bad_start || t > P.avail) atomicAdd(s.perr, 1u);  // a draw needed a word past the twisted end
     }
     pp.mark(PH_EPILOGUE);

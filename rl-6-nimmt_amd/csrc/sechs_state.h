@@ -45,8 +45,8 @@ struct DevState {
     int pad2_;
     // pipelined twist-ahead (k_mt_ahead / RingPipe, sechs_env.hip):
     u32x4* pring;    // [kPipeRing/16][B] 16-B chunks: byte of absolute stream word p at p mod kPipeRing
-    uint32_t* pabsc; // [2][B] consumer position after a play launch (by launch parity)
-    uint32_t* ptend; // [2][B] end of the twisted words after a prep launch (by launch parity)
+    uint32_t* pabsc; // [kPipeSlots][B] consumer position after a play launch (by launch parity, or index mod 4)
+    uint32_t* ptend; // [kPipeSlots][B] end of the twisted words after a prep launch (the same)
     uint32_t* ptp;   // [B] twist pointer (MtGen's pos field), owned by k_mt_ahead
     uint32_t* perr;  // [1] play lanes that ran past the twisted words (must stay 0)
     // batched tournament (sn_league_config): per game the current game's
@@ -58,6 +58,7 @@ struct DevState {
     int32_t* lpf;    // [B] 1 (| 2: quirk Q6): lpc holds this step's non-external cards
 };
 
+constexpr int kPipeSlots = 4;    // pabsc / ptend buffers (SN_OPT_PIPE_DEPTH 2 cycles through 4)
 constexpr int kPipeRing = 2048;  // ring bytes per game (>= lead + one launch; whole-round twists lead by up to 1223)
 constexpr int kPipeLead = 600;   // words k_mt_ahead keeps twisted ahead of the consumer (<= 624)
 constexpr int kPipeWin = 240;    // of them, copied to LDS per lane at a k_play launch: a 4-player
@@ -835,6 +836,14 @@ struct sn_env {
     int twist_round;  // SN_OPT_TWIST_ROUND: k_mt_ahead twists whole MT rounds (8 instead of 12 B of MT traffic per word)
     int play_quad;    // SN_OPT_PLAY_QUAD: four lanes per game (k_play_quad) on the pipelined N = 4 path
     int pipe_serial;  // SECHS_PIPE_SERIAL=1 (diagnostics): each twist waits for the play launch before it (no overlap)
+    int pipe_depth;   // SN_OPT_PIPE_DEPTH: 2 = each twist leads the consumer of the launch two back, each play
+                      // launch waits for the twist two back (no wait on a just-finished kernel of the other queue)
+    int pl_cout;      // pabsc slot the last play launch wrote
+    uint64_t pi;      // play launches since the pipeline started (depth 2)
+    hipEvent_t evp[4], evt[4];  // depth 2: after play launch / twist i, slot i mod 4
+    int pipe_fused;   // SN_OPT_PIPE_FUSED: k_play_quad twists the rounds itself (no side stream, no cross-queue waits)
+    int pfused;       // the running pipeline was started fused (whole rounds from its start)
+    int pdeep;        // the running pipeline was started with depth 2
     sechs::DevState s;
     // pipelined twist-ahead (sechs_env.hip launch_pipe): a k_mt_ahead for the
     // next play launch may be in flight on `side` (ev_prep) after a rollout

@@ -25,6 +25,8 @@ SN_OPT_PLAY_SPLIT = 7
 SN_OPT_PLAY_QUAD = 8
 SN_OPT_TWIST_ROUND = 9
 SN_OPT_TWIST_EVERY = 10
+SN_OPT_PIPE_FUSED = 11
+SN_OPT_PIPE_DEPTH = 12
 SN_AGENT_RANDOM, SN_AGENT_MCS, SN_AGENT_EXTERNAL = 0, 1, 2
 
 class SnPuct(ctypes.Structure):

@@ -28,6 +28,12 @@ def venv(*a, **k):
         env.set_option(twist_every=int(os.environ["SECHS_TEST_TWIST_EVERY"]))
     if env.rng == "numpy" and os.environ.get("SECHS_TEST_TWIST_ROUND"):
         env.set_option(twist_round=int(os.environ["SECHS_TEST_TWIST_ROUND"]))
+    # SECHS_TEST_PIPE_DEPTH=2: twists lead the consumer two launches back
+    if env.rng == "numpy" and os.environ.get("SECHS_TEST_PIPE_DEPTH"):
+        env.set_option(pipe_depth=int(os.environ["SECHS_TEST_PIPE_DEPTH"]))
+    # SECHS_TEST_PIPE_FUSED=1: k_play_quad with the twist folded in, where it applies
+    if env.rng == "numpy" and os.environ.get("SECHS_TEST_PIPE_FUSED"):
+        env.set_option(pipe_fused=int(os.environ["SECHS_TEST_PIPE_FUSED"]))
     return env
 
 
@@ -532,10 +538,10 @@ def test_pipelined_overrun_is_an_error(N, lead):
     from rl_6_nimmt._native import PipeOverrunError
 
     env = venv(4096, N, seed=1, rng="numpy")
-    # exact-lead twists beside every launch: whole-round ones (the default) overshoot
+    # exact-lead twists beside every launch: whole-round ones (incl. the fused form) overshoot
     # a short lead by up to a round, and a twist per two launches adds 300 words to
     # it, so the first launches would not run dry -- the detection is the same
-    env.set_option(pipe_lead=lead, twist_round=0, twist_every=1)
+    env.set_option(pipe_lead=lead, twist_round=0, twist_every=1, pipe_fused=0, pipe_depth=1)
     env.reset()
     with pytest.raises(PipeOverrunError):
         env.rollout(20, check=True)
@@ -594,7 +600,7 @@ def test_pipelined_full_size_across_streams():
     assert env.pipe_errors() == 0
 
 
-@pytest.mark.parametrize("B,summ", [(65536, True), (1000, True), (4104, False)])
+@pytest.mark.parametrize("B,summ", [(65536, True), (1000, True), (4104, False), (1008, False)])
 def test_quad_kernel_equals_one_lane_kernel(B, summ):
     """k_play_quad (four lanes per game: seat / row lanes, DPP quad
     reductions, SN_OPT_PLAY_QUAD) and the one-lane k_play consume the same
@@ -603,9 +609,9 @@ def test_quad_kernel_equals_one_lane_kernel(B, summ):
     and without obs; then hands, scores, results and the exported numpy
     states agree, and a 1-game reference session check via the oracle."""
     outs = {}
-    for quad in (1, 0):
+    for quad in (2, 1, 0):  # 2: the fused form (SN_OPT_PIPE_FUSED, when B is a multiple of 16)
         env = venv(B, 4, seed=77, rng="numpy", include_summaries=summ)
-        env.set_option(play_quad=quad)
+        env.set_option(play_quad=min(quad, 1), pipe_fused=int(quad == 2))
         env.reset()
         got = []
         for T, obs in ((10, True), (1, True), (7, False), (23, True)):
@@ -618,10 +624,11 @@ def test_quad_kernel_equals_one_lane_kernel(B, summ):
         assert env.pipe_errors() == 0
         outs[quad] = got
         env.close()
-    for a, b in zip(outs[1], outs[0]):
-        assert a.keys() == b.keys()
-        for k in a:
-            assert np.array_equal(a[k], b[k]), k
+    for v in (2, 1):
+        for a, b in zip(outs[v], outs[0]):
+            assert a.keys() == b.keys()
+            for k in a:
+                assert np.array_equal(a[k], b[k]), (v, k)
     ref = O.VecOracle(min(B, 256), 4, rng_mode=O.RNG_NUMPY_MT, seed=77)
     ref.reset()
     rr, rd, ra, ro = ref.rollout(10, include_summaries=summ, want_obs=True)

@@ -22,7 +22,7 @@ def load(path):
 ks = [k for k in load(sys.argv[1]) if "k_play" in k[2] or "k_mt_ahead" in k[2]]
 ks.sort()
 plays = [k for k in ks if "k_play" in k[2]]
-aheads = [k for k in ks if "k_mt_ahead<false>" in k[2]]
+aheads = [k for k in ks if "k_mt_ahead<false" in k[2]]
 print("plays", len(plays), "aheads", len(aheads))
 gaps, durs, adurs, periods = [], [], [], []
 for a, b in zip(plays[-60:-1], plays[-59:]):
