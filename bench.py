@@ -76,10 +76,8 @@ def parse():
                     help="SN_OPT_PLAY_QUAD: four lanes per game, k_play_quad (default: the library's, 0)")
     ap.add_argument("--twist-round", type=int, default=None, choices=[0, 1],
                     help="SN_OPT_TWIST_ROUND: whole-round MT19937 twists in k_mt_ahead (default: the library's, 1)")
-    ap.add_argument("--twist-every", type=int, default=None, choices=[1, 2],
-                    help="SN_OPT_TWIST_EVERY: one k_mt_ahead per 1 or 2 play launches (default: the library's)")
-    ap.add_argument("--pipe-depth", type=int, default=None, choices=[1, 2],
-                    help="SN_OPT_PIPE_DEPTH: twists lead / plays wait one or two launches back (default: the library's)")
+    ap.add_argument("--twist-every", type=int, default=None, choices=[1, 2, 3, 4],
+                    help="SN_OPT_TWIST_EVERY: one k_mt_ahead per 1 .. 4 play launches (default: the library's)")
     ap.add_argument("--pipe-fused", type=int, default=None, choices=[0, 1],
                     help="SN_OPT_PIPE_FUSED: k_play_quad twists the MT rounds itself (default: the library's)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
@@ -857,8 +855,7 @@ def main():
     env = VecSechsNimmtEnv(B, N_PLAYERS, seed=0, game_offset=rank * B, rng=args.rng)
     if args.rng == "numpy":
         env.set_option(pipe_gpw=args.pipe_gpw, play_split=args.play_split, play_quad=args.play_quad,
-                       twist_round=args.twist_round, twist_every=args.twist_every, pipe_fused=args.pipe_fused,
-                       pipe_depth=args.pipe_depth)
+                       twist_round=args.twist_round, twist_every=args.twist_every, pipe_fused=args.pipe_fused)
     env.reset()
     out = make_out(env, B, not args.no_obs)
     wall, kern_ms, kt = time_rollouts(env, out, args.steps, args.warmup, world)

@@ -168,11 +168,13 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          once, each new word written once: 8 instead of 12
                          B of MT-state traffic per word); 0: exactly the
                          words the lead needs.  Same words either way.
-     SN_OPT_TWIST_EVERY  K = 1 (default) or 2: one k_mt_ahead per K play
-                         launches, twisting K launches' words at once (the
-                         lead grows by 300 words per extra launch; the ring
-                         holds them); the play launches between two twists
-                         carry no cross-stream wait.
+     SN_OPT_TWIST_EVERY  K = 1 .. 4 (default 2): play launches in groups of
+                         K; one k_mt_ahead beside the first launch of each
+                         group twists 600 K words past the consumer (the
+                         next 2K launches' draws), and that launch waits for
+                         the twist of the group before only -- per group one
+                         cross-stream wait and one record instead of one per
+                         launch.
      SN_OPT_PIPE_FUSED   1: pipelined numpy-compat rollouts that qualify for
                          k_play_quad (and B a multiple of 16) run it with the
                          twist folded in: each launch twists one whole round
@@ -180,18 +182,12 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          after it (no side stream, no cross-queue waits);
                          0 (default): k_mt_ahead beside the play launches.
                          Same words, same outputs.
-     SN_OPT_PIPE_DEPTH   2: each twist-ahead leads the consumer position of
-                         the play launch two back (by 1 200 words, four
-                         launches) and each play launch waits for the twist
-                         two back, so neither queue waits on a kernel of the
-                         other that has only just finished; 1 (default): the
-                         launch before.  Same words, same outputs.
    A pipelined (numpy-compat) rollout records its ordering event on the
    caller's stream before it returns; later calls only wait on that event,
    so the caller may destroy the stream after the call. */
 enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3, SN_OPT_TIMING = 4, SN_OPT_PIPE_GPW = 5,
        SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7, SN_OPT_PLAY_QUAD = 8, SN_OPT_TWIST_ROUND = 9,
-       SN_OPT_TWIST_EVERY = 10, SN_OPT_PIPE_FUSED = 11, SN_OPT_PIPE_DEPTH = 12 };
+       SN_OPT_TWIST_EVERY = 10, SN_OPT_PIPE_FUSED = 11 };
 sn_status sn_set_option(sn_env* env, int option, int value);
 /* pipelined rollouts whose draws ran past the twisted words (must be 0; a
    nonzero count means those games' draws are wrong) [sync].  The count is
@@ -402,6 +398,11 @@ typedef struct {
 sn_status sn_puct_root_rows(sn_env* env, const sn_puct* q, void* rows, int bf16, void* stream);
 sn_status sn_puct_init(sn_env* env, const sn_puct* q, const float* root_logits, void* stream);
 sn_status sn_puct_deal(sn_env* env, const sn_puct* q, void* stream);
+/* sn_puct_deal for rollouts r0 .. r0 + nr - 1 in one launch: rollout r's
+   initial state at ro_out + ((r - r0) * num_decisions + d) * 48 int32 (the
+   layout of sn_puct.rollouts); point sn_puct.rollouts at rollout r's slice
+   and run its steps there -- the same states, dealt with nr x D lanes. */
+sn_status sn_puct_deal_batch(sn_env* env, const sn_puct* q, int r0, int nr, void* ro_out, void* stream);
 sn_status sn_puct_rows(sn_env* env, const sn_puct* q, int n_cur, void* rows, int bf16, void* stream);
 sn_status sn_puct_step(sn_env* env, const sn_puct* q, const float* logits, int t, int n_cur, void* stream);
 /* Layer-1 split of the rollout MLP (MultiHeadedMLP 48 -> H -> ...), in

@@ -267,6 +267,102 @@ struct AheadArgs {
     int complete;  // ROUND: always complete a partly twisted round (SN_OPT_PIPE_FUSED's start: whole rounds after)
 };
 
+// One whole MT19937 round of game G, twisted by the whole wave in LDS (w:
+// 624 words; k_mt_ahead's whole-round twists, k_play_quad's fused ones), its
+// tempered low bytes to the ring at stream positions te .. te + 623 (te is
+// 8-aligned: rounds are 624 = 78 x 8 words).  numpy's in-place order in
+// three dependency-free phases: words 0..226 read old words only (mt[i+1],
+// mt[i+397]); 227..453 read old mt[i+1] and the new mt[i-227] of phase 1;
+// 454..623 the new mt[i-227] of phase 2 (and mt[623] the new mt[0]).  One
+// HBM read and one write per word (k_mt_ahead's partial twists read the
+// i+397 input a second time).  Returns the old mt[0] (the one word the
+// sync-time untwist cannot recover, mt0).
+// v: the round's old words (word 64k + lane in v[k]), loaded by the caller
+// (a round ahead: mt_round_load)
+__device__ __forceinline__ void mt_round_load(const DevState& s, int64_t G, uint32_t lane, uint32_t (&v)[10]) {
+    const uint32_t* st = s.mt + G * kMtN;
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+        const uint32_t i = 64u * k + lane;
+        v[k] = (i < (uint32_t)kMtN) ? st[i] : 0u;
+    }
+}
+
+__device__ __forceinline__ void mt_round_to_lds(uint32_t lane, uint32_t* w, const uint32_t (&v)[10]) {
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+        const uint32_t i = 64u * k + lane;
+        if (i < (uint32_t)kMtN) w[i] = v[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+// w holds the round's old words (mt_round_to_lds, or k_play_quad's LDS-DMA)
+__device__ __forceinline__ uint32_t mt_twist_round(const DevState& s, int64_t G, uint32_t lane, uint32_t* w,
+                                                     uint32_t te) {
+    constexpr uint32_t D = kMtN - kMtM;  // 227
+    uint32_t* st = s.mt + G * kMtN;
+    const uint32_t old0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)w[0]);
+    uint32_t nv[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {  // phase 1: i < 227
+        const uint32_t i = 64u * k + lane;
+        nv[k] = (i < D) ? mt_mix(w[i], w[i + 1u], w[i + kMtM]) : 0u;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t i = 64u * k + lane;
+        if (i < D) w[i] = nv[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+    for (int k = 0; k < 4; k++) {  // phase 2: 227 <= i < 454
+        const uint32_t i = D + 64u * k + lane;
+        nv[k] = (i < 2u * D) ? mt_mix(w[i], w[i + 1u], w[i - D]) : 0u;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t i = D + 64u * k + lane;
+        if (i < 2u * D) w[i] = nv[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+    for (int k = 0; k < 3; k++) {  // phase 3: 454 <= i < 624
+        const uint32_t i = 2u * D + 64u * k + lane;
+        nv[k] = (i < (uint32_t)kMtN) ? mt_mix(w[i], w[(i + 1u == (uint32_t)kMtN) ? 0u : i + 1u], w[i - D]) : 0u;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const uint32_t i = 2u * D + 64u * k + lane;
+        if (i < (uint32_t)kMtN) w[i] = nv[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // the new round to HBM (state words), its tempered low bytes to the ring
+    // (4 per dword: dword d holds stream positions te + 4d .. te + 4d + 3)
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+        const uint32_t i = 64u * k + lane;
+        if (i < (uint32_t)kMtN) st_nt(&st[i], w[i], SECHS_NT_MORE);
+    }
+    uint8_t* ring = (uint8_t*)s.pring;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const uint32_t d = 64u * k + lane;
+        if (d < (uint32_t)kMtN / 4u) {
+            const u32x4 x = *(const u32x4*)(w + 4u * d);
+            const uint32_t y = (mt_temper(x.x) & 0xFFu) | ((mt_temper(x.y) & 0xFFu) << 8) |
+                               ((mt_temper(x.z) & 0xFFu) << 16) | ((mt_temper(x.w) & 0xFFu) << 24);
+            const uint32_t ri = (te + 4u * d) & (uint32_t)(kPipeRing - 1);
+            st_nt((uint32_t*)(ring + ((int64_t)(ri >> 4) * s.B + G) * 16 + (ri & 12u)), y, SECHS_NT_MORE);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the LDS reads before the area's next use
+    return old0;
+}
+
 // ROUND (SN_OPT_TWIST_ROUND): twist whole MT rounds instead of exactly the
 // words the lead needs.  A twist that is due first completes the current
 // round (the per-64-word form below), then -- if the lead is still short --
@@ -329,17 +425,17 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
     };
     // Word-0 crossings of this launch (wave-uniform count): the overwritten
     // old mt[0] of each.  k_pipe_code's untwist needs one per round the array
-    // runs ahead of the consumer -- two with SN_OPT_TWIST_EVERY = 2 (a lead
-    // of 900 words + a whole round) -- so mt0[g] keeps the newest, mt0[B + g]
-    // the one before; kept in registers here, so no load follows a store of
-    // this launch.
-    uint32_t ncross = 0u, old0a = 0u, old0b = 0u;
+    // runs ahead of the consumer -- up to three with SN_OPT_TWIST_EVERY = 3
+    // (a lead of 1 800 words) -- so mt0[k B + g] keeps the k-th newest; kept
+    // in registers here, so no load follows a store of this launch.
+    uint32_t ncross = 0u, old0[kMt0Levels] = {};
     auto cross = [&](bool hit, uint32_t old) {
         const uint64_t m = __ballot(hit);
         if (m) {
             const uint32_t v = __shfl(old, (int)__builtin_ctzll(m));
-            if (ncross == 0u) old0a = v;
-            else old0b = v;
+#pragma unroll
+            for (int k = kMt0Levels - 1; k > 0; k--) old0[k] = old0[k - 1];  // newest first
+            old0[0] = v;
             ncross++;
         }
     };
@@ -390,48 +486,29 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
         while (Tn > (uint32_t)kMtN) Tn -= kMtN;
     }
     if constexpr (ROUND) {
-        if (lead >= 0 && lead + (int32_t)n < a.lead) {  // one whole round, in LDS
-            __shared__ uint32_t wround[kBlock / 64][kMtN];
+        // whole rounds in LDS while the lead is short (one per twist at K <= 2, up to kMt0Levels - 1)
+        for (int rr = 0; rr < kMt0Levels - 1 && lead >= 0 && lead + (int32_t)(te - t0) < a.lead; rr++) {
+            __shared__ __attribute__((aligned(16))) uint32_t wround[kBlock / 64][kMtN];
             uint32_t* w = wround[threadIdx.x >> 6];
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the completing words' stores first
-            for (uint32_t i = lane; i < (uint32_t)kMtN; i += 64u) w[i] = st[i];
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            cross(true, w[0]);  // old mt[0]: the one word the untwist cannot recover
-            for (uint32_t q = 0; q < (uint32_t)(kMtN + 63) / 64u; q++) {
-                const uint32_t i = 64u * q + lane;
-                uint32_t v = 0u;
-                if (i < (uint32_t)kMtN) {
-                    // numpy's in-place order, 64 words at a time: mt[i+1] (old; mt[0] new for i = 623),
-                    // mt[i+397] (old, i < 227) or mt[i-227] (new, twisted >= 3 chunks ago)
-                    v = mt_mix(w[i], w[(i + 1u == (uint32_t)kMtN) ? 0u : i + 1u], w[(i < D) ? i + kMtM : i - D]);
-                }
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the chunk's reads before its writes
-                if (i < (uint32_t)kMtN) {
-                    w[i] = v;
-                    st_nt(&st[i], v, SECHS_NT_MORE);
-                }
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                // tempered low bytes, 4 per dword (te is 8-aligned, 624 = 156 dwords)
-                const uint32_t y = mt_temper(v) & 0xFFu;
-                const uint32_t d = y | (__shfl_down(y, 1) << 8) | (__shfl_down(y, 2) << 16) | (__shfl_down(y, 3) << 24);
-                const uint32_t ri = (te + i) & (uint32_t)(kPipeRing - 1);
-                if ((lane & 3u) == 0u && i < (uint32_t)kMtN)
-                    st_nt((uint32_t*)(ring + ((int64_t)(ri >> 4) * B + g) * 16 + (ri & 12u)), d, SECHS_NT_MORE);
-            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the words twisted before: stored first
+            uint32_t v[10];
+            mt_round_load(s, g, lane, v);  // all ten loads in flight at once
+            mt_round_to_lds(lane, w, v);
+            // three dependency-free phases (mt_twist_round); old mt[0]: the one word the untwist cannot recover
+            cross(true, mt_twist_round(s, g, lane, w, te));
             te += kMtN;
             Tn = kMtN;
         }
     }
-    SN_DASSERT(ncross <= 2u);
+    SN_DASSERT(ncross <= (uint32_t)kMt0Levels);
     if (lane == 0u) {
         s.ptp[g] = Tn;
         s.ptend[(int64_t)a.tout * B + g] = te;
-        if (ncross == 1u) {
-            s.mt0[B + g] = s.mt0[g];
-            s.mt0[g] = old0a;
-        } else if (ncross >= 2u) {
-            s.mt0[B + g] = old0a;
-            s.mt0[g] = old0b;
+        if (ncross) {  // the stack of crossings, newest first: this launch's, then the older ones
+            uint32_t stk[kMt0Levels];
+            for (int k = 0; k < kMt0Levels; k++) stk[k] = s.mt0[k * B + g];
+            for (int k = 0; k < kMt0Levels; k++)
+                s.mt0[k * B + g] = (k < (int)ncross) ? old0[k] : stk[k - (int)ncross];
         }
     }
 }
@@ -456,8 +533,9 @@ __global__ void k_pipe_code(DevState s, int cin, int tin) {
     // Descending j keeps every input available: y[j] needs new[j] and
     // new[j-227] (j >= 227) or old[j+397] (j < 227: restored already, or
     // never twisted when j + 397 >= tp); old[j] = top(y[j]) | low(y[j-1]),
-    // old[0]'s low half from mt0 (newest crossing first, then the one before).
-    for (int lvl = 0; rem > kMtN && lvl < 2; lvl++) {
+    // old[0]'s low half from mt0 (newest crossing first, then the ones before).
+    int lvl = 0;
+    for (; rem > kMtN && lvl < kMt0Levels; lvl++) {
         constexpr uint32_t D = kMtN - kMtM;
         SN_DASSERT(tp >= 1u && tp <= (uint32_t)kMtN);
         if (tp < 1u || tp > (uint32_t)kMtN) break;
@@ -470,11 +548,12 @@ __global__ void k_pipe_code(DevState s, int cin, int tin) {
             a[j] = (yj & 0x80000000u) | (ym & 0x7fffffffu);
             yj = ym;
         }
-        a[0] = (yj & 0x80000000u) | (s.mt0[g] & 0x7fffffffu);
-        s.mt0[g] = s.mt0[s.B + g];  // the crossing before is now the newest
+        a[0] = (yj & 0x80000000u) | (s.mt0[lvl * s.B + g] & 0x7fffffffu);
         rem -= (int32_t)tp;
         tp = kMtN;
     }
+    for (int k = 0; lvl && k < kMt0Levels; k++)  // the crossings not undone are the newest now
+        s.mt0[k * s.B + g] = (k + lvl < kMt0Levels) ? s.mt0[(k + lvl) * s.B + g] : 0u;
     SN_DASSERT(rem <= kMtN);
     s.mt_pos[g] = tp | ((uint32_t)max(rem, 0) << 16);
 }
@@ -1364,7 +1443,7 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
         {(void**)&s.sum_res, sizeof(int32_t) * N * B},     {(void**)&s.episodes, sizeof(int32_t) * B},
         {(void**)&s.mt_pos, sizeof(uint32_t) * B},         {(void**)&s.ctr, sizeof(uint64_t) * B},
         {(void**)&s.mt, rng_mode == SN_RNG_NUMPY_MT ? sizeof(uint32_t) * kMtN * B : 4},
-        {(void**)&s.mt0, sizeof(uint32_t) * 2 * B},  // [0]: newest crossing, [1]: the one before (k_mt_ahead)
+        {(void**)&s.mt0, sizeof(uint32_t) * kMt0Levels * B},  // [0]: newest crossing, then the ones before
     };
     for (auto& a : allocs) {
         if (hipMalloc(a.p, a.bytes) != hipSuccess) {
@@ -1379,10 +1458,11 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
     e->pipe_lead = kPipeLead;
     e->phase = -1;
     e->play_split = 1;
+    // measured: three-phase whole-round twists and
+    // one twist per two play launches: 0.093 -> 0.085-0.088 ms per step
     e->twist_round = 1;
-    e->twist_every = 1;
-    e->pipe_fused = 0;
-    e->pipe_depth = 1;
+    e->twist_every = 2;
+    e->pipe_fused = 0;  // measured slower: the twist's latency lands inside the play waves
     e->play_quad = 0;  // measured: k_play_quad alone is no faster and slows the concurrent twist
     {
         const char* ps = getenv("SECHS_PIPE_SERIAL");
@@ -1416,9 +1496,8 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
             sn_destroy(e);
             return fail(SN_EHIP, "stream/event creation failed");
         }
-        for (int k = 0; k < 4; k++)
-            if (hipEventCreateWithFlags(&e->evp[k], evf) != hipSuccess ||
-                hipEventCreateWithFlags(&e->evt[k], evf) != hipSuccess) {
+        for (int k = 0; k < 2; k++)
+            if (hipEventCreateWithFlags(&e->evt[k], evf) != hipSuccess) {
                 sn_destroy(e);
                 return fail(SN_EHIP, "stream/event creation failed");
             }
@@ -1457,10 +1536,8 @@ sn_status sn_destroy(sn_env* e) {
     if (e->ev_prep) (void)hipEventDestroy(e->ev_prep);
     if (e->ev_main) (void)hipEventDestroy(e->ev_main);
     if (e->ev_play) (void)hipEventDestroy(e->ev_play);
-    for (int k = 0; k < 4; k++) {
-        if (e->evp[k]) (void)hipEventDestroy(e->evp[k]);
+    for (int k = 0; k < 2; k++)
         if (e->evt[k]) (void)hipEventDestroy(e->evt[k]);
-    }
     if (e->perr_host) (void)hipHostFree(e->perr_host);
     if (e->hbuf) (void)hipHostFree(e->hbuf);
     if (e->side) (void)hipStreamDestroy(e->side);
@@ -1519,7 +1596,7 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
             e->play_split = value;
             return SN_OK;
         case SN_OPT_TWIST_EVERY:
-            if (value < 1 || value > 2) return fail(SN_EINVAL, "twist every must be 1 or 2");
+            if (value < 1 || value > 4) return fail(SN_EINVAL, "twist every must be 1 .. 4");
             e->twist_every = value;
             return SN_OK;
         case SN_OPT_TWIST_ROUND:
@@ -1529,10 +1606,6 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
         case SN_OPT_PLAY_QUAD:
             if (value < 0 || value > 1) return fail(SN_EINVAL, "play quad must be 0 or 1");
             e->play_quad = value;
-            return SN_OK;
-        case SN_OPT_PIPE_DEPTH:
-            if (value < 1 || value > 2) return fail(SN_EINVAL, "pipe depth must be 1 or 2");
-            e->pipe_depth = value;
             return SN_OK;
         case SN_OPT_PIPE_FUSED:
             if (value < 0 || value > 1) return fail(SN_EINVAL, "pipe fused must be 0 or 1");
@@ -1775,10 +1848,6 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     a.ring_lds = kPipeSlot;
     a.vec_out = ((((uintptr_t)a.rewards) & 15) == 0) && ((((uintptr_t)a.actions_out) & 3) == 0);
     const dim3 pg((unsigned)((s.B + kBlock / 64 - 1) / (kBlock / 64)));
-    // SN_OPT_TWIST_EVERY = K: a twist-ahead launch beside every K-th play
-    // launch, leading the consumer of the launch before it by K + 1 launches'
-    // draws (600 words per extra launch pair, + 300 per further launch: the
-    // tail bound of §4 with one more launch per step of K)
     const int64_t B = s.B, N = s.N;
     // four lanes per game (k_play_quad): N = 4 DrunkHamster seats, 48-byte
     // 16-B aligned obs rows (or none); anything else keeps k_play
@@ -1787,30 +1856,32 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     // SN_OPT_PIPE_FUSED: k_play_quad twists whole rounds itself (whole waves of games)
     const bool fused = e->pipe_fused && quad_ok && (B % kQuadGames) == 0;
     const bool quad = fused || (e->play_quad && quad_ok);
-    // SN_OPT_PIPE_DEPTH 2 (not fused): twist i leads the consumer of play i-2
-    // by 4 launches' words (1 200) and play i waits for twist i-2, so neither
-    // queue waits on a kernel of the other that has only just finished
-    const bool deep = !fused && e->pipe_depth == 2;
-    if (e->pvalid && ((e->pfused != 0) != fused || (e->pdeep != 0) != deep)) {  // restart in the other form
+    // SN_OPT_TWIST_EVERY = K: play launches in groups of K; beside the first
+    // launch p of group G runs twist G, leading the consumer position of
+    // launch p-1 by 600 K words -- the 2K launches p .. p+2K-1, i.e. K
+    // launch pairs of the §4 tail bound -- and launch p waits for twist G-1
+    // only, which had a whole group of launches to finish.  Per group, one
+    // record and one wait on the caller's stream (K = 1: the launch before).
+    // Slots: pabsc by launch index mod 4, ptend by group parity (INIT =
+    // launch -1 / twist -1).  The ring holds the lead + a round for K <= 4.
+    const int K = fused ? 1 : e->twist_every;
+    const bool round_tw = fused || e->twist_round;
+    if (e->pvalid && ((e->pfused != 0) != fused || e->pK != K)) {  // restart in the other form
         const sn_status r = sn_pipe_sync(e, st);
         if (r != SN_OK) return r;
     }
-    const int K = (fused || deep) ? 1 : e->twist_every;
-    const int lead = e->pipe_lead + (K - 1) * 300 + (deep ? 600 : 0);
-    if (!e->pvalid) {  // start the pipeline from mt_pos: twist kPipeLead ahead, synchronously
-        const int p = (int)(e->pcount & 1u);
+    const int lead = e->pipe_lead * K;
+    if (!e->pvalid) {  // start the pipeline from mt_pos: twist the lead ahead, synchronously
         // fused: complete a partly twisted round, so that the play launches twist whole rounds only
-        const AheadArgs aa{deep ? 3 : 1 - p, 0, deep ? 3 : p, lead, e->perr_host_dev, fused ? 1 : 0};
-        e->tw_out = p, e->pl_tin = p, e->pphase = 0, e->pl_cout = 1 - p;
-        if (deep) e->tw_out = 3, e->pl_cout = 3, e->pi = 0;  // INIT = play -1 and twist -1 (slot 3)
-        if (e->twist_round || fused) hipLaunchKernelGGL((k_mt_ahead<true, true>), pg, dim3(kBlock), 0, st, s, aa);
+        const AheadArgs aa{3, 0, 1, lead, e->perr_host_dev, fused ? 1 : 0};
+        e->tw_out = 1, e->pl_cout = 3, e->pphase = 0;
+        if (round_tw) hipLaunchKernelGGL((k_mt_ahead<true, true>), pg, dim3(kBlock), 0, st, s, aa);
         else hipLaunchKernelGGL((k_mt_ahead<true, false>), pg, dim3(kBlock), 0, st, s, aa);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(e->ev_prep, st));
-        if (deep) HIP_TRY(hipEventRecord(e->evp[3], st));
         e->pvalid = 1;
         e->pfused = fused ? 1 : 0;
-        e->pdeep = deep ? 1 : 0;
+        e->pK = K;
     } else if (st != e->play_st) {  // another caller stream: order behind the last pipelined k_play
         HIP_TRY(hipStreamWaitEvent(st, e->ev_play, 0));
     }
@@ -1837,63 +1908,28 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         if (a.done) c.done = a.done + (int64_t)t0 * B;
         if (a.actions_out) c.actions_out = a.actions_out + (int64_t)t0 * B * N;
         if (a.obs) c.obs = a.obs + (int64_t)t0 * B * N * a.obs_stride;
-        const int p = (int)(e->pcount & 1u);
+        const uint64_t p = e->pphase;
+        c.pipe_cin = (int)((p + 3u) & 3u), c.pipe_cout = (int)(p & 3u);
         if (fused) {  // one launch on the caller's stream: it twists the rounds its successors read
-            c.pipe_cin = 1 - p, c.pipe_cout = p, c.pipe_t = e->tw_out, c.pipe_tout = 1 - e->tw_out;
+            c.pipe_t = (int)((p + 1u) & 1u), c.pipe_tout = (int)(p & 1u);
             if (e->tn < e->tcap) e->tev_tw[e->tn] = 0;
             hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
             if (tv) HIP_TRY(hipEventRecord(tv[0], st));
             hipLaunchKernelGGL(k_play_quad, dim3(qblk), dim3(kBlock), qshmem, st, s, c);
             HIP_TRY(hipGetLastError());
             if (tv) HIP_TRY(hipEventRecord(tv[1], st));
-            e->tw_out = 1 - e->tw_out;
-            e->pl_tin = e->tw_out;
-            e->pl_cout = p;
+            e->tw_out = c.pipe_tout;
+            e->pl_cout = c.pipe_cout;
             e->pcount++;
             e->pphase++;
             continue;
         }
-        if (deep) {
-            const uint64_t i = e->pi;
-            const int ti = (int)(i & 3u);
-            const int tsl = (i >= 2u) ? (int)((i - 2u) & 3u) : 3;  // twist i-2 (INIT for the first two)
-            c.pipe_cin = (int)((i + 3u) & 3u), c.pipe_cout = ti, c.pipe_t = tsl;
-            if (i >= 2u) HIP_TRY(hipStreamWaitEvent(st, e->evt[tsl], 0));  // finished a launch ago, as a rule
-            if (e->tn < e->tcap) e->tev_tw[e->tn] = 1;
-            hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
-            if (tv) HIP_TRY(hipEventRecord(tv[0], st));
-            if (quad) {
-                hipLaunchKernelGGL(k_play_quad, dim3(qblk), dim3(kBlock), qshmem, st, s, c);
-                HIP_TRY(hipGetLastError());
-            } else {
-                const sn_status r = pipe_play(s, c, gpw, nblk, shmem, st);
-                if (r != SN_OK) return r;
-            }
-            if (tv) HIP_TRY(hipEventRecord(tv[1], st));
-            HIP_TRY(hipEventRecord(e->evp[ti], st));
-            // twist i, beside play i: leads the consumer of play i-2 (INIT's for the first two);
-            // SECHS_PIPE_SERIAL=1 (diagnostics) orders it after play i instead
-            const int csl = e->pipe_serial ? ti : tsl;
-            HIP_TRY(hipStreamWaitEvent(e->side, e->evp[csl], 0));
-            if (tv) HIP_TRY(hipEventRecord(tv[2], e->side));
-            const AheadArgs aa{csl, (int)((i + 3u) & 3u), ti, lead, e->perr_host_dev};
-            if (e->twist_round) hipLaunchKernelGGL((k_mt_ahead<false, true>), pg, dim3(kBlock), 0, e->side, s, aa);
-            else hipLaunchKernelGGL((k_mt_ahead<false, false>), pg, dim3(kBlock), 0, e->side, s, aa);
-            HIP_TRY(hipGetLastError());
-            if (tv) HIP_TRY(hipEventRecord(tv[3], e->side));
-            HIP_TRY(hipEventRecord(e->evt[ti], e->side));
-            HIP_TRY(hipEventRecord(e->ev_prep, e->side));
-            e->tw_out = ti, e->pl_cout = ti;
-            e->pi++;
-            e->pcount++;
-            continue;
-        }
-        const bool twist_now = (e->pphase % K) == 0;           // a twist-ahead launch beside this play launch
-        const bool wait_now = (K == 1) || (e->pphase % K) == 1;  // the first play launch after one
-        c.pipe_cin = 1 - p, c.pipe_cout = p, c.pipe_t = e->pl_tin;
-        if (wait_now) HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));  // this launch's words are twisted
-        if (twist_now) HIP_TRY(hipEventRecord(e->ev_main, st));         // the previous launch's consumption is final
-        if (e->tn < e->tcap) e->tev_tw[e->tn] = twist_now ? 1 : 0;
+        const uint64_t G = p / (uint64_t)K;
+        const bool first = (p % (uint64_t)K) == 0u;  // twist G beside this launch
+        c.pipe_t = (int)((G + 1u) & 1u);              // twist G-1's end (INIT's for group 0)
+        if (first && G >= 1u) HIP_TRY(hipStreamWaitEvent(st, e->evt[(G + 1u) & 1u], 0));  // twist G-1
+        if (first && !e->pipe_serial) HIP_TRY(hipEventRecord(e->ev_main, st));  // launch p-1's consumption is final
+        if (e->tn < e->tcap) e->tev_tw[e->tn] = first ? 1 : 0;
         hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
         if (tv) HIP_TRY(hipEventRecord(tv[0], st));
         if (quad) {
@@ -1904,22 +1940,21 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
             if (r != SN_OK) return r;
         }
         if (tv) HIP_TRY(hipEventRecord(tv[1], st));
-        if (twist_now) {
-            // the next launches' twist, beside this one: leads the consumer of the launch before.
-            // SECHS_PIPE_SERIAL=1 (diagnostics: solo kernel times) orders it after this launch instead
+        if (first) {
+            // twist G, beside this launch (SECHS_PIPE_SERIAL=1, diagnostics: after it -- solo kernel times)
             if (e->pipe_serial) HIP_TRY(hipEventRecord(e->ev_main, st));
             HIP_TRY(hipStreamWaitEvent(e->side, e->ev_main, 0));
             if (tv) HIP_TRY(hipEventRecord(tv[2], e->side));
-            const AheadArgs aa{1 - p, e->tw_out, 1 - e->tw_out, lead, e->perr_host_dev};
-            if (e->twist_round) hipLaunchKernelGGL((k_mt_ahead<false, true>), pg, dim3(kBlock), 0, e->side, s, aa);
+            const AheadArgs aa{c.pipe_cin, c.pipe_t, (int)(G & 1u), lead, e->perr_host_dev};
+            if (round_tw) hipLaunchKernelGGL((k_mt_ahead<false, true>), pg, dim3(kBlock), 0, e->side, s, aa);
             else hipLaunchKernelGGL((k_mt_ahead<false, false>), pg, dim3(kBlock), 0, e->side, s, aa);
             HIP_TRY(hipGetLastError());
             if (tv) HIP_TRY(hipEventRecord(tv[3], e->side));
+            HIP_TRY(hipEventRecord(e->evt[G & 1u], e->side));
             HIP_TRY(hipEventRecord(e->ev_prep, e->side));
-            e->tw_out = 1 - e->tw_out;
-            e->pl_tin = e->tw_out;  // the play launches from the next one on read this twist's end
+            e->tw_out = (int)(G & 1u);
         }
-        e->pl_cout = p;
+        e->pl_cout = c.pipe_cout;
         e->pcount++;
         e->pphase++;
     }

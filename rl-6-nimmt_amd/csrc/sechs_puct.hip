@@ -161,9 +161,7 @@ __global__ void k_puct_init(PuctArgs a, const float* logits) {
 // _draw_env + _deal_hands (mcts.py:108-127): the decider is seat 0 of the
 // rollout game, opponents are dealt from its memory
 template <int N>
-__global__ void k_puct_deal(DevState s, PuctArgs a) {
-    const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (d >= a.D) return;
+__device__ __forceinline__ void deal_one(const DevState& s, const PuctArgs& a, int64_t d, uint32_t rollout, int32_t* ro) {
     int64_t g;
     int p;
     dec_to_gp(a, d, g, p);
@@ -172,9 +170,8 @@ __global__ void k_puct_deal(DevState s, PuctArgs a) {
     const uint64_t gid = s.game_offset + (uint64_t)g;
     PhiloxGen gen;
     ByteBuf buf;
-    gen.load(a.seed_lo ^ puct_step_of(a), a.seed_hi, ((uint64_t)(uint32_t)gid << 32) | ((uint64_t)p << 28) | ((uint64_t)a.rollout << 8),
+    gen.load(a.seed_lo ^ puct_step_of(a), a.seed_hi, ((uint64_t)(uint32_t)gid << 32) | ((uint64_t)p << 28) | ((uint64_t)rollout << 8),
              0ull, buf);
-    int32_t* ro = a.ro + d * kRoWords;
     const Board b = load_board(s, g);
     const Hand me = load_hand(s, p, g);
     const uint32_t n = (uint32_t)a.n;
@@ -198,6 +195,25 @@ __global__ void k_puct_deal(DevState s, PuctArgs a) {
     }
     ro[40] = 0;   // outcome
     ro[41] = -1;  // first move (index into the root's legal list)
+}
+
+template <int N>
+__global__ void k_puct_deal(DevState s, PuctArgs a) {
+    const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= a.D) return;
+    deal_one<N>(s, a, d, a.rollout, a.ro + d * kRoWords);
+}
+
+// rollouts r0 .. r0 + nr - 1 of every decision in one launch (nr x D lanes
+// instead of D: the deal is a latency-bound chain of Philox draws per lane),
+// rollout r's state at ro_out + ((r - r0) D + d) kRoWords -- the rollout then
+// runs on that slice in place (sn_puct.rollouts pointed at it)
+template <int N>
+__global__ void k_puct_deal_batch(DevState s, PuctArgs a, uint32_t r0, int nr, int32_t* ro_out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.D * nr) return;
+    const int64_t k = i / a.D, d = i - k * a.D;
+    deal_one<N>(s, a, d, r0 + (uint32_t)k, ro_out + i * kRoWords);
 }
 
 // candidate rows of every seat of every rollout game: row (d, q, k)
@@ -1286,6 +1302,19 @@ sn_status sn_puct_deal(sn_env* e, const sn_puct* q, void* stream) {
     if (st != SN_OK) return st;
     hipStream_t s = (hipStream_t)stream;
     SN_DISPATCH_N(e->s.N, hipLaunchKernelGGL((k_puct_deal<NN>), dim3(grid_for(a.D)), dim3(kBlock), 0, s, e->s, a));
+    HIP_TRY(hipGetLastError());
+    return SN_OK;
+}
+
+sn_status sn_puct_deal_batch(sn_env* e, const sn_puct* q, int r0, int nr, void* ro_out, void* stream) {
+    PuctArgs a{};
+    sn_status st = puct_args(e, q, a);
+    if (st != SN_OK) return st;
+    if (r0 < 0 || nr < 1 || !ro_out) return set_error(SN_EINVAL, "need r0 >= 0, nr >= 1 and an output buffer");
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t lanes = a.D * nr;
+    SN_DISPATCH_N(e->s.N, hipLaunchKernelGGL((k_puct_deal_batch<NN>), dim3(grid_for(lanes)), dim3(kBlock), 0, s, e->s, a,
+                                             (uint32_t)r0, nr, (int32_t*)ro_out));
     HIP_TRY(hipGetLastError());
     return SN_OK;
 }

@@ -183,36 +183,6 @@ __device__ __forceinline__ uint32_t quad_place(uint32_t& rlo, uint32_t& rhi, uin
     return pen;
 }
 
-// SN_OPT_PIPE_FUSED: one whole MT19937 round of game G, twisted by the
-// whole wave in LDS (w: 624 words of the wave's idle obs staging area), its
-// tempered low bytes to the ring at stream positions te .. te + 623 (te is
-// 8-aligned: rounds are 624 = 78 x 8 words).  numpy's in-place order in
-// three dependency-free phases: words 0..226 read old words only (mt[i+1],
-// mt[i+397]); 227..453 read old mt[i+1] and the new mt[i-227] of phase 1;
-// 454..623 the new mt[i-227] of phase 2 (and mt[623] the new mt[0]).  One
-// HBM read and one write per word (k_mt_ahead's partial twists read the
-// i+397 input a second time).  Returns the old mt[0] (the one word the
-// sync-time untwist cannot recover, mt0).
-// v: the round's old words (word 64k + lane in v[k]), loaded by the caller
-// (a round ahead: quad_round_load)
-__device__ __forceinline__ void quad_round_load(const DevState& s, int64_t G, uint32_t lane, uint32_t (&v)[10]) {
-    const uint32_t* st = s.mt + G * kMtN;
-#pragma unroll
-    for (int k = 0; k < 10; k++) {
-        const uint32_t i = 64u * k + lane;
-        v[k] = (i < (uint32_t)kMtN) ? st[i] : 0u;
-    }
-}
-
-__device__ __forceinline__ void quad_round_to_lds(uint32_t lane, uint32_t* w, const uint32_t (&v)[10]) {
-#pragma unroll
-    for (int k = 0; k < 10; k++) {
-        const uint32_t i = 64u * k + lane;
-        if (i < (uint32_t)kMtN) w[i] = v[k];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-}
-
 // The round's old words by LDS-DMA (global_load_lds_dwordx4, 1 KiB per
 // wave instruction, no VGPRs): three instructions for the 2 496 bytes.
 // Issued as inline asm, so hipcc neither counts them nor makes the step
@@ -234,72 +204,6 @@ __device__ __forceinline__ void quad_round_issue(const DevState& s, int64_t G, u
     if (lane < (uint32_t)(kMtN * 4 - 2048) / 16u) glds16(src + 2048, dst + 2048u);
 }
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// w holds the round's old words (quad_round_to_lds / quad_round_issue + vm_drain)
-__device__ __forceinline__ uint32_t quad_twist_round(const DevState& s, int64_t G, uint32_t lane, uint32_t* w,
-                                                     uint32_t te) {
-    constexpr uint32_t D = kMtN - kMtM;  // 227
-    uint32_t* st = s.mt + G * kMtN;
-    const uint32_t old0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)w[0]);
-    uint32_t nv[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {  // phase 1: i < 227
-        const uint32_t i = 64u * k + lane;
-        nv[k] = (i < D) ? mt_mix(w[i], w[i + 1u], w[i + kMtM]) : 0u;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint32_t i = 64u * k + lane;
-        if (i < D) w[i] = nv[k];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#pragma unroll
-    for (int k = 0; k < 4; k++) {  // phase 2: 227 <= i < 454
-        const uint32_t i = D + 64u * k + lane;
-        nv[k] = (i < 2u * D) ? mt_mix(w[i], w[i + 1u], w[i - D]) : 0u;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint32_t i = D + 64u * k + lane;
-        if (i < 2u * D) w[i] = nv[k];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#pragma unroll
-    for (int k = 0; k < 3; k++) {  // phase 3: 454 <= i < 624
-        const uint32_t i = 2u * D + 64u * k + lane;
-        nv[k] = (i < (uint32_t)kMtN) ? mt_mix(w[i], w[(i + 1u == (uint32_t)kMtN) ? 0u : i + 1u], w[i - D]) : 0u;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const uint32_t i = 2u * D + 64u * k + lane;
-        if (i < (uint32_t)kMtN) w[i] = nv[k];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    // the new round to HBM (state words), its tempered low bytes to the ring
-    // (4 per dword: dword d holds stream positions te + 4d .. te + 4d + 3)
-#pragma unroll
-    for (int k = 0; k < 10; k++) {
-        const uint32_t i = 64u * k + lane;
-        if (i < (uint32_t)kMtN) st_nt(&st[i], w[i], SECHS_NT_MORE);
-    }
-    uint8_t* ring = (uint8_t*)s.pring;
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const uint32_t d = 64u * k + lane;
-        if (d < (uint32_t)kMtN / 4u) {
-            const u32x4 x = *(const u32x4*)(w + 4u * d);
-            const uint32_t y = (mt_temper(x.x) & 0xFFu) | ((mt_temper(x.y) & 0xFFu) << 8) |
-                               ((mt_temper(x.z) & 0xFFu) << 16) | ((mt_temper(x.w) & 0xFFu) << 24);
-            const uint32_t ri = (te + 4u * d) & (uint32_t)(kPipeRing - 1);
-            st_nt((uint32_t*)(ring + ((int64_t)(ri >> 4) * s.B + G) * 16 + (ri & 12u)), y, SECHS_NT_MORE);
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the LDS reads before the area's next use
-    return old0;
-}
 
 // compare-exchange of two sort keys
 __device__ __forceinline__ void qce(uint32_t& a, uint32_t& b) {
@@ -385,7 +289,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_play_quad(DevState s, PlayArgs a)
             const int64_t G = g0 + (tw_fly >> 2);
             const uint32_t teG = (uint32_t)__builtin_amdgcn_readlane((int)te0, tw_fly);
             // (SECHS_QUAD_DBG bit 4, timing diagnostics only: the DMA and its wait, no twist)
-            const uint32_t old0 = (a.dbg & 16) ? 0u : quad_twist_round(s, G, (uint32_t)lane, rbuf, teG);
+            const uint32_t old0 = (a.dbg & 16) ? 0u : mt_twist_round(s, G, (uint32_t)lane, rbuf, teG);
             if (lane == tw_fly) my_old0 = old0;
             if (gl == (tw_fly >> 2)) twisted = 1u;
             tw_fly = -1;
@@ -516,8 +420,8 @@ __global__ __launch_bounds__(kBlock, 4) void k_play_quad(DevState s, PlayArgs a)
             tw_issue();
             tw_finish();
         }
-        if (q == 0 && twisted) {  // the crossing before becomes mt0[1] (k_pipe_code's second untwist level)
-            s.mt0[B + g] = s.mt0[g];
+        if (q == 0 && twisted) {  // push the crossing (k_pipe_code's untwist levels, newest first)
+            for (int k = kMt0Levels - 1; k > 0; k--) s.mt0[k * B + g] = s.mt0[(k - 1) * B + g];
             s.mt0[g] = my_old0;
         }
     }

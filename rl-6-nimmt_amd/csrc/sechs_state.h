@@ -38,8 +38,8 @@ struct DevState {
     uint32_t* mt;
     uint32_t* mt_pos;
     uint64_t* ctr;
-    uint32_t* mt0;   // [2][B] old-round mt[0] of the newest word-0 crossing (export of straddling codes),
-                     // then the crossing before it (k_mt_ahead / k_pipe_code untwist, two rounds)
+    uint32_t* mt0;   // [kMt0Levels][B] old-round mt[0] of the newest word-0 crossing (export of straddling
+                     // codes), then the crossings before it (k_mt_ahead / k_pipe_code untwist, several rounds)
     u32x4* ring;     // [ring_w/16][B] low bytes of the words k_mt_prep twisted ahead
     int ring_w;      // ring words per game (multiple of 64), 0 = no ring
     int pad2_;
@@ -58,8 +58,9 @@ struct DevState {
     int32_t* lpf;    // [B] 1 (| 2: quirk Q6): lpc holds this step's non-external cards
 };
 
-constexpr int kPipeSlots = 4;    // pabsc / ptend buffers (SN_OPT_PIPE_DEPTH 2 cycles through 4)
-constexpr int kPipeRing = 2048;  // ring bytes per game (>= lead + one launch; whole-round twists lead by up to 1223)
+constexpr int kMt0Levels = 5;    // word-0 crossings kept in mt0 (the lead of SN_OPT_TWIST_EVERY = 4 spans up to four)
+constexpr int kPipeSlots = 4;    // pabsc buffers (by play launch index mod 4; ptend uses 2, by twist parity)
+constexpr int kPipeRing = 4096;  // ring bytes per game (>= the lead 600 K + a whole round's overshoot: 3 023 at K = 4)
 constexpr int kPipeLead = 600;   // words k_mt_ahead keeps twisted ahead of the consumer (<= 624)
 constexpr int kPipeWin = 240;    // of them, copied to LDS per lane at a k_play launch: a 4-player
                                   // episode draws 193.5 words, P(> 240) = 7e-6 per game (the rest come
@@ -831,24 +832,22 @@ struct sn_env {
     int lg_mpc[16], lg_mmax[16];  // MCSAgent agents: mc_per_card, mc_max
     int phase;        // every game's env-steps since its deal, mod 10, when they are in lockstep; -1 unknown
     int play_split;   // SN_OPT_PLAY_SPLIT: role-split k_play for lockstep DrunkHamster rollouts
-    int twist_every;  // SN_OPT_TWIST_EVERY: a k_mt_ahead beside every K-th play launch (K = 1, 2)
-    int tw_out, pl_tin, pphase;  // pipeline: ptend buffer of the last twist / the next play reads; launches since start
+    int twist_every;  // SN_OPT_TWIST_EVERY: a k_mt_ahead beside every K-th play launch (K = 1, 2, 3)
+    int tw_out;       // pipeline: ptend slot of the last twist
+    uint64_t pphase;  // pipeline: play launches since it started
     int twist_round;  // SN_OPT_TWIST_ROUND: k_mt_ahead twists whole MT rounds (8 instead of 12 B of MT traffic per word)
     int play_quad;    // SN_OPT_PLAY_QUAD: four lanes per game (k_play_quad) on the pipelined N = 4 path
     int pipe_serial;  // SECHS_PIPE_SERIAL=1 (diagnostics): each twist waits for the play launch before it (no overlap)
-    int pipe_depth;   // SN_OPT_PIPE_DEPTH: 2 = each twist leads the consumer of the launch two back, each play
-                      // launch waits for the twist two back (no wait on a just-finished kernel of the other queue)
     int pl_cout;      // pabsc slot the last play launch wrote
-    uint64_t pi;      // play launches since the pipeline started (depth 2)
-    hipEvent_t evp[4], evt[4];  // depth 2: after play launch / twist i, slot i mod 4
+    int pK;           // SN_OPT_TWIST_EVERY of the running pipeline
+    hipEvent_t evt[2];  // after twist G, slot G mod 2
     int pipe_fused;   // SN_OPT_PIPE_FUSED: k_play_quad twists the rounds itself (no side stream, no cross-queue waits)
     int pfused;       // the running pipeline was started fused (whole rounds from its start)
-    int pdeep;        // the running pipeline was started with depth 2
     sechs::DevState s;
     // pipelined twist-ahead (sechs_env.hip launch_pipe): a k_mt_ahead for the
     // next play launch may be in flight on `side` (ev_prep) after a rollout
     int pvalid;         // ring + ptend/pabsc/ptp are the live RNG state (mt_pos is stale)
-    uint64_t pcount;    // play launches so far (parity selects the pabsc / ptend buffers)
+    uint64_t pcount;    // pipelined play launches so far
     hipStream_t side;
     hipEvent_t ev_prep, ev_main, ev_play;  // ev_play: after the last pipelined k_play (recorded on that call's stream)
     hipStream_t play_st;  // that stream's handle VALUE, compared only (never used: the caller may destroy it)

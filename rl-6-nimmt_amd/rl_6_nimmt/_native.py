@@ -26,7 +26,6 @@ SN_OPT_PLAY_QUAD = 8
 SN_OPT_TWIST_ROUND = 9
 SN_OPT_TWIST_EVERY = 10
 SN_OPT_PIPE_FUSED = 11
-SN_OPT_PIPE_DEPTH = 12
 SN_AGENT_RANDOM, SN_AGENT_MCS, SN_AGENT_EXTERNAL = 0, 1, 2
 
 class SnPuct(ctypes.Structure):
@@ -99,6 +98,7 @@ SIGNATURES = {
     "sn_puct_root_rows": ([_P, _P, _P, _I, _P], _I),
     "sn_puct_init": ([_P, _P, _P, _P], _I),
     "sn_puct_deal": ([_P, _P, _P], _I),
+    "sn_puct_deal_batch": ([_P, _P, _I, _I, _P, _P], _I),
     "sn_puct_rows": ([_P, _P, _I, _P, _I, _P], _I),
     "sn_puct_step": ([_P, _P, _P, _I, _I, _P], _I),
     "sn_puct_seat_cols": ([_P, _P, _I, _P, _I, _P, _I, _P], _I),

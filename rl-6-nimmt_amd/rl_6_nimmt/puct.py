@@ -247,6 +247,10 @@ class BatchedPUCT:
         # launch per step); "mfma": layer 1 per candidate row on the matrix cores as well
         # (sn_puct_mlp_mfma); "gemm": per-seat rows + a PyTorch GEMM + sn_puct_mlp
         self.mlp_layer1 = os.environ.get("SECHS_MLP_LAYER1", "seats")
+        # the seats / mfma rollout loop deals this many rollouts per launch
+        # (sn_puct_deal_batch into a [deal_batch][D][48] buffer, each rollout
+        # then running on its slice); 0: one sn_puct_deal per rollout (A/B, tests)
+        self.deal_batch = int(os.environ.get("SECHS_PUCT_DEAL_BATCH", "16"))
         self._step_dev = torch.zeros((1,), dtype=torch.int32, device=dev)
 
     # ------------------------------------------------------------ policy net on the device
@@ -382,13 +386,24 @@ class BatchedPUCT:
                     mlp = L.sn_puct_mlp_seats
                     wargs = (nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p), nat.ptr(head), nat.ptr(logits), st)
                 lp = nat.ptr(logits)
-                for r in range(self.n_mc(n)):
+                RB, nmc = self.deal_batch, self.n_mc(n)
+                if RB > 0:
+                    rob = self._deal_buf(RB)
+                    stride = self.D * 48 * 4  # bytes of one rollout's states
+                for r in range(nmc):
                     q.rollout = r
-                    nat.check(deal(h, qr, st), "sn_puct_deal")
+                    if RB > 0:
+                        if r % RB == 0:
+                            nat.check(L.sn_puct_deal_batch(h, qr, r, min(RB, nmc - r), rob.data_ptr(), st),
+                                      "sn_puct_deal_batch")
+                        q.rollouts = rob.data_ptr() + (r % RB) * stride
+                    else:
+                        nat.check(deal(h, qr, st), "sn_puct_deal")
                     for t in range(n):
                         nat.check(mlp(h, qr, n - t, *wargs), "sn_puct_mlp_seats")
                         nat.check(step(h, qr, lp, t, n - t, st), "sn_puct_step")
-                self.rows_evaluated += self.n_mc(n) * S * (n * (n + 1) // 2)
+                q.rollouts = self.ro.data_ptr()
+                self.rows_evaluated += nmc * S * (n * (n + 1) // 2)
                 return
             for r in range(self.n_mc(n)):
                 q.rollout = r
@@ -463,6 +478,12 @@ class BatchedPUCT:
                            torch.empty((kp * S * 10,), dtype=self.net_dtype, device=dev),
                            torch.zeros((S * 10,), dtype=self.net_dtype, device=dev))
         return self._sbufs
+
+    def _deal_buf(self, RB):
+        """[RB][D_max][48] int32: the initial states of RB rollouts (sn_puct_deal_batch)"""
+        if getattr(self, "_robuf", None) is None or self._robuf.shape[0] != RB:
+            self._robuf = torch.zeros((RB, self.D_max, 48), dtype=torch.int32, device=self.env.device)
+        return self._robuf
 
     def _fused_bufs(self):
         """seat rows [D_max*N][56] bf16, cards [D_max*N*10] f32, base

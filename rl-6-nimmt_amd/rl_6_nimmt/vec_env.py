@@ -186,14 +186,12 @@ class VecSechsNimmtEnv:
 
     # ------------------------------------------------------------ numpy RNG bridge
     def set_option(self, ring_words=None, chunk_steps=None, pipeline=None, pipe_gpw=None, pipe_lead=None,
-                   play_split=None, play_quad=None, twist_round=None, twist_every=None, pipe_fused=None,
-                   pipe_depth=None):
+                   play_split=None, play_quad=None, twist_round=None, twist_every=None, pipe_fused=None):
         """rollout tuning (include/sechs.h SN_OPT_*; all numpy-compat only except play_split,
         the role-split kernel of philox handles; play_quad: four lanes per game on the
         pipelined 4-player path, k_play_quad; twist_round: whole-round MT twists in
-        k_mt_ahead; twist_every: one twist-ahead launch per 1 or 2 play launches; pipe_fused:
-        k_play_quad twists the rounds itself, no side stream; pipe_depth: 2 = twists lead the
-        consumer two launches back, plays wait for the twist two back); results never
+        k_mt_ahead; twist_every: one twist-ahead launch per K = 1 .. 4 play launches; pipe_fused:
+        k_play_quad twists the rounds itself, no side stream); results never
         depend on it
         (except pipe_lead < 600, a test knob that makes overruns -- PipeOverrunError -- likely)"""
         if pipe_lead is not None:
@@ -208,8 +206,6 @@ class VecSechsNimmtEnv:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_TWIST_ROUND, int(twist_round)), "sn_set_option")
         if play_quad is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PLAY_QUAD, int(play_quad)), "sn_set_option")
-        if pipe_depth is not None:
-            nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPE_DEPTH, int(pipe_depth)), "sn_set_option")
         if pipe_fused is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPE_FUSED, int(pipe_fused)), "sn_set_option")
         if pipeline is not None:

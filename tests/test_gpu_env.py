@@ -22,15 +22,12 @@ def venv(*a, **k):
     from rl_6_nimmt.vec_env import VecSechsNimmtEnv
 
     env = VecSechsNimmtEnv(*a, **k)
-    # SECHS_TEST_TWIST_EVERY=2: the same parity tests with one twist-ahead per two play launches
+    # SECHS_TEST_TWIST_EVERY=2 / 3: the same parity tests with one twist-ahead per 2 / 3 play launches
     # SECHS_TEST_TWIST_ROUND=0: with exact-lead (partial) twists instead of whole rounds
     if env.rng == "numpy" and os.environ.get("SECHS_TEST_TWIST_EVERY"):
         env.set_option(twist_every=int(os.environ["SECHS_TEST_TWIST_EVERY"]))
     if env.rng == "numpy" and os.environ.get("SECHS_TEST_TWIST_ROUND"):
         env.set_option(twist_round=int(os.environ["SECHS_TEST_TWIST_ROUND"]))
-    # SECHS_TEST_PIPE_DEPTH=2: twists lead the consumer two launches back
-    if env.rng == "numpy" and os.environ.get("SECHS_TEST_PIPE_DEPTH"):
-        env.set_option(pipe_depth=int(os.environ["SECHS_TEST_PIPE_DEPTH"]))
     # SECHS_TEST_PIPE_FUSED=1: k_play_quad with the twist folded in, where it applies
     if env.rng == "numpy" and os.environ.get("SECHS_TEST_PIPE_FUSED"):
         env.set_option(pipe_fused=int(os.environ["SECHS_TEST_PIPE_FUSED"]))
@@ -541,7 +538,7 @@ def test_pipelined_overrun_is_an_error(N, lead):
     # exact-lead twists beside every launch: whole-round ones (incl. the fused form) overshoot
     # a short lead by up to a round, and a twist per two launches adds 300 words to
     # it, so the first launches would not run dry -- the detection is the same
-    env.set_option(pipe_lead=lead, twist_round=0, twist_every=1, pipe_fused=0, pipe_depth=1)
+    env.set_option(pipe_lead=lead, twist_round=0, twist_every=1, pipe_fused=0)
     env.reset()
     with pytest.raises(PipeOverrunError):
         env.rollout(20, check=True)

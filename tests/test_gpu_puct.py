@@ -690,7 +690,8 @@ def test_league_puct_kernels_on_tournament_decisions(monkeypatch):
     def league():
         torch.manual_seed(0)
         t = BatchedTournament(192, 2, 4, seed=13)
-        for name, a in [("P", PUCTAgent(mc_max=12, mc_per_card=3)), ("R0", DrunkHamster()), ("R1", DrunkHamster())]:
+        for name, a in [("P", PUCTAgent(mc_max=12, mc_per_card=3)), ("R0", DrunkHamster()), ("R1", DrunkHamster()),
+                        ("R2", DrunkHamster())]:
             t.add_player(name, a)
         return t
 
@@ -718,6 +719,26 @@ def test_league_puct_kernels_on_tournament_decisions(monkeypatch):
     assert eng.D > 0 and not bool(live.all())
     _check_mlp_kernels(env, eng, 10, live=live)
     t.close()
+
+
+def test_batched_deal_equals_per_rollout_deals(monkeypatch):
+    """sn_puct_deal_batch (rollouts dealt 16 / 3 per launch, each rollout
+    running on its slice of the batch buffer) and one sn_puct_deal per
+    rollout deal the same states from the same Philox streams: a whole PUCT
+    search gives identical statistics, histograms and moves"""
+    res = {}
+    for rb in ("16", "0", "3"):
+        monkeypatch.setenv("SECHS_PUCT_DEAL_BATCH", rb)
+        env, eng = _engine(B=300, dtype=torch.bfloat16, mc_max=12, mc_per_card=3, seed=17)
+        assert eng.mlp_layer1 in ("seats", "mfma") and eng.deal_batch == int(rb)
+        acts = [eng.decide(10).clone()]
+        env.step(acts[-1])
+        acts.append(eng.decide(9).clone())
+        torch.cuda.synchronize()
+        res[rb] = (acts, eng.stats.clone(), eng.hist.clone())
+    for rb in ("16", "3"):
+        assert all(torch.equal(a, b) for a, b in zip(res[rb][0], res["0"][0])), rb
+        assert torch.equal(res[rb][1], res["0"][1]) and torch.equal(res[rb][2], res["0"][2]), rb
 
 
 def _bf16_forward_bound(x, layers, head_w, head_b, u=2.0 ** -8, l1_roundings=2):

@@ -20,12 +20,12 @@ def main():
     e = lambda k, d: int(os.environ.get(k, d))  # noqa: E731
     env = VecSechsNimmtEnv(65536, 4, seed=0, rng="numpy")
     env.set_option(play_quad=e("FD_QUAD", 1), pipe_fused=e("FD_FUSED", 0), twist_round=e("FD_ROUND", 0),
-                   twist_every=e("FD_EVERY", 1), pipe_depth=e("FD_DEPTH", 1))
+                   twist_every=e("FD_EVERY", 1))
     env.reset()
     out = bench.make_out(env, 65536, True)
     wall, kern_ms, kt = bench.time_rollouts(env, out, 100, 10, 1)
     torch.cuda.synchronize()
-    print(json.dumps({"cfg": {k: os.environ.get(k) for k in ("FD_QUAD", "FD_FUSED", "FD_ROUND", "FD_EVERY", "FD_DEPTH",
+    print(json.dumps({"cfg": {k: os.environ.get(k) for k in ("FD_QUAD", "FD_FUSED", "FD_ROUND", "FD_EVERY",
                                                                "SECHS_PIPE_SERIAL", "SECHS_QUAD_DBG")},
                       "ms_per_step": wall / 100 * 1e3, "launch_ms": kern_ms, "play_ms": kt["k_play"],
                       "ahead_ms": kt.get("k_mt_ahead"), "pipe_errors": env.pipe_errors()}))
