@@ -56,7 +56,8 @@ ALGO_BYTES_PER_STEP = (33 * N_PLAYERS + 57) + 47 * N_PLAYERS  # 377 B at N = 4
 # applied by tools/pmc_traffic.py.  PMC counters cannot be read inside a plain
 # run, so the committed summary of the current kernels is reported beside the
 # live timing.
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r04_pmc_traffic_{rng}.json")
+PMC_TRAFFIC = {"numpy": os.path.join(ROOT, "profiles", "r05_pmc_traffic_numpy.json"),  # tools/r05_final.sh
+               "philox": os.path.join(ROOT, "profiles", "r04_pmc_traffic_philox.json")}
 
 
 def parse():
@@ -813,7 +814,7 @@ def bench_acer(games, episodes=3):
 
 
 def pmc_traffic(rng, games):
-    path = PMC_TRAFFIC.format(rng=rng)
+    path = PMC_TRAFFIC[rng]
     if games != 65536 or not os.path.exists(path):
         return None, None
     rec = json.load(open(path))

@@ -403,6 +403,14 @@ sn_status sn_puct_deal(sn_env* env, const sn_puct* q, void* stream);
    layout of sn_puct.rollouts); point sn_puct.rollouts at rollout r's slice
    and run its steps there -- the same states, dealt with nr x D lanes. */
 sn_status sn_puct_deal_batch(sn_env* env, const sn_puct* q, int r0, int nr, void* ro_out, void* stream);
+/* Rollouts r0 .. r0 + nr - 1 of every decision in one launch, from the
+   states sn_puct_deal_batch dealt into ro_base: per workgroup a group of
+   decisions runs every step (sn_puct_mlp_seats' rows, MFMA layer 1 + 2 and
+   head into logits in LDS, then sn_puct_step's seat-lane step) of each
+   rollout in order -- the same values as the launch-per-step loop (N <= 8;
+   weights as sn_puct_mlp_seats). */
+sn_status sn_puct_rollouts(sn_env* env, const sn_puct* q, int r0, int nr, void* ro_base, const void* w1s,
+                           const float* w1c, const void* w2, const float* head, void* stream);
 sn_status sn_puct_rows(sn_env* env, const sn_puct* q, int n_cur, void* rows, int bf16, void* stream);
 sn_status sn_puct_step(sn_env* env, const sn_puct* q, const float* logits, int t, int n_cur, void* stream);
 /* Layer-1 split of the rollout MLP (MultiHeadedMLP 48 -> H -> ...), in

@@ -356,7 +356,7 @@ __device__ __forceinline__ uint32_t mt_twist_round(const DevState& s, int64_t G,
             const uint32_t y = (mt_temper(x.x) & 0xFFu) | ((mt_temper(x.y) & 0xFFu) << 8) |
                                ((mt_temper(x.z) & 0xFFu) << 16) | ((mt_temper(x.w) & 0xFFu) << 24);
             const uint32_t ri = (te + 4u * d) & (uint32_t)(kPipeRing - 1);
-            st_nt((uint32_t*)(ring + ((int64_t)(ri >> 4) * s.B + G) * 16 + (ri & 12u)), y, SECHS_NT_MORE);
+            st_nt((uint32_t*)(ring + ring_byte(ri, G, s.B)), y, SECHS_NT_MORE);  // ri is 4-aligned
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the LDS reads before the area's next use
@@ -400,7 +400,7 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
             if (k < rem) {
                 const uint32_t v = st[(Tp + kMtN - rem + k) % (uint32_t)kMtN];
                 const uint32_t ri = (c + k) & (uint32_t)(kPipeRing - 1);
-                ring[((int64_t)(ri >> 4) * B + g) * 16 + (ri & 15u)] = (uint8_t)(mt_temper(v) & 0xFFu);
+                ring[ring_byte(ri, g, B)] = (uint8_t)(mt_temper(v) & 0xFFu);
             }
         }
         if (lane == 0u) s.pabsc[(int64_t)a.cin * B + g] = c;
@@ -421,7 +421,7 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
         const uint32_t y = mt_temper(v) & 0xFFu;
         const uint32_t d = y | (__shfl_down(y, 1) << 8) | (__shfl_down(y, 2) << 16) | (__shfl_down(y, 3) << 24);
         const uint32_t ri = (t0 + j) & (uint32_t)(kPipeRing - 1);
-        if ((lane & 3u) == 0u && j < n) st_nt((uint32_t*)(ring + ((int64_t)(ri >> 4) * B + g) * 16 + (ri & 12u)), d, SECHS_NT_MORE);
+        if ((lane & 3u) == 0u && j < n) st_nt((uint32_t*)(ring + ring_byte(ri, g, B)), d, SECHS_NT_MORE);  // ri 4-aligned
     };
     // Word-0 crossings of this launch (wave-uniform count): the overwritten
     // old mt[0] of each.  k_pipe_code's untwist needs one per round the array
@@ -520,42 +520,59 @@ __device__ __forceinline__ uint32_t mt_untwist_y_dev(uint32_t t) {
     return (((lsb ? (t ^ 0x9908b0dfu) : t)) << 1) | lsb;
 }
 
-__global__ void k_pipe_code(DevState s, int cin, int tin) {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= s.B) return;
+__global__ __launch_bounds__(kBlock) void k_pipe_code(DevState s, int cin, int tin) {
+    const int64_t g = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);  // one wave per game
+    if (g >= s.B) return;  // whole waves
+    const uint32_t lane = threadIdx.x & 63u;
     int32_t rem = (int32_t)(s.ptend[(int64_t)tin * s.B + g] - s.pabsc[(int64_t)cin * s.B + g]);
-    if (rem < 0) atomicAdd(s.perr, 1u);  // an overrun (already counted): the stream is lost
+    if (rem < 0 && lane == 0u) atomicAdd(s.perr, 1u);  // an overrun (already counted): the stream is lost
     uint32_t tp = s.ptp[g];
-    // The array ran ahead of the consumer's round (a whole-round twist,
-    // SN_OPT_TWIST_ROUND, or the 900-word lead of SN_OPT_TWIST_EVERY = 2):
-    // undo its newest round's twisted words [0, tp) in place (new -> old),
-    // the host mt_unstraddle, until the unconsumed words fit one array.
-    // Descending j keeps every input available: y[j] needs new[j] and
-    // new[j-227] (j >= 227) or old[j+397] (j < 227: restored already, or
-    // never twisted when j + 397 >= tp); old[j] = top(y[j]) | low(y[j-1]),
-    // old[0]'s low half from mt0 (newest crossing first, then the ones before).
+    // The array ran ahead of the consumer's round (whole-round twists, or
+    // the K-group lead of SN_OPT_TWIST_EVERY): undo its newest round's
+    // twisted words [0, tp) in place (new -> old), the host mt_unstraddle,
+    // until the unconsumed words fit one array.  With y[j] the twist's
+    // intermediate (top(old[j]) | low(old[j+1])): y[j] = U(new[j] ^ X[j]),
+    // X[j] = new[j-227] for j >= 227 -- all from new words, in parallel --
+    // and old[j+397] for j < 227, whose y[j+396], y[j+397] the first phase
+    // gave (or the word was never twisted: j + 397 >= tp); then old[j] =
+    // top(y[j]) | low(y[j-1]), old[0]'s low half from mt0 (newest crossing
+    // first, then the ones before).  One wave per game, in LDS.
+    __shared__ uint32_t sw[kBlock / 64][kMtN], sy[kBlock / 64][kMtN];
+    uint32_t* w = sw[threadIdx.x >> 6];
+    uint32_t* y = sy[threadIdx.x >> 6];
+    uint32_t* a = s.mt + g * kMtN;
+    constexpr uint32_t D = kMtN - kMtM;
     int lvl = 0;
+    if (rem > kMtN) {
+        for (uint32_t j = lane; j < (uint32_t)kMtN; j += 64u) w[j] = a[j];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
     for (; rem > kMtN && lvl < kMt0Levels; lvl++) {
-        constexpr uint32_t D = kMtN - kMtM;
         SN_DASSERT(tp >= 1u && tp <= (uint32_t)kMtN);
         if (tp < 1u || tp > (uint32_t)kMtN) break;
-        uint32_t* a = s.mt + g * kMtN;
-        auto X = [&](uint32_t j) { return a[(j >= D) ? j - D : j + kMtM]; };
-        uint32_t yj = mt_untwist_y_dev(a[tp - 1] ^ X(tp - 1));
-        for (int j = (int)tp - 1; j >= 1; j--) {
-            const uint32_t jm = (uint32_t)(j - 1);
-            const uint32_t ym = mt_untwist_y_dev(a[jm] ^ X(jm));
-            a[j] = (yj & 0x80000000u) | (ym & 0x7fffffffu);
-            yj = ym;
+        for (uint32_t j = D + lane; j < tp; j += 64u) y[j] = mt_untwist_y_dev(w[j] ^ w[j - D]);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        for (uint32_t j = lane; j < min(D, tp); j += 64u) {
+            const uint32_t k = j + kMtM;  // 397 .. 623
+            const uint32_t old_k = (k < tp) ? ((y[k] & 0x80000000u) | (y[k - 1u] & 0x7fffffffu)) : w[k];
+            y[j] = mt_untwist_y_dev(w[j] ^ old_k);
         }
-        a[0] = (yj & 0x80000000u) | (s.mt0[lvl * s.B + g] & 0x7fffffffu);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        const uint32_t m0 = s.mt0[lvl * s.B + g];
+        for (uint32_t j = lane; j < tp; j += 64u)
+            w[j] = (y[j] & 0x80000000u) | ((j ? y[j - 1u] : m0) & 0x7fffffffu);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         rem -= (int32_t)tp;
         tp = kMtN;
     }
-    for (int k = 0; lvl && k < kMt0Levels; k++)  // the crossings not undone are the newest now
-        s.mt0[k * s.B + g] = (k + lvl < kMt0Levels) ? s.mt0[(k + lvl) * s.B + g] : 0u;
+    if (lvl) {
+        for (uint32_t j = lane; j < (uint32_t)kMtN; j += 64u) a[j] = w[j];
+        if (lane == 0u)
+            for (int k = 0; k < kMt0Levels; k++)  // the crossings not undone are the newest now
+                s.mt0[k * s.B + g] = (k + lvl < kMt0Levels) ? s.mt0[(k + lvl) * s.B + g] : 0u;
+    }
     SN_DASSERT(rem <= kMtN);
-    s.mt_pos[g] = tp | ((uint32_t)max(rem, 0) << 16);
+    if (lane == 0u) s.mt_pos[g] = tp | ((uint32_t)max(rem, 0) << 16);
 }
 
 // ---- k_play phase profiler (diagnostics; built only with -DSECHS_PHASE_PROF,
@@ -1784,7 +1801,8 @@ sn_status sn_pipe_sync(sn_env* e, hipStream_t st) {
     HIP_TRY(hipEventRecord(e->ev_prep, e->side));
     HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));
     // the last play launch wrote pabsc[pl_cout]; the last twist ptend[tw_out]
-    hipLaunchKernelGGL(k_pipe_code, dim3(grid_for(e->s.B)), dim3(kBlock), 0, st, e->s, e->pl_cout, e->tw_out);
+    hipLaunchKernelGGL(k_pipe_code, dim3((unsigned)((e->s.B + kBlock / 64 - 1) / (kBlock / 64))), dim3(kBlock), 0, st,
+                       e->s, e->pl_cout, e->tw_out);
     HIP_TRY(hipGetLastError());
     e->pvalid = 0;
     return SN_OK;

@@ -1001,6 +1001,120 @@ __global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(PuctArgs a, int N, in
     }
 }
 
+// ---- whole rollouts in one kernel (sn_puct_rollouts) ----------------------
+// Every rollout step of k_puct_mlp_seats + k_puct_step_seats touches one
+// decision's rollout state, its seats' logits and its statistics only, so a
+// workgroup can carry a group of 64 / L decisions (their 64 seat rows, L
+// lanes per decision) through whole rollouts -- every step of rollouts
+// r0 .. r0 + nr - 1, in order, rollout r's first move chosen by PUCT from the
+// statistics rollouts < r backed up -- with no other workgroup involved:
+// per step, the seats' rows (phase 1), the per-seat layer-1 MFMA (phase 2),
+// the candidates' tiles (phase 3) into logits in LDS, then wave 0 runs
+// step_seat on them.  The same code, the same values: identical statistics
+// to the two-launches-per-step loop, without its 2 n x n_mc launches per
+// decision search (each ~10-20 us at small n_cur) and the logits' HBM trip.
+// Rollout r's state is ro_base + (r - r0) * D * kRoWords (sn_puct_deal_batch
+// dealt it).
+template <int N, int L>
+__global__ __launch_bounds__(256, 2) void k_puct_rollouts(DevState s, PuctArgs a, int r0, int nr, int32_t* ro_base,
+                                                         const uint16_t* w1s, const float* w1c, const uint16_t* w2,
+                                                         const float* head) {
+    constexpr int TNT = 2;
+    constexpr int kWaves = kBlock / 64;
+    constexpr int DG = 64 / L;  // decisions per group
+    __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kMlpLdsK];            // W2 [128][120]
+    __shared__ __attribute__((aligned(16))) uint16_t sRow[kSeatBlock * kSeatRowLds];  // seat rows [64][72]
+    __shared__ __attribute__((aligned(16))) uint16_t sBase[kSeatBlock * kBaseLds];    // base [64][120]
+    __shared__ __attribute__((aligned(16))) float sCard[kSeatBlock * kHand];
+    __shared__ __attribute__((aligned(16))) float sLogit[kSeatBlock * kHand];
+    __shared__ __attribute__((aligned(16))) float sC[kMlpK];
+    __shared__ __attribute__((aligned(16))) uint32_t sH2[kMlpM / 2];
+    __shared__ uint16_t sLut[kLutSize];
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63, col = lane & 31, half = lane >> 5;
+    build_row_lut(sLut);
+    for (int i = tid; i < kMlpM * (kMlpK / 8); i += blockDim.x) {
+        const int o = i / (kMlpK / 8), c = i - o * (kMlpK / 8);
+        *(uint4*)&sW[o * kMlpLdsK + 8 * c] = *(const uint4*)&w2[o * kMlpK + 8 * c];
+    }
+    for (int i = tid; i < kMlpK; i += blockDim.x) sC[i] = w1c[i];
+    load_head_pairs(head, sH2);
+    bf16x8_t w1f[kSeatRowK / 16];
+#pragma unroll
+    for (int ks = 0; ks < kSeatRowK / 16; ks++)
+        w1f[ks] = __builtin_bit_cast(bf16x8_t, *(const uint4*)&w1s[(32 * wave + col) * kSeatRowK + 16 * ks + 8 * half]);
+    const int sl = tid >> 2, part = tid & 3;  // phase 1: four lanes per seat
+    const int64_t groups = (a.D + DG - 1) / DG;
+    for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+        const int64_t d0 = grp * DG;
+        const int nseat = (int)min<int64_t>(DG, a.D - d0) * N;
+        for (int r = r0; r < r0 + nr; r++) {
+            PuctArgs ar = a;
+            ar.rollout = (uint32_t)r;
+            ar.ro = ro_base + (int64_t)(r - r0) * a.D * kRoWords;
+            for (int t = 0; t < a.n; t++) {
+                const int m = a.n - t;
+                __syncthreads();  // the last step's state writes and LDS reads are done
+                // phase 1: the seats' rows and card features (rows past the group's seats repeat its last)
+                const SeatIn in = seat_load(ar, N, d0 * N + min(sl, nseat - 1), part);
+                seat_row_part(in, m, part, sRow + sl * kSeatRowLds, sCard + sl * kHand, sLut);
+                __syncthreads();
+                // phase 2: base[seat][j] = sum_k W1s[j][k] rows[seat][k]; wave w: outputs j in [32w, 32w + 32)
+                {
+                    f32x16_t acc[2];
+#pragma unroll
+                    for (int ks = 0; ks < kSeatRowK / 16; ks++) {
+                        const int k0 = 16 * ks + 8 * half;
+#pragma unroll
+                        for (int nt = 0; nt < 2; nt++) {
+                            const bf16x8_t bfr =
+                                __builtin_bit_cast(bf16x8_t, *(const uint4*)&sRow[(32 * nt + col) * kSeatRowLds + k0]);
+                            const f32x16_t zero = {};
+                            acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1f[ks], bfr, ks ? acc[nt] : zero, 0, 0, 0);
+                        }
+                    }
+#pragma unroll
+                    for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+                        for (int rr = 0; rr < 16; rr += 2) {
+                            const int j = 32 * wave + (rr & 3) + 8 * (rr >> 2) + 4 * half;
+                            if (j < kMlpK)
+                                *(uint32_t*)&sBase[(32 * nt + col) * kBaseLds + j] = pack_bf16(acc[nt][rr], acc[nt][rr + 1]);
+                        }
+                }
+                __syncthreads();
+                // phase 3: the group's candidate rows, 64 per tile, logits to LDS
+                const uint32_t rows = (uint32_t)nseat * (uint32_t)m;
+                const uint32_t tiles = (rows + 32u * TNT - 1u) / (32u * TNT);
+                for (uint32_t tile = (uint32_t)wave; tile < tiles; tile += kWaves) {
+                    uint32_t rw[TNT];
+                    float x[TNT];
+                    const uint16_t* brow[TNT];
+#pragma unroll
+                    for (int nt = 0; nt < TNT; nt++) {
+                        rw[nt] = tile * 32u * TNT + 32u * nt + (uint32_t)col;
+                        const uint32_t rc = rw[nt] < rows ? rw[nt] : rows - 1u;
+                        const uint32_t q = rc / (uint32_t)m;
+                        x[nt] = sCard[q * kHand + (rc - q * (uint32_t)m)];
+                        brow[nt] = sBase + q * kBaseLds;
+                    }
+                    float out[TNT];
+                    mlp_tile<TNT>(brow, x, sW, sC, sH2, col, half, out);
+#pragma unroll
+                    for (int nt = 0; nt < TNT; nt++)
+                        if (half == 0 && rw[nt] < rows) sLogit[rw[nt]] = out[nt];
+                }
+                __syncthreads();
+                // the step: wave 0, L lanes per decision (step_seat, as k_puct_step_seats)
+                if (wave == 0)
+                    step_seat<N, L>(
+                        s, ar, [&](int64_t dd, int q, int k) { return sLogit[((dd - d0) * N + q) * m + k]; }, t, m,
+                        d0 * L + lane);
+            }
+        }
+    }
+}
+
 // ---- layer 1 per candidate on MFMA too (sn_puct_mlp_mfma) ------------------
 // k_puct_mlp_seats factors layer 1 into a per-seat MFMA product (base) plus
 // a per-candidate card column built on the VALU: ~9 VALU per MFMA in the
@@ -1432,6 +1546,38 @@ sn_status sn_puct_mlp_seats(sn_env* e, const sn_puct* q, int n_cur, const void* 
     hipLaunchKernelGGL(k_puct_mlp_seats, dim3((unsigned)std::min<int64_t>(groups, 2ll * cus)), dim3(kBlock), 0,
                        (hipStream_t)stream, a, e->s.N, n_cur, (const uint16_t*)w1s, w1c, (const uint16_t*)w2, head,
                        logits);
+    HIP_TRY(hipGetLastError());
+    return SN_OK;
+}
+
+sn_status sn_puct_rollouts(sn_env* e, const sn_puct* q, int r0, int nr, void* ro_base, const void* w1s, const float* w1c,
+                           const void* w2, const float* head, void* stream) {
+    PuctArgs a{};
+    sn_status st = puct_args(e, q, a);
+    if (st != SN_OK) return st;
+    if (r0 < 0 || nr < 1 || !ro_base) return set_error(SN_EINVAL, "need r0 >= 0, nr >= 1 and the dealt states");
+    if (!w1s || !w1c || !w2 || !head) return set_error(SN_EINVAL, "NULL argument");
+    if ((((uintptr_t)w1s) | ((uintptr_t)w2) | ((uintptr_t)w1c) | ((uintptr_t)head)) & 15)
+        return set_error(SN_EINVAL, "w1s / w2 / w1c / head must be 16-B aligned");
+    if (e->s.N > 8) return set_error(SN_EUNSUPPORTED, "sn_puct_rollouts: N <= 8");
+    hipStream_t s = (hipStream_t)stream;
+    const int Lw = e->s.N <= 2 ? 2 : e->s.N <= 4 ? 4 : 8;
+    const int64_t groups = (a.D + 64 / Lw - 1) / (64 / Lw);
+    const dim3 grid((unsigned)std::min<int64_t>(groups, 2ll * e->cus));
+#define SN_ROLLOUTS(NN_, L_)                                                                                      \
+    hipLaunchKernelGGL((k_puct_rollouts<NN_, L_>), grid, dim3(kBlock), 0, s, e->s, a, r0, nr, (int32_t*)ro_base, \
+                       (const uint16_t*)w1s, w1c, (const uint16_t*)w2, head)
+    switch (e->s.N) {
+        case 1: SN_ROLLOUTS(1, 2); break;
+        case 2: SN_ROLLOUTS(2, 2); break;
+        case 3: SN_ROLLOUTS(3, 4); break;
+        case 4: SN_ROLLOUTS(4, 4); break;
+        case 5: SN_ROLLOUTS(5, 8); break;
+        case 6: SN_ROLLOUTS(6, 8); break;
+        case 7: SN_ROLLOUTS(7, 8); break;
+        default: SN_ROLLOUTS(8, 8); break;
+    }
+#undef SN_ROLLOUTS
     HIP_TRY(hipGetLastError());
     return SN_OK;
 }

@@ -70,7 +70,7 @@ static __device__ __noinline__ uint64_t quad_slow8(const uint8_t* ring, int64_t 
     const uint32_t k = min(8u, left);
     for (uint32_t i = 0; i < k; i++) {
         const uint32_t ri = (pos + i) & (uint32_t)(kPipeRing - 1);
-        r |= (uint64_t)ring[((int64_t)(ri >> 4) * B + g) * 16 + (ri & 15u)] << (8u * i);
+        r |= (uint64_t)ring[ring_byte(ri, g, B)] << (8u * i);
     }
     return r;
 }
@@ -98,7 +98,7 @@ struct QuadPipe {
         const uint32_t q0 = (c0 & (uint32_t)(kPipeRing - 1)) >> 4;
         const uint32_t nch = (off + win + 15u) >> 4;
         for (uint32_t i = (uint32_t)q; i < nch; i += 4u)  // the quad copies its window 4 chunks at a time
-            *(u32x4*)(lds_slot + 16u * i) = s.pring[(int64_t)((q0 + i) & (uint32_t)(kPipeRing / 16 - 1)) * B + g];
+            *(u32x4*)(lds_slot + 16u * i) = s.pring[ring16(q0 + i, g, B)];
     }
     // bytes t .. t+7
     __device__ __forceinline__ uint64_t peek8(uint32_t t) const {

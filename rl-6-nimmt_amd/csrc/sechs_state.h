@@ -44,7 +44,7 @@ struct DevState {
     int ring_w;      // ring words per game (multiple of 64), 0 = no ring
     int pad2_;
     // pipelined twist-ahead (k_mt_ahead / RingPipe, sechs_env.hip):
-    u32x4* pring;    // [kPipeRing/16][B] 16-B chunks: byte of absolute stream word p at p mod kPipeRing
+    u32x4* pring;    // [kPipeRing/64][B] 64-B chunks: byte of absolute stream word p at p mod kPipeRing (ring_byte)
     uint32_t* pabsc; // [kPipeSlots][B] consumer position after a play launch (by launch parity, or index mod 4)
     uint32_t* ptend; // [kPipeSlots][B] end of the twisted words after a prep launch (the same)
     uint32_t* ptp;   // [B] twist pointer (MtGen's pos field), owned by k_mt_ahead
@@ -61,7 +61,22 @@ struct DevState {
 constexpr int kMt0Levels = 5;    // word-0 crossings kept in mt0 (the lead of SN_OPT_TWIST_EVERY = 4 spans up to four)
 constexpr int kPipeSlots = 4;    // pabsc buffers (by play launch index mod 4; ptend uses 2, by twist parity)
 constexpr int kPipeRing = 4096;  // ring bytes per game (>= the lead 600 K + a whole round's overshoot: 3 023 at K = 4)
-constexpr int kPipeLead = 600;   // words k_mt_ahead keeps twisted ahead of the consumer (<= 624)
+
+// pring layout: 64-byte chunks interleaved over games -- stream positions
+// 64 c .. 64 c + 63 of game g at chunk c * B + g -- so a twist wave's
+// tempered bytes of 64 consecutive words fill one whole 64-B line (16-B
+// chunks left 48 of every 64 bytes of each written line to other games:
+// 4x the write traffic), and a play wave's 16-B window reads of 64
+// consecutive games still cover one 4-KB run per instruction group.
+// ring16: the u32x4 index of the 16-B unit u (positions 16 u .. 16 u + 15)
+__host__ __device__ __forceinline__ int64_t ring16(uint32_t u, int64_t g, int64_t B) {
+    u &= (uint32_t)(kPipeRing / 16 - 1);
+    return ((int64_t)(u >> 2) * B + g) * 4 + (u & 3u);
+}
+// byte offset of stream position ri (mod kPipeRing) of game g
+__host__ __device__ __forceinline__ int64_t ring_byte(uint32_t ri, int64_t g, int64_t B) {
+    return ring16(ri >> 4, g, B) * 16 + (ri & 15u);
+}constexpr int kPipeLead = 600;   // words k_mt_ahead keeps twisted ahead of the consumer (<= 624)
 constexpr int kPipeWin = 240;    // of them, copied to LDS per lane at a k_play launch: a 4-player
                                   // episode draws 193.5 words, P(> 240) = 7e-6 per game (the rest come
                                   // from HBM); 304 -> 240 measured 7.46 -> 7.60 G env-steps/s interleaved
@@ -252,7 +267,7 @@ static __device__ __noinline__ PipeSlow pipe_slow(const uint8_t* ring, int64_t B
     r.k = min(8u, left);
     for (uint32_t i = 0; i < r.k; i++) {
         const uint32_t ri = (pos + i) & (uint32_t)(kPipeRing - 1);
-        r.bytes |= (uint64_t)ring[((int64_t)(ri >> 4) * B + g) * 16 + (ri & 15u)] << (8u * i);
+        r.bytes |= (uint64_t)ring[ring_byte(ri, g, B)] << (8u * i);
     }
     if (r.k == 0u) {
         atomicAdd(err, 1u);
@@ -285,7 +300,7 @@ struct RingPipe {
         const uint32_t q0 = (c0 & (uint32_t)(kPipeRing - 1)) >> 4;
         const uint32_t nch = (off + win + 15u) >> 4;
         for (uint32_t i = 0; i < nch; i++) {
-            const u32x4 c = s.pring[(int64_t)((q0 + i) & (uint32_t)(kPipeRing / 16 - 1)) * B + g];
+            const u32x4 c = s.pring[ring16(q0 + i, g, B)];
             *(uint64_t*)(lds_slot + 16u * i) = (uint64_t)c.x | ((uint64_t)c.y << 32);
             *(uint64_t*)(lds_slot + 16u * i + 8u) = (uint64_t)c.z | ((uint64_t)c.w << 32);
         }

@@ -251,6 +251,11 @@ class BatchedPUCT:
         # (sn_puct_deal_batch into a [deal_batch][D][48] buffer, each rollout
         # then running on its slice); 0: one sn_puct_deal per rollout (A/B, tests)
         self.deal_batch = int(os.environ.get("SECHS_PUCT_DEAL_BATCH", "16"))
+        # "1": the seats path's rollouts run whole in one kernel per deal batch (sn_puct_rollouts:
+        # decision groups per workgroup, logits in LDS -- measured slower, 0.72 vs 0.87 G playout
+        # env-steps/s: two groups in flight per CU leave each step's latency chain exposed);
+        # "0" (default): a launch per step
+        self.fused_rollouts = os.environ.get("SECHS_PUCT_ROLLOUTS", "0") != "0"
         self._step_dev = torch.zeros((1,), dtype=torch.int32, device=dev)
 
     # ------------------------------------------------------------ policy net on the device
@@ -387,6 +392,15 @@ class BatchedPUCT:
                     wargs = (nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p), nat.ptr(head), nat.ptr(logits), st)
                 lp = nat.ptr(logits)
                 RB, nmc = self.deal_batch, self.n_mc(n)
+                if self.fused_rollouts and self.mlp_layer1 == "seats" and RB > 0 and N <= 8:
+                    rob = self._deal_buf(RB)
+                    for r0 in range(0, nmc, RB):
+                        nr = min(RB, nmc - r0)
+                        nat.check(L.sn_puct_deal_batch(h, qr, r0, nr, rob.data_ptr(), st), "sn_puct_deal_batch")
+                        nat.check(L.sn_puct_rollouts(h, qr, r0, nr, rob.data_ptr(), nat.ptr(w1s), nat.ptr(w1c),
+                                                     nat.ptr(w2p), nat.ptr(head), st), "sn_puct_rollouts")
+                    self.rows_evaluated += nmc * S * (n * (n + 1) // 2)
+                    return
                 if RB > 0:
                     rob = self._deal_buf(RB)
                     stride = self.D * 48 * 4  # bytes of one rollout's states

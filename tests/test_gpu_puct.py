@@ -678,9 +678,9 @@ def test_league_puct_kernels_on_tournament_decisions(monkeypatch):
     """the tournament branches of the PUCT kernels (players_of,
     absent seats q >= k of 2- and 3-player games, the live/dead seat lanes)
     on a BatchedTournament decision list (a PUCT agent among DrunkHamsters,
-    2..4 players): k_puct_step_seats and the one-lane k_puct_step give
-    identical records over whole games (the same Philox uniforms, the same
-    cards), and on the live seats of a fresh deal's decision list the fused
+    2..4 players): the whole-rollout kernel (sn_puct_rollouts),
+    k_puct_step_seats and the one-lane k_puct_step give identical records
+    over whole games (the same Philox uniforms, the same cards), and on the live seats of a fresh deal's decision list the fused
     rollout-logit kernels equal the split PyTorch path and the module's
     forward (_check_mlp_kernels)"""
     from rl_6_nimmt import _native as nat
@@ -696,16 +696,19 @@ def test_league_puct_kernels_on_tournament_decisions(monkeypatch):
         return t
 
     recs = {}
-    for lanes in ("1", "0"):
+    # whole rollouts in one kernel (sn_puct_rollouts), the seat-lane step and the one-lane step
+    for form, rollouts, lanes in (("fused", "1", "1"), ("seats", "0", "1"), ("lane", "0", "0")):
+        monkeypatch.setenv("SECHS_PUCT_ROLLOUTS", rollouts)
         monkeypatch.setenv("SECHS_PUCT_STEP_SEATS", lanes)
         t = league()
-        recs[lanes] = t.play_games(2).cpu()
+        recs[form] = t.play_games(2).cpu()
         assert t.mode == "step"
         t.close()
-    assert torch.equal(recs["1"], recs["0"])
-    k = recs["1"][..., 0] & 15
+    assert torch.equal(recs["fused"], recs["lane"]) and torch.equal(recs["seats"], recs["lane"])
+    k = recs["lane"][..., 0] & 15
     assert int(k.min()) == 2 and int(k.max()) == 4  # absent seats on the lists
     monkeypatch.delenv("SECHS_PUCT_STEP_SEATS")
+    monkeypatch.delenv("SECHS_PUCT_ROLLOUTS")
     t = league()
     t.play_games(1)
     env = t.env
@@ -739,6 +742,29 @@ def test_batched_deal_equals_per_rollout_deals(monkeypatch):
     for rb in ("16", "3"):
         assert all(torch.equal(a, b) for a, b in zip(res[rb][0], res["0"][0])), rb
         assert torch.equal(res[rb][1], res["0"][1]) and torch.equal(res[rb][2], res["0"][2]), rb
+
+
+def test_fused_rollouts_equal_step_launches(monkeypatch):
+    """sn_puct_rollouts (whole rollouts per decision group in one kernel,
+    logits in LDS) and the launch-per-step loop (sn_puct_mlp_seats +
+    sn_puct_step) compute the same logits and draw the same uniforms: a
+    whole PUCT search gives identical statistics, histograms and moves --
+    4 players (one 16-decision group per 64 seats) and 3 players (48 live
+    seat rows per group), a ragged last group"""
+    for N, B in ((4, 300), (3, 97)):
+        res = {}
+        for rollouts in ("1", "0"):
+            monkeypatch.setenv("SECHS_PUCT_ROLLOUTS", rollouts)
+            env, eng = _engine(B=B, N=N, dtype=torch.bfloat16, mc_max=12, mc_per_card=3, seed=23)
+            assert eng.fused_rollouts == (rollouts == "1")
+            acts = [eng.decide(10).clone()]
+            env.step(acts[-1])
+            acts.append(eng.decide(9).clone())
+            torch.cuda.synchronize()
+            res[rollouts] = (acts, eng.stats.clone(), eng.hist.clone(), eng.rows_evaluated)
+        assert all(torch.equal(a, b) for a, b in zip(res["1"][0], res["0"][0])), N
+        assert torch.equal(res["1"][1], res["0"][1]) and torch.equal(res["1"][2], res["0"][2]), N
+        assert res["1"][3] == res["0"][3]
 
 
 def _bf16_forward_bound(x, layers, head_w, head_b, u=2.0 ** -8, l1_roundings=2):
