@@ -1013,8 +1013,9 @@ __global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(PuctArgs a, int N, in
 // step_seat on them.  The same code, the same values: identical statistics
 // to the two-launches-per-step loop, without its 2 n x n_mc launches per
 // decision search (each ~10-20 us at small n_cur) and the logits' HBM trip.
-// Rollout r's state is ro_base + (r - r0) * D * kRoWords (sn_puct_deal_batch
-// dealt it).
+// Rollout r's initial states are ro_base + (r - r0) * D * kRoWords
+// (sn_puct_deal_batch dealt them); the group's copy in LDS is the one the
+// steps read and write.
 template <int N, int L>
 __global__ __launch_bounds__(256, 2) void k_puct_rollouts(DevState s, PuctArgs a, int r0, int nr, int32_t* ro_base,
                                                          const uint16_t* w1s, const float* w1c, const uint16_t* w2,
@@ -1029,6 +1030,7 @@ __global__ __launch_bounds__(256, 2) void k_puct_rollouts(DevState s, PuctArgs a
     __shared__ __attribute__((aligned(16))) float sLogit[kSeatBlock * kHand];
     __shared__ __attribute__((aligned(16))) float sC[kMlpK];
     __shared__ __attribute__((aligned(16))) uint32_t sH2[kMlpM / 2];
+    __shared__ __attribute__((aligned(16))) int32_t sRo[DG * kRoWords];  // the group's rollout states
     __shared__ uint16_t sLut[kLutSize];
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63, col = lane & 31, half = lane >> 5;
@@ -1051,7 +1053,15 @@ __global__ __launch_bounds__(256, 2) void k_puct_rollouts(DevState s, PuctArgs a
         for (int r = r0; r < r0 + nr; r++) {
             PuctArgs ar = a;
             ar.rollout = (uint32_t)r;
-            ar.ro = ro_base + (int64_t)(r - r0) * a.D * kRoWords;
+            // the rollout's states live in LDS for its steps (read by phase 1 and the step, written by
+            // the step; discarded after the backup): ar.ro addresses them by decision index
+            __syncthreads();  // the last rollout's steps are done with sRo
+            {
+                const int32_t* src = ro_base + ((int64_t)(r - r0) * a.D + d0) * kRoWords;
+                const int words = (int)min<int64_t>(DG, a.D - d0) * kRoWords;
+                for (int i = tid; i < words; i += blockDim.x) sRo[i] = src[i];
+            }
+            ar.ro = sRo - d0 * kRoWords;
             for (int t = 0; t < a.n; t++) {
                 const int m = a.n - t;
                 __syncthreads();  // the last step's state writes and LDS reads are done
