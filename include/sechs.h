@@ -168,7 +168,7 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          once, each new word written once: 8 instead of 12
                          B of MT-state traffic per word); 0: exactly the
                          words the lead needs.  Same words either way.
-     SN_OPT_TWIST_EVERY  K = 1 .. 4 (default 2): play launches in groups of
+     SN_OPT_TWIST_EVERY  K = 1 .. 4 (default 4): play launches in groups of
                          K; one k_mt_ahead beside the first launch of each
                          group twists 600 K words past the consumer (the
                          next 2K launches' draws), and that launch waits for
@@ -407,8 +407,8 @@ sn_status sn_puct_deal_batch(sn_env* env, const sn_puct* q, int r0, int nr, void
    states sn_puct_deal_batch dealt into ro_base: per workgroup a group of
    decisions runs every step (sn_puct_mlp_seats' rows, MFMA layer 1 + 2 and
    head into logits in LDS, then sn_puct_step's seat-lane step) of each
-   rollout in order -- the same values as the launch-per-step loop (N <= 8;
-   weights as sn_puct_mlp_seats). */
+   rollout in order -- the same values as the launch-per-step loop (3 <= N
+   <= 8; weights as sn_puct_mlp_seats). */
 sn_status sn_puct_rollouts(sn_env* env, const sn_puct* q, int r0, int nr, void* ro_base, const void* w1s,
                            const float* w1c, const void* w2, const float* head, void* stream);
 sn_status sn_puct_rows(sn_env* env, const sn_puct* q, int n_cur, void* rows, int bf16, void* stream);

@@ -1475,10 +1475,15 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
     e->pipe_lead = kPipeLead;
     e->phase = -1;
     e->play_split = 1;
-    // measured: three-phase whole-round twists and
-    // one twist per two play launches: 0.093 -> 0.085-0.088 ms per step
+    // measured: three-phase whole-round twists, the
+    // ring in 64-B chunks and one twist per four play launches: 0.0861 ->
+    // 0.0775 ms per step same box (K = 1 -> 4; K = 2: 0.0792, 3: 0.0783)
     e->twist_round = 1;
-    e->twist_every = 2;
+    e->twist_every = 4;
+    {
+        const char* te = getenv("SECHS_TWIST_EVERY");  // default override (A/B runs of whole legs)
+        if (te && atoi(te) >= 1 && atoi(te) <= 4) e->twist_every = atoi(te);
+    }
     e->pipe_fused = 0;  // measured slower: the twist's latency lands inside the play waves
     e->play_quad = 0;  // measured: k_play_quad alone is no faster and slows the concurrent twist
     {

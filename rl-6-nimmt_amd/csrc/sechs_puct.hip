@@ -1003,35 +1003,39 @@ __global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(PuctArgs a, int N, in
 
 // ---- whole rollouts in one kernel (sn_puct_rollouts) ----------------------
 // Every rollout step of k_puct_mlp_seats + k_puct_step_seats touches one
-// decision's rollout state, its seats' logits and its statistics only, so a
-// workgroup can carry a group of 64 / L decisions (their 64 seat rows, L
+// decision's rollout state, its seats' logits and its statistics only, so
+// ONE WAVE can carry a group of 64 / L decisions (their <= 64 seat rows, L
 // lanes per decision) through whole rollouts -- every step of rollouts
-// r0 .. r0 + nr - 1, in order, rollout r's first move chosen by PUCT from the
-// statistics rollouts < r backed up -- with no other workgroup involved:
-// per step, the seats' rows (phase 1), the per-seat layer-1 MFMA (phase 2),
-// the candidates' tiles (phase 3) into logits in LDS, then wave 0 runs
-// step_seat on them.  The same code, the same values: identical statistics
-// to the two-launches-per-step loop, without its 2 n x n_mc launches per
-// decision search (each ~10-20 us at small n_cur) and the logits' HBM trip.
-// Rollout r's initial states are ro_base + (r - r0) * D * kRoWords
-// (sn_puct_deal_batch dealt them); the group's copy in LDS is the one the
-// steps read and write.
+// r0 .. r0 + nr - 1, in order, rollout r's first move chosen by PUCT from
+// the statistics rollouts < r backed up -- with no other wave involved and
+// no barrier: per step the seats' rows (phase 1, a lane per seat), the
+// per-seat layer-1 MFMA (phase 2: 4 output tiles x 2 seat halves x 4
+// k-steps), the candidates' 64-row tiles (phase 3, mlp_tile) into logits in
+// LDS, then step_seat on them.  The same code, the same values as the
+// two-launches-per-step loop.  A workgroup of four waves shares W2 in LDS
+// (one workgroup per CU: four groups in flight per CU, each wave's MFMA
+// chain keeping its SIMD busy), each wave has its own rows / base / cards /
+// logits / rollout states.  (The first form -- a workgroup per group, four
+// barriers per step -- ran 12 us per group-step: two groups in flight per
+// CU, slower than the launch-per-step loop.)  Rollout r's initial states
+// are ro_base + (r - r0) * D * kRoWords (sn_puct_deal_batch dealt them); the
+// wave's copy in LDS is the one the steps read and write.
+constexpr int kRollWaveLds = kSeatBlock * kSeatRowLds * 2 + kSeatBlock * kBaseLds * 2 + kSeatBlock * kHand * 4 +
+                             16 * kRoWords * 4;  // rows (aliased by logits) + base + cards + states: 30 208 B
+
 template <int N, int L>
-__global__ __launch_bounds__(256, 2) void k_puct_rollouts(DevState s, PuctArgs a, int r0, int nr, int32_t* ro_base,
+__global__ __launch_bounds__(256, 1) void k_puct_rollouts(DevState s, PuctArgs a, int r0, int nr, int32_t* ro_base,
                                                          const uint16_t* w1s, const float* w1c, const uint16_t* w2,
                                                          const float* head) {
     constexpr int TNT = 2;
     constexpr int kWaves = kBlock / 64;
     constexpr int DG = 64 / L;  // decisions per group
-    __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kMlpLdsK];            // W2 [128][120]
-    __shared__ __attribute__((aligned(16))) uint16_t sRow[kSeatBlock * kSeatRowLds];  // seat rows [64][72]
-    __shared__ __attribute__((aligned(16))) uint16_t sBase[kSeatBlock * kBaseLds];    // base [64][120]
-    __shared__ __attribute__((aligned(16))) float sCard[kSeatBlock * kHand];
-    __shared__ __attribute__((aligned(16))) float sLogit[kSeatBlock * kHand];
+    static_assert(DG <= 16, "states fit (N >= 3: L >= 4)");
+    __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kMlpLdsK];  // W2 [128][120], shared
     __shared__ __attribute__((aligned(16))) float sC[kMlpK];
     __shared__ __attribute__((aligned(16))) uint32_t sH2[kMlpM / 2];
-    __shared__ __attribute__((aligned(16))) int32_t sRo[DG * kRoWords];  // the group's rollout states
     __shared__ uint16_t sLut[kLutSize];
+    __shared__ __attribute__((aligned(16))) uint8_t sWave[kWaves][kRollWaveLds];
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63, col = lane & 31, half = lane >> 5;
     build_row_lut(sLut);
@@ -1041,37 +1045,47 @@ __global__ __launch_bounds__(256, 2) void k_puct_rollouts(DevState s, PuctArgs a
     }
     for (int i = tid; i < kMlpK; i += blockDim.x) sC[i] = w1c[i];
     load_head_pairs(head, sH2);
-    bf16x8_t w1f[kSeatRowK / 16];
+    __syncthreads();  // the only barrier: the waves run independently from here
+    uint16_t* sRow = (uint16_t*)sWave[wave];                                // [64][72]
+    float* sLogit = (float*)sWave[wave];                                    // [64 x 10], aliases sRow (dead by then)
+    uint16_t* sBase = sRow + kSeatBlock * kSeatRowLds;                      // [64][120]
+    float* sCard = (float*)(sBase + kSeatBlock * kBaseLds);                 // [64][10]
+    int32_t* sRo = (int32_t*)(sCard + kSeatBlock * kHand);                  // [DG][48]
+    // phase 2's A fragments: W1s rows 32 mt + col, the four k-steps, all four output tiles
+    bf16x8_t w1f[4][kSeatRowK / 16];
 #pragma unroll
-    for (int ks = 0; ks < kSeatRowK / 16; ks++)
-        w1f[ks] = __builtin_bit_cast(bf16x8_t, *(const uint4*)&w1s[(32 * wave + col) * kSeatRowK + 16 * ks + 8 * half]);
-    const int sl = tid >> 2, part = tid & 3;  // phase 1: four lanes per seat
+    for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+        for (int ks = 0; ks < kSeatRowK / 16; ks++)
+            w1f[mt][ks] =
+                __builtin_bit_cast(bf16x8_t, *(const uint4*)&w1s[(32 * mt + col) * kSeatRowK + 16 * ks + 8 * half]);
     const int64_t groups = (a.D + DG - 1) / DG;
-    for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+    auto fence = [] { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); };
+    for (int64_t grp = (int64_t)blockIdx.x * kWaves + wave; grp < groups; grp += (int64_t)gridDim.x * kWaves) {
         const int64_t d0 = grp * DG;
-        const int nseat = (int)min<int64_t>(DG, a.D - d0) * N;
+        const int nd = (int)min<int64_t>(DG, a.D - d0);
+        const int nseat = nd * N;
         for (int r = r0; r < r0 + nr; r++) {
             PuctArgs ar = a;
             ar.rollout = (uint32_t)r;
-            // the rollout's states live in LDS for its steps (read by phase 1 and the step, written by
-            // the step; discarded after the backup): ar.ro addresses them by decision index
-            __syncthreads();  // the last rollout's steps are done with sRo
             {
                 const int32_t* src = ro_base + ((int64_t)(r - r0) * a.D + d0) * kRoWords;
-                const int words = (int)min<int64_t>(DG, a.D - d0) * kRoWords;
-                for (int i = tid; i < words; i += blockDim.x) sRo[i] = src[i];
+                for (int i = lane; i < nd * kRoWords; i += 64) sRo[i] = src[i];
             }
             ar.ro = sRo - d0 * kRoWords;
+            fence();
             for (int t = 0; t < a.n; t++) {
                 const int m = a.n - t;
-                __syncthreads();  // the last step's state writes and LDS reads are done
-                // phase 1: the seats' rows and card features (rows past the group's seats repeat its last)
-                const SeatIn in = seat_load(ar, N, d0 * N + min(sl, nseat - 1), part);
-                seat_row_part(in, m, part, sRow + sl * kSeatRowLds, sCard + sl * kHand, sLut);
-                __syncthreads();
-                // phase 2: base[seat][j] = sum_k W1s[j][k] rows[seat][k]; wave w: outputs j in [32w, 32w + 32)
+                // phase 1: lane = seat (rows past the group's seats repeat its last), its four parts
+#pragma unroll
+                for (int part = 0; part < 4; part++) {
+                    const SeatIn in = seat_load(ar, N, d0 * N + min(lane, nseat - 1), part);
+                    seat_row_part(in, m, part, sRow + lane * kSeatRowLds, sCard + lane * kHand, sLut);
+                }
+                fence();
+                // phase 2: base[seat][j] = sum_k W1s[j][k] rows[seat][k]
                 {
-                    f32x16_t acc[2];
+                    f32x16_t acc[4][2];
 #pragma unroll
                     for (int ks = 0; ks < kSeatRowK / 16; ks++) {
                         const int k0 = 16 * ks + 8 * half;
@@ -1080,23 +1094,29 @@ __global__ __launch_bounds__(256, 2) void k_puct_rollouts(DevState s, PuctArgs a
                             const bf16x8_t bfr =
                                 __builtin_bit_cast(bf16x8_t, *(const uint4*)&sRow[(32 * nt + col) * kSeatRowLds + k0]);
                             const f32x16_t zero = {};
-                            acc[nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1f[ks], bfr, ks ? acc[nt] : zero, 0, 0, 0);
+#pragma unroll
+                            for (int mt = 0; mt < 4; mt++)
+                                acc[mt][nt] =
+                                    __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1f[mt][ks], bfr, ks ? acc[mt][nt] : zero, 0, 0, 0);
                         }
                     }
 #pragma unroll
-                    for (int nt = 0; nt < 2; nt++)
+                    for (int mt = 0; mt < 4; mt++)
 #pragma unroll
-                        for (int rr = 0; rr < 16; rr += 2) {
-                            const int j = 32 * wave + (rr & 3) + 8 * (rr >> 2) + 4 * half;
-                            if (j < kMlpK)
-                                *(uint32_t*)&sBase[(32 * nt + col) * kBaseLds + j] = pack_bf16(acc[nt][rr], acc[nt][rr + 1]);
-                        }
+                        for (int nt = 0; nt < 2; nt++)
+#pragma unroll
+                            for (int rr = 0; rr < 16; rr += 2) {
+                                const int j = 32 * mt + (rr & 3) + 8 * (rr >> 2) + 4 * half;
+                                if (j < kMlpK)
+                                    *(uint32_t*)&sBase[(32 * nt + col) * kBaseLds + j] =
+                                        pack_bf16(acc[mt][nt][rr], acc[mt][nt][rr + 1]);
+                            }
                 }
-                __syncthreads();
-                // phase 3: the group's candidate rows, 64 per tile, logits to LDS
+                fence();
+                // phase 3: the group's candidate rows, 64 per tile, logits to LDS (over the dead rows)
                 const uint32_t rows = (uint32_t)nseat * (uint32_t)m;
                 const uint32_t tiles = (rows + 32u * TNT - 1u) / (32u * TNT);
-                for (uint32_t tile = (uint32_t)wave; tile < tiles; tile += kWaves) {
+                for (uint32_t tile = 0; tile < tiles; tile++) {
                     uint32_t rw[TNT];
                     float x[TNT];
                     const uint16_t* brow[TNT];
@@ -1110,16 +1130,17 @@ __global__ __launch_bounds__(256, 2) void k_puct_rollouts(DevState s, PuctArgs a
                     }
                     float out[TNT];
                     mlp_tile<TNT>(brow, x, sW, sC, sH2, col, half, out);
+                    if (tile == 0) fence();  // every lane's phase-2 row reads are done before logits land on them
 #pragma unroll
                     for (int nt = 0; nt < TNT; nt++)
                         if (half == 0 && rw[nt] < rows) sLogit[rw[nt]] = out[nt];
                 }
-                __syncthreads();
-                // the step: wave 0, L lanes per decision (step_seat, as k_puct_step_seats)
-                if (wave == 0)
-                    step_seat<N, L>(
-                        s, ar, [&](int64_t dd, int q, int k) { return sLogit[((dd - d0) * N + q) * m + k]; }, t, m,
-                        d0 * L + lane);
+                fence();
+                // the step: L lanes per decision (step_seat, as k_puct_step_seats)
+                step_seat<N, L>(
+                    s, ar, [&](int64_t dd, int q, int k) { return sLogit[((dd - d0) * N + q) * m + k]; }, t, m,
+                    d0 * L + lane);
+                fence();
             }
         }
     }
@@ -1569,17 +1590,15 @@ sn_status sn_puct_rollouts(sn_env* e, const sn_puct* q, int r0, int nr, void* ro
     if (!w1s || !w1c || !w2 || !head) return set_error(SN_EINVAL, "NULL argument");
     if ((((uintptr_t)w1s) | ((uintptr_t)w2) | ((uintptr_t)w1c) | ((uintptr_t)head)) & 15)
         return set_error(SN_EINVAL, "w1s / w2 / w1c / head must be 16-B aligned");
-    if (e->s.N > 8) return set_error(SN_EUNSUPPORTED, "sn_puct_rollouts: N <= 8");
+    if (e->s.N < 3 || e->s.N > 8) return set_error(SN_EUNSUPPORTED, "sn_puct_rollouts: 3 <= N <= 8");
     hipStream_t s = (hipStream_t)stream;
     const int Lw = e->s.N <= 2 ? 2 : e->s.N <= 4 ? 4 : 8;
     const int64_t groups = (a.D + 64 / Lw - 1) / (64 / Lw);
-    const dim3 grid((unsigned)std::min<int64_t>(groups, 2ll * e->cus));
+    const dim3 grid((unsigned)std::min<int64_t>((groups + kBlock / 64 - 1) / (kBlock / 64), (int64_t)e->cus));  // 1 per CU
 #define SN_ROLLOUTS(NN_, L_)                                                                                      \
     hipLaunchKernelGGL((k_puct_rollouts<NN_, L_>), grid, dim3(kBlock), 0, s, e->s, a, r0, nr, (int32_t*)ro_base, \
                        (const uint16_t*)w1s, w1c, (const uint16_t*)w2, head)
     switch (e->s.N) {
-        case 1: SN_ROLLOUTS(1, 2); break;
-        case 2: SN_ROLLOUTS(2, 2); break;
         case 3: SN_ROLLOUTS(3, 4); break;
         case 4: SN_ROLLOUTS(4, 4); break;
         case 5: SN_ROLLOUTS(5, 8); break;

@@ -392,7 +392,7 @@ class BatchedPUCT:
                     wargs = (nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p), nat.ptr(head), nat.ptr(logits), st)
                 lp = nat.ptr(logits)
                 RB, nmc = self.deal_batch, self.n_mc(n)
-                if self.fused_rollouts and self.mlp_layer1 == "seats" and RB > 0 and N <= 8:
+                if self.fused_rollouts and self.mlp_layer1 == "seats" and RB > 0 and 3 <= N <= 8:
                     rob = self._deal_buf(RB)
                     for r0 in range(0, nmc, RB):
                         nr = min(RB, nmc - r0)
