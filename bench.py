@@ -77,8 +77,8 @@ def parse():
                     help="SN_OPT_PLAY_QUAD: four lanes per game, k_play_quad (default: the library's, 0)")
     ap.add_argument("--twist-round", type=int, default=None, choices=[0, 1],
                     help="SN_OPT_TWIST_ROUND: whole-round MT19937 twists in k_mt_ahead (default: the library's, 1)")
-    ap.add_argument("--twist-every", type=int, default=None, choices=[1, 2, 3, 4],
-                    help="SN_OPT_TWIST_EVERY: one k_mt_ahead per 1 .. 4 play launches (default: the library's)")
+    ap.add_argument("--twist-every", type=int, default=None, choices=[1, 2, 3, 4, 5],
+                    help="SN_OPT_TWIST_EVERY: one k_mt_ahead per 1 .. 5 play launches (default: the library's)")
     ap.add_argument("--pipe-fused", type=int, default=None, choices=[0, 1],
                     help="SN_OPT_PIPE_FUSED: k_play_quad twists the MT rounds itself (default: the library's)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")

@@ -168,7 +168,7 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          once, each new word written once: 8 instead of 12
                          B of MT-state traffic per word); 0: exactly the
                          words the lead needs.  Same words either way.
-     SN_OPT_TWIST_EVERY  K = 1 .. 4 (default 4): play launches in groups of
+     SN_OPT_TWIST_EVERY  K = 1 .. 5 (default 4): play launches in groups of
                          K; one k_mt_ahead beside the first launch of each
                          group twists 600 K words past the consumer (the
                          next 2K launches' draws), and that launch waits for

@@ -1482,7 +1482,7 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
     e->twist_every = 4;
     {
         const char* te = getenv("SECHS_TWIST_EVERY");  // default override (A/B runs of whole legs)
-        if (te && atoi(te) >= 1 && atoi(te) <= 4) e->twist_every = atoi(te);
+        if (te && atoi(te) >= 1 && atoi(te) <= 5) e->twist_every = atoi(te);
     }
     e->pipe_fused = 0;  // measured slower: the twist's latency lands inside the play waves
     e->play_quad = 0;  // measured: k_play_quad alone is no faster and slows the concurrent twist
@@ -1618,7 +1618,7 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
             e->play_split = value;
             return SN_OK;
         case SN_OPT_TWIST_EVERY:
-            if (value < 1 || value > 4) return fail(SN_EINVAL, "twist every must be 1 .. 4");
+            if (value < 1 || value > 5) return fail(SN_EINVAL, "twist every must be 1 .. 5");
             e->twist_every = value;
             return SN_OK;
         case SN_OPT_TWIST_ROUND:
@@ -1886,7 +1886,8 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     // only, which had a whole group of launches to finish.  Per group, one
     // record and one wait on the caller's stream (K = 1: the launch before).
     // Slots: pabsc by launch index mod 4, ptend by group parity (INIT =
-    // launch -1 / twist -1).  The ring holds the lead + a round for K <= 4.
+    // launch -1 / twist -1).  The ring holds the lead + a round for K <= 5
+    // (3 623 words), and mt0 the five word-0 crossings that span.
     const int K = fused ? 1 : e->twist_every;
     const bool round_tw = fused || e->twist_round;
     if (e->pvalid && ((e->pfused != 0) != fused || e->pK != K)) {  // restart in the other form

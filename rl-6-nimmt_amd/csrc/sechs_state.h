@@ -58,9 +58,9 @@ struct DevState {
     int32_t* lpf;    // [B] 1 (| 2: quirk Q6): lpc holds this step's non-external cards
 };
 
-constexpr int kMt0Levels = 5;    // word-0 crossings kept in mt0 (the lead of SN_OPT_TWIST_EVERY = 4 spans up to four)
+constexpr int kMt0Levels = 5;    // word-0 crossings kept in mt0 (a K = 5 lead + a round spans up to five)
 constexpr int kPipeSlots = 4;    // pabsc buffers (by play launch index mod 4; ptend uses 2, by twist parity)
-constexpr int kPipeRing = 4096;  // ring bytes per game (>= the lead 600 K + a whole round's overshoot: 3 023 at K = 4)
+constexpr int kPipeRing = 4096;  // ring bytes per game (>= the lead 600 K + a whole round's overshoot: 3 623 at K = 5)
 
 // pring layout: 64-byte chunks interleaved over games -- stream positions
 // 64 c .. 64 c + 63 of game g at chunk c * B + g -- so a twist wave's

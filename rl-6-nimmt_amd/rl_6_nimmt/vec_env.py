@@ -190,7 +190,7 @@ class VecSechsNimmtEnv:
         """rollout tuning (include/sechs.h SN_OPT_*; all numpy-compat only except play_split,
         the role-split kernel of philox handles; play_quad: four lanes per game on the
         pipelined 4-player path, k_play_quad; twist_round: whole-round MT twists in
-        k_mt_ahead; twist_every: one twist-ahead launch per K = 1 .. 4 play launches; pipe_fused:
+        k_mt_ahead; twist_every: one twist-ahead launch per K = 1 .. 5 play launches; pipe_fused:
         k_play_quad twists the rounds itself, no side stream); results never
         depend on it
         (except pipe_lead < 600, a test knob that makes overruns -- PipeOverrunError -- likely)"""
