@@ -65,8 +65,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=None,
                     help="GPUs of this node, one rank each (default: WORLD_SIZE, else 1); without a launcher, N > 1 "
                          "starts torch.distributed.run over N ranks as a child process")
-    ap.add_argument("--steps", type=int, default=100, help="timed launches (episodes)")
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200, help="timed launches (episodes)")
+    ap.add_argument("--warmup", type=int, default=20,
+                    help="untimed launches first (several twist groups: the pipeline in its steady state)")
     ap.add_argument("--games", type=int, default=65536, help="games per GPU")
     ap.add_argument("--rng", default="numpy", choices=["numpy", "philox"])
     ap.add_argument("--no-obs", action="store_true", help="do not emit observations (not the headline)")
