@@ -56,6 +56,7 @@ ALGO_BYTES_PER_STEP = (33 * N_PLAYERS + 57) + 47 * N_PLAYERS  # 377 B at N = 4
 # applied by tools/pmc_traffic.py.  PMC counters cannot be read inside a plain
 # run, so the committed summary of the current kernels is reported beside the
 # live timing.
+LIB_TWIST_EVERY = 4  # the library's SN_OPT_TWIST_EVERY default (include/sechs.h)
 PMC_TRAFFIC = {"numpy": os.path.join(ROOT, "profiles", "r05_pmc_traffic_numpy.json"),  # tools/r05_final.sh
                "philox": os.path.join(ROOT, "profiles", "r04_pmc_traffic_philox.json")}
 
@@ -888,6 +889,7 @@ def main():
     # twist-ahead k_mt_ahead runs concurrently on a side stream and is
     # reported beside it; the whole step is `step_ms`)
     play_ms = kt["k_play"]
+    twist_k = args.twist_every or LIB_TWIST_EVERY
     achieved = launch_steps * ALGO_BYTES_PER_STEP / (play_ms * 1e-3) / 1e9
     per_kernel, traffic_src = pmc_traffic(args.rng, B) if not args.no_obs else (None, None)
     traffic = per_kernel.get("k_play<4") if per_kernel else None
@@ -937,11 +939,16 @@ def main():
             "algo_bytes_per_launch": launch_steps * ALGO_BYTES_PER_STEP,
             "step_ms": kern_ms,
             "step_frac": launch_steps * ALGO_BYTES_PER_STEP / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-            "concurrent": ({"kernel": "k_mt_ahead<false> (side stream, next launch's MT19937 twist-ahead)",
+            "concurrent": ({"kernel": "k_mt_ahead<false, true> (side stream: one dispatch per twist_every play "
+                                      "launches, whole MT19937 rounds ahead of the consumer)",
                             "kernel_ms": kt.get("k_mt_ahead"),
-                            "traffic": per_kernel.get("k_mt_ahead") if per_kernel else None}
+                            "traffic": per_kernel.get("k_mt_ahead") if per_kernel else None,
+                            "traffic_unit": "HBM bytes per twist dispatch (PMC)"}
                            if args.rng == "numpy" else None),
-            "step_traffic": sum(per_kernel.values()) if per_kernel else None,
+            # one twist dispatch per K play launches (SN_OPT_TWIST_EVERY): its traffic per launch is 1/K
+            "step_traffic": ((per_kernel.get("k_play<4", 0.0) + per_kernel.get("k_mt_ahead", 0.0) / twist_k)
+                             if per_kernel else None),
+            "twist_every": twist_k if args.rng == "numpy" else None,
         },
         "episodes_checksum": {"episodes": int(eps.sum().item()) * world, "mean_score_per_seat": (tot / (eps.sum().item() * world)).tolist()},
     }
