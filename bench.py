@@ -405,9 +405,12 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
     fused = eng.fused_mlp and eng._net is not None and eng._net.fused() is not None
     seats = fused and eng.mlp_layer1 in ("seats", "mfma")
     mfma1 = fused and eng.mlp_layer1 == "mfma"  # layer 1 per candidate row on MFMA (sn_puct_mlp_mfma)
+    whole = seats and not mfma1 and eng.fused_rollouts and eng.deal_batch > 0  # sn_puct_rollouts
     tflops = eng.rows_evaluated * 29800 / wall / 1e12
     sq4 = None  # SQ counters of the rollout MLP kernel (tools/r04_puct_pmc.sh, eager launches)
     try:
+        if whole:
+            raise KeyError("the r04 SQ pass measured k_puct_mlp_seats, not k_puct_rollouts")
         c = json.load(open(os.path.join(ROOT, "profiles", "r04_sq_config4_kernels.json")))["k_puct_mlp_seats"]
         sq4 = {"mfma_busy_cycles_per_launch": c["SQ_VALU_MFMA_BUSY_CYCLES"] / c["dispatches_per_pass"],
                "valu_per_wave": c["SQ_INSTS_VALU_per_wave"], "mfma_per_wave": c["SQ_INSTS_MFMA"] / c["SQ_WAVES"],
@@ -421,7 +424,10 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
         # MFMA peak, over the whole game's wall time (every kernel included)
         roof = {"bound": "mfma", "achieved": tflops, "peak": 2500.0, "unit": "TFLOP/s", "frac": tflops / 2500.0,
                 "traffic": None, "algo_flop_per_row": 29800, "sq": sq4,
-                "kernel": ("rollout step = sn_puct_mlp_mfma (MFMA: seat rows, layer 1 per candidate row, layer 2, "
+                "kernel": ("whole rollouts = sn_puct_deal_batch (16 rollouts' deals) + sn_puct_rollouts (one wave per "
+                           "group of 8 decisions: every step's seat rows, MFMA layer 1 + 2 and head into logits in LDS, "
+                           "the seat-lane step; two waves per SIMD); whole-game wall time") if whole
+                else ("rollout step = sn_puct_mlp_mfma (MFMA: seat rows, layer 1 per candidate row, layer 2, "
                            "head in one persistent kernel) + k_puct_step_seats; whole-game wall time") if mfma1
                 else ("rollout step = sn_puct_mlp_seats (MFMA: seat rows, layer 1 per seat, card column, "
                       "layer 2, head in one persistent kernel) + k_puct_step_seats; whole-game wall time") if seats

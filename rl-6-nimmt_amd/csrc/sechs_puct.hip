@@ -708,11 +708,13 @@ __global__ void k_puct_step(DevState s, PuctArgs a, const void* logits, int ls, 
 // candidate k's logit of seat q of decision dd
 template <int N, int L, class Logit>
 __device__ __forceinline__ void step_seat(const DevState& s, const PuctArgs& a, Logit logit, int t, int n_cur,
-                                          int64_t i) {
+                                          int64_t i, int64_t d_hi = -1, int64_t d_dead = -1) {
     const int64_t d = i / L;
     const int q = (int)(i & (L - 1));
-    const bool live = d < a.D;
-    const int64_t dd = live ? d : a.D - 1;  // lanes past the last decision follow along (shuffles), write nothing
+    // lanes past the last decision (or past d_hi, with d_dead a decision they may read) follow along
+    // (shuffles) and write nothing
+    const bool live = d < a.D && (d_hi < 0 || d < d_hi);
+    const int64_t dd = live ? d : (d_dead >= 0 ? d_dead : a.D - 1);
     int64_t g;
     int p;
     dec_to_gp(a, dd, g, p);
@@ -1020,17 +1022,18 @@ __global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(PuctArgs a, int N, in
 // CU, slower than the launch-per-step loop.)  Rollout r's initial states
 // are ro_base + (r - r0) * D * kRoWords (sn_puct_deal_batch dealt them); the
 // wave's copy in LDS is the one the steps read and write.
-constexpr int kRollWaveLds = kSeatBlock * kSeatRowLds * 2 + kSeatBlock * kBaseLds * 2 + kSeatBlock * kHand * 4 +
-                             16 * kRoWords * 4;  // rows (aliased by logits) + base + cards + states: 30 208 B
+constexpr int kRollSeats = 32;  // seats per wave's group (32 / L... 64 / L / 2 decisions)
+constexpr int kRollWaveLds = kRollSeats * kSeatRowLds * 2 + kRollSeats * kBaseLds * 2 + kRollSeats * kHand * 4 +
+                             8 * kRoWords * 4;  // rows (aliased by logits) + base + cards + states: 15 104 B
 
 template <int N, int L>
-__global__ __launch_bounds__(256, 1) void k_puct_rollouts(DevState s, PuctArgs a, int r0, int nr, int32_t* ro_base,
+__global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a, int r0, int nr, int32_t* ro_base,
                                                          const uint16_t* w1s, const float* w1c, const uint16_t* w2,
                                                          const float* head) {
-    constexpr int TNT = 2;
-    constexpr int kWaves = kBlock / 64;
-    constexpr int DG = 64 / L;  // decisions per group
-    static_assert(DG <= 16, "states fit (N >= 3: L >= 4)");
+    constexpr int TNT = 1;  // 32-row tiles: 64 accumulator registers (two waves per SIMD: 256 registers each)
+    constexpr int kWaves = 512 / 64;  // two per SIMD
+    constexpr int DG = kRollSeats / L;  // decisions per group
+    static_assert(DG <= 8 && DG * N <= kRollSeats, "a group's seats and states fit");
     __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kMlpLdsK];  // W2 [128][120], shared
     __shared__ __attribute__((aligned(16))) float sC[kMlpK];
     __shared__ __attribute__((aligned(16))) uint32_t sH2[kMlpM / 2];
@@ -1046,21 +1049,14 @@ __global__ __launch_bounds__(256, 1) void k_puct_rollouts(DevState s, PuctArgs a
     for (int i = tid; i < kMlpK; i += blockDim.x) sC[i] = w1c[i];
     load_head_pairs(head, sH2);
     __syncthreads();  // the only barrier: the waves run independently from here
-    uint16_t* sRow = (uint16_t*)sWave[wave];                                // [64][72]
-    float* sLogit = (float*)sWave[wave];                                    // [64 x 10], aliases sRow (dead by then)
-    uint16_t* sBase = sRow + kSeatBlock * kSeatRowLds;                      // [64][120]
-    float* sCard = (float*)(sBase + kSeatBlock * kBaseLds);                 // [64][10]
-    int32_t* sRo = (int32_t*)(sCard + kSeatBlock * kHand);                  // [DG][48]
-    // phase 2's A fragments: W1s rows 32 mt + col, the four k-steps, all four output tiles
-    bf16x8_t w1f[4][kSeatRowK / 16];
-#pragma unroll
-    for (int mt = 0; mt < 4; mt++)
-#pragma unroll
-        for (int ks = 0; ks < kSeatRowK / 16; ks++)
-            w1f[mt][ks] =
-                __builtin_bit_cast(bf16x8_t, *(const uint4*)&w1s[(32 * mt + col) * kSeatRowK + 16 * ks + 8 * half]);
+    uint16_t* sRow = (uint16_t*)sWave[wave];                 // [32][72]
+    float* sLogit = (float*)sWave[wave];                     // [32 x 10], aliases sRow (dead by then)
+    uint16_t* sBase = sRow + kRollSeats * kSeatRowLds;       // [32][120]
+    float* sCard = (float*)(sBase + kRollSeats * kBaseLds);  // [32][10]
+    int32_t* sRo = (int32_t*)(sCard + kRollSeats * kHand);   // [DG][48]
     const int64_t groups = (a.D + DG - 1) / DG;
     auto fence = [] { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); };
+    const int sl = lane & (kRollSeats - 1), p0 = lane >> 5;  // phase 1: seat sl, parts p0 and p0 + 2
     for (int64_t grp = (int64_t)blockIdx.x * kWaves + wave; grp < groups; grp += (int64_t)gridDim.x * kWaves) {
         const int64_t d0 = grp * DG;
         const int nd = (int)min<int64_t>(DG, a.D - d0);
@@ -1076,41 +1072,43 @@ __global__ __launch_bounds__(256, 1) void k_puct_rollouts(DevState s, PuctArgs a
             fence();
             for (int t = 0; t < a.n; t++) {
                 const int m = a.n - t;
-                // phase 1: lane = seat (rows past the group's seats repeat its last), its four parts
+                // phase 1: two lanes per seat (rows past the group's seats repeat its last)
 #pragma unroll
-                for (int part = 0; part < 4; part++) {
-                    const SeatIn in = seat_load(ar, N, d0 * N + min(lane, nseat - 1), part);
-                    seat_row_part(in, m, part, sRow + lane * kSeatRowLds, sCard + lane * kHand, sLut);
+                for (int pp = 0; pp < 2; pp++) {
+                    const int part = p0 + 2 * pp;
+                    const SeatIn in = seat_load(ar, N, d0 * N + min(sl, nseat - 1), part);
+                    seat_row_part(in, m, part, sRow + sl * kSeatRowLds, sCard + sl * kHand, sLut);
                 }
                 fence();
-                // phase 2: base[seat][j] = sum_k W1s[j][k] rows[seat][k]
+                // phase 2: base[seat][j] = sum_k W1s[j][k] rows[seat][k] (one 32-seat tile)
                 {
-                    f32x16_t acc[4][2];
+                    // the A fragments (W1s rows 32 mt + col) from L1 / L2 per step: held across phase 3
+                    // they would spill (two waves per SIMD: 256 registers each)
+                    bf16x8_t w1f[4][kSeatRowK / 16];
+#pragma unroll
+                    for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+                        for (int ks = 0; ks < kSeatRowK / 16; ks++)
+                            w1f[mt][ks] = __builtin_bit_cast(
+                                bf16x8_t, *(const uint4*)&w1s[(32 * mt + col) * kSeatRowK + 16 * ks + 8 * half]);
+                    f32x16_t acc[4];
 #pragma unroll
                     for (int ks = 0; ks < kSeatRowK / 16; ks++) {
-                        const int k0 = 16 * ks + 8 * half;
+                        const bf16x8_t bfr =
+                            __builtin_bit_cast(bf16x8_t, *(const uint4*)&sRow[col * kSeatRowLds + 16 * ks + 8 * half]);
+                        const f32x16_t zero = {};
 #pragma unroll
-                        for (int nt = 0; nt < 2; nt++) {
-                            const bf16x8_t bfr =
-                                __builtin_bit_cast(bf16x8_t, *(const uint4*)&sRow[(32 * nt + col) * kSeatRowLds + k0]);
-                            const f32x16_t zero = {};
-#pragma unroll
-                            for (int mt = 0; mt < 4; mt++)
-                                acc[mt][nt] =
-                                    __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1f[mt][ks], bfr, ks ? acc[mt][nt] : zero, 0, 0, 0);
-                        }
+                        for (int mt = 0; mt < 4; mt++)
+                            acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1f[mt][ks], bfr, ks ? acc[mt] : zero, 0, 0, 0);
                     }
 #pragma unroll
                     for (int mt = 0; mt < 4; mt++)
 #pragma unroll
-                        for (int nt = 0; nt < 2; nt++)
-#pragma unroll
-                            for (int rr = 0; rr < 16; rr += 2) {
-                                const int j = 32 * mt + (rr & 3) + 8 * (rr >> 2) + 4 * half;
-                                if (j < kMlpK)
-                                    *(uint32_t*)&sBase[(32 * nt + col) * kBaseLds + j] =
-                                        pack_bf16(acc[mt][nt][rr], acc[mt][nt][rr + 1]);
-                            }
+                        for (int rr = 0; rr < 16; rr += 2) {
+                            const int j = 32 * mt + (rr & 3) + 8 * (rr >> 2) + 4 * half;
+                            if (j < kMlpK)
+                                *(uint32_t*)&sBase[col * kBaseLds + j] = pack_bf16(acc[mt][rr], acc[mt][rr + 1]);
+                        }
                 }
                 fence();
                 // phase 3: the group's candidate rows, 64 per tile, logits to LDS (over the dead rows)
@@ -1136,10 +1134,11 @@ __global__ __launch_bounds__(256, 1) void k_puct_rollouts(DevState s, PuctArgs a
                         if (half == 0 && rw[nt] < rows) sLogit[rw[nt]] = out[nt];
                 }
                 fence();
-                // the step: L lanes per decision (step_seat, as k_puct_step_seats)
+                // the step: L lanes per decision (step_seat, as k_puct_step_seats); lanes past the
+                // group's DG decisions (the upper half of the wave) follow along and write nothing
                 step_seat<N, L>(
                     s, ar, [&](int64_t dd, int q, int k) { return sLogit[((dd - d0) * N + q) * m + k]; }, t, m,
-                    d0 * L + lane);
+                    d0 * L + lane, d0 + nd, d0);
                 fence();
             }
         }
@@ -1593,10 +1592,10 @@ sn_status sn_puct_rollouts(sn_env* e, const sn_puct* q, int r0, int nr, void* ro
     if (e->s.N < 3 || e->s.N > 8) return set_error(SN_EUNSUPPORTED, "sn_puct_rollouts: 3 <= N <= 8");
     hipStream_t s = (hipStream_t)stream;
     const int Lw = e->s.N <= 2 ? 2 : e->s.N <= 4 ? 4 : 8;
-    const int64_t groups = (a.D + 64 / Lw - 1) / (64 / Lw);
-    const dim3 grid((unsigned)std::min<int64_t>((groups + kBlock / 64 - 1) / (kBlock / 64), (int64_t)e->cus));  // 1 per CU
+    const int64_t groups = (a.D + kRollSeats / Lw - 1) / (kRollSeats / Lw);
+    const dim3 grid((unsigned)std::min<int64_t>((groups + 7) / 8, (int64_t)e->cus));  // one 8-wave workgroup per CU
 #define SN_ROLLOUTS(NN_, L_)                                                                                      \
-    hipLaunchKernelGGL((k_puct_rollouts<NN_, L_>), grid, dim3(kBlock), 0, s, e->s, a, r0, nr, (int32_t*)ro_base, \
+    hipLaunchKernelGGL((k_puct_rollouts<NN_, L_>), grid, dim3(512), 0, s, e->s, a, r0, nr, (int32_t*)ro_base,     \
                        (const uint16_t*)w1s, w1c, (const uint16_t*)w2, head)
     switch (e->s.N) {
         case 3: SN_ROLLOUTS(3, 4); break;
