@@ -1030,7 +1030,7 @@ template <int N, int L>
 __global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a, int r0, int nr, int32_t* ro_base,
                                                          const uint16_t* w1s, const float* w1c, const uint16_t* w2,
                                                          const float* head) {
-    constexpr int TNT = 1;  // 32-row tiles: 64 accumulator registers (two waves per SIMD: 256 registers each)
+    constexpr int TNT = 2;
     constexpr int kWaves = 512 / 64;  // two per SIMD
     constexpr int DG = kRollSeats / L;  // decisions per group
     static_assert(DG <= 8 && DG * N <= kRollSeats, "a group's seats and states fit");

@@ -193,7 +193,7 @@ class FusedMLP:
 
 class BatchedPUCT:
     def __init__(self, env, actor, mc_per_card=10, mc_max=100, c_puct=2.0, seed=0, seats_mask=None, puct_root=True,
-                 net_dtype=torch.bfloat16, mcs_num_cards=104, graph=False, max_decisions=None):
+                 net_dtype=torch.bfloat16, mcs_num_cards=104, graph=False, max_decisions=None, fused_rollouts=None):
         # `actor` stays where the caller keeps it (the drop-in agents run it
         # on the host): inference uses a device copy in net_dtype (sync_net),
         # the training losses run on the actor's own device (actor_device).
@@ -251,11 +251,13 @@ class BatchedPUCT:
         # (sn_puct_deal_batch into a [deal_batch][D][48] buffer, each rollout
         # then running on its slice); 0: one sn_puct_deal per rollout (A/B, tests)
         self.deal_batch = int(os.environ.get("SECHS_PUCT_DEAL_BATCH", "16"))
-        # "1": the seats path's rollouts run whole in one kernel per deal batch (sn_puct_rollouts:
-        # decision groups per workgroup, logits in LDS -- measured slower, 0.72 vs 0.87 G playout
-        # env-steps/s: two groups in flight per CU leave each step's latency chain exposed);
-        # "0" (default): a launch per step
-        self.fused_rollouts = os.environ.get("SECHS_PUCT_ROLLOUTS", "0") != "0"
+        # whole rollouts in one kernel per deal batch (sn_puct_rollouts: a wave per group of 8
+        # decisions, logits in LDS; 0.96 vs 0.87 G playout env-steps/s on config 4) or a launch
+        # per step (fused_rollouts=False: the tournament's engines, where the whole-rollout kernel
+        # measured slower); SECHS_PUCT_ROLLOUTS=0 / 1 overrides (A/B runs, tests)
+        env_ro = os.environ.get("SECHS_PUCT_ROLLOUTS")
+        self.fused_rollouts = (env_ro != "0") if env_ro is not None else (True if fused_rollouts is None
+                                                                            else bool(fused_rollouts))
         self._step_dev = torch.zeros((1,), dtype=torch.int32, device=dev)
 
     # ------------------------------------------------------------ policy net on the device
