@@ -409,12 +409,15 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
     tflops = eng.rows_evaluated * 29800 / wall / 1e12
     sq4 = None  # SQ counters of the rollout MLP kernel (tools/r04_puct_pmc.sh, eager launches)
     try:
-        if whole:
-            raise KeyError("the r04 SQ pass measured k_puct_mlp_seats, not k_puct_rollouts")
-        c = json.load(open(os.path.join(ROOT, "profiles", "r04_sq_config4_kernels.json")))["k_puct_mlp_seats"]
+        if whole:  # tools/r05_puct_pmc.sh (eager launches)
+            src = "profiles/r05_sq_config4_rollouts.json"
+            c = json.load(open(os.path.join(ROOT, src)))["void k_puct_rollouts<4, 4>"]
+        else:
+            src = "profiles/r04_sq_config4_kernels.json"
+            c = json.load(open(os.path.join(ROOT, src)))["k_puct_mlp_seats"]
         sq4 = {"mfma_busy_cycles_per_launch": c["SQ_VALU_MFMA_BUSY_CYCLES"] / c["dispatches_per_pass"],
                "valu_per_wave": c["SQ_INSTS_VALU_per_wave"], "mfma_per_wave": c["SQ_INSTS_MFMA"] / c["SQ_WAVES"],
-               "source": "profiles/r04_sq_config4_kernels.json"}
+               "valu_per_mfma": c["SQ_INSTS_VALU"] / c["SQ_INSTS_MFMA"], "source": src}
     except (OSError, KeyError, ValueError, ZeroDivisionError):
         pass
     if fused:
