@@ -405,10 +405,12 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
     fused = eng.fused_mlp and eng._net is not None and eng._net.fused() is not None
     seats = fused and eng.mlp_layer1 in ("seats", "mfma")
     mfma1 = fused and eng.mlp_layer1 == "mfma"  # layer 1 per candidate row on MFMA (sn_puct_mlp_mfma)
-    whole = seats and not mfma1 and eng.fused_rollouts and eng.deal_batch > 0  # sn_puct_rollouts
+    whole = seats and eng.fused_rollouts and eng.deal_batch > 0  # sn_puct_rollouts(_mfma)
     tflops = eng.rows_evaluated * 29800 / wall / 1e12
     sq4 = None  # SQ counters of the rollout MLP kernel (tools/r04_puct_pmc.sh, eager launches)
     try:
+        if whole and mfma1:
+            raise KeyError("no SQ pass of sn_puct_rollouts_mfma")
         if whole:  # tools/r05_puct_pmc.sh (eager launches)
             src = "profiles/r05_sq_config4_rollouts.json"
             c = json.load(open(os.path.join(ROOT, src)))["void k_puct_rollouts<4, 4>"]
@@ -427,9 +429,10 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
         # MFMA peak, over the whole game's wall time (every kernel included)
         roof = {"bound": "mfma", "achieved": tflops, "peak": 2500.0, "unit": "TFLOP/s", "frac": tflops / 2500.0,
                 "traffic": None, "algo_flop_per_row": 29800, "sq": sq4,
-                "kernel": ("whole rollouts = sn_puct_deal_batch (16 rollouts' deals) + sn_puct_rollouts (one wave per "
-                           "group of 8 decisions: every step's seat rows, MFMA layer 1 + 2 and head into logits in LDS, "
-                           "the seat-lane step; two waves per SIMD); whole-game wall time") if whole
+                "kernel": ("whole rollouts = sn_puct_deal_batch (16 rollouts' deals) + sn_puct_rollouts"
+                           + ("_mfma" if mfma1 else "") + " (one wave per group of 8 decisions: every step's seat "
+                           "rows, MFMA layer 1 + 2 and head into logits in LDS, the seat-lane step; two waves per "
+                           "SIMD); whole-game wall time") if whole
                 else ("rollout step = sn_puct_mlp_mfma (MFMA: seat rows, layer 1 per candidate row, layer 2, "
                            "head in one persistent kernel) + k_puct_step_seats; whole-game wall time") if mfma1
                 else ("rollout step = sn_puct_mlp_seats (MFMA: seat rows, layer 1 per seat, card column, "

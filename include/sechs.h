@@ -411,6 +411,9 @@ sn_status sn_puct_deal_batch(sn_env* env, const sn_puct* q, int r0, int nr, void
    <= 8; weights as sn_puct_mlp_seats). */
 sn_status sn_puct_rollouts(sn_env* env, const sn_puct* q, int r0, int nr, void* ro_base, const void* w1s,
                            const float* w1c, const void* w2, const float* head, void* stream);
+/* The same with layer 1 per candidate row on MFMA (sn_puct_mlp_mfma's arithmetic; w2q as there). */
+sn_status sn_puct_rollouts_mfma(sn_env* env, const sn_puct* q, int r0, int nr, void* ro_base, const void* w1s,
+                                const void* w2q, const float* head, void* stream);
 sn_status sn_puct_rows(sn_env* env, const sn_puct* q, int n_cur, void* rows, int bf16, void* stream);
 sn_status sn_puct_step(sn_env* env, const sn_puct* q, const float* logits, int t, int n_cur, void* stream);
 /* Layer-1 split of the rollout MLP (MultiHeadedMLP 48 -> H -> ...), in

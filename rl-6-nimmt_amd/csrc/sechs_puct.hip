@@ -1003,148 +1003,6 @@ __global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(PuctArgs a, int N, in
     }
 }
 
-// ---- whole rollouts in one kernel (sn_puct_rollouts) ----------------------
-// Every rollout step of k_puct_mlp_seats + k_puct_step_seats touches one
-// decision's rollout state, its seats' logits and its statistics only, so
-// ONE WAVE can carry a group of 64 / L decisions (their <= 64 seat rows, L
-// lanes per decision) through whole rollouts -- every step of rollouts
-// r0 .. r0 + nr - 1, in order, rollout r's first move chosen by PUCT from
-// the statistics rollouts < r backed up -- with no other wave involved and
-// no barrier: per step the seats' rows (phase 1, a lane per seat), the
-// per-seat layer-1 MFMA (phase 2: 4 output tiles x 2 seat halves x 4
-// k-steps), the candidates' 64-row tiles (phase 3, mlp_tile) into logits in
-// LDS, then step_seat on them.  The same code, the same values as the
-// two-launches-per-step loop.  A workgroup of four waves shares W2 in LDS
-// (one workgroup per CU: four groups in flight per CU, each wave's MFMA
-// chain keeping its SIMD busy), each wave has its own rows / base / cards /
-// logits / rollout states.  (The first form -- a workgroup per group, four
-// barriers per step -- ran 12 us per group-step: two groups in flight per
-// CU, slower than the launch-per-step loop.)  Rollout r's initial states
-// are ro_base + (r - r0) * D * kRoWords (sn_puct_deal_batch dealt them); the
-// wave's copy in LDS is the one the steps read and write.
-constexpr int kRollSeats = 32;  // seats per wave's group (32 / L... 64 / L / 2 decisions)
-constexpr int kRollWaveLds = kRollSeats * kSeatRowLds * 2 + kRollSeats * kBaseLds * 2 + kRollSeats * kHand * 4 +
-                             8 * kRoWords * 4;  // rows (aliased by logits) + base + cards + states: 15 104 B
-
-template <int N, int L>
-__global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a, int r0, int nr, int32_t* ro_base,
-                                                         const uint16_t* w1s, const float* w1c, const uint16_t* w2,
-                                                         const float* head) {
-    constexpr int TNT = 2;
-    constexpr int kWaves = 512 / 64;  // two per SIMD
-    constexpr int DG = kRollSeats / L;  // decisions per group
-    static_assert(DG <= 8 && DG * N <= kRollSeats, "a group's seats and states fit");
-    __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kMlpLdsK];  // W2 [128][120], shared
-    __shared__ __attribute__((aligned(16))) float sC[kMlpK];
-    __shared__ __attribute__((aligned(16))) uint32_t sH2[kMlpM / 2];
-    __shared__ uint16_t sLut[kLutSize];
-    __shared__ __attribute__((aligned(16))) uint8_t sWave[kWaves][kRollWaveLds];
-    const int tid = threadIdx.x;
-    const int wave = tid >> 6, lane = tid & 63, col = lane & 31, half = lane >> 5;
-    build_row_lut(sLut);
-    for (int i = tid; i < kMlpM * (kMlpK / 8); i += blockDim.x) {
-        const int o = i / (kMlpK / 8), c = i - o * (kMlpK / 8);
-        *(uint4*)&sW[o * kMlpLdsK + 8 * c] = *(const uint4*)&w2[o * kMlpK + 8 * c];
-    }
-    for (int i = tid; i < kMlpK; i += blockDim.x) sC[i] = w1c[i];
-    load_head_pairs(head, sH2);
-    __syncthreads();  // the only barrier: the waves run independently from here
-    uint16_t* sRow = (uint16_t*)sWave[wave];                 // [32][72]
-    float* sLogit = (float*)sWave[wave];                     // [32 x 10], aliases sRow (dead by then)
-    uint16_t* sBase = sRow + kRollSeats * kSeatRowLds;       // [32][120]
-    float* sCard = (float*)(sBase + kRollSeats * kBaseLds);  // [32][10]
-    int32_t* sRo = (int32_t*)(sCard + kRollSeats * kHand);   // [DG][48]
-    const int64_t groups = (a.D + DG - 1) / DG;
-    auto fence = [] { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); };
-    const int sl = lane & (kRollSeats - 1), p0 = lane >> 5;  // phase 1: seat sl, parts p0 and p0 + 2
-    for (int64_t grp = (int64_t)blockIdx.x * kWaves + wave; grp < groups; grp += (int64_t)gridDim.x * kWaves) {
-        const int64_t d0 = grp * DG;
-        const int nd = (int)min<int64_t>(DG, a.D - d0);
-        const int nseat = nd * N;
-        for (int r = r0; r < r0 + nr; r++) {
-            PuctArgs ar = a;
-            ar.rollout = (uint32_t)r;
-            {
-                const int32_t* src = ro_base + ((int64_t)(r - r0) * a.D + d0) * kRoWords;
-                for (int i = lane; i < nd * kRoWords; i += 64) sRo[i] = src[i];
-            }
-            ar.ro = sRo - d0 * kRoWords;
-            fence();
-            for (int t = 0; t < a.n; t++) {
-                const int m = a.n - t;
-                // phase 1: two lanes per seat (rows past the group's seats repeat its last)
-#pragma unroll
-                for (int pp = 0; pp < 2; pp++) {
-                    const int part = p0 + 2 * pp;
-                    const SeatIn in = seat_load(ar, N, d0 * N + min(sl, nseat - 1), part);
-                    seat_row_part(in, m, part, sRow + sl * kSeatRowLds, sCard + sl * kHand, sLut);
-                }
-                fence();
-                // phase 2: base[seat][j] = sum_k W1s[j][k] rows[seat][k] (one 32-seat tile)
-                {
-                    // the A fragments (W1s rows 32 mt + col) from L1 / L2 per step: held across phase 3
-                    // they would spill (two waves per SIMD: 256 registers each)
-                    bf16x8_t w1f[4][kSeatRowK / 16];
-#pragma unroll
-                    for (int mt = 0; mt < 4; mt++)
-#pragma unroll
-                        for (int ks = 0; ks < kSeatRowK / 16; ks++)
-                            w1f[mt][ks] = __builtin_bit_cast(
-                                bf16x8_t, *(const uint4*)&w1s[(32 * mt + col) * kSeatRowK + 16 * ks + 8 * half]);
-                    f32x16_t acc[4];
-#pragma unroll
-                    for (int ks = 0; ks < kSeatRowK / 16; ks++) {
-                        const bf16x8_t bfr =
-                            __builtin_bit_cast(bf16x8_t, *(const uint4*)&sRow[col * kSeatRowLds + 16 * ks + 8 * half]);
-                        const f32x16_t zero = {};
-#pragma unroll
-                        for (int mt = 0; mt < 4; mt++)
-                            acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1f[mt][ks], bfr, ks ? acc[mt] : zero, 0, 0, 0);
-                    }
-#pragma unroll
-                    for (int mt = 0; mt < 4; mt++)
-#pragma unroll
-                        for (int rr = 0; rr < 16; rr += 2) {
-                            const int j = 32 * mt + (rr & 3) + 8 * (rr >> 2) + 4 * half;
-                            if (j < kMlpK)
-                                *(uint32_t*)&sBase[col * kBaseLds + j] = pack_bf16(acc[mt][rr], acc[mt][rr + 1]);
-                        }
-                }
-                fence();
-                // phase 3: the group's candidate rows, 64 per tile, logits to LDS (over the dead rows)
-                const uint32_t rows = (uint32_t)nseat * (uint32_t)m;
-                const uint32_t tiles = (rows + 32u * TNT - 1u) / (32u * TNT);
-                for (uint32_t tile = 0; tile < tiles; tile++) {
-                    uint32_t rw[TNT];
-                    float x[TNT];
-                    const uint16_t* brow[TNT];
-#pragma unroll
-                    for (int nt = 0; nt < TNT; nt++) {
-                        rw[nt] = tile * 32u * TNT + 32u * nt + (uint32_t)col;
-                        const uint32_t rc = rw[nt] < rows ? rw[nt] : rows - 1u;
-                        const uint32_t q = rc / (uint32_t)m;
-                        x[nt] = sCard[q * kHand + (rc - q * (uint32_t)m)];
-                        brow[nt] = sBase + q * kBaseLds;
-                    }
-                    float out[TNT];
-                    mlp_tile<TNT>(brow, x, sW, sC, sH2, col, half, out);
-                    if (tile == 0) fence();  // every lane's phase-2 row reads are done before logits land on them
-#pragma unroll
-                    for (int nt = 0; nt < TNT; nt++)
-                        if (half == 0 && rw[nt] < rows) sLogit[rw[nt]] = out[nt];
-                }
-                fence();
-                // the step: L lanes per decision (step_seat, as k_puct_step_seats); lanes past the
-                // group's DG decisions (the upper half of the wave) follow along and write nothing
-                step_seat<N, L>(
-                    s, ar, [&](int64_t dd, int q, int k) { return sLogit[((dd - d0) * N + q) * m + k]; }, t, m,
-                    d0 * L + lane, d0 + nd, d0);
-                fence();
-            }
-        }
-    }
-}
-
 // ---- layer 1 per candidate on MFMA too (sn_puct_mlp_mfma) ------------------
 // k_puct_mlp_seats factors layer 1 into a per-seat MFMA product (base) plus
 // a per-candidate card column built on the VALU: ~9 VALU per MFMA in the
@@ -1281,6 +1139,174 @@ __global__ __launch_bounds__(256, 2) void k_puct_mlp_mfma(PuctArgs a, int N, int
             else run_sub(buf, i - pend_cnt, rows, rbase);
         }
         pend_first = tiles - defer, pend_cnt = defer, pend_rows = rows, pend_rbase = rbase;
+    }
+}
+
+// ---- whole rollouts in one kernel (sn_puct_rollouts) ----------------------
+// Every rollout step of k_puct_mlp_seats + k_puct_step_seats touches one
+// decision's rollout state, its seats' logits and its statistics only, so
+// ONE WAVE can carry a group of 64 / L decisions (their <= 64 seat rows, L
+// lanes per decision) through whole rollouts -- every step of rollouts
+// r0 .. r0 + nr - 1, in order, rollout r's first move chosen by PUCT from
+// the statistics rollouts < r backed up -- with no other wave involved and
+// no barrier: per step the seats' rows (phase 1, a lane per seat), the
+// per-seat layer-1 MFMA (phase 2: 4 output tiles x 2 seat halves x 4
+// k-steps), the candidates' 64-row tiles (phase 3, mlp_tile) into logits in
+// LDS, then step_seat on them.  The same code, the same values as the
+// two-launches-per-step loop.  A workgroup of four waves shares W2 in LDS
+// (one workgroup per CU: four groups in flight per CU, each wave's MFMA
+// chain keeping its SIMD busy), each wave has its own rows / base / cards /
+// logits / rollout states.  (The first form -- a workgroup per group, four
+// barriers per step -- ran 12 us per group-step: two groups in flight per
+// CU, slower than the launch-per-step loop.)  Rollout r's initial states
+// are ro_base + (r - r0) * D * kRoWords (sn_puct_deal_batch dealt them); the
+// wave's copy in LDS is the one the steps read and write.
+constexpr int kRollSeats = 32;  // seats per wave's group (32 / L... 64 / L / 2 decisions)
+constexpr int kRollWaveLds = kRollSeats * kSeatRowLds * 2 + kRollSeats * kBaseLds * 2 + kRollSeats * kHand * 4 +
+                             8 * kRoWords * 4;  // rows (aliased by logits) + base + cards + states: 15 104 B
+
+// MF: layer 1 per candidate row on MFMA as well (mlp2_subtile, w2 = w2q, sn_puct_mlp_mfma's
+// arithmetic; no phase 2, the logits over the unused base rows), else sn_puct_mlp_seats'.
+template <int N, int L, bool MF = false>
+__global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a, int r0, int nr, int32_t* ro_base,
+                                                         const uint16_t* w1s, const float* w1c, const uint16_t* w2,
+                                                         const float* head) {
+    constexpr int TNT = 2;
+    constexpr int kWaves = 512 / 64;  // two per SIMD
+    constexpr int DG = kRollSeats / L;  // decisions per group
+    static_assert(DG <= 8 && DG * N <= kRollSeats, "a group's seats and states fit");
+    constexpr int kWld = MF ? kMlp2Lds : kMlpLdsK, kWk = MF ? kMlp2K : kMlpK;
+    __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kWld];  // W2 [128][120] (w2q [128][136]), shared
+    __shared__ __attribute__((aligned(16))) float sC[kMlpK];
+    __shared__ __attribute__((aligned(16))) uint32_t sH2[kMlpM / 2];
+    __shared__ uint16_t sLut[kLutSize];
+    __shared__ __attribute__((aligned(16))) uint8_t sWave[kWaves][kRollWaveLds];
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63, col = lane & 31, half = lane >> 5;
+    build_row_lut(sLut);
+    for (int i = tid; i < kMlpM * (kWk / 8); i += blockDim.x) {
+        const int o = i / (kWk / 8), c = i - o * (kWk / 8);
+        *(uint4*)&sW[o * kWld + 8 * c] = *(const uint4*)&w2[o * kWk + 8 * c];
+    }
+    if (!MF)
+        for (int i = tid; i < kMlpK; i += blockDim.x) sC[i] = w1c[i];
+    load_head_pairs(head, sH2);
+    __syncthreads();  // the only barrier: the waves run independently from here
+    uint16_t* sRow = (uint16_t*)sWave[wave];                 // [32][72]
+    uint16_t* sBase = sRow + kRollSeats * kSeatRowLds;       // [32][120]
+    // [32 x 10]: over sRow once phase 2 is done with it, or (MF: rows live through phase 3) over the base
+    float* sLogit = MF ? (float*)sBase : (float*)sWave[wave];
+    float* sCard = (float*)(sBase + kRollSeats * kBaseLds);  // [32][10]
+    int32_t* sRo = (int32_t*)(sCard + kRollSeats * kHand);   // [DG][48]
+    const int64_t groups = (a.D + DG - 1) / DG;
+    auto fence = [] { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); };
+    const int sl = lane & (kRollSeats - 1), p0 = lane >> 5;  // phase 1: seat sl, parts p0 and p0 + 2
+    for (int64_t grp = (int64_t)blockIdx.x * kWaves + wave; grp < groups; grp += (int64_t)gridDim.x * kWaves) {
+        const int64_t d0 = grp * DG;
+        const int nd = (int)min<int64_t>(DG, a.D - d0);
+        const int nseat = nd * N;
+        for (int r = r0; r < r0 + nr; r++) {
+            PuctArgs ar = a;
+            ar.rollout = (uint32_t)r;
+            {
+                const int32_t* src = ro_base + ((int64_t)(r - r0) * a.D + d0) * kRoWords;
+                for (int i = lane; i < nd * kRoWords; i += 64) sRo[i] = src[i];
+            }
+            ar.ro = sRo - d0 * kRoWords;
+            fence();
+            for (int t = 0; t < a.n; t++) {
+                const int m = a.n - t;
+                // phase 1: two lanes per seat (rows past the group's seats repeat its last)
+#pragma unroll
+                for (int pp = 0; pp < 2; pp++) {
+                    const int part = p0 + 2 * pp;
+                    const SeatIn in = seat_load(ar, N, d0 * N + min(sl, nseat - 1), part);
+                    seat_row_part(in, m, part, sRow + sl * kSeatRowLds, sCard + sl * kHand, sLut);
+                }
+                fence();
+                if constexpr (MF) {
+                    // layer 1 (per candidate row) + layer 2 + head on MFMA, 32 rows per sub-tile
+                    bf16x8_t w1f[4][4];
+#pragma unroll
+                    for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+                        for (int ks = 0; ks < 4; ks++)
+                            w1f[mt][ks] = __builtin_bit_cast(
+                                bf16x8_t, *(const uint4*)&w1s[(32 * mt + col) * kSeatRowK + 16 * ks + 8 * half]);
+                    const uint32_t rows = (uint32_t)nseat * (uint32_t)m;
+                    for (uint32_t t32 = 0; t32 < (rows + 31u) / 32u; t32++) {
+                        const uint32_t rw = 32u * t32 + (uint32_t)col;
+                        const uint32_t rc = rw < rows ? rw : rows - 1u;
+                        const uint32_t q = rc / (uint32_t)m;
+                        const uint32_t card = __float_as_uint(sCard[q * kHand + (rc - q * (uint32_t)m)]) >> 16;
+                        float out;
+                        mlp2_subtile(w1f, sRow + q * kSeatRowLds, card, sW, sH2, col, half, out);
+                        if (half == 0 && rw < rows) sLogit[rw] = out;
+                    }
+                } else {
+                // phase 2: base[seat][j] = sum_k W1s[j][k] rows[seat][k] (one 32-seat tile)
+                {
+                    // the A fragments (W1s rows 32 mt + col) from L1 / L2 per step: held across phase 3
+                    // they would spill (two waves per SIMD: 256 registers each)
+                    bf16x8_t w1f[4][kSeatRowK / 16];
+#pragma unroll
+                    for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+                        for (int ks = 0; ks < kSeatRowK / 16; ks++)
+                            w1f[mt][ks] = __builtin_bit_cast(
+                                bf16x8_t, *(const uint4*)&w1s[(32 * mt + col) * kSeatRowK + 16 * ks + 8 * half]);
+                    f32x16_t acc[4];
+#pragma unroll
+                    for (int ks = 0; ks < kSeatRowK / 16; ks++) {
+                        const bf16x8_t bfr =
+                            __builtin_bit_cast(bf16x8_t, *(const uint4*)&sRow[col * kSeatRowLds + 16 * ks + 8 * half]);
+                        const f32x16_t zero = {};
+#pragma unroll
+                        for (int mt = 0; mt < 4; mt++)
+                            acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1f[mt][ks], bfr, ks ? acc[mt] : zero, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+                        for (int rr = 0; rr < 16; rr += 2) {
+                            const int j = 32 * mt + (rr & 3) + 8 * (rr >> 2) + 4 * half;
+                            if (j < kMlpK)
+                                *(uint32_t*)&sBase[col * kBaseLds + j] = pack_bf16(acc[mt][rr], acc[mt][rr + 1]);
+                        }
+                }
+                fence();
+                // phase 3: the group's candidate rows, 64 per tile, logits to LDS (over the dead rows)
+                const uint32_t rows = (uint32_t)nseat * (uint32_t)m;
+                const uint32_t tiles = (rows + 32u * TNT - 1u) / (32u * TNT);
+                for (uint32_t tile = 0; tile < tiles; tile++) {
+                    uint32_t rw[TNT];
+                    float x[TNT];
+                    const uint16_t* brow[TNT];
+#pragma unroll
+                    for (int nt = 0; nt < TNT; nt++) {
+                        rw[nt] = tile * 32u * TNT + 32u * nt + (uint32_t)col;
+                        const uint32_t rc = rw[nt] < rows ? rw[nt] : rows - 1u;
+                        const uint32_t q = rc / (uint32_t)m;
+                        x[nt] = sCard[q * kHand + (rc - q * (uint32_t)m)];
+                        brow[nt] = sBase + q * kBaseLds;
+                    }
+                    float out[TNT];
+                    mlp_tile<TNT>(brow, x, sW, sC, sH2, col, half, out);
+                    if (tile == 0) fence();  // every lane's phase-2 row reads are done before logits land on them
+#pragma unroll
+                    for (int nt = 0; nt < TNT; nt++)
+                        if (half == 0 && rw[nt] < rows) sLogit[rw[nt]] = out[nt];
+                }
+                }
+                fence();
+                // the step: L lanes per decision (step_seat, as k_puct_step_seats); lanes past the
+                // group's DG decisions (the upper half of the wave) follow along and write nothing
+                step_seat<N, L>(
+                    s, ar, [&](int64_t dd, int q, int k) { return sLogit[((dd - d0) * N + q) * m + k]; }, t, m,
+                    d0 * L + lane, d0 + nd, d0);
+                fence();
+            }
+        }
     }
 }
 
@@ -1580,13 +1606,26 @@ sn_status sn_puct_mlp_seats(sn_env* e, const sn_puct* q, int n_cur, const void* 
     return SN_OK;
 }
 
+static sn_status puct_rollouts(sn_env* e, const sn_puct* q, int r0, int nr, void* ro_base, const void* w1s,
+                               const float* w1c, const void* w2, const float* head, void* stream, bool mf);
+
 sn_status sn_puct_rollouts(sn_env* e, const sn_puct* q, int r0, int nr, void* ro_base, const void* w1s, const float* w1c,
                            const void* w2, const float* head, void* stream) {
+    return puct_rollouts(e, q, r0, nr, ro_base, w1s, w1c, w2, head, stream, false);
+}
+
+sn_status sn_puct_rollouts_mfma(sn_env* e, const sn_puct* q, int r0, int nr, void* ro_base, const void* w1s,
+                                const void* w2q, const float* head, void* stream) {
+    return puct_rollouts(e, q, r0, nr, ro_base, w1s, nullptr, w2q, head, stream, true);
+}
+
+static sn_status puct_rollouts(sn_env* e, const sn_puct* q, int r0, int nr, void* ro_base, const void* w1s,
+                               const float* w1c, const void* w2, const float* head, void* stream, bool mf) {
     PuctArgs a{};
     sn_status st = puct_args(e, q, a);
     if (st != SN_OK) return st;
     if (r0 < 0 || nr < 1 || !ro_base) return set_error(SN_EINVAL, "need r0 >= 0, nr >= 1 and the dealt states");
-    if (!w1s || !w1c || !w2 || !head) return set_error(SN_EINVAL, "NULL argument");
+    if (!w1s || (!w1c && !mf) || !w2 || !head) return set_error(SN_EINVAL, "NULL argument");
     if ((((uintptr_t)w1s) | ((uintptr_t)w2) | ((uintptr_t)w1c) | ((uintptr_t)head)) & 15)
         return set_error(SN_EINVAL, "w1s / w2 / w1c / head must be 16-B aligned");
     if (e->s.N < 3 || e->s.N > 8) return set_error(SN_EUNSUPPORTED, "sn_puct_rollouts: 3 <= N <= 8");
@@ -1594,9 +1633,15 @@ sn_status sn_puct_rollouts(sn_env* e, const sn_puct* q, int r0, int nr, void* ro
     const int Lw = e->s.N <= 2 ? 2 : e->s.N <= 4 ? 4 : 8;
     const int64_t groups = (a.D + kRollSeats / Lw - 1) / (kRollSeats / Lw);
     const dim3 grid((unsigned)std::min<int64_t>((groups + 7) / 8, (int64_t)e->cus));  // one 8-wave workgroup per CU
-#define SN_ROLLOUTS(NN_, L_)                                                                                      \
-    hipLaunchKernelGGL((k_puct_rollouts<NN_, L_>), grid, dim3(512), 0, s, e->s, a, r0, nr, (int32_t*)ro_base,     \
-                       (const uint16_t*)w1s, w1c, (const uint16_t*)w2, head)
+#define SN_ROLLOUTS(NN_, L_)                                                                                        \
+    do {                                                                                                            \
+        if (mf)                                                                                                     \
+            hipLaunchKernelGGL((k_puct_rollouts<NN_, L_, true>), grid, dim3(512), 0, s, e->s, a, r0, nr,             \
+                               (int32_t*)ro_base, (const uint16_t*)w1s, w1c, (const uint16_t*)w2, head);             \
+        else                                                                                                        \
+            hipLaunchKernelGGL((k_puct_rollouts<NN_, L_, false>), grid, dim3(512), 0, s, e->s, a, r0, nr,            \
+                               (int32_t*)ro_base, (const uint16_t*)w1s, w1c, (const uint16_t*)w2, head);             \
+    } while (0)
     switch (e->s.N) {
         case 3: SN_ROLLOUTS(3, 4); break;
         case 4: SN_ROLLOUTS(4, 4); break;

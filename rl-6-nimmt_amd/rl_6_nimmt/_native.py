@@ -100,6 +100,7 @@ SIGNATURES = {
     "sn_puct_deal": ([_P, _P, _P], _I),
     "sn_puct_deal_batch": ([_P, _P, _I, _I, _P, _P], _I),
     "sn_puct_rollouts": ([_P, _P, _I, _I, _P, _P, _P, _P, _P, _P], _I),
+    "sn_puct_rollouts_mfma": ([_P, _P, _I, _I, _P, _P, _P, _P, _P], _I),
     "sn_puct_rows": ([_P, _P, _I, _P, _I, _P], _I),
     "sn_puct_step": ([_P, _P, _P, _I, _I, _P], _I),
     "sn_puct_seat_cols": ([_P, _P, _I, _P, _I, _P, _I, _P], _I),

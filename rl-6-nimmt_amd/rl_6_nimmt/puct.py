@@ -394,13 +394,18 @@ class BatchedPUCT:
                     wargs = (nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p), nat.ptr(head), nat.ptr(logits), st)
                 lp = nat.ptr(logits)
                 RB, nmc = self.deal_batch, self.n_mc(n)
-                if self.fused_rollouts and self.mlp_layer1 == "seats" and RB > 0 and 3 <= N <= 8:
+                if self.fused_rollouts and RB > 0 and 3 <= N <= 8:
                     rob = self._deal_buf(RB)
+                    w2q = self._net.w2q() if self.mlp_layer1 == "mfma" else None
                     for r0 in range(0, nmc, RB):
                         nr = min(RB, nmc - r0)
                         nat.check(L.sn_puct_deal_batch(h, qr, r0, nr, rob.data_ptr(), st), "sn_puct_deal_batch")
-                        nat.check(L.sn_puct_rollouts(h, qr, r0, nr, rob.data_ptr(), nat.ptr(w1s), nat.ptr(w1c),
-                                                     nat.ptr(w2p), nat.ptr(head), st), "sn_puct_rollouts")
+                        if w2q is not None:
+                            nat.check(L.sn_puct_rollouts_mfma(h, qr, r0, nr, rob.data_ptr(), nat.ptr(w1s), nat.ptr(w2q),
+                                                              nat.ptr(head), st), "sn_puct_rollouts_mfma")
+                        else:
+                            nat.check(L.sn_puct_rollouts(h, qr, r0, nr, rob.data_ptr(), nat.ptr(w1s), nat.ptr(w1c),
+                                                         nat.ptr(w2p), nat.ptr(head), st), "sn_puct_rollouts")
                     self.rows_evaluated += nmc * S * (n * (n + 1) // 2)
                     return
                 if RB > 0:
