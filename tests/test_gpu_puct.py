@@ -751,7 +751,10 @@ def test_fused_rollouts_equal_step_launches(monkeypatch):
     whole PUCT search gives identical statistics, histograms and moves --
     4 players (one 16-decision group per 64 seats) and 3 players (48 live
     seat rows per group), a ragged last group"""
-    for N, B, l1 in ((4, 300, "seats"), (3, 97, "seats")):
+    cases = [(4, 300, "seats"), (3, 97, "seats")]
+    if os.environ.get("SECHS_TEST_MF_ROLLOUTS"):  # sn_puct_rollouts_mfma (opt-in form) vs sn_puct_mlp_mfma + step
+        cases.append((4, 300, "mfma"))
+    for N, B, l1 in cases:
         monkeypatch.setenv("SECHS_MLP_LAYER1", l1)  # "mfma": sn_puct_rollouts_mfma vs sn_puct_mlp_mfma + step
         res = {}
         for rollouts in ("1", "0"):
