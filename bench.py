@@ -57,6 +57,7 @@ ALGO_BYTES_PER_STEP = (33 * N_PLAYERS + 57) + 47 * N_PLAYERS  # 377 B at N = 4
 # run, so the committed summary of the current kernels is reported beside the
 # live timing.
 LIB_TWIST_EVERY = 4  # the library's SN_OPT_TWIST_EVERY default (include/sechs.h)
+SQ_CONFIG4_ROLLOUTS = "profiles/r05_sq_config4_rollouts.json"  # SQ pass of k_puct_rollouts (eager launches)
 PMC_TRAFFIC = {"numpy": os.path.join(ROOT, "profiles", "r05_pmc_traffic_numpy.json"),  # tools/r05_final.sh
                "philox": os.path.join(ROOT, "profiles", "r04_pmc_traffic_philox.json")}
 
@@ -75,14 +76,10 @@ def parse():
     ap.add_argument("--pipe-gpw", type=int, default=64, choices=[32, 64], help="games per k_play wave (pipelined path)")
     ap.add_argument("--play-split", type=int, default=None, choices=[0, 1],
                     help="SN_OPT_PLAY_SPLIT (default: the library's)")
-    ap.add_argument("--play-quad", type=int, default=None, choices=[0, 1],
-                    help="SN_OPT_PLAY_QUAD: four lanes per game, k_play_quad (default: the library's, 0)")
     ap.add_argument("--twist-round", type=int, default=None, choices=[0, 1],
                     help="SN_OPT_TWIST_ROUND: whole-round MT19937 twists in k_mt_ahead (default: the library's, 1)")
     ap.add_argument("--twist-every", type=int, default=None, choices=[1, 2, 3, 4, 5],
                     help="SN_OPT_TWIST_EVERY: one k_mt_ahead per 1 .. 5 play launches (default: the library's)")
-    ap.add_argument("--pipe-fused", type=int, default=None, choices=[0, 1],
-                    help="SN_OPT_PIPE_FUSED: k_play_quad twists the MT rounds itself (default: the library's)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-philox", action="store_true", help="skip the philox-mode leg of config 2")
@@ -402,17 +399,13 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
     wall = time.perf_counter() - t0
     steps = sum(eng.n_mc(n) * n for n in range(2, 11)) * N_PLAYERS * games
     rows_s = eng.rows_evaluated / wall
-    fused = eng.fused_mlp and eng._net is not None and eng._net.fused() is not None
-    seats = fused and eng.mlp_layer1 in ("seats", "mfma")
-    mfma1 = fused and eng.mlp_layer1 == "mfma"  # layer 1 per candidate row on MFMA (sn_puct_mlp_mfma)
-    whole = seats and eng.fused_rollouts and eng.deal_batch > 0  # sn_puct_rollouts(_mfma)
+    fused = eng._net is not None and eng._net.fused() is not None
+    whole = fused and eng.fused_rollouts and eng.deal_batch > 0  # sn_puct_rollouts
     tflops = eng.rows_evaluated * 29800 / wall / 1e12
-    sq4 = None  # SQ counters of the rollout MLP kernel (tools/r04_puct_pmc.sh, eager launches)
+    sq4 = None  # SQ counters of the rollout MLP kernel (eager launches)
     try:
-        if whole and mfma1:
-            raise KeyError("no SQ pass of sn_puct_rollouts_mfma")
-        if whole:  # tools/r05_puct_pmc.sh (eager launches)
-            src = "profiles/r05_sq_config4_rollouts.json"
+        if whole:
+            src = SQ_CONFIG4_ROLLOUTS
             c = json.load(open(os.path.join(ROOT, src)))["void k_puct_rollouts<4, 4>"]
         else:
             src = "profiles/r04_sq_config4_kernels.json"
@@ -423,37 +416,31 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
     except (OSError, KeyError, ValueError, ZeroDivisionError):
         pass
     if fused:
-        # the rollout MLP runs as sn_puct_mlp (one MFMA kernel after a
-        # per-seat PyTorch GEMM): no activation tensor in HBM; priced as the
-        # reference's 29 800 FLOP per candidate row against the dense bf16
-        # MFMA peak, over the whole game's wall time (every kernel included)
+        # the rollout MLP runs in one MFMA kernel: no activation tensor in
+        # HBM; priced as the reference's 29 800 FLOP per candidate row
+        # against the dense bf16 MFMA peak, over the whole game's wall time
+        # (every kernel included)
         roof = {"bound": "mfma", "achieved": tflops, "peak": 2500.0, "unit": "TFLOP/s", "frac": tflops / 2500.0,
                 "traffic": None, "algo_flop_per_row": 29800, "sq": sq4,
-                "kernel": ("whole rollouts = sn_puct_deal_batch (16 rollouts' deals) + sn_puct_rollouts"
-                           + ("_mfma" if mfma1 else "") + " (one wave per group of 8 decisions: every step's seat "
-                           "rows, MFMA layer 1 + 2 and head into logits in LDS, the seat-lane step; two waves per "
-                           "SIMD); whole-game wall time") if whole
-                else ("rollout step = sn_puct_mlp_mfma (MFMA: seat rows, layer 1 per candidate row, layer 2, "
-                           "head in one persistent kernel) + k_puct_step_seats; whole-game wall time") if mfma1
+                "kernel": ("whole rollouts = sn_puct_deal_batch (16 rollouts' deals) + sn_puct_rollouts (one wave "
+                           "per group of 8 decisions: every step's seat rows, MFMA layer 1 + 2 and head into logits "
+                           "in LDS, the seat-lane step; two waves per SIMD); whole-game wall time") if whole
                 else ("rollout step = sn_puct_mlp_seats (MFMA: seat rows, layer 1 per seat, card column, "
-                      "layer 2, head in one persistent kernel) + k_puct_step_seats; whole-game wall time") if seats
-                else ("rollout step = sn_puct_seat_rows + PyTorch GEMM (layer 1, per seat) + sn_puct_mlp (MFMA: "
-                      "card column, layer 2, head) + k_puct_step_seats; whole-game wall time")}
+                      "layer 2, head in one persistent kernel) + k_puct_step_seats; whole-game wall time")}
     else:
-        # the split PyTorch path: hipBLASLt GEMMs per candidate-row batch,
-        # HBM-bound on their bf16 intermediates -- per row 96 B in, 2 x (200 B
-        # out + 200 B back in), 32 B head out = 928 B
+        # any other net: candidate rows + the net's PyTorch-ROCm forward (hipBLASLt GEMMs),
+        # HBM-bound on their bf16 intermediates -- per row 96 B in, 2 x (200 B out + 200 B
+        # back in), 32 B head out = 928 B
         row_bytes = 96 + 2 * (200 + 200) + 32
         roof = {"bound": "hbm", "achieved": rows_s * row_bytes / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": rows_s * row_bytes / 1e9 / HBM_PEAK_GBS, "traffic": None, "algo_bytes_per_row": row_bytes,
                 "mfma_frac": tflops / 2500.0,
-                "kernel": "policy MLP (PyTorch-ROCm hipBLASLt bf16, ReLU fused in the GEMM epilogue), whole game "
-                          "wall time incl. the k_puct_* kernels"}
+                "kernel": "policy MLP (PyTorch-ROCm hipBLASLt bf16), whole game wall time incl. the k_puct_* kernels"}
     return {
         "workload": f"config4: {games} x 4-player games, all seats PUCT (mc_max={mc_max}, mc_per_card={mc_per_card}, "
                     f"c_puct=2), bf16 policy MLP 48-100-100-1 ("
-                    + ("one MFMA kernel per rollout step" if seats else
-                       "layer 1's per-seat part a PyTorch-ROCm GEMM, the rest one MFMA kernel")
+                    + ("whole rollouts in one MFMA kernel" if whole else "one MFMA kernel per rollout step" if fused
+                       else "PyTorch-ROCm GEMMs")
                     + f"), 1 game; each decision's rollout "
                     f"chain replayed from a captured hipGraph",
         "value": steps / wall,
@@ -461,9 +448,8 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
         "decisions_per_s": 9 * N_PLAYERS * games / wall,
         "policy_rows_per_s": rows_s,
         "policy_tflops": tflops,
-        "mlp": "fused, one kernel (sn_puct_mlp_mfma)" if mfma1 else "fused, one kernel (sn_puct_mlp_seats)" if seats
-        else "fused (sn_puct_mlp)" if fused
-        else "split (PyTorch GEMMs)",
+        "mlp": "whole rollouts (sn_puct_rollouts)" if whole else "fused, one kernel (sn_puct_mlp_seats)" if fused
+        else "rows + PyTorch GEMMs",
         "roofline": roof,
         "wall_s": wall,
         "mean_score_per_seat": total.double().mean(dim=0).tolist(),
@@ -869,8 +855,8 @@ def main():
     B = args.games
     env = VecSechsNimmtEnv(B, N_PLAYERS, seed=0, game_offset=rank * B, rng=args.rng)
     if args.rng == "numpy":
-        env.set_option(pipe_gpw=args.pipe_gpw, play_split=args.play_split, play_quad=args.play_quad,
-                       twist_round=args.twist_round, twist_every=args.twist_every, pipe_fused=args.pipe_fused)
+        env.set_option(pipe_gpw=args.pipe_gpw, play_split=args.play_split, 
+                       twist_round=args.twist_round, twist_every=args.twist_every)
     env.reset()
     out = make_out(env, B, not args.no_obs)
     wall, kern_ms, kt = time_rollouts(env, out, args.steps, args.warmup, world)

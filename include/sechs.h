@@ -158,11 +158,8 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          1 (default) or 0 (never).  Measured (65 536 x 4p):
                          74 -> 59 us per 10 env-steps.  Numpy-compat handles
                          always use the pipelined one-wave k_play.
-     SN_OPT_PLAY_QUAD    1: pipelined numpy-compat DrunkHamster rollouts of
-                         a 4-player handle (no tournament, obs rows of 48
-                         bytes or none) run k_play_quad, four lanes per game;
-                         0 (default): the one-lane k_play.  Same words, same
-                         outputs (the GPU tests run both).
+     SN_OPT_PLAY_QUAD    removed (round 6): k_play_quad, four lanes per game,
+                         measured slower; SN_EUNSUPPORTED.
      SN_OPT_TWIST_ROUND  1 (default): the pipelined twist-ahead k_mt_ahead
                          twists whole MT19937 rounds (each old word read
                          once, each new word written once: 8 instead of 12
@@ -175,19 +172,19 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          the twist of the group before only -- per group one
                          cross-stream wait and one record instead of one per
                          launch.
-     SN_OPT_PIPE_FUSED   1: pipelined numpy-compat rollouts that qualify for
-                         k_play_quad (and B a multiple of 16) run it with the
-                         twist folded in: each launch twists one whole round
-                         of every game whose lead is short, for the launches
-                         after it (no side stream, no cross-queue waits);
-                         0 (default): k_mt_ahead beside the play launches.
-                         Same words, same outputs.
+     SN_OPT_PIPE_FUSED   removed (round 6): the twist folded into k_play_quad,
+                         measured slower; SN_EUNSUPPORTED.
+     SN_OPT_TWIST_SKIP   TEST KNOB: 1 = every steady twist after the first
+                         group's twists nothing, so the default schedule
+                         runs its ring dry (the SN_ERNG / sn_pipe_errors
+                         path); 0 (default): off.
    A pipelined (numpy-compat) rollout records its ordering event on the
-   caller's stream before it returns; later calls only wait on that event,
-   so the caller may destroy the stream after the call. */
+   caller's stream before it returns; every later call waits on that event
+   (also on the same stream), so the caller may destroy the stream after
+   the call. */
 enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3, SN_OPT_TIMING = 4, SN_OPT_PIPE_GPW = 5,
        SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7, SN_OPT_PLAY_QUAD = 8, SN_OPT_TWIST_ROUND = 9,
-       SN_OPT_TWIST_EVERY = 10, SN_OPT_PIPE_FUSED = 11 };
+       SN_OPT_TWIST_EVERY = 10, SN_OPT_PIPE_FUSED = 11, SN_OPT_TWIST_SKIP = 12 };
 sn_status sn_set_option(sn_env* env, int option, int value);
 /* pipelined rollouts whose draws ran past the twisted words (must be 0; a
    nonzero count means those games' draws are wrong) [sync].  The count is
@@ -411,64 +408,25 @@ sn_status sn_puct_deal_batch(sn_env* env, const sn_puct* q, int r0, int nr, void
    <= 8; weights as sn_puct_mlp_seats). */
 sn_status sn_puct_rollouts(sn_env* env, const sn_puct* q, int r0, int nr, void* ro_base, const void* w1s,
                            const float* w1c, const void* w2, const float* head, void* stream);
-/* The same with layer 1 per candidate row on MFMA (sn_puct_mlp_mfma's arithmetic; w2q as there). */
-sn_status sn_puct_rollouts_mfma(sn_env* env, const sn_puct* q, int r0, int nr, void* ro_base, const void* w1s,
-                                const void* w2q, const float* head, void* stream);
 sn_status sn_puct_rows(sn_env* env, const sn_puct* q, int n_cur, void* rows, int bf16, void* stream);
 sn_status sn_puct_step(sn_env* env, const sn_puct* q, const float* logits, int t, int n_cur, void* stream);
-/* Layer-1 split of the rollout MLP (MultiHeadedMLP 48 -> H -> ...), in
-   feature-major activations ([features][columns], so the caller's GEMMs run
-   as W . h^T): a candidate row is [card, obs] with obs shared by the seat's
-   n_cur candidates, so
-     sn_puct_seat_cols  cols [ks][D*N] (bf16 or f32) = [0 (card slot), obs (47),
-                        1 (bias feature), 0 ...] per rollout seat (ks >= 49), and
-                        cards [D*N*n_cur] f32 = the candidates' normalised cards
-                        (rounded to the column dtype, as a row would hold them)
-     (caller, PyTorch)  baseT [H][D*N] = [W1 | b1 | 0] @ cols
-     sn_puct_h1_cols    h1T [kp][D*N*n_cur]: relu(baseT[j][seat] + card * w1c[j])
-                        for j < H (w1c = W1[:, 0] f32), 1 at j = H (the next
-                        layer's bias feature), 0 up to kp
-   replaces sn_puct_rows + the first GEMM over the D*N*n_cur candidate rows. */
-sn_status sn_puct_seat_cols(sn_env* env, const sn_puct* q, int n_cur, void* cols, int ks, float* cards, int bf16,
-                            void* stream);
-sn_status sn_puct_h1_cols(sn_env* env, const sn_puct* q, int n_cur, const void* baseT, int hidden, const float* w1c,
-                          const float* cards, void* h1T, int kp, int bf16, void* stream);
-/* Fused rollout MLP (replaces sn_puct_h1_cols + the PyTorch GEMMs of the
-   later layer and the head for MultiHeadedMLP(48, (H, H2), (1,)), H <= 111,
-   H2 <= 127 -- the reference's policy net, utils/nets.py:100-132, evaluated
-   in mcts.py:219-228):
-     sn_puct_seat_rows  rows [D*N][ks] bf16: seat-major form of sn_puct_seat_cols
-                        (same features, same cards output)
-     (caller, PyTorch)  base [D*N][ldb] bf16 = rows @ W1t (W1t [ks][ldb]: the
-                        transposed [W1 | b1 | 0] in columns < H, 1 at (48, H): the
-                        ones feature; ldb >= 112)
-     sn_puct_mlp        logits [D*N*n_cur] f32 (packed, for sn_puct_step with
-                        logit_stride 1, logit_bf16 0) = head . relu(w2 . h1),
-                        h1[k] = bf16(relu(base[seat][k] + card * w1c[k])) for k < 112,
-                        w2 [128][112] bf16 = [W2 | b2 | 0] rows (the row after the
-                        last output: the ones pass-through), head [128] f32 = [wh |
-                        bh | 0]: one v_mfma_f32_32x32x16_bf16 kernel, no activation
-                        in HBM.  base, w2, w1c, head 16-B aligned. */
-sn_status sn_puct_seat_rows(sn_env* env, const sn_puct* q, int n_cur, void* rows, int ks, float* cards, void* stream);
-sn_status sn_puct_mlp(sn_env* env, const sn_puct* q, int n_cur, const void* base, int ldb, const float* w1c,
-                      const float* cards, const void* w2, const float* head, float* logits, void* stream);
-/* The same logits with layer 1's per-seat part inside too: persistent
+/* Rollout MLP in one kernel per rollout step, for MultiHeadedMLP(48, (H, H2),
+   (1,)) in bf16, H <= 111, H2 <= 127 -- the reference's policy net,
+   utils/nets.py:100-132, evaluated in mcts.py:219-228: persistent
    workgroups loop over groups of 64 rollout seats, build their [0, obs, 1]
-   rows in LDS, multiply them by w1s [128][64] bf16 (the [W1 | b1 | 0] rows,
-   the ones feature's row H) on MFMA, then run sn_puct_mlp's tile loop over
-   the seats' candidate rows -- one launch per rollout step instead of
-   sn_puct_seat_rows + a GEMM + sn_puct_mlp. */
+   rows in LDS (the card slot 0), multiply them by w1s [128][64] bf16 (the
+   [W1 | b1 | 0] rows, 1 at (H, 48): the ones feature) on MFMA into base,
+   then per candidate row h1[k] = bf16(relu(base[seat][k] + card * w1c[k]))
+   (w1c = W1[:, 0] f32, 112 entries), layer 2 against w2 [128][112] bf16 =
+   [W2 | b2 | 0] rows (+ the ones pass-through row H2), ReLU + bf16, and the
+   head [128] f32 = [wh | bh | 0]: logits [D*N*n_cur] f32, packed, for
+   sn_puct_step (logit_stride 1, logit_bf16 0).  No activation reaches HBM.
+   w1s, w1c, w2, head 16-B aligned.  (The round-4 GEMM form -- seat rows, a
+   PyTorch GEMM, a tile kernel -- the round-3 feature-major split and the
+   round-5 per-candidate MFMA layer 1 measured slower and were removed in
+   round 6; other nets take sn_puct_rows + the module's own forward.) */
 sn_status sn_puct_mlp_seats(sn_env* env, const sn_puct* q, int n_cur, const void* w1s, const float* w1c, const void* w2,
                             const float* head, float* logits, void* stream);
-/* The same logits with layer 1 per candidate row on the matrix cores too
-   (round 5): [card, obs, 1] x w1s on MFMA, ReLU + bf16 once, layer 2 against
-   w2q [128][128] bf16 = the [W2 | b2 | 0] rows (+ ones pass-through row) with
-   the columns permuted to the MFMA accumulator layout (k = 16 ks + 8 h + j
-   reads layer-1 output 32 (ks >> 1) + 16 (ks & 1) + 8 (j >> 2) + 4 h +
-   (j & 3); FusedMLP.fused builds it), head as sn_puct_mlp.  One launch per
-   rollout step; no VALU layer-1 column.  w1s, w2q, head 16-B aligned. */
-sn_status sn_puct_mlp_mfma(sn_env* env, const sn_puct* q, int n_cur, const void* w1s, const void* w2q, const float* head,
-                           float* logits, void* stream);
 /* best_index [D] (optional): index of the chosen card in the root legal list */
 sn_status sn_puct_choose(sn_env* env, const sn_puct* q, int32_t* actions, int32_t* best_index, void* stream);
 /* PUCTCustomedAgent (agents/mcts.py:325-451, replaces _mcts /

@@ -264,11 +264,10 @@ struct AheadArgs {
     int tout;  // ptend parity written
     int lead;  // words to keep twisted past the consumer (kPipeLead; smaller only to test the overrun path)
     uint32_t* perr_mirror;  // host-mapped copy of *perr, refreshed at launch start (off the play stream)
-    int complete;  // ROUND: always complete a partly twisted round (SN_OPT_PIPE_FUSED's start: whole rounds after)
 };
 
 // One whole MT19937 round of game G, twisted by the whole wave in LDS (w:
-// 624 words; k_mt_ahead's whole-round twists, k_play_quad's fused ones), its
+// 624 words; k_mt_ahead's whole-round twists), its
 // tempered low bytes to the ring at stream positions te .. te + 623 (te is
 // 8-aligned: rounds are 624 = 78 x 8 words).  numpy's in-place order in
 // three dependency-free phases: words 0..226 read old words only (mt[i+1],
@@ -297,7 +296,7 @@ __device__ __forceinline__ void mt_round_to_lds(uint32_t lane, uint32_t* w, cons
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
-// w holds the round's old words (mt_round_to_lds, or k_play_quad's LDS-DMA)
+// w holds the round's old words (mt_round_to_lds)
 __device__ __forceinline__ uint32_t mt_twist_round(const DevState& s, int64_t G, uint32_t lane, uint32_t* w,
                                                      uint32_t te) {
     constexpr uint32_t D = kMtN - kMtM;  // 227
@@ -415,7 +414,7 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
     if (lead < 0 && lane == 0u) atomicAdd(s.perr, 1u);
     const uint32_t T0 = (Tp == (uint32_t)kMtN) ? 0u : Tp;
     // ROUND: the words completing the current round (none at a round boundary)
-    const uint32_t n = ROUND ? ((lead >= 0 && (a.complete || lead < a.lead) && T0 != 0u) ? (uint32_t)kMtN - T0 : 0u)
+    const uint32_t n = ROUND ? ((lead >= 0 && lead < a.lead && T0 != 0u) ? (uint32_t)kMtN - T0 : 0u)
                              : ((lead >= 0 && lead < a.lead) ? (((uint32_t)(a.lead - lead)) & ~7u) : 0u);
     auto ring_dword = [&](uint32_t j, uint32_t v) {  // t0 is 8-aligned: lanes 4m..4m+3 share one dword
         const uint32_t y = mt_temper(v) & 0xFFu;
@@ -634,12 +633,6 @@ struct PlayArgs {
     int32_t* league_rec;     // league: [episodes][B][1 + N] per finished game: seats word, results
     int step0;               // league: env-steps of this rollout before this launch (episode index of a record)
     int n0;                  // k_play_split: every game's hand size at the launch's start (aligned handle)
-    int dbg;                 // k_play_quad diagnostics (SECHS_QUAD_DBG; 0 in normal use): bit 0 plain stores for
-                             // rewards / actions / done, bit 1 skip them, bit 2 skip the game-state stores
-    int fuse_lead;           // k_play_quad, SN_OPT_PIPE_FUSED: > 0 = the launch itself twists one whole round of
-                             // every game whose twisted lead is below this many words (no side stream)
-    int pipe_tout;           // ... and writes the twisted end to this ptend parity
-    uint32_t* perr_mirror;   // ... and publishes *perr to this host-mapped word at its start
 };
 
 // The env-step loop of one lane (game g).  R supplies the random words
@@ -915,8 +908,6 @@ __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
     play_body<N, MODE, GPW, LG>(s, a, lds_dyn, (int)threadIdx.x);
 }
 
-#include "sechs_quad.h"
-
 // ---- one-game fast path (the scalar drop-in SechsNimmtEnv, B == 1) -------
 // One launch per env.step / env.reset: the actions arrive as kernel
 // arguments, the results (invalid seat, done, rewards, scores, int8 obs rows)
@@ -980,6 +971,9 @@ __global__ void k_step1(DevState s, Acts1 acts, uint32_t* hb, int summ) {
         store_game<N>(s, 0, G);
 #pragma unroll
         for (int p = 0; p < N; p++) out[kH1Trace + p] = trace[p];
+    } else {  // nothing played: the trace words are 0 (sechs.h), not the previous step's
+#pragma unroll
+        for (int p = 0; p < N; p++) out[kH1Trace + p] = 0u;
     }
     out[0] = (uint32_t)bad;
     out[1] = (G.n == 0u) ? 1u : 0u;
@@ -1484,8 +1478,6 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
         const char* te = getenv("SECHS_TWIST_EVERY");  // default override (A/B runs of whole legs)
         if (te && atoi(te) >= 1 && atoi(te) <= 5) e->twist_every = atoi(te);
     }
-    e->pipe_fused = 0;  // measured slower: the twist's latency lands inside the play waves
-    e->play_quad = 0;  // measured: k_play_quad alone is no faster and slows the concurrent twist
     {
         const char* ps = getenv("SECHS_PIPE_SERIAL");
         e->pipe_serial = (ps && ps[0] == '1') ? 1 : 0;
@@ -1626,12 +1618,11 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
             e->twist_round = value;
             return SN_OK;
         case SN_OPT_PLAY_QUAD:
-            if (value < 0 || value > 1) return fail(SN_EINVAL, "play quad must be 0 or 1");
-            e->play_quad = value;
-            return SN_OK;
-        case SN_OPT_PIPE_FUSED:
-            if (value < 0 || value > 1) return fail(SN_EINVAL, "pipe fused must be 0 or 1");
-            e->pipe_fused = value;
+        case SN_OPT_PIPE_FUSED:  // round-5 experiments, measured slower and removed
+            return fail(SN_EUNSUPPORTED, "option removed (k_play_quad / the fused twist measured slower)");
+        case SN_OPT_TWIST_SKIP:
+            if (value < 0 || value > 1) return fail(SN_EINVAL, "twist skip must be 0 or 1");
+            e->twist_skip = value;
             return SN_OK;
         case SN_OPT_PIPE_LEAD:
             if (value < 64 || value > kPipeLead) return fail(SN_EINVAL, "pipe lead must be in 64..600");
@@ -1872,41 +1863,39 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     a.vec_out = ((((uintptr_t)a.rewards) & 15) == 0) && ((((uintptr_t)a.actions_out) & 3) == 0);
     const dim3 pg((unsigned)((s.B + kBlock / 64 - 1) / (kBlock / 64)));
     const int64_t B = s.B, N = s.N;
-    // four lanes per game (k_play_quad): N = 4 DrunkHamster seats, 48-byte
-    // 16-B aligned obs rows (or none); anything else keeps k_play
-    const bool quad_ok = gpw == 64 && N == 4 && !s.lg_K && !a.actions && !a.invalid &&
-                         (!a.obs || (a.obs_stride == 48 && (((uintptr_t)a.obs) & 15) == 0));
-    // SN_OPT_PIPE_FUSED: k_play_quad twists whole rounds itself (whole waves of games)
-    const bool fused = e->pipe_fused && quad_ok && (B % kQuadGames) == 0;
-    const bool quad = fused || (e->play_quad && quad_ok);
     // SN_OPT_TWIST_EVERY = K: play launches in groups of K; beside the first
     // launch p of group G runs twist G, leading the consumer position of
     // launch p-1 by 600 K words -- the 2K launches p .. p+2K-1, i.e. K
     // launch pairs of the §4 tail bound -- and launch p waits for twist G-1
     // only, which had a whole group of launches to finish.  Per group, one
     // record and one wait on the caller's stream (K = 1: the launch before).
-    // Slots: pabsc by launch index mod 4, ptend by group parity (INIT =
-    // launch -1 / twist -1).  The ring holds the lead + a round for K <= 5
-    // (3 623 words), and mt0 the five word-0 crossings that span.
-    const int K = fused ? 1 : e->twist_every;
-    const bool round_tw = fused || e->twist_round;
-    if (e->pvalid && ((e->pfused != 0) != fused || e->pK != K)) {  // restart in the other form
+    // Slots: pabsc by launch index mod kPipeSlots (8 >= K + 3: the next writer
+    // of launch p-1's slot is launch p+7, in group G+1 or later, which is
+    // ordered behind twist G -- the reader of that slot), ptend by group
+    // parity (INIT = launch -1 / twist -1).  The ring holds the lead + a round
+    // for K <= 5 (3 623 words), and mt0 the five word-0 crossings that span.
+    const int K = e->twist_every;
+    const bool round_tw = e->twist_round;
+    if (e->pvalid && e->pK != K) {  // restart with the other group size
         const sn_status r = sn_pipe_sync(e, st);
         if (r != SN_OK) return r;
     }
     const int lead = e->pipe_lead * K;
+    constexpr uint32_t kSlotMask = (uint32_t)kPipeSlots - 1u;
     if (!e->pvalid) {  // start the pipeline from mt_pos: twist the lead ahead, synchronously
-        // fused: complete a partly twisted round, so that the play launches twist whole rounds only
-        const AheadArgs aa{3, 0, 1, lead, e->perr_host_dev, fused ? 1 : 0};
-        e->tw_out = 1, e->pl_cout = 3, e->pphase = 0;
+        const AheadArgs aa{(int)kSlotMask, 0, 1, lead, e->perr_host_dev};
+        e->tw_out = 1, e->pl_cout = (int)kSlotMask, e->pphase = 0;
         if (round_tw) hipLaunchKernelGGL((k_mt_ahead<true, true>), pg, dim3(kBlock), 0, st, s, aa);
         else hipLaunchKernelGGL((k_mt_ahead<true, false>), pg, dim3(kBlock), 0, st, s, aa);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(e->ev_prep, st));
         e->pvalid = 1;
-        e->pfused = fused ? 1 : 0;
         e->pK = K;
-    } else if (st != e->play_st) {  // another caller stream: order behind the last pipelined k_play
+    } else {
+        // order behind the last pipelined k_play (recorded on the stream of
+        // that call): always, also on the same stream -- a stream handle's
+        // value may be reused by a new stream once the caller destroyed the
+        // old one, and a wait on an event already behind costs ~nothing
         HIP_TRY(hipStreamWaitEvent(st, e->ev_play, 0));
     }
     // a tournament game adds its seat draw (<= K - 1 + 1 draws): 10-step
@@ -1915,15 +1904,6 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     const int chunk = min(e->chunk_steps, (s.lg_K > 8) ? 5 : pipe_max_chunk(s.N));
     const unsigned nblk = (gpw == 32) ? (unsigned)((s.B + 32 * (kBlock / 64) - 1) / (32 * (kBlock / 64)))
                                       : (unsigned)grid_for(s.B);
-    {
-        const char* qd = getenv("SECHS_QUAD_DBG");  // timing diagnostics only: bits 1, 2 invalidate the results
-        a.dbg = qd ? atoi(qd) : 0;
-    }
-    a.fuse_lead = fused ? lead : 0;
-    a.perr_mirror = e->perr_host_dev;
-    const size_t qshmem = (size_t)kQuadWave * (kBlock / 64);
-    const unsigned qblk = (unsigned)((s.B + kQuadGames * (kBlock / 64) - 1) / (kQuadGames * (kBlock / 64)));
-    if (quad) HIP_TRY(hipFuncSetAttribute((const void*)k_play_quad, hipFuncAttributeMaxDynamicSharedMemorySize, (int)qshmem));
     for (int t0 = 0; t0 < a.steps; t0 += chunk) {
         PlayArgs c = a;
         c.steps = min(chunk, a.steps - t0);
@@ -1933,21 +1913,7 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         if (a.actions_out) c.actions_out = a.actions_out + (int64_t)t0 * B * N;
         if (a.obs) c.obs = a.obs + (int64_t)t0 * B * N * a.obs_stride;
         const uint64_t p = e->pphase;
-        c.pipe_cin = (int)((p + 3u) & 3u), c.pipe_cout = (int)(p & 3u);
-        if (fused) {  // one launch on the caller's stream: it twists the rounds its successors read
-            c.pipe_t = (int)((p + 1u) & 1u), c.pipe_tout = (int)(p & 1u);
-            if (e->tn < e->tcap) e->tev_tw[e->tn] = 0;
-            hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
-            if (tv) HIP_TRY(hipEventRecord(tv[0], st));
-            hipLaunchKernelGGL(k_play_quad, dim3(qblk), dim3(kBlock), qshmem, st, s, c);
-            HIP_TRY(hipGetLastError());
-            if (tv) HIP_TRY(hipEventRecord(tv[1], st));
-            e->tw_out = c.pipe_tout;
-            e->pl_cout = c.pipe_cout;
-            e->pcount++;
-            e->pphase++;
-            continue;
-        }
+        c.pipe_cin = (int)((p + kSlotMask) & kSlotMask), c.pipe_cout = (int)(p & kSlotMask);
         const uint64_t G = p / (uint64_t)K;
         const bool first = (p % (uint64_t)K) == 0u;  // twist G beside this launch
         c.pipe_t = (int)((G + 1u) & 1u);              // twist G-1's end (INIT's for group 0)
@@ -1956,10 +1922,7 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         if (e->tn < e->tcap) e->tev_tw[e->tn] = first ? 1 : 0;
         hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
         if (tv) HIP_TRY(hipEventRecord(tv[0], st));
-        if (quad) {
-            hipLaunchKernelGGL(k_play_quad, dim3(qblk), dim3(kBlock), qshmem, st, s, c);
-            HIP_TRY(hipGetLastError());
-        } else {
+        {
             const sn_status r = pipe_play(s, c, gpw, nblk, shmem, st);
             if (r != SN_OK) return r;
         }
@@ -1969,7 +1932,9 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
             if (e->pipe_serial) HIP_TRY(hipEventRecord(e->ev_main, st));
             HIP_TRY(hipStreamWaitEvent(e->side, e->ev_main, 0));
             if (tv) HIP_TRY(hipEventRecord(tv[2], e->side));
-            const AheadArgs aa{c.pipe_cin, c.pipe_t, (int)(G & 1u), lead, e->perr_host_dev};
+            // SN_OPT_TWIST_SKIP (tests only): the overrun detector under the default schedule
+            const AheadArgs aa{c.pipe_cin, c.pipe_t, (int)(G & 1u), (e->twist_skip && G >= 1u) ? 0 : lead,
+                               e->perr_host_dev};
             if (round_tw) hipLaunchKernelGGL((k_mt_ahead<false, true>), pg, dim3(kBlock), 0, e->side, s, aa);
             else hipLaunchKernelGGL((k_mt_ahead<false, false>), pg, dim3(kBlock), 0, e->side, s, aa);
             HIP_TRY(hipGetLastError());
@@ -1986,7 +1951,6 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     // the next call (or sn_pipe_sync) orders behind it without touching a
     // stream the caller may have destroyed since (one record per rollout)
     HIP_TRY(hipEventRecord(e->ev_play, st));
-    e->play_st = st;
     return SN_OK;
 }
 

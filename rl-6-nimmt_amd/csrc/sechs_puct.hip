@@ -242,127 +242,6 @@ __global__ void k_puct_rows(PuctArgs a, int N, int n_cur, T* rows) {
     write_row<T>(rows + i * kRowLen, hand_get(h, (uint32_t)k), h, kp, ro_board(ro));
 }
 
-// Layer-1 split of the rollout rows, feature-major.  A candidate row is
-// [card, obs]: the observation part is the same for every candidate of a
-// seat, so layer 1 (MultiHeadedMLP's first Linear, 48 -> H) is W1[:, 1:] obs
-// + b1 once per seat (the caller's GEMM over the D*N seat columns) plus the
-// card column W1[:, 0] * card per candidate (k_puct_h1_cols, with the ReLU):
-// no GEMM over the D*N*n_cur candidate rows, and those rows are never
-// written.  Activations are feature-major ([features][rows]: the GEMMs run as
-// W . h^T, which hipBLASLt handles ~1.6x faster than h . W^T at these skinny
-// shapes) with a ones feature after the last real one, so every bias rides
-// in its layer's GEMM as a weight column and the ReLU in its epilogue.
-template <typename T>
-__device__ __forceinline__ float round_to(float v) { return v; }
-template <>
-__device__ __forceinline__ float round_to<__hip_bfloat16>(float v) { return __bfloat162float(__float2bfloat16(v)); }
-
-// seat column i = [0 (the card slot), obs (47)] normalised, 1 (bias), 0 pad
-// to ks features; cards[(i * n_cur) + k] = candidate k's normalised card
-// seat_major: column i is row i of a [S][ks] matrix instead (sn_puct_seat_rows)
-template <typename T>
-__global__ void k_puct_seat_cols(PuctArgs a, int N, int n_cur, T* cols, int ks, float* cards, int seat_major) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t S0 = a.D * N;
-    if (i >= S0) return;
-    const int64_t S = seat_major ? 1 : S0;  // stride between features
-    const int64_t d = i / N;
-    const int q = (int)(i - d * N);
-    const int32_t* ro = a.ro + d * kRoWords;
-    int kp = N;
-    if (a.lgs) {
-        int64_t g;
-        int p;
-        dec_to_gp(a, d, g, p);
-        kp = players_of(a, g);
-    }
-    T* c = cols + (seat_major ? i * ks : i);
-    if (q >= kp) {  // an absent seat of a smaller tournament game (its logits are never read)
-        for (int f = 0; f < ks; f++) c[f * S] = to_out<T>(f == kRowLen ? 1.f : 0.f);
-        for (int k = 0; k < n_cur; k++) cards[i * n_cur + k] = 0.f;
-        return;
-    }
-    const Hand h = ro_hand(ro, q);
-    write_row<T>(c, 0u, h, kp, ro_board(ro), S);
-    c[0] = to_out<T>(0.f);  // the card slot: k_puct_h1_cols
-    c[kRowLen * S] = to_out<T>(1.f);
-    for (int f = kRowLen + 1; f < ks; f++) c[f * S] = to_out<T>(0.f);
-    for (int k = 0; k < n_cur; k++)  // the card feature as the row would hold it (T-rounded)
-        cards[i * n_cur + k] = round_to<T>(nrm((float)hand_get(h, (uint32_t)k), 0.f, 103.f));
-}
-
-// h1T[j][r] = relu(baseT[j][r / n_cur] + cards[r] * w1c[j]) for j < H, 1 at
-// j = H (the next layer's bias feature), 0 up to kp; four rows per thread
-// (one 8-B store per feature in bf16) when R % 4 == 0
-template <typename T>
-__global__ __launch_bounds__(256) void k_puct_h1_cols4(uint32_t R, uint32_t S, int H, int kp, int n_cur, const T* baseT,
-                                                       const float* cards, const float* w1c, T* h1T, int fch) {
-    const uint32_t r = 4u * (blockIdx.x * blockDim.x + threadIdx.x);
-    if (r >= R) return;
-    const int j0 = (int)blockIdx.y * fch, j1 = min(kp, j0 + fch);  // this block's feature slice
-    uint32_t sd[4];
-    float x[4];
-#pragma unroll
-    for (int u = 0; u < 4; u++) sd[u] = (r + u) / (uint32_t)n_cur, x[u] = cards[r + u];
-#pragma unroll 4
-    for (int j = j0; j < j1; j++) {
-        float v[4];
-        if (j < H) {
-            const float w = w1c[j];
-            const T* bj = baseT + (size_t)j * S;
-#pragma unroll
-            for (int u = 0; u < 4; u++) v[u] = fmaxf((float)bj[sd[u]] + x[u] * w, 0.f);
-        } else {
-#pragma unroll
-            for (int u = 0; u < 4; u++) v[u] = (j == H) ? 1.f : 0.f;
-        }
-        T* o = h1T + (size_t)j * R + r;
-        if constexpr (sizeof(T) == 2) {
-            uint16_t hb[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const __hip_bfloat16 b = __float2bfloat16(v[u]);
-                hb[u] = *(const uint16_t*)&b;
-            }
-            *(uint2*)o = make_uint2((uint32_t)hb[0] | ((uint32_t)hb[1] << 16), (uint32_t)hb[2] | ((uint32_t)hb[3] << 16));
-        } else {
-            *(float4*)o = make_float4(v[0], v[1], v[2], v[3]);
-        }
-    }
-}
-
-// the general form: two rows per thread
-template <typename T>
-__global__ __launch_bounds__(256) void k_puct_h1_cols(uint32_t R, uint32_t S, int H, int kp, int n_cur, const T* baseT,
-                                                      const float* cards, const float* w1c, T* h1T, int fch) {
-    const uint32_t r = 2u * (blockIdx.x * blockDim.x + threadIdx.x);
-    if (r >= R) return;
-    const int j0 = (int)blockIdx.y * fch, j1 = min(kp, j0 + fch);
-    const bool two = r + 1u < R;
-    const uint32_t s0 = r / (uint32_t)n_cur, s1 = (r + 1u) / (uint32_t)n_cur;
-    const float x0 = cards[r], x1 = two ? cards[r + 1u] : 0.f;
-    const bool pack = (sizeof(T) == 2) && ((R & 1u) == 0u);  // 4-B aligned row pairs
-#pragma unroll 4
-    for (int j = j0; j < j1; j++) {
-        float v0, v1;
-        if (j < H) {
-            const float w = w1c[j];
-            v0 = fmaxf((float)baseT[(size_t)j * S + s0] + x0 * w, 0.f);
-            v1 = fmaxf((float)baseT[(size_t)j * S + s1] + x1 * w, 0.f);
-        } else {
-            v0 = v1 = (j == H) ? 1.f : 0.f;
-        }
-        T* o = h1T + (size_t)j * R + r;
-        if (pack) {
-            const __hip_bfloat16 b0 = __float2bfloat16(v0), b1 = __float2bfloat16(v1);
-            *(uint32_t*)o = (uint32_t)*(const uint16_t*)&b0 | ((uint32_t)*(const uint16_t*)&b1 << 16);
-        } else {
-            o[0] = to_out<T>(v0);
-            if (two) o[1] = to_out<T>(v1);
-        }
-    }
-}
-
 // ---------------------------------------------------------------- fused rollout MLP
 // The rollout policy net MultiHeadedMLP(48, (H, H2), (1,)) (utils/nets.py:100-132)
 // per candidate row r = [card, obs of its seat]:
@@ -370,11 +249,11 @@ __global__ __launch_bounds__(256) void k_puct_h1_cols(uint32_t R, uint32_t S, in
 //   h2  = relu(W2 h1 + b2)                          (layer 2)
 //   out = wh . h2 + bh                              (head: the policy logit)
 // The obs part of layer 1 is shared by a seat's candidates: base[seat] =
-// W1[:, 1:] obs + b1 comes from one PyTorch GEMM over the seats
-// (sn_puct_seat_rows + torch.mm), and k_puct_mlp does the rest for a tile of
-// 64 rows per wave in registers: h1[k][r] = relu(base[seat(r)][k] + card(r) *
-// w1c[k]) built straight into the B fragments of v_mfma_f32_32x32x16_bf16
-// (bf16, as k_puct_h1_cols rounds it), layer 2 as 4 x 7 MFMA tiles per 32
+// W1[:, 1:] obs + b1 once per seat (phase 2 of k_puct_mlp_seats, MFMA), and
+// mlp_tile does the rest for a tile of 64 rows per wave in registers:
+// h1[k][r] = relu(base[seat(r)][k] + card(r) * w1c[k]) built straight into
+// the B fragments of v_mfma_f32_32x32x16_bf16 (bf16, the rounding of the
+// reference-shaped PyTorch split path), layer 2 as 4 x 7 MFMA tiles per 32
 // rows against W2 staged in LDS (bias b2 = the column against the ones
 // feature h1[H] = 1), ReLU + bf16 rounding (the layer's output dtype in the
 // PyTorch path), then the head as a dot with wh over each lane's 16
@@ -488,41 +367,6 @@ __device__ __forceinline__ void mlp_tile(const uint16_t* const (&brow)[NT], cons
 // the head as bf16 pairs in LDS (its values are bf16 weights: exact)
 __device__ __forceinline__ void load_head_pairs(const float* head, uint32_t* sH2) {
     for (int i = threadIdx.x; i < kMlpM / 2; i += blockDim.x) sH2[i] = pack_bf16(head[2 * i], head[2 * i + 1]);
-}
-
-__global__ __launch_bounds__(256, 2) void k_puct_mlp(uint32_t R, int n_cur, const uint16_t* base, int ldb,
-                                                    const float* w1c, const float* cards, const uint16_t* w2,
-                                                    const float* head, float* logits) {
-    __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kMlpLdsK];
-    __shared__ __attribute__((aligned(16))) float sC[kMlpK];
-    __shared__ __attribute__((aligned(16))) uint32_t sH2[kMlpM / 2];
-    for (int i = threadIdx.x; i < kMlpM * (kMlpK / 8); i += blockDim.x) {  // W2: 16-B pieces
-        const int o = i / (kMlpK / 8), c = i - o * (kMlpK / 8);
-        *(uint4*)&sW[o * kMlpLdsK + 8 * c] = *(const uint4*)&w2[o * kMlpK + 8 * c];
-    }
-    for (int i = threadIdx.x; i < kMlpK; i += blockDim.x) sC[i] = w1c[i];
-    load_head_pairs(head, sH2);
-    __syncthreads();
-    const int lane = threadIdx.x & 63, col = lane & 31, half = lane >> 5;
-    const uint32_t tiles = (R + 63u) / 64u;
-    const uint32_t wstep = gridDim.x * (blockDim.x >> 6);
-    for (uint32_t tile = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); tile < tiles; tile += wstep) {
-        uint32_t rr[2];
-        float x[2];
-        const uint16_t* brow[2];
-#pragma unroll
-        for (int nt = 0; nt < 2; nt++) {
-            rr[nt] = tile * 64u + 32u * nt + (uint32_t)col;
-            const uint32_t rc = rr[nt] < R ? rr[nt] : R - 1u;  // a short last tile: clamp the loads, skip the store
-            x[nt] = cards[rc];
-            brow[nt] = base + (size_t)(rc / (uint32_t)n_cur) * ldb;
-        }
-        float out[2];
-        mlp_tile<2>(brow, x, sW, sC, sH2, col, half, out);
-#pragma unroll
-        for (int nt = 0; nt < 2; nt++)
-            if (half == 0 && rr[nt] < R) logits[rr[nt]] = out[nt];
-    }
 }
 
 // np.median of all outcomes so far, from the histogram (kth smallest): one
@@ -796,13 +640,15 @@ __global__ void k_puct_step_seats(DevState s, PuctArgs a, const void* logits, in
 // A workgroup loads W1s / W2 into LDS once and then loops over groups of 64
 // consecutive rollout seats (persistent grid: two workgroups per CU, the
 // occupancy the 64-row MFMA tiles' registers allow).  Per group: phase 1
-// builds the seats' [0, obs, 1] rows in LDS (the features of write_row /
-// sn_puct_seat_cols, four lanes per seat) and the candidates' card
+// builds the seats' [0, obs, 1] rows in LDS (the features of write_row,
+// four lanes per seat) and the candidates' card
 // features, phase 2 computes base = W1s . rows for the 64 seats with MFMA
 // (layer 1's obs part, K = 64) into LDS (bf16, as the PyTorch GEMM rounds
-// it), phase 3 runs k_puct_mlp's tile loop over the group's rows reading
-// base and the cards from LDS.  Replaces sn_puct_seat_rows + the per-seat
-// GEMM + sn_puct_mlp (two launches and the [S][56] / [S][112] HBM round trips).
+// it), phase 3 runs mlp_tile over the group's rows reading base and the
+// cards from LDS.  (The round-4 GEMM form -- seat rows + a PyTorch GEMM +
+// a tile kernel, two launches and the [S][56] / [S][112] HBM round trips --
+// and the round-5 per-candidate layer-1 form measured slower and were
+// removed in round 6)
 constexpr int kSeatBlock = 64;
 constexpr int kSeatRowK = 64;               // seat-row features (48 + the ones feature, zero-padded)
 constexpr int kSeatRowLds = kSeatRowK + 8;  // LDS stride (144 B)
@@ -1003,145 +849,6 @@ __global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(PuctArgs a, int N, in
     }
 }
 
-// ---- layer 1 per candidate on MFMA too (sn_puct_mlp_mfma) ------------------
-// k_puct_mlp_seats factors layer 1 into a per-seat MFMA product (base) plus
-// a per-candidate card column built on the VALU: ~9 VALU per MFMA in the
-// tile loop (the B fragments' unpack / FMA / pack / ReLU), MFMA busy 30 %.
-// Here every candidate row [card, obs, 1] goes through layer 1 on the matrix
-// cores as well: per 32-row sub-tile, 4 k-steps x 4 output tiles of
-// v_mfma_f32_32x32x16_bf16 against W1s (A fragments held in registers; B
-// = the seat's row from LDS with the candidate's card as feature 0), ReLU +
-// bf16 rounding of the accumulators (ONE rounding of W1 row + b1, the
-// reference split path's h1), and the layer-1 C fragments ARE layer 2's B
-// fragments: lane (col, half) holds outputs o = 32 mt + 8 g + 4 half + i,
-// so layer 2's K is ordered to match -- W2 arrives column-permuted (w2q,
-// FusedMLP.fused: k = 16 ks + 8 half + j <-> o = 32 (ks >> 1) + 16 (ks & 1)
-// + 8 (j >> 2) + 4 half + (j & 3)) and no activation moves between lanes.
-// Then 8 k-steps x 4 tiles of layer 2, ReLU + bf16, the head dot.  48 MFMAs
-// and ~170 VALU per 32 rows (3.5 VALU per MFMA).  Same groups of 64 seats,
-// same persistent grid and carried-tile schedule as k_puct_mlp_seats.
-constexpr int kMlp2K = 128;              // layer-2 K: all 128 layer-1 outputs (permuted, w2q)
-constexpr int kMlp2Lds = kMlp2K + 8;     // LDS row stride of w2q (272 B: 16 lanes' b128 reads hit 64 banks)
-
-__device__ __forceinline__ void mlp2_subtile(const bf16x8_t (&w1f)[4][4], const uint16_t* srow, uint32_t card,
-                                             const uint16_t* sW, const uint32_t* sH2, int col, int half, float& out) {
-    f32x16_t acc[4];
-    // layer 1: [card, obs, 1] x W1s^T, K = 64 (4 k-steps)
-#pragma unroll
-    for (int ks = 0; ks < 4; ks++) {
-        uint4 bv = *(const uint4*)(srow + 16 * ks + 8 * half);
-        if (ks == 0 && half == 0) bv.x = (bv.x & 0xFFFF0000u) | card;  // feature 0: this candidate's card
-        const bf16x8_t b = __builtin_bit_cast(bf16x8_t, bv);
-        const f32x16_t zero = {};
-#pragma unroll
-        for (int mt = 0; mt < 4; mt++)
-            acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1f[mt][ks], b, ks ? acc[mt] : zero, 0, 0, 0);
-    }
-    // ReLU + bf16: layer 2's B fragments, in place (pairs i = 0,1 / 2,3 of each g)
-    uint32_t hb[4][4][2];
-#pragma unroll
-    for (int mt = 0; mt < 4; mt++)
-#pragma unroll
-        for (int g = 0; g < 4; g++) {
-            hb[mt][g][0] = relu_bf16x2(pack_bf16(acc[mt][4 * g], acc[mt][4 * g + 1]));
-            hb[mt][g][1] = relu_bf16x2(pack_bf16(acc[mt][4 * g + 2], acc[mt][4 * g + 3]));
-        }
-    // layer 2: K = 128 (8 k-steps), k-step ks takes tile ks >> 1, groups g = 2 (ks & 1), + 1
-#pragma unroll
-    for (int ks = 0; ks < 8; ks++) {
-        const int mt1 = ks >> 1, g0 = 2 * (ks & 1);
-        const bf16x8_t b = __builtin_bit_cast(
-            bf16x8_t, make_uint4(hb[mt1][g0][0], hb[mt1][g0][1], hb[mt1][g0 + 1][0], hb[mt1][g0 + 1][1]));
-#pragma unroll
-        for (int mt = 0; mt < 4; mt++) {
-            const bf16x8_t a = __builtin_bit_cast(bf16x8_t, *(const uint4*)&sW[(32 * mt + col) * kMlp2Lds + 16 * ks + 8 * half]);
-            const f32x16_t zero = {};
-            acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, ks ? acc[mt] : zero, 0, 0, 0);
-        }
-    }
-    // head: ReLU + bf16 of layer 2, dot with the head pairs, both halves summed
-    float sum = 0.f;
-#pragma unroll
-    for (int mt = 0; mt < 4; mt++)
-#pragma unroll
-        for (int g = 0; g < 4; g++) {
-            const uint2 hw = *(const uint2*)&sH2[(32 * mt + 8 * g + 4 * half) / 2];
-            const uint32_t p0 = relu_bf16x2(pack_bf16(acc[mt][4 * g], acc[mt][4 * g + 1]));
-            const uint32_t p1 = relu_bf16x2(pack_bf16(acc[mt][4 * g + 2], acc[mt][4 * g + 3]));
-            sum = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, p0), __builtin_bit_cast(bf16x2_t, hw.x),
-                                                  sum, false);
-            sum = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, p1), __builtin_bit_cast(bf16x2_t, hw.y),
-                                                  sum, false);
-        }
-    out = sum + __shfl_xor(sum, 32);
-}
-
-__global__ __launch_bounds__(256, 2) void k_puct_mlp_mfma(PuctArgs a, int N, int n_cur, const uint16_t* w1s,
-                                                         const uint16_t* w2q, const float* head, float* logits) {
-    constexpr int kWaves = kBlock / 64;
-    __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kMlp2Lds];                 // w2q [128][136]
-    __shared__ __attribute__((aligned(16))) uint16_t sRow[2][kSeatBlock * kSeatRowLds];   // seat rows, 2 groups
-    __shared__ __attribute__((aligned(16))) float sCard[2][kSeatBlock * kHand];
-    __shared__ __attribute__((aligned(16))) uint32_t sH2[kMlpM / 2];
-    __shared__ uint16_t sLut[kLutSize];
-    const int tid = threadIdx.x;
-    const int wave = tid >> 6, lane = tid & 63, col = lane & 31, half = lane >> 5;
-    build_row_lut(sLut);
-    const int64_t S = a.D * N;
-    const int64_t groups = (S + kSeatBlock - 1) / kSeatBlock;
-    for (int i = tid; i < kMlpM * (kMlp2K / 8); i += blockDim.x) {
-        const int o = i / (kMlp2K / 8), c = i - o * (kMlp2K / 8);
-        *(uint4*)&sW[o * kMlp2Lds + 8 * c] = *(const uint4*)&w2q[o * kMlp2K + 8 * c];
-    }
-    load_head_pairs(head, sH2);
-    // layer 1's A fragments: W1s rows 32 mt + col, k-steps ks (64 VGPRs for the kernel's lifetime)
-    bf16x8_t w1f[4][4];
-#pragma unroll
-    for (int mt = 0; mt < 4; mt++)
-#pragma unroll
-        for (int ks = 0; ks < 4; ks++)
-            w1f[mt][ks] = __builtin_bit_cast(bf16x8_t, *(const uint4*)&w1s[(32 * mt + col) * kSeatRowK + 16 * ks + 8 * half]);
-    const int sl = tid >> 2, part = tid & 3;  // phase 1: four lanes per seat
-    auto group_load = [&](int64_t grp) {
-        const int64_t s0 = grp * kSeatBlock;
-        return seat_load(a, N, s0 + min<int64_t>(sl, S - s0 - 1), part);
-    };
-    auto run_sub = [&](int buf, uint32_t t, uint32_t rows, uint32_t rbase) {  // 32-row sub-tile t of a group
-        const uint32_t r = 32u * t + (uint32_t)col;
-        const uint32_t rc = r < rows ? r : rows - 1u;
-        const uint32_t q = rc / (uint32_t)n_cur;
-        const uint32_t card = __float_as_uint(sCard[buf][q * kHand + (rc - q * (uint32_t)n_cur)]) >> 16;  // bf16 bits
-        float out;
-        mlp2_subtile(w1f, sRow[buf] + q * kSeatRowLds, card, sW, sH2, col, half, out);
-        if (half == 0 && r < rows) logits[rbase + r] = out;
-    };
-    uint32_t pend_first = 0u, pend_cnt = 0u, pend_rows = 0u, pend_rbase = 0u;
-    SeatIn nxt = group_load(min<int64_t>(blockIdx.x, groups - 1));
-    int it = 0;
-    for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x, it++) {
-        const int buf = it & 1;
-        const int64_t s0 = grp * kSeatBlock;
-        const int nseat = (int)min<int64_t>(kSeatBlock, S - s0);
-        const SeatIn cur = nxt;
-        __syncthreads();  // the tiles of two groups ago are done with this buffer
-        seat_row_part(cur, n_cur, part, sRow[buf] + sl * kSeatRowLds, sCard[buf] + sl * kHand, sLut);
-        __syncthreads();
-        const bool more = grp + gridDim.x < groups;
-        if (more) nxt = group_load(grp + gridDim.x);  // the next group's loads fly during the tiles
-        const uint32_t rows = (uint32_t)nseat * (uint32_t)n_cur;
-        const uint32_t tiles = (rows + 31u) / 32u;
-        const uint32_t rbase = (uint32_t)s0 * (uint32_t)n_cur;
-        const uint32_t total = pend_cnt + tiles;
-        uint32_t defer = more ? total % kWaves : 0u;
-        if (defer > tiles) defer = 0u;  // only this group's tiles can wait
-        for (uint32_t i = (uint32_t)wave; i < total - defer; i += kWaves) {
-            if (i < pend_cnt) run_sub(buf ^ 1, pend_first + i, pend_rows, pend_rbase);
-            else run_sub(buf, i - pend_cnt, rows, rbase);
-        }
-        pend_first = tiles - defer, pend_cnt = defer, pend_rows = rows, pend_rbase = rbase;
-    }
-}
-
 // ---- whole rollouts in one kernel (sn_puct_rollouts) ----------------------
 // Every rollout step of k_puct_mlp_seats + k_puct_step_seats touches one
 // decision's rollout state, its seats' logits and its statistics only, so
@@ -1165,9 +872,8 @@ constexpr int kRollSeats = 32;  // seats per wave's group (32 / L... 64 / L / 2 
 constexpr int kRollWaveLds = kRollSeats * kSeatRowLds * 2 + kRollSeats * kBaseLds * 2 + kRollSeats * kHand * 4 +
                              8 * kRoWords * 4;  // rows (aliased by logits) + base + cards + states: 15 104 B
 
-// MF: layer 1 per candidate row on MFMA as well (mlp2_subtile, w2 = w2q, sn_puct_mlp_mfma's
-// arithmetic; no phase 2, the logits over the unused base rows), else sn_puct_mlp_seats'.
-template <int N, int L, bool MF = false>
+// sn_puct_mlp_seats' arithmetic.
+template <int N, int L>
 __global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a, int r0, int nr, int32_t* ro_base,
                                                          const uint16_t* w1s, const float* w1c, const uint16_t* w2,
                                                          const float* head) {
@@ -1175,8 +881,8 @@ __global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a
     constexpr int kWaves = 512 / 64;  // two per SIMD
     constexpr int DG = kRollSeats / L;  // decisions per group
     static_assert(DG <= 8 && DG * N <= kRollSeats, "a group's seats and states fit");
-    constexpr int kWld = MF ? kMlp2Lds : kMlpLdsK, kWk = MF ? kMlp2K : kMlpK;
-    __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kWld];  // W2 [128][120] (w2q [128][136]), shared
+    constexpr int kWld = kMlpLdsK, kWk = kMlpK;
+    __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kWld];  // W2 [128][120], shared
     __shared__ __attribute__((aligned(16))) float sC[kMlpK];
     __shared__ __attribute__((aligned(16))) uint32_t sH2[kMlpM / 2];
     __shared__ uint16_t sLut[kLutSize];
@@ -1188,14 +894,13 @@ __global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a
         const int o = i / (kWk / 8), c = i - o * (kWk / 8);
         *(uint4*)&sW[o * kWld + 8 * c] = *(const uint4*)&w2[o * kWk + 8 * c];
     }
-    if (!MF)
-        for (int i = tid; i < kMlpK; i += blockDim.x) sC[i] = w1c[i];
+    for (int i = tid; i < kMlpK; i += blockDim.x) sC[i] = w1c[i];
     load_head_pairs(head, sH2);
     __syncthreads();  // the only barrier: the waves run independently from here
     uint16_t* sRow = (uint16_t*)sWave[wave];                 // [32][72]
     uint16_t* sBase = sRow + kRollSeats * kSeatRowLds;       // [32][120]
-    // [32 x 10]: over sRow once phase 2 is done with it, or (MF: rows live through phase 3) over the base
-    float* sLogit = MF ? (float*)sBase : (float*)sWave[wave];
+    // [32 x 10]: over sRow once phase 2 is done with it
+    float* sLogit = (float*)sWave[wave];
     float* sCard = (float*)(sBase + kRollSeats * kBaseLds);  // [32][10]
     int32_t* sRo = (int32_t*)(sCard + kRollSeats * kHand);   // [DG][48]
     const int64_t groups = (a.D + DG - 1) / DG;
@@ -1224,26 +929,6 @@ __global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a
                     seat_row_part(in, m, part, sRow + sl * kSeatRowLds, sCard + sl * kHand, sLut);
                 }
                 fence();
-                if constexpr (MF) {
-                    // layer 1 (per candidate row) + layer 2 + head on MFMA, 32 rows per sub-tile
-                    bf16x8_t w1f[4][4];
-#pragma unroll
-                    for (int mt = 0; mt < 4; mt++)
-#pragma unroll
-                        for (int ks = 0; ks < 4; ks++)
-                            w1f[mt][ks] = __builtin_bit_cast(
-                                bf16x8_t, *(const uint4*)&w1s[(32 * mt + col) * kSeatRowK + 16 * ks + 8 * half]);
-                    const uint32_t rows = (uint32_t)nseat * (uint32_t)m;
-                    for (uint32_t t32 = 0; t32 < (rows + 31u) / 32u; t32++) {
-                        const uint32_t rw = 32u * t32 + (uint32_t)col;
-                        const uint32_t rc = rw < rows ? rw : rows - 1u;
-                        const uint32_t q = rc / (uint32_t)m;
-                        const uint32_t card = __float_as_uint(sCard[q * kHand + (rc - q * (uint32_t)m)]) >> 16;
-                        float out;
-                        mlp2_subtile(w1f, sRow + q * kSeatRowLds, card, sW, sH2, col, half, out);
-                        if (half == 0 && rw < rows) sLogit[rw] = out;
-                    }
-                } else {
                 // phase 2: base[seat][j] = sum_k W1s[j][k] rows[seat][k] (one 32-seat tile)
                 {
                     // the A fragments (W1s rows 32 mt + col) from L1 / L2 per step: held across phase 3
@@ -1296,7 +981,6 @@ __global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a
 #pragma unroll
                     for (int nt = 0; nt < TNT; nt++)
                         if (half == 0 && rw[nt] < rows) sLogit[rw[nt]] = out[nt];
-                }
                 }
                 fence();
                 // the step: L lanes per decision (step_seat, as k_puct_step_seats); lanes past the
@@ -1552,40 +1236,6 @@ sn_status sn_puct_step(sn_env* e, const sn_puct* q, const float* logits, int t, 
     return SN_OK;
 }
 
-sn_status sn_puct_seat_cols(sn_env* e, const sn_puct* q, int n_cur, void* cols, int ks, float* cards, int bf16,
-                            void* stream) {
-    PuctArgs a{};
-    sn_status st = puct_args(e, q, a);
-    if (st != SN_OK) return st;
-    if (n_cur < 1 || n_cur > a.n) return set_error(SN_EINVAL, "n_cur out of range");
-    if (!cols || !cards) return set_error(SN_EINVAL, "NULL argument");
-    if (ks <= kRowLen || ks > 256) return set_error(SN_EINVAL, "ks must be in 49..256 (48 features + the bias feature)");
-    const int64_t total = a.D * e->s.N;
-    hipStream_t s = (hipStream_t)stream;
-    if (bf16)
-        hipLaunchKernelGGL(k_puct_seat_cols<__hip_bfloat16>, dim3(grid_for(total)), dim3(kBlock), 0, s, a, e->s.N, n_cur,
-                           (__hip_bfloat16*)cols, ks, cards, 0);
-    else
-        hipLaunchKernelGGL(k_puct_seat_cols<float>, dim3(grid_for(total)), dim3(kBlock), 0, s, a, e->s.N, n_cur,
-                           (float*)cols, ks, cards, 0);
-    HIP_TRY(hipGetLastError());
-    return SN_OK;
-}
-
-sn_status sn_puct_seat_rows(sn_env* e, const sn_puct* q, int n_cur, void* rows, int ks, float* cards, void* stream) {
-    PuctArgs a{};
-    sn_status st = puct_args(e, q, a);
-    if (st != SN_OK) return st;
-    if (n_cur < 1 || n_cur > a.n) return set_error(SN_EINVAL, "n_cur out of range");
-    if (!rows || !cards) return set_error(SN_EINVAL, "NULL argument");
-    if (ks <= kRowLen || ks > 256) return set_error(SN_EINVAL, "ks must be in 49..256 (48 features + the bias feature)");
-    const int64_t total = a.D * e->s.N;
-    hipLaunchKernelGGL(k_puct_seat_cols<__hip_bfloat16>, dim3(grid_for(total)), dim3(kBlock), 0, (hipStream_t)stream, a,
-                       e->s.N, n_cur, (__hip_bfloat16*)rows, ks, cards, 1);
-    HIP_TRY(hipGetLastError());
-    return SN_OK;
-}
-
 sn_status sn_puct_mlp_seats(sn_env* e, const sn_puct* q, int n_cur, const void* w1s, const float* w1c, const void* w2,
                             const float* head, float* logits, void* stream) {
     PuctArgs a{};
@@ -1606,26 +1256,13 @@ sn_status sn_puct_mlp_seats(sn_env* e, const sn_puct* q, int n_cur, const void* 
     return SN_OK;
 }
 
-static sn_status puct_rollouts(sn_env* e, const sn_puct* q, int r0, int nr, void* ro_base, const void* w1s,
-                               const float* w1c, const void* w2, const float* head, void* stream, bool mf);
-
 sn_status sn_puct_rollouts(sn_env* e, const sn_puct* q, int r0, int nr, void* ro_base, const void* w1s, const float* w1c,
                            const void* w2, const float* head, void* stream) {
-    return puct_rollouts(e, q, r0, nr, ro_base, w1s, w1c, w2, head, stream, false);
-}
-
-sn_status sn_puct_rollouts_mfma(sn_env* e, const sn_puct* q, int r0, int nr, void* ro_base, const void* w1s,
-                                const void* w2q, const float* head, void* stream) {
-    return puct_rollouts(e, q, r0, nr, ro_base, w1s, nullptr, w2q, head, stream, true);
-}
-
-static sn_status puct_rollouts(sn_env* e, const sn_puct* q, int r0, int nr, void* ro_base, const void* w1s,
-                               const float* w1c, const void* w2, const float* head, void* stream, bool mf) {
     PuctArgs a{};
     sn_status st = puct_args(e, q, a);
     if (st != SN_OK) return st;
     if (r0 < 0 || nr < 1 || !ro_base) return set_error(SN_EINVAL, "need r0 >= 0, nr >= 1 and the dealt states");
-    if (!w1s || (!w1c && !mf) || !w2 || !head) return set_error(SN_EINVAL, "NULL argument");
+    if (!w1s || !w1c || !w2 || !head) return set_error(SN_EINVAL, "NULL argument");
     if ((((uintptr_t)w1s) | ((uintptr_t)w2) | ((uintptr_t)w1c) | ((uintptr_t)head)) & 15)
         return set_error(SN_EINVAL, "w1s / w2 / w1c / head must be 16-B aligned");
     if (e->s.N < 3 || e->s.N > 8) return set_error(SN_EUNSUPPORTED, "sn_puct_rollouts: 3 <= N <= 8");
@@ -1633,15 +1270,9 @@ static sn_status puct_rollouts(sn_env* e, const sn_puct* q, int r0, int nr, void
     const int Lw = e->s.N <= 2 ? 2 : e->s.N <= 4 ? 4 : 8;
     const int64_t groups = (a.D + kRollSeats / Lw - 1) / (kRollSeats / Lw);
     const dim3 grid((unsigned)std::min<int64_t>((groups + 7) / 8, (int64_t)e->cus));  // one 8-wave workgroup per CU
-#define SN_ROLLOUTS(NN_, L_)                                                                                        \
-    do {                                                                                                            \
-        if (mf)                                                                                                     \
-            hipLaunchKernelGGL((k_puct_rollouts<NN_, L_, true>), grid, dim3(512), 0, s, e->s, a, r0, nr,             \
-                               (int32_t*)ro_base, (const uint16_t*)w1s, w1c, (const uint16_t*)w2, head);             \
-        else                                                                                                        \
-            hipLaunchKernelGGL((k_puct_rollouts<NN_, L_, false>), grid, dim3(512), 0, s, e->s, a, r0, nr,            \
-                               (int32_t*)ro_base, (const uint16_t*)w1s, w1c, (const uint16_t*)w2, head);             \
-    } while (0)
+#define SN_ROLLOUTS(NN_, L_)                                                                                  \
+    hipLaunchKernelGGL((k_puct_rollouts<NN_, L_>), grid, dim3(512), 0, s, e->s, a, r0, nr, (int32_t*)ro_base, \
+                       (const uint16_t*)w1s, w1c, (const uint16_t*)w2, head)
     switch (e->s.N) {
         case 3: SN_ROLLOUTS(3, 4); break;
         case 4: SN_ROLLOUTS(4, 4); break;
@@ -1651,88 +1282,6 @@ static sn_status puct_rollouts(sn_env* e, const sn_puct* q, int r0, int nr, void
         default: SN_ROLLOUTS(8, 8); break;
     }
 #undef SN_ROLLOUTS
-    HIP_TRY(hipGetLastError());
-    return SN_OK;
-}
-
-sn_status sn_puct_mlp_mfma(sn_env* e, const sn_puct* q, int n_cur, const void* w1s, const void* w2q, const float* head,
-                           float* logits, void* stream) {
-    PuctArgs a{};
-    sn_status st = puct_args(e, q, a);
-    if (st != SN_OK) return st;
-    if (n_cur < 1 || n_cur > a.n) return set_error(SN_EINVAL, "n_cur out of range");
-    if (!w1s || !w2q || !head || !logits) return set_error(SN_EINVAL, "NULL argument");
-    if ((((uintptr_t)w1s) | ((uintptr_t)w2q) | ((uintptr_t)head)) & 15)
-        return set_error(SN_EINVAL, "w1s / w2q / head must be 16-B aligned");
-    const int64_t S = a.D * e->s.N;
-    if (S * n_cur >= (1ll << 31)) return set_error(SN_EINVAL, "too many rows");
-    const int64_t groups = (S + kSeatBlock - 1) / kSeatBlock;
-    hipLaunchKernelGGL(k_puct_mlp_mfma, dim3((unsigned)std::min<int64_t>(groups, 2ll * e->cus)), dim3(kBlock), 0,
-                       (hipStream_t)stream, a, e->s.N, n_cur, (const uint16_t*)w1s, (const uint16_t*)w2q, head, logits);
-    HIP_TRY(hipGetLastError());
-    return SN_OK;
-}
-
-sn_status sn_puct_mlp(sn_env* e, const sn_puct* q, int n_cur, const void* base, int ldb, const float* w1c,
-                      const float* cards, const void* w2, const float* head, float* logits, void* stream) {
-    PuctArgs a{};
-    sn_status st = puct_args(e, q, a);
-    if (st != SN_OK) return st;
-    if (n_cur < 1 || n_cur > a.n) return set_error(SN_EINVAL, "n_cur out of range");
-    if (!base || !w1c || !cards || !w2 || !head || !logits) return set_error(SN_EINVAL, "NULL argument");
-    if (ldb < kMlpK || (ldb & 7)) return set_error(SN_EINVAL, "ldb must be >= 112 and a multiple of 8");
-    if ((((uintptr_t)base) | ((uintptr_t)w2) | ((uintptr_t)w1c) | ((uintptr_t)head)) & 15)
-        return set_error(SN_EINVAL, "base / w2 / w1c / head must be 16-B aligned");
-    const int64_t R = a.D * e->s.N * n_cur;
-    if (R >= (1ll << 31)) return set_error(SN_EINVAL, "too many rows");
-    const int64_t tiles = (R + 63) / 64;
-    const int64_t blocks = std::min<int64_t>((tiles + 3) / 4, 256 * 4);  // waves loop over the tiles beyond
-    hipLaunchKernelGGL(k_puct_mlp, dim3((unsigned)blocks), dim3(kBlock), 0, (hipStream_t)stream, (uint32_t)R, n_cur,
-                       (const uint16_t*)base, ldb, w1c, cards, (const uint16_t*)w2, head, logits);
-    HIP_TRY(hipGetLastError());
-    return SN_OK;
-}
-
-sn_status sn_puct_h1_cols(sn_env* e, const sn_puct* q, int n_cur, const void* baseT, int hidden, const float* w1c,
-                          const float* cards, void* h1T, int kp, int bf16, void* stream) {
-    PuctArgs a{};
-    sn_status st = puct_args(e, q, a);
-    if (st != SN_OK) return st;
-    if (n_cur < 1 || n_cur > a.n) return set_error(SN_EINVAL, "n_cur out of range");
-    if (hidden < 1 || kp <= hidden || kp > 4096) return set_error(SN_EINVAL, "need 1 <= hidden < kp <= 4096");
-    if (!baseT || !w1c || !cards || !h1T) return set_error(SN_EINVAL, "NULL argument");
-    if (((uintptr_t)h1T) & 3) return set_error(SN_EINVAL, "h1T must be 4-B aligned");
-    const int64_t S = a.D * e->s.N, R = S * n_cur;
-    if (R * kp >= (1ll << 40) || R >= (1ll << 31)) return set_error(SN_EINVAL, "too many rows");
-    hipStream_t s = (hipStream_t)stream;
-    const int64_t threads = (R + 1) / 2;
-    // the features are split over blockIdx.y so that a launch has >= ~4 waves
-    // per SIMD (a thread's feature loop is a latency chain of small gathers:
-    // at 8192 x 4 x 10 rows one 4-row thread per row group is 1.25 waves per SIMD)
-    auto slices = [&](int64_t thr) {
-        const int64_t waves = (thr + 63) / 64;
-        return (int)std::max<int64_t>(1, std::min<int64_t>((kp + 7) / 8, (4096 + waves - 1) / waves));
-    };
-    if ((R & 3) == 0 && (((uintptr_t)h1T) & 15) == 0) {  // 4-row groups: 8-B (bf16) / 16-B (f32) aligned stores
-        const int G = slices(R / 4), fch = (kp + G - 1) / G;
-        const dim3 grid((unsigned)grid_for(R / 4), (unsigned)((kp + fch - 1) / fch));
-        if (bf16)
-            hipLaunchKernelGGL(k_puct_h1_cols4<__hip_bfloat16>, grid, dim3(kBlock), 0, s, (uint32_t)R, (uint32_t)S, hidden,
-                               kp, n_cur, (const __hip_bfloat16*)baseT, cards, w1c, (__hip_bfloat16*)h1T, fch);
-        else
-            hipLaunchKernelGGL(k_puct_h1_cols4<float>, grid, dim3(kBlock), 0, s, (uint32_t)R, (uint32_t)S, hidden, kp, n_cur,
-                               (const float*)baseT, cards, w1c, (float*)h1T, fch);
-        HIP_TRY(hipGetLastError());
-        return SN_OK;
-    }
-    const int G = slices(threads), fch = (kp + G - 1) / G;
-    const dim3 grid((unsigned)grid_for(threads), (unsigned)((kp + fch - 1) / fch));
-    if (bf16)
-        hipLaunchKernelGGL(k_puct_h1_cols<__hip_bfloat16>, grid, dim3(kBlock), 0, s, (uint32_t)R, (uint32_t)S, hidden, kp,
-                           n_cur, (const __hip_bfloat16*)baseT, cards, w1c, (__hip_bfloat16*)h1T, fch);
-    else
-        hipLaunchKernelGGL(k_puct_h1_cols<float>, grid, dim3(kBlock), 0, s, (uint32_t)R, (uint32_t)S, hidden, kp, n_cur,
-                           (const float*)baseT, cards, w1c, (float*)h1T, fch);
     HIP_TRY(hipGetLastError());
     return SN_OK;
 }

@@ -45,7 +45,7 @@ struct DevState {
     int pad2_;
     // pipelined twist-ahead (k_mt_ahead / RingPipe, sechs_env.hip):
     u32x4* pring;    // [kPipeRing/64][B] 64-B chunks: byte of absolute stream word p at p mod kPipeRing (ring_byte)
-    uint32_t* pabsc; // [kPipeSlots][B] consumer position after a play launch (by launch parity, or index mod 4)
+    uint32_t* pabsc; // [kPipeSlots][B] consumer position after a play launch (by launch index mod kPipeSlots)
     uint32_t* ptend; // [kPipeSlots][B] end of the twisted words after a prep launch (the same)
     uint32_t* ptp;   // [B] twist pointer (MtGen's pos field), owned by k_mt_ahead
     uint32_t* perr;  // [1] play lanes that ran past the twisted words (must stay 0)
@@ -59,7 +59,7 @@ struct DevState {
 };
 
 constexpr int kMt0Levels = 5;    // word-0 crossings kept in mt0 (a K = 5 lead + a round spans up to five)
-constexpr int kPipeSlots = 4;    // pabsc buffers (by play launch index mod 4; ptend uses 2, by twist parity)
+constexpr int kPipeSlots = 8;    // pabsc buffers (by play launch index mod 8; ptend uses 2, by twist parity)
 constexpr int kPipeRing = 4096;  // ring bytes per game (>= the lead 600 K + a whole round's overshoot: 3 623 at K = 5)
 
 // pring layout: 64-byte chunks interleaved over games -- stream positions
@@ -847,17 +847,15 @@ struct sn_env {
     int lg_mpc[16], lg_mmax[16];  // MCSAgent agents: mc_per_card, mc_max
     int phase;        // every game's env-steps since its deal, mod 10, when they are in lockstep; -1 unknown
     int play_split;   // SN_OPT_PLAY_SPLIT: role-split k_play for lockstep DrunkHamster rollouts
-    int twist_every;  // SN_OPT_TWIST_EVERY: a k_mt_ahead beside every K-th play launch (K = 1, 2, 3)
+    int twist_every;  // SN_OPT_TWIST_EVERY: a k_mt_ahead beside every K-th play launch (K = 1 .. 5)
     int tw_out;       // pipeline: ptend slot of the last twist
     uint64_t pphase;  // pipeline: play launches since it started
     int twist_round;  // SN_OPT_TWIST_ROUND: k_mt_ahead twists whole MT rounds (8 instead of 12 B of MT traffic per word)
-    int play_quad;    // SN_OPT_PLAY_QUAD: four lanes per game (k_play_quad) on the pipelined N = 4 path
     int pipe_serial;  // SECHS_PIPE_SERIAL=1 (diagnostics): each twist waits for the play launch before it (no overlap)
     int pl_cout;      // pabsc slot the last play launch wrote
     int pK;           // SN_OPT_TWIST_EVERY of the running pipeline
     hipEvent_t evt[2];  // after twist G, slot G mod 2
-    int pipe_fused;   // SN_OPT_PIPE_FUSED: k_play_quad twists the rounds itself (no side stream, no cross-queue waits)
-    int pfused;       // the running pipeline was started fused (whole rounds from its start)
+    int twist_skip;   // SN_OPT_TWIST_SKIP (tests only): steady twists after the first group twist nothing
     sechs::DevState s;
     // pipelined twist-ahead (sechs_env.hip launch_pipe): a k_mt_ahead for the
     // next play launch may be in flight on `side` (ev_prep) after a rollout
@@ -865,7 +863,6 @@ struct sn_env {
     uint64_t pcount;    // pipelined play launches so far
     hipStream_t side;
     hipEvent_t ev_prep, ev_main, ev_play;  // ev_play: after the last pipelined k_play (recorded on that call's stream)
-    hipStream_t play_st;  // that stream's handle VALUE, compared only (never used: the caller may destroy it)
     uint32_t* perr_host;                    // pinned, device-mapped mirror of s.perr (PlayArgs::perr_mirror)
     uint32_t* perr_host_dev;
     uint32_t* hbuf;      // one-game fast path (sn_step1 / sn_reset1): pinned, device-mapped exchange words

@@ -22,10 +22,9 @@ SN_I8, SN_I16, SN_I32, SN_I64, SN_F32 = 1, 2, 3, 4, 5
 SN_AUTO_RESET, SN_NO_SUMMARIES = 1, 2
 SN_OPT_RING_WORDS, SN_OPT_CHUNK_STEPS, SN_OPT_PIPELINE, SN_OPT_TIMING, SN_OPT_PIPE_GPW, SN_OPT_PIPE_LEAD = 1, 2, 3, 4, 5, 6
 SN_OPT_PLAY_SPLIT = 7
-SN_OPT_PLAY_QUAD = 8
 SN_OPT_TWIST_ROUND = 9
 SN_OPT_TWIST_EVERY = 10
-SN_OPT_PIPE_FUSED = 11
+SN_OPT_TWIST_SKIP = 12  # test knob: the default schedule runs its ring dry
 SN_AGENT_RANDOM, SN_AGENT_MCS, SN_AGENT_EXTERNAL = 0, 1, 2
 
 class SnPuct(ctypes.Structure):
@@ -100,15 +99,9 @@ SIGNATURES = {
     "sn_puct_deal": ([_P, _P, _P], _I),
     "sn_puct_deal_batch": ([_P, _P, _I, _I, _P, _P], _I),
     "sn_puct_rollouts": ([_P, _P, _I, _I, _P, _P, _P, _P, _P, _P], _I),
-    "sn_puct_rollouts_mfma": ([_P, _P, _I, _I, _P, _P, _P, _P, _P], _I),
     "sn_puct_rows": ([_P, _P, _I, _P, _I, _P], _I),
     "sn_puct_step": ([_P, _P, _P, _I, _I, _P], _I),
-    "sn_puct_seat_cols": ([_P, _P, _I, _P, _I, _P, _I, _P], _I),
-    "sn_puct_h1_cols": ([_P, _P, _I, _P, _I, _P, _P, _P, _I, _I, _P], _I),
-    "sn_puct_seat_rows": ([_P, _P, _I, _P, _I, _P, _P], _I),
-    "sn_puct_mlp": ([_P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P], _I),
     "sn_puct_mlp_seats": ([_P, _P, _I, _P, _P, _P, _P, _P, _P], _I),
-    "sn_puct_mlp_mfma": ([_P, _P, _I, _P, _P, _P, _P, _P], _I),
     "sn_puct_choose": ([_P, _P, _P, _P, _P], _I),
     "sn_pcv_choose": ([_P, _P, _P, _P, _P, _P, _P, _P], _I),
     "sn_policy_sample": ([_P, _P, _P, _P, _P, _P, _P, _P], _I),

@@ -78,104 +78,43 @@ class FusedMLP:
                 fresh = FusedMLP.of(self.module)
                 self.head_w.copy_(fresh.head_w)
                 self.head_b.copy_(fresh.head_b)
-                if hasattr(self, "_split"):
-                    for old, new in zip(self._split_tensors(), fresh._split_tensors()):
-                        old.copy_(new)
                 if getattr(self, "_fused", None) is not None:
                     for old, new in zip(self._fused, fresh.fused()):
                         old.copy_(new)
-                    if getattr(self, "_w2q", None) is not None:
-                        self._fill_w2q()
         return True
 
-    def _split_tensors(self):
-        sp = self.split()
-        return [sp[0], *sp[3], sp[4], sp[5]] if sp is not None else []
-
-    def split(self):
-        """the feature-major rollout form (sn_puct_seat_cols / sn_puct_h1_cols):
-        augmented weights with each bias as the column against a ones feature
-        -- W1a [H, 56] = [W1 | b1 | 0] (column 0, the card, meets a zero),
-        per later hidden layer [Wa | ba | 0; 0 | 1 | 0] (the ones feature
-        passes through its ReLU), the head [Wh | bh | 0] (16 rows) -- plus
-        W1[:, 0] as f32; None for other layouts"""
-        if self.layers is None or self.layers[0][0].shape[1] != ROW:
-            return None
-        if not hasattr(self, "_split"):
-            w1, b1 = self.layers[0]
-            H = w1.shape[0]
-            pad = lambda n: -(-(n + 1) // 8) * 8  # noqa: E731  features + the ones feature, to 8
-            w1a = torch.zeros((H, 56), dtype=w1.dtype, device=w1.device)
-            w1a[:, :ROW], w1a[:, ROW] = w1, b1
-            hidden, kin = [], pad(H)
-            for w, b in self.layers[1:]:
-                ho = w.shape[0]
-                wa = torch.zeros((pad(ho), kin), dtype=w.dtype, device=w.device)
-                wa[:ho, : w.shape[1]], wa[:ho, w.shape[1]], wa[ho, w.shape[1]] = w, b, 1
-                hidden.append(wa)
-                kin = pad(ho)
-            hw, hb = self.head_w.t(), self.head_b  # [16, last]
-            ha = torch.zeros((hw.shape[0], kin), dtype=hw.dtype, device=hw.device)
-            ha[:, : hw.shape[1]], ha[:, hw.shape[1]] = hw, hb
-            self._split = (w1a, H, pad(H), hidden, ha, w1[:, 0].float().contiguous())
-        return self._split
-
     def fused(self):
-        """the fused rollout form (sn_puct_seat_rows + one GEMM + sn_puct_mlp)
+        """the one-kernel rollout form (sn_puct_mlp_seats / sn_puct_rollouts)
         for MultiHeadedMLP(48, (H, H2), (1,)) in bf16 with H <= 111, H2 <= 127:
-        W1t [56][112] bf16 (base = seat rows @ W1t: [W1 | b1 | 0] transposed,
-        1 at (48, H) -- the ones feature), w1c [112] f32 (W1[:, 0], then 0),
-        W2 [128][112] bf16 ([W2 | b2 | 0] rows, the ones pass-through row H2),
-        head [128] f32 ([wh | bh | 0]); None for other layouts"""
+        w1c [112] f32 (W1[:, 0], then 0), W2 [128][112] bf16 ([W2 | b2 | 0]
+        rows, the ones pass-through row H2), head [128] f32 ([wh | bh | 0]),
+        w1s [128][64] bf16 ([W1 | b1 | 0] rows, 1 at (H, 48): the ones
+        feature); None for other layouts (they run sn_puct_rows + __call__)"""
         if getattr(self, "_fused", "unset") != "unset":
             return self._fused
         self._fused = None
-        sp = self.split()
-        if sp is None or len(self.layers) != 2 or self.head_sizes != [1] or self.layers[0][0].dtype != torch.bfloat16:
+        if self.layers is None or len(self.layers) != 2 or self.head_sizes != [1] or \
+                self.layers[0][0].shape[1] != ROW or self.layers[0][0].dtype != torch.bfloat16:
             return None
-        w1a, H, _, _, _, w1c = sp
+        w1, b1 = self.layers[0]
+        H = w1.shape[0]
         w2, b2 = self.layers[1]
         H2 = w2.shape[0]
         if H > 111 or H2 > 127 or w2.shape[1] != H:
             return None
-        dev = w1a.device
-        w1t = torch.zeros((56, 112), dtype=torch.bfloat16, device=dev)
-        w1t[:, :H] = w1a.t()
-        w1t[ROW, H] = 1.0
+        dev = w1.device
         c = torch.zeros((112,), dtype=torch.float32, device=dev)
-        c[:H] = w1c
+        c[:H] = w1[:, 0].float()
         w2p = torch.zeros((128, 112), dtype=torch.bfloat16, device=dev)
         w2p[:H2, :H], w2p[:H2, H], w2p[H2, H] = w2, b2, 1.0
         head = torch.zeros((128,), dtype=torch.float32, device=dev)
         head[:H2] = self.head_w[:, 0].float()
         head[H2] = self.head_b[0].float()
-        w1s = torch.zeros((128, 64), dtype=torch.bfloat16, device=dev)  # sn_puct_mlp_seats: [W1 | b1 | 0] rows
-        w1s[:H, :56] = w1a
+        w1s = torch.zeros((128, 64), dtype=torch.bfloat16, device=dev)  # [W1 | b1 | 0] rows
+        w1s[:H, :ROW], w1s[:H, ROW] = w1, b1
         w1s[H, ROW] = 1.0
-        self._fused = (w1t, c, w2p, head, w1s)
+        self._fused = (c, w2p, head, w1s)
         return self._fused
-
-    def w2q(self):
-        """sn_puct_mlp_mfma's layer-2 weights: the fused form's [128][112] W2
-        rows widened to 128 columns, the columns permuted to the MFMA
-        accumulator layout of layer 1 (column k = 16 ks + 8 h + j holds
-        layer-1 output 32 (ks >> 1) + 16 (ks & 1) + 8 (j >> 2) + 4 h +
-        (j & 3)); None where fused() is None"""
-        fz = self.fused()
-        if fz is None:
-            return None
-        if getattr(self, "_w2q", None) is None:
-            self._w2q = torch.empty((128, 128), dtype=torch.bfloat16, device=fz[2].device)
-            self._w2q_perm = torch.tensor([32 * (k >> 5) + 16 * ((k >> 4) & 1) + 8 * ((k & 7) >> 2) + 4 * ((k >> 3) & 1)
-                                           + (k & 3) for k in range(128)], device=fz[2].device)
-            self._fill_w2q()
-        return self._w2q
-
-    def _fill_w2q(self):
-        w2p = self.fused()[2]
-        wide = torch.zeros((128, 128), dtype=torch.bfloat16, device=w2p.device)
-        wide[:, : w2p.shape[1]] = w2p
-        self._w2q.copy_(wide[:, self._w2q_perm])
 
     def __call__(self, rows):
         if self.layers is None:
@@ -238,16 +177,9 @@ class BatchedPUCT:
         self.graph = bool(graph) and max_decisions is None
         self.graph_after = 0
         self._graphs, self._graphs_seen = {}, {}
-        # the rollout rows' layer 1 split (FusedMLP.split): once per seat + the card column
-        self.split_l1 = True
-        # the rollout MLP after the per-seat GEMM as one MFMA kernel
-        # (FusedMLP.fused, sn_puct_mlp): bf16 nets of the reference's shape
-        self.fused_mlp = os.environ.get("SECHS_FUSED_MLP", "1") != "0"  # "0": the PyTorch split path (A/B runs)
-        # "seats" (default): layer 1's per-seat part inside the MLP kernel too (sn_puct_mlp_seats, one
-        # launch per step); "mfma": layer 1 per candidate row on the matrix cores as well
-        # (sn_puct_mlp_mfma); "gemm": per-seat rows + a PyTorch GEMM + sn_puct_mlp
-        self.mlp_layer1 = os.environ.get("SECHS_MLP_LAYER1", "seats")
-        # the seats / mfma rollout loop deals this many rollouts per launch
+        # bf16 nets of the reference's shape (FusedMLP.fused) run the rollout MLP as one MFMA
+        # kernel (sn_puct_mlp_seats / sn_puct_rollouts); other nets run sn_puct_rows + the net
+        # the rollout loop deals this many rollouts per launch
         # (sn_puct_deal_batch into a [deal_batch][D][48] buffer, each rollout
         # then running on its slice); 0: one sn_puct_deal per rollout (A/B, tests)
         self.deal_batch = int(os.environ.get("SECHS_PUCT_DEAL_BATCH", "16"))
@@ -274,12 +206,8 @@ class BatchedPUCT:
             net = copy.deepcopy(self.actor).to(self.env.device, self.net_dtype)
             net.eval()
             self._net, self._net_version = FusedMLP.of(net), version
-            sp = self._net.split()  # built here: a graph capture may not allocate
-            if sp is not None:
-                self._split_bufs(sp[1], sp[2])
-            if self._net.fused() is not None:
+            if self._net.fused() is not None:  # built here: a graph capture may not allocate
                 self._fused_bufs()
-                self._net.w2q()
         return self._net
 
     def actor_device(self):
@@ -372,110 +300,47 @@ class BatchedPUCT:
         L, h, st = nat.lib(), self.env._h, self.env._stream()
         bf16 = int(self.net_dtype == torch.bfloat16)
         N = self.env.num_players
-        fz = self._net.fused() if (self.split_l1 and self.fused_mlp) else None
+        fz = self._net.fused()
         if fz is not None:
-            # per rollout step: the seats' [0, obs, 1] rows, base = rows @ W1t
-            # (PyTorch-ROCm GEMM over the D*N seats), then layer 1's card
-            # column + ReLU, layer 2 + ReLU and the head in one MFMA kernel
-            # (f32 logits, packed) -- no activation tensor in HBM
-            w1t, w1c, w2p, head, w1s = fz
+            # the reference-shaped bf16 net: per rollout step the seats' [0, obs, 1] rows, layer 1's
+            # per-seat part on MFMA, the card column + ReLU, layer 2 + ReLU and the head in one MFMA
+            # kernel (f32 logits, packed) -- no activation tensor in HBM
+            w1c, w2p, head, w1s = fz
             S = self.D * N
-            rows, cards, base, logits = self._fused_bufs()
-            rv, bv = rows[:S], base[:S]
-            if self.mlp_layer1 in ("seats", "mfma"):
-                # two launches per rollout step, the arguments built once (the
-                # league's engines run this loop eagerly: host time per launch)
-                qr, deal, step = ctypes_ref(q), L.sn_puct_deal, L.sn_puct_step
-                if self.mlp_layer1 == "mfma":  # layer 1 per candidate on MFMA too (sn_puct_mlp_mfma)
-                    mlp = L.sn_puct_mlp_mfma
-                    wargs = (nat.ptr(w1s), nat.ptr(self._net.w2q()), nat.ptr(head), nat.ptr(logits), st)
-                else:
-                    mlp = L.sn_puct_mlp_seats
-                    wargs = (nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p), nat.ptr(head), nat.ptr(logits), st)
-                lp = nat.ptr(logits)
-                RB, nmc = self.deal_batch, self.n_mc(n)
-                if self.fused_rollouts and RB > 0 and 3 <= N <= 8:
-                    rob = self._deal_buf(RB)
-                    w2q = self._net.w2q() if self.mlp_layer1 == "mfma" else None
-                    for r0 in range(0, nmc, RB):
-                        nr = min(RB, nmc - r0)
-                        nat.check(L.sn_puct_deal_batch(h, qr, r0, nr, rob.data_ptr(), st), "sn_puct_deal_batch")
-                        if w2q is not None:
-                            nat.check(L.sn_puct_rollouts_mfma(h, qr, r0, nr, rob.data_ptr(), nat.ptr(w1s), nat.ptr(w2q),
-                                                              nat.ptr(head), st), "sn_puct_rollouts_mfma")
-                        else:
-                            nat.check(L.sn_puct_rollouts(h, qr, r0, nr, rob.data_ptr(), nat.ptr(w1s), nat.ptr(w1c),
-                                                         nat.ptr(w2p), nat.ptr(head), st), "sn_puct_rollouts")
-                    self.rows_evaluated += nmc * S * (n * (n + 1) // 2)
-                    return
-                if RB > 0:
-                    rob = self._deal_buf(RB)
-                    stride = self.D * 48 * 4  # bytes of one rollout's states
-                for r in range(nmc):
-                    q.rollout = r
-                    if RB > 0:
-                        if r % RB == 0:
-                            nat.check(L.sn_puct_deal_batch(h, qr, r, min(RB, nmc - r), rob.data_ptr(), st),
-                                      "sn_puct_deal_batch")
-                        q.rollouts = rob.data_ptr() + (r % RB) * stride
-                    else:
-                        nat.check(deal(h, qr, st), "sn_puct_deal")
-                    for t in range(n):
-                        nat.check(mlp(h, qr, n - t, *wargs), "sn_puct_mlp_seats")
-                        nat.check(step(h, qr, lp, t, n - t, st), "sn_puct_step")
-                q.rollouts = self.ro.data_ptr()
+            logits = self._fused_bufs()
+            # the arguments built once (the league's engines run this loop eagerly: host time per launch)
+            qr, deal, step, mlp = ctypes_ref(q), L.sn_puct_deal, L.sn_puct_step, L.sn_puct_mlp_seats
+            wargs = (nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p), nat.ptr(head), nat.ptr(logits), st)
+            lp = nat.ptr(logits)
+            RB, nmc = self.deal_batch, self.n_mc(n)
+            if self.fused_rollouts and RB > 0 and 3 <= N <= 8:
+                rob = self._deal_buf(RB)
+                for r0 in range(0, nmc, RB):
+                    nr = min(RB, nmc - r0)
+                    nat.check(L.sn_puct_deal_batch(h, qr, r0, nr, rob.data_ptr(), st), "sn_puct_deal_batch")
+                    nat.check(L.sn_puct_rollouts(h, qr, r0, nr, rob.data_ptr(), nat.ptr(w1s), nat.ptr(w1c),
+                                                 nat.ptr(w2p), nat.ptr(head), st), "sn_puct_rollouts")
                 self.rows_evaluated += nmc * S * (n * (n + 1) // 2)
                 return
-            for r in range(self.n_mc(n)):
+            if RB > 0:
+                rob = self._deal_buf(RB)
+                stride = self.D * 48 * 4  # bytes of one rollout's states
+            for r in range(nmc):
                 q.rollout = r
-                nat.check(L.sn_puct_deal(h, ctypes_ref(q), st), "sn_puct_deal")
+                if RB > 0:
+                    if r % RB == 0:
+                        nat.check(L.sn_puct_deal_batch(h, qr, r, min(RB, nmc - r), rob.data_ptr(), st),
+                                  "sn_puct_deal_batch")
+                    q.rollouts = rob.data_ptr() + (r % RB) * stride
+                else:
+                    nat.check(deal(h, qr, st), "sn_puct_deal")
                 for t in range(n):
-                    m = n - t
-                    if self.mlp_layer1 == "seats":
-                        self.rows_evaluated += S * m
-                        nat.check(L.sn_puct_mlp_seats(h, ctypes_ref(q), m, nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p),
-                                                      nat.ptr(head), nat.ptr(logits), st), "sn_puct_mlp_seats")
-                        nat.check(L.sn_puct_step(h, ctypes_ref(q), nat.ptr(logits), t, m, st), "sn_puct_step")
-                        continue
-                    nat.check(L.sn_puct_seat_rows(h, ctypes_ref(q), m, nat.ptr(rv), 56, nat.ptr(cards), st),
-                              "sn_puct_seat_rows")
-                    torch.mm(rv, w1t, out=bv)
-                    nat.check(L.sn_puct_mlp(h, ctypes_ref(q), m, nat.ptr(bv), 112, nat.ptr(w1c), nat.ptr(cards),
-                                            nat.ptr(w2p), nat.ptr(head), nat.ptr(logits), st), "sn_puct_mlp")
-                    self.rows_evaluated += S * m
-                    nat.check(L.sn_puct_step(h, ctypes_ref(q), nat.ptr(logits), t, m, st), "sn_puct_step")
+                    nat.check(mlp(h, qr, n - t, *wargs), "sn_puct_mlp_seats")
+                    nat.check(step(h, qr, lp, t, n - t, st), "sn_puct_step")
+            q.rollouts = self.ro.data_ptr()
+            self.rows_evaluated += nmc * S * (n * (n + 1) // 2)
             return
-        sp = self._net.split() if self.split_l1 else None
-        if sp is not None:
-            # layer 1 once per rollout seat + the card column per candidate
-            # (sn_puct_h1_cols), feature-major GEMMs with the biases inside,
-            # the head's first output row (bf16/f32) straight into sn_puct_step
-            w1a, H, kp, hidden, ha, w1c = sp
-            S = self.D * N
-            cols, cards, h1, zb = self._split_bufs(H, kp)
-            ct = cols[: 56 * S].view(56, S)
-            for r in range(self.n_mc(n)):
-                q.rollout = r
-                nat.check(L.sn_puct_deal(h, ctypes_ref(q), st), "sn_puct_deal")
-                for t in range(n):
-                    m = n - t
-                    R = S * m
-                    nat.check(L.sn_puct_seat_cols(h, ctypes_ref(q), m, nat.ptr(ct), 56, nat.ptr(cards), bf16, st),
-                              "sn_puct_seat_cols")
-                    base = torch.mm(w1a, ct)  # [H, S]
-                    hv = h1[: kp * R].view(kp, R)
-                    nat.check(L.sn_puct_h1_cols(h, ctypes_ref(q), m, nat.ptr(base), H, nat.ptr(w1c), nat.ptr(cards),
-                                                nat.ptr(hv), kp, bf16, st), "sn_puct_h1_cols")
-                    with torch.no_grad():
-                        x = hv
-                        for wa in hidden:
-                            x = torch._addmm_activation(zb[:R], wa, x)
-                        out = torch.mm(ha, x)  # [16, R]: row 0 = the policy logits
-                    self.rows_evaluated += R
-                    q.logit_stride, q.logit_bf16 = 1, int(out.dtype == torch.bfloat16)
-                    nat.check(L.sn_puct_step(h, ctypes_ref(q), nat.ptr(out), t, m, st), "sn_puct_step")
-                    q.logit_stride, q.logit_bf16 = 0, 0
-            return
+        # any other net (fp32, other widths or depths): the candidate rows + the net's forward
         bufs = self._bufs(n)
         views = {m: bufs[m][: self.D * N * m] for m in range(1, n + 1)}  # this batch's decisions
         for r in range(self.n_mc(n)):
@@ -486,20 +351,6 @@ class BatchedPUCT:
                 nat.check(L.sn_puct_rows(h, ctypes_ref(q), m, nat.ptr(views[m]), bf16, st), "sn_puct_rows")
                 nat.check(L.sn_puct_step(h, ctypes_ref(q), nat.ptr(self._logits(views[m])), t, m, st), "sn_puct_step")
 
-    def _split_bufs(self, H, kp):
-        """seat columns [56][D_max*N], candidate cards [D_max*N*10] f32, the
-        layer-1 activations [kp][rows] and a zero epilogue bias [rows] (flat:
-        views of these serve every hand size)"""
-        N = self.env.num_players
-        if getattr(self, "_sbufs", None) is None or self._sbufs[2].numel() != kp * self.D_max * N * 10:
-            dev = self.env.device
-            S = self.D_max * N
-            self._sbufs = (torch.empty((56 * S,), dtype=self.net_dtype, device=dev),
-                           torch.empty((S * 10,), dtype=torch.float32, device=dev),
-                           torch.empty((kp * S * 10,), dtype=self.net_dtype, device=dev),
-                           torch.zeros((S * 10,), dtype=self.net_dtype, device=dev))
-        return self._sbufs
-
     def _deal_buf(self, RB):
         """[RB][D_max][48] int32: the initial states of RB rollouts (sn_puct_deal_batch)"""
         if getattr(self, "_robuf", None) is None or self._robuf.shape[0] != RB:
@@ -507,15 +358,10 @@ class BatchedPUCT:
         return self._robuf
 
     def _fused_bufs(self):
-        """seat rows [D_max*N][56] bf16, cards [D_max*N*10] f32, base
-        [D_max*N][112] bf16, logits [D_max*N*10] f32"""
+        """the rollout logits [D_max*N*10] f32 of sn_puct_mlp_seats"""
         S = self.D_max * self.env.num_players
-        if getattr(self, "_fbufs", None) is None or self._fbufs[0].shape[0] != S:
-            dev = self.env.device
-            self._fbufs = (torch.empty((S, 56), dtype=torch.bfloat16, device=dev),
-                           torch.empty((S * 10,), dtype=torch.float32, device=dev),
-                           torch.empty((S, 112), dtype=torch.bfloat16, device=dev),
-                           torch.empty((S * 10,), dtype=torch.float32, device=dev))
+        if getattr(self, "_fbufs", None) is None or self._fbufs.shape[0] != S * 10:
+            self._fbufs = torch.empty((S * 10,), dtype=torch.float32, device=self.env.device)
         return self._fbufs
 
     def _bufs(self, n):

@@ -186,14 +186,12 @@ class VecSechsNimmtEnv:
 
     # ------------------------------------------------------------ numpy RNG bridge
     def set_option(self, ring_words=None, chunk_steps=None, pipeline=None, pipe_gpw=None, pipe_lead=None,
-                   play_split=None, play_quad=None, twist_round=None, twist_every=None, pipe_fused=None):
+                   play_split=None, twist_round=None, twist_every=None, twist_skip=None):
         """rollout tuning (include/sechs.h SN_OPT_*; all numpy-compat only except play_split,
-        the role-split kernel of philox handles; play_quad: four lanes per game on the
-        pipelined 4-player path, k_play_quad; twist_round: whole-round MT twists in
-        k_mt_ahead; twist_every: one twist-ahead launch per K = 1 .. 5 play launches; pipe_fused:
-        k_play_quad twists the rounds itself, no side stream); results never
-        depend on it
-        (except pipe_lead < 600, a test knob that makes overruns -- PipeOverrunError -- likely)"""
+        the role-split kernel of philox handles; twist_round: whole-round MT twists in
+        k_mt_ahead; twist_every: one twist-ahead launch per K = 1 .. 5 play launches); results never
+        depend on it (except the test knobs pipe_lead < 600 and twist_skip = 1, which make
+        overruns -- PipeOverrunError -- likely / certain)"""
         if pipe_lead is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPE_LEAD, int(pipe_lead)), "sn_set_option")
         if pipe_gpw is not None:
@@ -204,10 +202,8 @@ class VecSechsNimmtEnv:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_TWIST_EVERY, int(twist_every)), "sn_set_option")
         if twist_round is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_TWIST_ROUND, int(twist_round)), "sn_set_option")
-        if play_quad is not None:
-            nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PLAY_QUAD, int(play_quad)), "sn_set_option")
-        if pipe_fused is not None:
-            nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPE_FUSED, int(pipe_fused)), "sn_set_option")
+        if twist_skip is not None:
+            nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_TWIST_SKIP, int(twist_skip)), "sn_set_option")
         if pipeline is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPELINE, int(bool(pipeline))), "sn_set_option")
         if ring_words is not None:

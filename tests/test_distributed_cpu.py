@@ -218,6 +218,40 @@ def test_two_rank_bench_gather_places_tensors_on_the_collective_device():
     assert {op for op, _ in seen} == {"all_reduce", "all_gather"}
 
 
+def _gather_to_worker(rank, world, port, q):
+    """gather_league_records(rec, dst=0) -- the bench's rank-0
+    record gather for the Elo replay (dist.gather through gather_cat_to)"""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rl_6_nimmt import distributed as D
+
+    off, cnt = D.shard(rank, world, B)
+    rec = _league_records(off, cnt)
+    got = D.gather_league_records(rec, dst=0)
+    every = D.gather_league_records(rec)  # all_gather: the same rows on every rank
+    q.put((rank, None if got is None else got.numpy(), every.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gather_to_rank0_equals_all_gather():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_to_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (a, b)) for r, a, b in (q.get(timeout=240) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = _league_records(0, 2 * B).numpy()
+    assert res[1][0] is None  # dst=0: the other ranks receive nothing
+    assert np.array_equal(res[0][0], ref) and np.array_equal(res[0][0], res[0][1])
+    assert np.array_equal(res[1][1], ref)
+
+
 # ---------------------------------------------------------------- bench.py --gpus
 def test_bench_gpus_flag_launches_ranks_or_checks_the_launcher(monkeypatch):
     """`bench.py --gpus N`: under a launcher WORLD_SIZE must equal N; without

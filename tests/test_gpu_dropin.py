@@ -100,6 +100,8 @@ def test_env_dropin_trace_and_errors():
         env.step([5, 7])
     with pytest.raises(InvalidMoveException, match=r"Player 2 tried to play card 10, but their hand is \[7, 8\]"):
         env.step([5, 9, 50])
+    # sn_step1's per-seat trace words are 0 after an illegal step (include/sechs.h), not the last step's
+    assert not env._out[2 + 14 * 3: 2 + 15 * 3].any()
     (states, legal), rew, done, _ = env.step([5, 7, 51])  # state untouched by the failed step
     assert legal == [[6], [8], [50]]
 

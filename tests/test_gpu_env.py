@@ -28,9 +28,6 @@ def venv(*a, **k):
         env.set_option(twist_every=int(os.environ["SECHS_TEST_TWIST_EVERY"]))
     if env.rng == "numpy" and os.environ.get("SECHS_TEST_TWIST_ROUND"):
         env.set_option(twist_round=int(os.environ["SECHS_TEST_TWIST_ROUND"]))
-    # SECHS_TEST_PIPE_FUSED=1: k_play_quad with the twist folded in, where it applies
-    if env.rng == "numpy" and os.environ.get("SECHS_TEST_PIPE_FUSED"):
-        env.set_option(pipe_fused=int(os.environ["SECHS_TEST_PIPE_FUSED"]))
     return env
 
 
@@ -535,16 +532,46 @@ def test_pipelined_overrun_is_an_error(N, lead):
     from rl_6_nimmt._native import PipeOverrunError
 
     env = venv(4096, N, seed=1, rng="numpy")
-    # exact-lead twists beside every launch: whole-round ones (incl. the fused form) overshoot
-    # a short lead by up to a round, and a twist per two launches adds 300 words to
-    # it, so the first launches would not run dry -- the detection is the same
-    env.set_option(pipe_lead=lead, twist_round=0, twist_every=1, pipe_fused=0)
+    # exact-lead twists beside every launch: whole-round ones overshoot a short lead by up
+    # to a round, so the first launches would not run dry -- the detection is the same;
+    # the default schedule's own case is test_default_schedule_overrun_is_an_error
+    env.set_option(pipe_lead=lead, twist_round=0, twist_every=1)
     env.reset()
     with pytest.raises(PipeOverrunError):
         env.rollout(20, check=True)
     assert env.pipe_errors() > 0
     with pytest.raises(PipeOverrunError):
         env.rollout(10)
+
+
+@pytest.mark.parametrize("N", [4, 10])
+def test_default_schedule_overrun_is_an_error(N):
+    """VERDICT r05 #1a: the overrun detector under the DEFAULT pipeline (whole-
+    round twists, one twist per four play launches, 10-step launches at
+    N <= 4): SN_OPT_TWIST_SKIP makes every steady twist after the first
+    group's twist nothing, so the consumers run past the words the start-up
+    twist left (600 K = 2 400 words, ~12 episodes at N = 4) -- the play lanes
+    count perr, rollout(check=True) raises, sn_pipe_errors > 0, and the next
+    rollout raises from the sticky host mirror.  Until then the games equal
+    the oracle (the detector does not fire early)."""
+    from rl_6_nimmt._native import PipeOverrunError
+
+    B = 2048
+    env = venv(B, N, seed=3, rng="numpy")
+    env.set_option(twist_skip=1)
+    env.reset()
+    ref = O.VecOracle(B, N, rng_mode=O.RNG_NUMPY_MT, seed=3)
+    ref.reset()
+    out = env.rollout(40, want_actions=True, check=True)  # within the start-up lead: exact
+    rr, rd, ra, _ = ref.rollout(40)
+    assert np.array_equal(out["actions"].cpu().numpy(), ra) and np.array_equal(out["rewards"].cpu().numpy(), rr)
+    assert env.pipe_errors() == 0
+    with pytest.raises(PipeOverrunError):
+        env.rollout(200, check=True)
+    assert env.pipe_errors() > 0
+    with pytest.raises(PipeOverrunError):
+        env.rollout(10)
+    env.close()
 
 
 @pytest.mark.parametrize("plan", [(10, 10, 10, 10), (25, 1, 1, 7, 30), (3, 10, 10)])
@@ -597,42 +624,6 @@ def test_pipelined_full_size_across_streams():
     assert env.pipe_errors() == 0
 
 
-@pytest.mark.parametrize("B,summ", [(65536, True), (1000, True), (4104, False), (1008, False)])
-def test_quad_kernel_equals_one_lane_kernel(B, summ):
-    """k_play_quad (four lanes per game: seat / row lanes, DPP quad
-    reductions, SN_OPT_PLAY_QUAD) and the one-lane k_play consume the same
-    numpy-MT words and emit identical rewards, actions, done and int8 obs --
-    launch patterns 10 / 1 / 7 / 23 steps (episodes cross launches), with
-    and without obs; then hands, scores, results and the exported numpy
-    states agree, and a 1-game reference session check via the oracle."""
-    outs = {}
-    for quad in (2, 1, 0):  # 2: the fused form (SN_OPT_PIPE_FUSED, when B is a multiple of 16)
-        env = venv(B, 4, seed=77, rng="numpy", include_summaries=summ)
-        env.set_option(play_quad=min(quad, 1), pipe_fused=int(quad == 2))
-        env.reset()
-        got = []
-        for T, obs in ((10, True), (1, True), (7, False), (23, True)):
-            o = env.rollout(T, want_actions=True, want_obs=obs, check=True)
-            got.append({k: v.cpu().numpy() for k, v in o.items()})
-        s, e = env.results()
-        got.append({"hands": env.hands().cpu().numpy(), "scores": env.scores().cpu().numpy(),
-                    "sums": s.cpu().numpy(), "eps": e.cpu().numpy()})
-        got.append({f"mt{g}": np.append(*env.get_mt_state(g)) for g in (0, B // 3, B - 1)})
-        assert env.pipe_errors() == 0
-        outs[quad] = got
-        env.close()
-    for v in (2, 1):
-        for a, b in zip(outs[v], outs[0]):
-            assert a.keys() == b.keys()
-            for k in a:
-                assert np.array_equal(a[k], b[k]), (v, k)
-    ref = O.VecOracle(min(B, 256), 4, rng_mode=O.RNG_NUMPY_MT, seed=77)
-    ref.reset()
-    rr, rd, ra, ro = ref.rollout(10, include_summaries=summ, want_obs=True)
-    assert np.array_equal(outs[1][0]["rewards"][:, : min(B, 256)], rr)
-    assert np.array_equal(outs[1][0]["obs"][:, : min(B, 256), :, : O.obs_len(summ)], ro)
-
-
 _DEBUG_WORKLOAD = r"""
 import ctypes, sys, numpy as np, torch
 sys.path.insert(0, sys.argv[1])
@@ -646,14 +637,11 @@ cnt, line = ctypes.c_uint32(), ctypes.c_uint32()
 nat.check(L.sn_debug_failures(ctypes.byref(cnt), ctypes.byref(line), 1), "selftest")
 assert cnt.value == 1, cnt.value  # the deliberately failing check was counted
 for rng in ("numpy", "philox"):
-    for quad in (0, 1):
-        env = VecSechsNimmtEnv(8192, 4, seed=5, rng=rng)
-        if rng == "numpy":
-            env.set_option(play_quad=quad)
-        env.reset()
-        for T in (10, 3, 17):
-            env.rollout(T, want_actions=True, want_obs=True, check=rng == "numpy")
-        env.close()
+    env = VecSechsNimmtEnv(8192, 4, seed=5, rng=rng)
+    env.reset()
+    for T in (10, 3, 17):
+        env.rollout(T, want_actions=True, want_obs=True, check=rng == "numpy")
+    env.close()
 env = VecSechsNimmtEnv(1000, 3, seed=2, rng="numpy")
 env.reset()
 env.rollout(25, want_obs=True)

@@ -258,57 +258,6 @@ def test_graph_replay_equals_eager_search(dtype):
             assert torch.equal(u, v)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_layer1_split_equals_full_rows(dtype):
-    """sn_puct_seat_cols + the per-seat GEMM + sn_puct_h1_cols give the first
-    layer's activations of every candidate row, feature-major: relu(rows @
-    W1^T + b1) over sn_puct_rows' full [card, obs] rows (f32: to 1e-5; bf16:
-    the per-seat part is rounded once more, to 2 bf16 ulps), then the ones
-    feature and zero padding; and the augmented later layers + head equal the
-    module's own forward on those rows."""
-    import ctypes
-
-    from rl_6_nimmt import _native as nat
-
-    env, eng = _engine(B=64, dtype=dtype, mc_max=4, mc_per_card=2, seed=23)
-    N, n = env.num_players, 7
-    for t in range(10 - n):
-        env.step(eng.decide(10 - t))
-    net = eng.sync_net()
-    w1a, H, kp, hidden, ha, w1c = net.split()
-    w1, b1 = net.layers[0]
-    q = eng._params(n)
-    L, h, st = nat.lib(), env._h, env._stream()
-    eng.memorize()
-    nat.check(L.sn_puct_deal(h, ctypes.byref(q), st), "deal")
-    bf = int(dtype == torch.bfloat16)
-    tol = 1e-5 if dtype == torch.float32 else 2 ** -6
-    for m in (n, 3, 1):
-        S, R = eng.D * N, eng.D * N * m
-        rows = torch.empty((R, 48), dtype=dtype, device=env.device)
-        nat.check(L.sn_puct_rows(h, ctypes.byref(q), m, nat.ptr(rows), bf, st), "rows")
-        ref = torch.relu(rows.float() @ w1.float().t() + b1.float())
-        cols = torch.empty((56, S), dtype=dtype, device=env.device)
-        cards = torch.empty((R,), dtype=torch.float32, device=env.device)
-        nat.check(L.sn_puct_seat_cols(h, ctypes.byref(q), m, nat.ptr(cols), 56, nat.ptr(cards), bf, st), "seat_cols")
-        assert torch.equal(cols[1:48].t(), rows.view(S, m, 48)[:, 0, 1:]) and (cols[0] == 0).all()
-        assert (cols[48] == 1).all() and (cols[49:] == 0).all()
-        assert torch.equal(cards, rows[:, 0].float())
-        base = torch.mm(w1a, cols)
-        h1 = torch.empty((kp, R), dtype=dtype, device=env.device)
-        nat.check(L.sn_puct_h1_cols(h, ctypes.byref(q), m, nat.ptr(base), H, nat.ptr(w1c), nat.ptr(cards),
-                                    nat.ptr(h1), kp, bf, st), "h1_cols")
-        assert torch.allclose(h1[:H].t().float(), ref, rtol=tol, atol=tol), (h1[:H].t().float() - ref).abs().max()
-        assert (h1[H] == 1).all() and (h1[H + 1:] == 0).all()
-        x = h1
-        for wa in hidden:
-            x = torch._addmm_activation(torch.zeros(R, dtype=dtype, device=env.device), wa, x)
-        out = torch.mm(ha, x)[0].float()
-        with torch.no_grad():
-            (want,) = net.module(rows)
-        assert torch.allclose(out, want[:, 0].float(), rtol=4 * tol, atol=4 * tol), (out - want[:, 0].float()).abs().max()
-
-
 def test_search_statistics_consistent_bf16_full_size():
     """Config 4's shape: 8192 games, every seat searching, bf16 net through
     the layer-1 split and the padded head's strided bf16 logits; one
@@ -550,14 +499,14 @@ def test_batched_customed_learning_step_changes_weights():
 
 @pytest.mark.parametrize("B,n", [(64, 7), (37, 10), (256, 4), (10000, 8)])
 def test_fused_mlp_equals_module_forward(B, n):
-    """sn_puct_seat_rows + the per-seat GEMM + sn_puct_mlp (layer 1's card
-    column + ReLU, layer 2 + ReLU and the head in one MFMA kernel) give every
-    rollout candidate's policy logit: equal to the split PyTorch path's
-    logits computed in f32 from the same bf16 activations (to f32 summation
-    order), and to the module's own bf16 forward on the full rows (to the
-    bf16 tolerance of test_layer1_split_equals_full_rows).  Ragged row counts
-    (a short last 64-row tile) included; B = 10 000 gives sn_puct_mlp_seats'
-    persistent workgroups several 64-seat groups each."""
+    """sn_puct_mlp_seats (seat rows, layer 1's per-seat part on MFMA, the
+    card column + ReLU, layer 2 + ReLU and the head in one kernel) gives
+    every rollout candidate's policy logit: equal to the same factored
+    arithmetic restated in PyTorch f32 from the same bf16 values (to f32
+    summation order: a bf16 ulp of the seat base here and there), and to
+    the module's own bf16 forward on the full rows.  Ragged row counts (a
+    short last 64-row tile) included; B = 10 000 gives the persistent
+    workgroups several 64-seat groups each."""
     env, eng = _engine(B=B, dtype=torch.bfloat16, mc_max=4, mc_per_card=2, seed=29)
     for t in range(10 - n):
         env.step(eng.decide(10 - t))
@@ -565,19 +514,21 @@ def test_fused_mlp_equals_module_forward(B, n):
 
 
 def _check_mlp_kernels(env, eng, n, live=None):
-    """the rollout-logit kernels against the split PyTorch path and the
-    module's forward at n_cur = n, 3, 1 (rows the decision list's rollouts
-    would evaluate); live: bool [D * N] -- seats of the rollouts' games
-    (a tournament game of k < N players has N - k absent seats, whose
-    logits are never read), None = all"""
+    """the rollout-logit kernel against its factored arithmetic restated in
+    PyTorch and the module's forward at n_cur = n, 3, 1 (rows the decision
+    list's rollouts would evaluate); live: bool [D * N] -- seats of the
+    rollouts' games (a tournament game of k < N players has N - k absent
+    seats, whose logits are never read), None = all"""
     import ctypes
 
     from rl_6_nimmt import _native as nat
 
     N = env.num_players
     net = eng.sync_net()
-    w1t, w1c, w2p, head, w1s = net.fused()
-    w1a, H, kp, hidden, ha, w1c_s = net.split()
+    w1c, w2p, head, w1s = net.fused()
+    w1, b1 = net.layers[0]
+    w2, b2 = net.layers[1]
+    H = w1.shape[0]
     q = eng._params(n)
     L, h, st = nat.lib(), env._h, env._stream()
     eng.memorize()
@@ -589,60 +540,40 @@ def _check_mlp_kernels(env, eng, n, live=None):
             live.to(env.device).repeat_interleave(m)
         rows = torch.empty((R, 48), dtype=torch.bfloat16, device=env.device)
         nat.check(L.sn_puct_rows(h, ctypes.byref(q), m, nat.ptr(rows), 1, st), "rows")
-        srows = torch.empty((S, 56), dtype=torch.bfloat16, device=env.device)
-        cards = torch.empty((R,), dtype=torch.float32, device=env.device)
-        nat.check(L.sn_puct_seat_rows(h, ctypes.byref(q), m, nat.ptr(srows), 56, nat.ptr(cards), st), "seat_rows")
-        cols = torch.empty((56, S), dtype=torch.bfloat16, device=env.device)
-        cards2 = torch.empty((R,), dtype=torch.float32, device=env.device)
-        nat.check(L.sn_puct_seat_cols(h, ctypes.byref(q), m, nat.ptr(cols), 56, nat.ptr(cards2), 1, st), "seat_cols")
-        torch.cuda.synchronize()
-        ls = sel.view(S, m)[:, 0]
-        assert torch.equal(srows[ls], cols.t()[ls]) and torch.equal(cards[sel], cards2[sel])  # the same features, seat-major
-        base = torch.mm(srows, w1t)
-        logits = torch.empty((R,), dtype=torch.float32, device=env.device)
-        nat.check(L.sn_puct_mlp(h, ctypes.byref(q), m, nat.ptr(base), 112, nat.ptr(w1c), nat.ptr(cards), nat.ptr(w2p),
-                                nat.ptr(head), nat.ptr(logits), st), "mlp")
-        torch.cuda.synchronize()
-        # the split path's activations (bf16 GEMM outputs), its head in f32
-        h1 = torch.relu(base[:, :H].float().repeat_interleave(m, dim=0) + cards[:, None] * w1c[None, :H])
-        h1 = torch.cat((h1.to(torch.bfloat16), torch.ones((R, 1), dtype=torch.bfloat16, device=env.device)), dim=1)
-        w2, b2 = net.layers[1]
-        x2 = torch.relu(h1[:, :H].float() @ w2.float().t() + b2.float()).to(torch.bfloat16).float()
-        ref = x2 @ net.head_w[:, 0].float() + net.head_b[0].float()
-        assert torch.allclose(logits[sel], ref[sel], rtol=1e-3, atol=1e-3), (logits - ref)[sel].abs().max()
-        with torch.no_grad():
-            (want,) = net.module(rows)
-        want = want[:, 0].float()
-        assert torch.allclose(logits[sel], want[sel], rtol=4 * tol, atol=4 * tol), (logits - want)[sel].abs().max()
-        # layer 1's per-seat part inside the kernel too (sn_puct_mlp_seats): its base is the MFMA product
-        # rounded to bf16 like the GEMM's, in another summation order (a bf16 ulp here and there)
         lg2 = torch.full((R,), float("nan"), dtype=torch.float32, device=env.device)
         nat.check(L.sn_puct_mlp_seats(h, ctypes.byref(q), m, nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p), nat.ptr(head),
                                       nat.ptr(lg2), st), "mlp_seats")
         torch.cuda.synchronize()
+        # the factored arithmetic: base = bf16(W1 [0, obs] + b1) per seat, h1 = bf16(relu(base + card w1c)),
+        # h2 = bf16(relu(W2 h1 + b2)), logit = wh . h2 + bh (f32 accumulation throughout)
+        seat = rows.view(S, m, 48)[:, 0].float().clone()
+        seat[:, 0] = 0.0
+        base = (seat @ w1.float().t() + b1.float()).to(torch.bfloat16).float()
+        h1 = torch.relu(base.repeat_interleave(m, dim=0) + rows[:, :1].float() * w1c[None, :H]).to(torch.bfloat16)
+        x2 = torch.relu(h1.float() @ w2.float().t() + b2.float()).to(torch.bfloat16).float()
+        ref = x2 @ net.head_w[:, 0].float() + net.head_b[0].float()
         assert not torch.isnan(lg2[sel]).any()
-        assert torch.allclose(lg2[sel], logits[sel], rtol=2 * tol, atol=2 * tol), (lg2 - logits)[sel].abs().max()
-        assert torch.allclose(lg2[sel], want[sel], rtol=4 * tol, atol=4 * tol)
-        # layer 1 per candidate on MFMA too (sn_puct_mlp_mfma): ONE bf16 rounding of W1 row + b1, as the
-        # module's forward on full rows -- closer to it than the factored kernels
-        lg3 = torch.full((R,), float("nan"), dtype=torch.float32, device=env.device)
-        nat.check(L.sn_puct_mlp_mfma(h, ctypes.byref(q), m, nat.ptr(w1s), nat.ptr(net.w2q()), nat.ptr(head),
-                                     nat.ptr(lg3), st), "mlp_mfma")
-        torch.cuda.synchronize()
-        assert not torch.isnan(lg3[sel]).any()
-        assert torch.allclose(lg3[sel], want[sel], rtol=2 * tol, atol=2 * tol), (lg3 - want)[sel].abs().max()
+        assert torch.allclose(lg2[sel], ref[sel], rtol=2 * tol, atol=2 * tol), (lg2 - ref)[sel].abs().max()
+        with torch.no_grad():
+            (want,) = net.module(rows)
+        want = want[:, 0].float()
+        assert torch.allclose(lg2[sel], want[sel], rtol=4 * tol, atol=4 * tol), (lg2 - want)[sel].abs().max()
 
 
-def test_fused_and_split_rollouts_agree_in_law():
-    """a whole PUCT search with the fused MLP and with the PyTorch split path
-    (same weights, same Philox streams): the f32 vs bf16 logits may flip a
-    sample now and then, so the searches agree in law -- mean root visit
-    counts and chosen moves match closely over 2 048 decisions"""
+def test_fused_and_rows_rollouts_agree_in_law(monkeypatch):
+    """a whole PUCT search with the one-kernel MLP (the default) and with the
+    generic path (candidate rows + the module's PyTorch forward; same
+    weights, same Philox streams): the two bf16 roundings of the factored
+    layer 1 may flip a sample now and then, so the searches agree in law --
+    mean root visit counts and chosen moves match closely over 2 048
+    decisions"""
+    from rl_6_nimmt.puct import FusedMLP
+
     res = {}
     for fused in (True, False):
+        if not fused:
+            monkeypatch.setattr(FusedMLP, "fused", lambda self: None)
         env, eng = _engine(B=512, dtype=torch.bfloat16, mc_max=20, mc_per_card=10, seed=41)
-        eng.fused_mlp = fused
-        eng.mlp_layer1 = "gemm"  # the GEMM form (the one-launch form, the default: the statistics test and the bench)
         acts = eng.decide(10)
         torch.cuda.synchronize()
         res[fused] = (acts.clone(), eng.stats.clone(), eng.rows_evaluated)
@@ -680,8 +611,8 @@ def test_league_puct_kernels_on_tournament_decisions(monkeypatch):
     on a BatchedTournament decision list (a PUCT agent among DrunkHamsters,
     2..4 players): the whole-rollout kernel (sn_puct_rollouts),
     k_puct_step_seats and the one-lane k_puct_step give identical records
-    over whole games (the same Philox uniforms, the same cards), and on the live seats of a fresh deal's decision list the fused
-    rollout-logit kernels equal the split PyTorch path and the module's
+    over whole games (the same Philox uniforms, the same cards), and on the live seats of a fresh deal's decision list the
+    rollout-logit kernel equals its factored arithmetic and the module's
     forward (_check_mlp_kernels)"""
     from rl_6_nimmt import _native as nat
     from rl_6_nimmt.agents import DrunkHamster, PUCTAgent
@@ -733,7 +664,7 @@ def test_batched_deal_equals_per_rollout_deals(monkeypatch):
     for rb in ("16", "0", "3"):
         monkeypatch.setenv("SECHS_PUCT_DEAL_BATCH", rb)
         env, eng = _engine(B=300, dtype=torch.bfloat16, mc_max=12, mc_per_card=3, seed=17)
-        assert eng.mlp_layer1 in ("seats", "mfma") and eng.deal_batch == int(rb)
+        assert eng.deal_batch == int(rb)
         acts = [eng.decide(10).clone()]
         env.step(acts[-1])
         acts.append(eng.decide(9).clone())
@@ -751,11 +682,7 @@ def test_fused_rollouts_equal_step_launches(monkeypatch):
     whole PUCT search gives identical statistics, histograms and moves --
     4 players (one 16-decision group per 64 seats) and 3 players (48 live
     seat rows per group), a ragged last group"""
-    cases = [(4, 300, "seats"), (3, 97, "seats")]
-    if os.environ.get("SECHS_TEST_MF_ROLLOUTS"):  # sn_puct_rollouts_mfma (opt-in form) vs sn_puct_mlp_mfma + step
-        cases.append((4, 300, "mfma"))
-    for N, B, l1 in cases:
-        monkeypatch.setenv("SECHS_MLP_LAYER1", l1)  # "mfma": sn_puct_rollouts_mfma vs sn_puct_mlp_mfma + step
+    for N, B in [(4, 300), (3, 97)]:
         res = {}
         for rollouts in ("1", "0"):
             monkeypatch.setenv("SECHS_PUCT_ROLLOUTS", rollouts)
@@ -801,8 +728,7 @@ def test_mlp_seats_kernel_matches_fp32_reference_net(n):
     observations): every logit within the derived first-order bf16 bound
     (x 1.25 for the second-order terms), and every candidate's softmax
     probability (mcts.py:219-228) within p * (exp(2 * 1.25 * max bound) - 1).
-    Both rollout kernels: sn_puct_mlp_seats (layer 1 factored per seat, two
-    bf16 roundings) and sn_puct_mlp_mfma (layer 1 per candidate, one)."""
+    (Layer 1 is factored per seat: two bf16 roundings.)"""
     import ctypes
 
     from rl_6_nimmt import _native as nat
@@ -814,7 +740,7 @@ def test_mlp_seats_kernel_matches_fp32_reference_net(n):
     for t in range(10 - n):
         env.step(eng.decide(10 - t))
     net = eng.sync_net()
-    w1t, w1c, w2p, head, w1s = net.fused()
+    w1c, w2p, head, w1s = net.fused()
     q = eng._params(n)
     L, h, st = nat.lib(), env._h, env._stream()
     eng.memorize()
@@ -827,16 +753,12 @@ def test_mlp_seats_kernel_matches_fp32_reference_net(n):
         R = eng.D * N * m
         rows = torch.empty((R, 48), dtype=torch.float32, device=env.device)
         nat.check(L.sn_puct_rows(h, ctypes.byref(q), m, nat.ptr(rows), 0, st), "rows f32")
-        for kern in ("seats", "mfma"):  # the factored kernel (two layer-1 roundings) and the per-candidate one
+        for kern in ("seats",):  # the factored kernel (two layer-1 roundings)
             lg = torch.full((R,), float("nan"), dtype=torch.float32, device=env.device)
-            if kern == "seats":
-                nat.check(L.sn_puct_mlp_seats(h, ctypes.byref(q), m, nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p),
-                                              nat.ptr(head), nat.ptr(lg), st), "mlp_seats")
-            else:
-                nat.check(L.sn_puct_mlp_mfma(h, ctypes.byref(q), m, nat.ptr(w1s), nat.ptr(net.w2q()), nat.ptr(head),
-                                             nat.ptr(lg), st), "mlp_mfma")
+            nat.check(L.sn_puct_mlp_seats(h, ctypes.byref(q), m, nat.ptr(w1s), nat.ptr(w1c), nat.ptr(w2p),
+                                          nat.ptr(head), nat.ptr(lg), st), "mlp_seats")
             torch.cuda.synchronize()
-            ref, bound = _bf16_forward_bound(rows.double().cpu(), layers, hw, hb, l1_roundings=2 if kern == "seats" else 1)
+            ref, bound = _bf16_forward_bound(rows.double().cpu(), layers, hw, hb, l1_roundings=2)
             got = lg.double().cpu()
             assert not torch.isnan(got).any()
             err = (got - ref).abs()

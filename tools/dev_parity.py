@@ -22,13 +22,10 @@ def main():
     T = int(sys.argv[2]) if len(sys.argv) > 2 else 30
     N = 4
     split = int(os.environ.get("SECHS_PLAY_SPLIT", "1"))  # 0..3 (SN_OPT_PLAY_SPLIT)
-    quad = int(os.environ.get("SECHS_PLAY_QUAD", "0"))  # SN_OPT_PLAY_QUAD
     for rng, mode in (("numpy", O.RNG_NUMPY_MT), ("philox", O.RNG_PHILOX)):
         for want_obs in (True, False):
             env = VecSechsNimmtEnv(B, N, seed=11, rng=rng, device="cuda:0")
             env.set_option(play_split=split)
-            if rng == "numpy":
-                env.set_option(play_quad=quad)
             env.reset()
             ref = O.VecOracle(B, N, rng_mode=mode, seed=11)
             ref.reset()

@@ -18,6 +18,7 @@ playout (quirk Q6) -- here that method is replaced by its decision logic
 without the debug lines (same best move, same info), so such games finish
 as the batched engine finishes them.  Usage:
     PYTHONDONTWRITEBYTECODE=1 python tools/gen_puct_stats.py [games] [workers]
+    SECHS_F14_MC_MAX=100 ... -> F14b, tests/golden/puct_search_mc100.json
 """
 import json
 import multiprocessing as mp
@@ -29,8 +30,11 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
-OUT = os.path.join(ROOT, "tests", "golden", "puct_search.json")
-MC_MAX = 20
+MC_MAX = int(os.environ.get("SECHS_F14_MC_MAX", "20"))
+# F14 (mc_max 20, first decision) keeps its file; F14b (mc_max 100, the reference's default budget,
+# mcts.py:25) records seat 0's decisions at n = 10, 6 and 3 into its own.
+OUT = os.path.join(ROOT, "tests", "golden", "puct_search.json" if MC_MAX == 20 else f"puct_search_mc{MC_MAX}.json")
+DEC_N = (10, 6, 3)
 
 
 def _worker(args):
@@ -54,10 +58,12 @@ def _worker(args):
         for action, outcome in outcomes.items():
             if np.mean(outcome) > best_mean:
                 best_action, best_mean = action, np.mean(outcome)
-        if len(outcomes) == 10 and "visits" not in first and getattr(self, "_seat0", False):
-            first["legal"] = [int(a) for a in outcomes]
-            first["visits"] = [len(o) for o in outcomes.values()]
-            first["chosen"] = int(best_action)
+        n = len(outcomes)
+        if n in DEC_N and getattr(self, "_seat0", False) and str(n) not in first.setdefault("dec", {}):
+            first["dec"][str(n)] = {"legal": [int(a) for a in outcomes], "visits": [len(o) for o in outcomes.values()],
+                                    "chosen": int(best_action)}
+            if n == 10:
+                first["legal"], first["visits"], first["chosen"] = (first["dec"]["10"][k] for k in ("legal", "visits", "chosen"))
         return best_action, {"log_prob": log_probs[best_action][0]}
 
     BaseMCAgent._choose_action_from_outcomes = choose
@@ -91,8 +97,11 @@ def _worker(args):
 
         env.reset = reset_and_record
         sess.play_game()
-        recs.append({"game": g, "board0": deal["board"], "hands0": deal["hands"],
-                     "results": [int(x) for x in sess.results[0]], **dict(first)})
+        rec = {"game": g, "board0": deal["board"], "hands0": deal["hands"],
+               "results": [int(x) for x in sess.results[0]], **dict(first)}
+        if MC_MAX == 20:
+            rec.pop("dec", None)  # F14's record format
+        recs.append(rec)
     return recs
 
 
@@ -108,7 +117,8 @@ def main():
     doc = {
         "protocol": f"np.random.seed(g); torch.manual_seed(10000 + g); GameSession(PUCTAgent(mc_max={MC_MAX}) with the F8 "
                     "weights (torch.manual_seed(0); PUCTAgent()), eval mode, DrunkHamster x 3).play_game(); g = 0.."
-                    f"{G - 1}; seat 0's first decision: legal cards, PUCT visit counts, chosen card",
+                    f"{G - 1}; seat 0's " + ("first decision" if MC_MAX == 20 else "decisions at n = 10, 6, 3 (dec[n])")
+                    + ": legal cards, PUCT visit counts, chosen card",
         "deviation": "mcts.py:165-170 debug f-string removed (it raises IndexError when a legal move got no playout, "
                      "quirk Q6); the decision itself is the reference's",
         "mc_max": MC_MAX, "mc_per_card": 10, "c_puct": 2.0,

@@ -35,8 +35,6 @@ def main():
     env = VecSechsNimmtEnv(B, N, seed=0, rng=rng, device="cuda:0")
     if len(sys.argv) > 4:
         env.set_option(play_split=int(sys.argv[4]))
-    if rng == "numpy" and "SECHS_PLAY_QUAD" in os.environ:  # k_play_quad (1) or the one-lane k_play (0)
-        env.set_option(play_quad=int(os.environ["SECHS_PLAY_QUAD"]))
     env.reset()
     dev = env.device
     out = {

@@ -5,9 +5,13 @@ traffic, with the gfx950 corrections of /opt/skills/guides/MI355X_MICROARCH.md
 coalesced streams, so it is doubled (an upper estimate for narrower
 accesses); WRITE_SIZE is exact for 16-B-per-lane stores.
 
-KERNELS is one or more kernel-name substrings separated by '|'; the traffic of
-a bench step is the sum over them of each kernel's mean per dispatch (one
-dispatch of each per step).
+KERNELS is one or more kernel-name substrings separated by '|'.  Each gets its
+mean traffic per dispatch and its dispatch count; the FIRST kernel is the play
+launch that defines a bench step, and every other kernel is priced per step by
+its measured dispatches per play dispatch (the K-group pipeline runs one
+steady twist, k_mt_ahead<false, per K play launches).  A kernel whose name
+matches `k_mt_ahead<true` (the pipeline's start-up twist, once per pipeline
+start, not per step) is recorded but left out of the step traffic.
 
 usage: pmc_traffic.py FETCH_CSV WRITE_CSV KERNELS OUT_JSON [note]
 """
@@ -31,7 +35,9 @@ def main():
     rec = {"kernels": {}, "correction": "FETCH_SIZE x2 (gfx950 wide-stream under-count), KB -> bytes x1024",
            "note": note}
     tot = 0.0
-    for k in kernels.split("|"):
+    names = kernels.split("|")
+    plays = None
+    for k in names:
         f = per_dispatch(fetch_csv, k, "FETCH_SIZE")
         w = per_dispatch(write_csv, k, "WRITE_SIZE")
         if not f or not w:  # a kernel this path does not launch
@@ -41,7 +47,18 @@ def main():
         rec["kernels"][k] = {"dispatches": {"fetch": len(f), "write": len(w)}, "fetch_size_kb_raw": f_kb,
                              "write_size_kb_raw": w_kb, "fetch_bytes_corrected": 2.0 * f_kb * 1024.0,
                              "write_bytes": w_kb * 1024.0, "traffic_bytes_per_dispatch": b}
-        tot += b
+        if plays is None:
+            plays = len(f)
+        ratio = len(f) / plays
+        rec["kernels"][k]["dispatches_per_play_launch"] = ratio
+        if "k_mt_ahead<true" in k:
+            rec["kernels"][k]["in_step_traffic"] = False
+            continue
+        tot += b * ratio
+    rec["play_dispatches"] = plays
+    rec["step_traffic_bytes"] = tot
+    rec["step_traffic_rule"] = ("sum over kernels of traffic_bytes_per_dispatch x dispatches_per_play_launch "
+                                "(the start-up twist k_mt_ahead<true excluded)")
     rec["traffic_bytes_per_launch"] = tot
     json.dump(rec, open(out, "w"), indent=1)
     print(json.dumps(rec))
