@@ -78,6 +78,8 @@ def parse():
                     help="SN_OPT_PLAY_SPLIT (default: the library's)")
     ap.add_argument("--twist-round", type=int, default=None, choices=[0, 1],
                     help="SN_OPT_TWIST_ROUND: whole-round MT19937 twists in k_mt_ahead (default: the library's, 1)")
+    ap.add_argument("--pipe-dec", type=int, default=None, choices=[0, 1],
+                    help="SN_OPT_PIPE_DEC: decode-ahead records (k_decode) for k_play (default: the library's, 1)")
     ap.add_argument("--twist-every", type=int, default=None, choices=[1, 2, 3, 4, 5],
                     help="SN_OPT_TWIST_EVERY: one k_mt_ahead per 1 .. 5 play launches (default: the library's)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
@@ -204,9 +206,9 @@ def time_rollouts(env, out, steps, warmup, world):
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if env.rng != "numpy":
         return t1 - t0, kern_ms, {"k_play": kern_ms, "launches": steps}
-    play_ms, ahead_ms, n = env.kernel_times()
+    play_ms, ahead_ms, dec_ms, n = env.kernel_times(with_decode=True)
     env.time_kernels(0)
-    return t1 - t0, kern_ms, {"k_play": play_ms, "k_mt_ahead": ahead_ms, "launches": n}
+    return t1 - t0, kern_ms, {"k_play": play_ms, "k_mt_ahead": ahead_ms, "k_decode": dec_ms, "launches": n}
 
 
 def make_out(env, games, with_obs):
@@ -855,8 +857,8 @@ def main():
     B = args.games
     env = VecSechsNimmtEnv(B, N_PLAYERS, seed=0, game_offset=rank * B, rng=args.rng)
     if args.rng == "numpy":
-        env.set_option(pipe_gpw=args.pipe_gpw, play_split=args.play_split, 
-                       twist_round=args.twist_round, twist_every=args.twist_every)
+        env.set_option(pipe_gpw=args.pipe_gpw, play_split=args.play_split, twist_round=args.twist_round,
+                       twist_every=args.twist_every, pipe_dec=args.pipe_dec)
     env.reset()
     out = make_out(env, B, not args.no_obs)
     wall, kern_ms, kt = time_rollouts(env, out, args.steps, args.warmup, world)
@@ -888,6 +890,8 @@ def main():
     # reported beside it; the whole step is `step_ms`)
     play_ms = kt["k_play"]
     twist_k = args.twist_every or LIB_TWIST_EVERY
+    play_mode = ("RNG_PHILOX" if args.rng != "numpy" else
+                 "RNG_NUMPY_DEC" if (kt.get("k_decode") or 0.0) > 0.0 else "RNG_NUMPY_PIPE")
     achieved = launch_steps * ALGO_BYTES_PER_STEP / (play_ms * 1e-3) / 1e9
     per_kernel, traffic_src = pmc_traffic(args.rng, B) if not args.no_obs else (None, None)
     traffic = per_kernel.get("k_play<4") if per_kernel else None
@@ -928,7 +932,7 @@ def main():
             "traffic_unit": "HBM bytes per k_play launch (PMC FETCH_SIZE x2 + WRITE_SIZE, separate passes)",
             "traffic_source": traffic_src,
             "real_frac": real_frac,
-            "kernel": f"k_play<4, {'RNG_NUMPY_PIPE' if args.rng == 'numpy' else 'RNG_PHILOX'}>: 10 env-steps of 65536 games",
+            "kernel": f"k_play<4, {play_mode}>: 10 env-steps of 65536 games",
             "kernel_ms": play_ms,
             "kernel_ms_source": ("HIP events around each k_play launch on its stream (sn_kernel_times), over a second "
                                  "pass of the same launches right after the timed one" if args.rng == "numpy" else
@@ -940,6 +944,10 @@ def main():
             "concurrent": ({"kernel": "k_mt_ahead<false, true> (side stream: one dispatch per twist_every play "
                                       "launches, whole MT19937 rounds ahead of the consumer)",
                             "kernel_ms": kt.get("k_mt_ahead"),
+                            "decode_kernel": "k_decode<4> (side stream, after the group's twist: the next group's "
+                                             "episode records -- draws, deals, stream offsets -- for k_play<4, "
+                                             "RNG_NUMPY_DEC>; SN_OPT_PIPE_DEC)",
+                            "decode_kernel_ms": kt.get("k_decode"),
                             "traffic": per_kernel.get("k_mt_ahead") if per_kernel else None,
                             "traffic_unit": "HBM bytes per twist dispatch (PMC)"}
                            if args.rng == "numpy" else None),

@@ -174,6 +174,15 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          launch.
      SN_OPT_PIPE_FUSED   removed (round 6): the twist folded into k_play_quad,
                          measured slower; SN_EUNSUPPORTED.
+     SN_OPT_PIPE_DEC     1: pipelined numpy-compat DrunkHamster rollouts
+                         with auto-reset of a plain handle of N <= 4 whose games
+                         are in lockstep (after sn_reset) decode ahead: on the
+                         side stream, after each group's twist, k_decode walks
+                         every game's ring and writes one record per episode
+                         (its draws, the next deal's sorted hands and rows, the
+                         stream offsets), and k_play plays from the records
+                         with no RNG work; 0 (default): k_play draws from the ring.
+                         Same words, same outputs, same exported numpy states.
      SN_OPT_TWIST_SKIP   TEST KNOB: 1 = every steady twist after the first
                          group's twists nothing, so the default schedule
                          runs its ring dry (the SN_ERNG / sn_pipe_errors
@@ -184,7 +193,7 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
    the call. */
 enum { SN_OPT_RING_WORDS = 1, SN_OPT_CHUNK_STEPS = 2, SN_OPT_PIPELINE = 3, SN_OPT_TIMING = 4, SN_OPT_PIPE_GPW = 5,
        SN_OPT_PIPE_LEAD = 6, SN_OPT_PLAY_SPLIT = 7, SN_OPT_PLAY_QUAD = 8, SN_OPT_TWIST_ROUND = 9,
-       SN_OPT_TWIST_EVERY = 10, SN_OPT_PIPE_FUSED = 11, SN_OPT_TWIST_SKIP = 12 };
+       SN_OPT_TWIST_EVERY = 10, SN_OPT_PIPE_FUSED = 11, SN_OPT_TWIST_SKIP = 12, SN_OPT_PIPE_DEC = 13 };
 sn_status sn_set_option(sn_env* env, int option, int value);
 /* pipelined rollouts whose draws ran past the twisted words (must be 0; a
    nonzero count means those games' draws are wrong) [sync].  The count is
@@ -195,6 +204,9 @@ sn_status sn_pipe_errors(sn_env* env, uint32_t* count);
 /* mean launch duration (ms) of the pipelined k_play and k_mt_ahead launches
    recorded since SN_OPT_TIMING was set; *n = launches recorded [sync] */
 sn_status sn_kernel_times(sn_env* env, float* play_ms, float* ahead_ms, int32_t* n);
+/* the same, and the mean duration of the k_decode launches (decode-ahead
+   mode; 0 if none ran) [sync] */
+sn_status sn_kernel_times_dec(sn_env* env, float* play_ms, float* ahead_ms, float* decode_ms, int32_t* n);
 /* Diagnostics (no reference counterpart): shader-clock cycles every k_play
    wave spent per phase of its step loop since the last call, summed over
    waves -- out[0..10] = prologue, obs, draws, resolve, output stores, deck
@@ -206,6 +218,16 @@ sn_status sn_kernel_times(sn_env* env, float* play_ms, float* ahead_ms, int32_t*
    (-DSECHS_PHASE_PROF) records them; the product build returns
    SN_EUNSUPPORTED [sync]. */
 sn_status sn_debug_phases(uint64_t* out, int n);
+/* k_puct_rollouts phase counters of a -DSECHS_PHASE_PROF build (diagnostics):
+   out[0..4] = shader-clock cycles summed over waves in the state copy-in, the
+   seat rows, the per-seat layer-1 MFMA, the candidate tiles and the step;
+   out[7] = waves; read and cleared.  SN_EUNSUPPORTED in the product library. */
+sn_status sn_debug_puct_phases(uint64_t* out, int n);
+/* pipeline words to the host (tests, diagnostics) [sync]: what 0 = pabsc[slot]
+   (consumer positions, slot kPipeSlots = the decoder's; B words), 1 =
+   ptend[slot] (B words), 2 = decode-ahead record slot (kDecQuads x B 16-B
+   pieces, piece-major).  No pipeline state is changed. */
+sn_status sn_debug_pipe_words(sn_env* env, int what, int slot, uint32_t* out);
 /* Device-side invariant checks (SN_DASSERT in sechs_device.h / sechs_env.hip:
    a played card is in its seat's hand, the cards of a step are distinct, a
    card goes to a row ending below it (or undercuts), rows hold 1..5 cards,

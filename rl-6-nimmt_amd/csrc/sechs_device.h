@@ -51,7 +51,9 @@ constexpr int kMtM = 397;
 // RNG_NUMPY_RING(_HBM): numpy-MT words pre-twisted by k_mt_prep, read from
 // an LDS copy of the ring (or straight from HBM when LDS is short); k_play only
 // RNG_NUMPY_PIPE: numpy-MT words twisted ahead by k_mt_ahead (the pipelined ring); k_play only
-enum RngMode { RNG_PHILOX = 0, RNG_NUMPY_MT = 1, RNG_NUMPY_RING = 2, RNG_NUMPY_RING_HBM = 3, RNG_NUMPY_PIPE = 4 };
+// RNG_NUMPY_DEC: decode-ahead records (k_decode decoded the draws and the deals from the pipelined ring); k_play only
+enum RngMode { RNG_PHILOX = 0, RNG_NUMPY_MT = 1, RNG_NUMPY_RING = 2, RNG_NUMPY_RING_HBM = 3, RNG_NUMPY_PIPE = 4,
+               RNG_NUMPY_DEC = 5 };
 
 // --------------------------------------------------------------------------
 // bull heads, env.py:224-239

@@ -264,6 +264,7 @@ struct AheadArgs {
     int tout;  // ptend parity written
     int lead;  // words to keep twisted past the consumer (kPipeLead; smaller only to test the overrun path)
     uint32_t* perr_mirror;  // host-mapped copy of *perr, refreshed at launch start (off the play stream)
+    int cin_copy;  // INIT: also write the start position to this pabsc slot (-1: none; decode-ahead: the play slot)
 };
 
 // One whole MT19937 round of game G, twisted by the whole wave in LDS (w:
@@ -402,7 +403,10 @@ __global__ __launch_bounds__(kBlock) void k_mt_ahead(DevState s, AheadArgs a) {
                 ring[ring_byte(ri, g, B)] = (uint8_t)(mt_temper(v) & 0xFFu);
             }
         }
-        if (lane == 0u) s.pabsc[(int64_t)a.cin * B + g] = c;
+        if (lane == 0u) {
+            s.pabsc[(int64_t)a.cin * B + g] = c;
+            if (a.cin_copy >= 0) s.pabsc[(int64_t)a.cin_copy * B + g] = c;
+        }
     } else {
         Tp = s.ptp[g];
         t0 = s.ptend[(int64_t)a.tin * B + g];
@@ -632,7 +636,9 @@ struct PlayArgs {
     int32_t* invalid;        // [B]
     int32_t* league_rec;     // league: [episodes][B][1 + N] per finished game: seats word, results
     int step0;               // league: env-steps of this rollout before this launch (episode index of a record)
-    int n0;                  // k_play_split: every game's hand size at the launch's start (aligned handle)
+    int n0;                  // k_play_split: every game's hand size at the launch's start (aligned handle);
+                             // RNG_NUMPY_DEC: the launch's first step within its episode (0..9)
+    int drec0, drec1;        // RNG_NUMPY_DEC: record slots of the launch's episode and of the next one
 };
 
 // The env-step loop of one lane (game g).  R supplies the random words
@@ -672,6 +678,101 @@ struct StreamSrc {
         deal_from_deck<N>(deck, s.C, G);
 #pragma unroll
         for (int p = 0; p < N; p++) SN_DASSERT(hand_strict(G.hand[p]) && hand_len(G.hand[p]) == (uint32_t)kHand);
+    }
+};
+
+// ---- decode-ahead records (SN_OPT_PIPE_DEC, the default for lockstep
+// DrunkHamster rollouts of a numpy-compat handle, N <= 4) -----------------
+// Every random decision of such a rollout depends on the word stream only
+// (the draw maxima are n - 1 for the known hand size n, the deal's are
+// 103..1), so k_decode, on the side stream beside the play launches, walks
+// each game's pipelined ring a group of launches ahead and writes one record
+// per game and episode; k_play<RNG_NUMPY_DEC> then plays from the records
+// and issues no RNG work: no draws, no swap targets, no Fisher-Yates swaps,
+// no hand sorting.  Record of an episode, 24 dwords as kDecQuads u32x4
+// pieces at drec[(slot * kDecQuads + q) * B + g] (a wave's piece q of 64
+// games is one 1-KB run):
+//   w0       stream position where the record starts (the first decoded
+//            step: step phi0 of the pipeline's first episode, else step 0)
+//   w1..w5   off[t], t = 0..9 (u16 pairs): words consumed from w0 through
+//            step t's draws (t = 9: through the deal that ends the episode)
+//   w6..w10  step t's draws, t = 0..8 (u16 each: seat p's index at bits 4p;
+//            step 9 holds one card, numpy draws nothing)
+//   w11      the next deal's row cards r0..r3 (bytes, env.py:108-110)
+//   w12..w23 the next deal's hands, seat p at w12 + 3p: the sorted legal list
+//            as lo32, hi32, hi (bytes 8, 9 | 0xFFFF0000), env.py:104-107
+constexpr int kDecWords = 4 * kDecQuads;
+
+__device__ __forceinline__ uint32_t dec_u16(const uint32_t (&w)[kDecWords], int base, int t) {
+    // u16 t of the u16 array at dword `base` (t wave-uniform, 0..9)
+    uint32_t v = 0u;
+#pragma unroll
+    for (int k = 0; k < 5; k++) v = (t >> 1 == k) ? w[base + k] : v;
+    return (t & 1) ? (v >> 16) : (v & 0xFFFFu);
+}
+
+template <int N>
+struct DecSrc {
+    uint32_t A[kDecWords];  // the launch's episode
+    uint32_t B1[11];        // the next episode: w0..w10 (its draws, offsets), when the launch crosses into it
+    int phi;                // the launch's first step within its episode
+
+    __device__ __forceinline__ void load(const DevState& s, const PlayArgs& a, int64_t g, bool cross) {
+        phi = a.n0;
+        const u32x4* ra = s.drec + (int64_t)a.drec0 * kDecQuads * s.B + g;
+#pragma unroll
+        for (int q = 0; q < kDecQuads; q++) {
+            const u32x4 v = ra[(int64_t)q * s.B];
+            A[4 * q] = v.x, A[4 * q + 1] = v.y, A[4 * q + 2] = v.z, A[4 * q + 3] = v.w;
+        }
+#pragma unroll
+        for (int k = 0; k < 11; k++) B1[k] = 0u;
+        if (cross) {
+            const u32x4* rb = s.drec + (int64_t)a.drec1 * kDecQuads * s.B + g;
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                const u32x4 v = rb[(int64_t)q * s.B];
+                B1[4 * q] = v.x, B1[4 * q + 1] = v.y, B1[4 * q + 2] = v.z;
+                if (q < 2) B1[4 * q + 3] = v.w;
+            }
+        }
+    }
+    __device__ __forceinline__ void draws(const Game<N>&, int t, uint32_t, bool, uint32_t (&idx)[N]) {
+        const int tau = phi + t;  // wave-uniform
+        uint32_t v;
+        if (tau < kHand) {
+            v = (tau < kHand - 1) ? dec_u16(A, 6, tau) : 0u;
+        } else {
+            uint32_t w[kDecWords];
+#pragma unroll
+            for (int k = 0; k < kDecWords; k++) w[k] = (k < 11) ? B1[k] : 0u;
+            v = (tau - kHand < kHand - 1) ? dec_u16(w, 6, tau - kHand) : 0u;
+        }
+#pragma unroll
+        for (int p = 0; p < N; p++) idx[p] = (v >> (4 * p)) & 15u;
+    }
+    __device__ __forceinline__ uint32_t league(const DevState&) { return 0u; }
+    __device__ __forceinline__ void deal(const DevState&, Game<N>& G, PhaseProf&) {  // the next episode's deal
+#pragma unroll
+        for (int p = 0; p < N; p++) {
+            G.hand[p].lo = (uint64_t)A[12 + 3 * p] | ((uint64_t)A[13 + 3 * p] << 32);
+            G.hand[p].hi = A[14 + 3 * p];
+            G.score[p] = 0;
+        }
+        const uint32_t rw = A[11];
+        const uint32_t r0 = rw & 0xFFu, r1 = (rw >> 8) & 0xFFu, r2 = (rw >> 16) & 0xFFu, r3 = rw >> 24;
+        G.b.lo = u32x4{r0, r1, r2, r3};
+        G.b.hi = u32x4{meta_row(r0), meta_row(r1), meta_row(r2), meta_row(r3)};
+        G.n = kHand;
+    }
+    // the stream position after the launch's last step (what sn_pipe_sync exports)
+    __device__ __forceinline__ uint32_t position(int steps) const {
+        const int last = phi + steps - 1;
+        if (last < kHand) return A[0] + dec_u16(A, 1, last);
+        uint32_t w[kDecWords];
+#pragma unroll
+        for (int k = 0; k < kDecWords; k++) w[k] = (k < 11) ? B1[k] : 0u;
+        return w[0] + dec_u16(w, 1, last - kHand);
     }
 };
 
@@ -873,7 +974,13 @@ __device__ __forceinline__ void play_body(const DevState& s, const PlayArgs& a, 
     load_results<N>(s, g, a.flags, sum_res, episodes);
     uint32_t lg = LG ? s.lgs[g] : 0u;
     ByteBuf buf;
-    if constexpr (MODE == RNG_NUMPY_PIPE) {
+    if constexpr (MODE == RNG_NUMPY_DEC) {
+        DecSrc<N> src;
+        src.load(s, a, g, a.n0 + a.steps > kHand);
+        pp.mark(PH_PROLOGUE);
+        play_steps<N, DecSrc<N>, 64, false>(s, a, g, lane, wave_lds, G, src, sum_res, episodes, pp, lg, 0, a.steps);
+        s.pabsc[(int64_t)a.pipe_cout * s.B + g] = src.position(a.steps);  // the consumer position (sn_pipe_sync)
+    } else if constexpr (MODE == RNG_NUMPY_PIPE) {
         RingPipe rng;
         rng.load(s, g, buf, wave_lds + a.wave_lds - GPW * a.ring_lds + lane * a.ring_lds, a.pipe_cin, a.pipe_t);
         pp.mark(PH_PROLOGUE);
@@ -906,6 +1013,109 @@ template <int N, int MODE, int GPW = 64, bool LG = false>
 __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_dyn[];
     play_body<N, MODE, GPW, LG>(s, a, lds_dyn, (int)threadIdx.x);
+}
+
+// k_decode: the decode-ahead producer.  One lane per game walks its
+// pipelined ring from the decoder position (pabsc[kDecSlot]) and writes the
+// records of episodes e0 .. e0 + ne - 1 (slots mod kDecRecords): per step
+// the N DrunkHamster draws legal[random_interval(n - 1)] in seat order
+// (agents/random.py:9, play.py:38-41; n = 10 - t), after step 9 the next
+// deal -- np.random.shuffle(arange(C)) as Fisher-Yates from the end
+// (env.py:99-112: j = random_interval(i), i = C-1 .. 1), the swaps in the
+// lane's LDS deck, the hands sorted -- and the stream offsets after every
+// step.  The same words in the same order as k_play's own draws and deals
+// (StreamSrc), so the games are the same.  phi0: the first episode starts at
+// that step (a pipeline started mid-episode).  The twist before it on the
+// same stream (ptend[tpar]) leads the decoder position by the lead.
+struct DecArgs {
+    int e0, ne, phi0, tpar;
+};
+
+// One lane per game.  Per episode the lane copies a RingPipe window of its
+// ring (kPipeWin bytes from the decoder position, all loads in flight at
+// once) to LDS and reads the words from there -- the draws through the byte
+// buffer, the shuffle targets straight from the window by position -- as
+// the play kernel's own RingPipe path does; the deck then overlays the dead
+// window.  (Reading the ring from HBM unit by unit was twice as slow: the
+// loop's loads waited one by one.)  Per lane: window (kPipeSlot) + swap
+// targets (104) at an odd 8-B stride.
+constexpr int kDecBlock = 128;
+constexpr int kDecLane = 376;  // >= kPipeSlot + 104, 47 x 8 B
+static_assert(kDecLane >= kPipeSlot + 104 && kDecLane % 8 == 0 && (kDecLane / 8) % 2 == 1, "decoder LDS lane");
+
+template <int N>
+__global__ __launch_bounds__(kDecBlock) void k_decode(DevState s, DecArgs d) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kDecBlock * kDecLane];
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * kDecBlock + threadIdx.x;
+    if (g >= s.B) return;
+    const int64_t B = s.B;
+    uint8_t* win = lds + threadIdx.x * kDecLane;  // the ring window; the deck once the targets are drawn
+    uint8_t* jslot = win + kPipeSlot;
+    uint32_t pos = s.pabsc[(int64_t)kDecSlot * B + g];
+    const uint32_t tend = s.ptend[(int64_t)d.tpar * B + g];
+    PhaseProf pq;
+    pq.start();
+    for (int i = 0; i < d.ne; i++) {
+        const int phi = (i == 0) ? d.phi0 : 0;
+        RingPipe rng;
+        ByteBuf buf;
+        rng.load_at(s, g, buf, win, pos, tend);  // an overrun (pos past tend) counts perr there
+        const uint32_t start = pos;
+        uint32_t off[5] = {0u, 0u, 0u, 0u, 0u}, dr[5] = {0u, 0u, 0u, 0u, 0u};
+        bool big = false;
+#pragma unroll
+        for (int t = 0; t < kHand - 1; t++) {  // steps 0..8: hand size n = 10 - t, draws random_interval(n - 1)
+            if (t >= phi) {
+                uint32_t idx[N];
+                rng_draws<N>(rng, buf, (uint32_t)(kHand - 1 - t), idx);
+                uint32_t v = 0u;
+#pragma unroll
+                for (int p = 0; p < N; p++) v |= idx[p] << (4 * p);
+                dr[t >> 1] |= v << (16 * (t & 1));
+                const uint32_t o = rng.consumed(buf) - start;
+                big = big || o > 0xFFFFu;
+                off[t >> 1] |= (o & 0xFFFFu) << (16 * (t & 1));
+            }
+        }
+        pq.mark(PR_DRAWS);
+        // step 9 plays each seat's last card (no draw), then the auto-reset deal
+        shuffle_targets(rng, buf, jslot, s.C);  // the window's own form (by position, no byte buffer)
+        pos = rng.consumed(buf);
+        pq.mark(PR_TARGETS);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the window reads before the deck's writes
+        for (int k = 0; k < s.C; k += 4) *(uint32_t*)(win + k) = (uint32_t)k * 0x01010101u + 0x03020100u;
+        shuffle_apply(win, jslot, s.C);
+        pq.mark(PR_APPLY);
+        Game<N> G;
+        deal_from_deck<N>(win, s.C, G);
+        pq.mark(PR_HANDS);
+        {
+            const uint32_t o = pos - start;
+            big = big || o > 0xFFFFu;
+            off[4] |= (o & 0xFFFFu) << 16;
+        }
+        if (big) atomicAdd(s.perr, 1u);  // cannot happen (an episode draws ~200 words); fail loudly
+        uint32_t hw[12];
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+            hw[3 * p] = (p < N) ? (uint32_t)G.hand[p].lo : 0u;
+            hw[3 * p + 1] = (p < N) ? (uint32_t)(G.hand[p].lo >> 32) : 0u;
+            hw[3 * p + 2] = (p < N) ? G.hand[p].hi : 0u;
+        }
+        const uint32_t rows = G.b.lo.x | (G.b.lo.y << 8) | (G.b.lo.z << 16) | (G.b.lo.w << 24);
+        u32x4* rec = s.drec + (int64_t)((d.e0 + i) % kDecRecords) * kDecQuads * B + g;
+        rec[0 * B] = u32x4{start, off[0], off[1], off[2]};
+        rec[1 * B] = u32x4{off[3], off[4], dr[0], dr[1]};
+        rec[2 * B] = u32x4{dr[2], dr[3], dr[4], rows};
+        rec[3 * B] = u32x4{hw[0], hw[1], hw[2], hw[3]};
+        rec[4 * B] = u32x4{hw[4], hw[5], hw[6], hw[7]};
+        rec[5 * B] = u32x4{hw[8], hw[9], hw[10], hw[11]};
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the deck reads before the next window's writes
+        pq.mark(PR_STORE);
+    }
+    pq.flush(lane, 1);
+    s.pabsc[(int64_t)kDecSlot * B + g] = pos;
 }
 
 // ---- one-game fast path (the scalar drop-in SechsNimmtEnv, B == 1) -------
@@ -1482,15 +1692,22 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
         const char* ps = getenv("SECHS_PIPE_SERIAL");
         e->pipe_serial = (ps && ps[0] == '1') ? 1 : 0;
     }
+    e->pipe_dec = 0;  // decode-ahead: measured slower so far, opt-in
+    {
+        const char* pd = getenv("SECHS_PIPE_DEC");  // default override (A/B runs of whole legs)
+        if (pd && (pd[0] == '0' || pd[0] == '1')) e->pipe_dec = pd[0] - '0';
+    }
     e->pvalid = 0;
     e->pcount = 0;
     if (rng_mode == SN_RNG_NUMPY_MT) {
         struct {
             void** p;
             size_t bytes;
-        } pal[] = {{(void**)&s.pring, (size_t)kPipeRing * B}, {(void**)&s.pabsc, sizeof(uint32_t) * kPipeSlots * B},
+        } pal[] = {{(void**)&s.pring, (size_t)kPipeRing * B},
+                   {(void**)&s.pabsc, sizeof(uint32_t) * (kPipeSlots + 1) * B},  // + the decoder's slot
                    {(void**)&s.ptend, sizeof(uint32_t) * kPipeSlots * B}, {(void**)&s.ptp, sizeof(uint32_t) * B},
-                   {(void**)&s.perr, sizeof(uint32_t)}};
+                   {(void**)&s.perr, sizeof(uint32_t)},
+                   {(void**)&s.drec, N <= kSplitMaxPlayers ? sizeof(u32x4) * kDecRecords * kDecQuads * B : 16}};
         for (auto& a : pal) {
             if (hipMalloc(a.p, a.bytes) != hipSuccess) {
                 sn_destroy(e);
@@ -1557,7 +1774,7 @@ sn_status sn_destroy(sn_env* e) {
     if (e->side) (void)hipStreamDestroy(e->side);
     free_timing(e);
     void* ps[] = {s.hand, s.row_lo, s.row_hi, s.score, s.sum_res, s.episodes, s.mt_pos, s.ctr, s.mt, s.mt0, s.ring,
-                  s.pring, s.pabsc, s.ptend, s.ptp, s.perr, s.lgs, s.lmem};
+                  s.pring, s.pabsc, s.ptend, s.ptp, s.perr, s.lgs, s.lmem, s.drec};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     delete e;
@@ -1565,7 +1782,7 @@ sn_status sn_destroy(sn_env* e) {
 }
 
 static void free_timing(sn_env* e) {
-    for (int i = 0; i < 4 * e->tcap; i++)
+    for (int i = 0; i < kTimingEvents * e->tcap; i++)
         if (e->tev[i]) (void)hipEventDestroy(e->tev[i]);
     delete[] e->tev;
     delete[] e->tev_tw;
@@ -1620,6 +1837,10 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
         case SN_OPT_PLAY_QUAD:
         case SN_OPT_PIPE_FUSED:  // round-5 experiments, measured slower and removed
             return fail(SN_EUNSUPPORTED, "option removed (k_play_quad / the fused twist measured slower)");
+        case SN_OPT_PIPE_DEC:
+            if (value < 0 || value > 1) return fail(SN_EINVAL, "pipe dec must be 0 or 1");
+            e->pipe_dec = value;
+            return SN_OK;
         case SN_OPT_TWIST_SKIP:
             if (value < 0 || value > 1) return fail(SN_EINVAL, "twist skip must be 0 or 1");
             e->twist_skip = value;
@@ -1634,10 +1855,10 @@ sn_status sn_set_option(sn_env* e, int option, int value) {
             HIP_TRY(hipDeviceSynchronize());
             free_timing(e);
             if (value) {
-                e->tev = new hipEvent_t[4 * value]();
+                e->tev = new hipEvent_t[kTimingEvents * value]();
                 e->tev_tw = new int[value]();
                 e->tcap = value;
-                for (int i = 0; i < 4 * value; i++) HIP_TRY(hipEventCreate(&e->tev[i]));
+                for (int i = 0; i < kTimingEvents * value; i++) HIP_TRY(hipEventCreate(&e->tev[i]));
             }
             return SN_OK;
         default: return fail(SN_EINVAL, "unknown option");
@@ -1853,13 +2074,53 @@ static sn_status pipe_play(const DevState& s, const PlayArgs& c, int gpw, unsign
 // Hand-off: HIP events both ways -- a wait and a record on the caller's
 // stream between play launches.  (Device-flag and in-launch hand-offs were
 // built and measured slower on gfx950)
+// one decode-ahead play launch (RNG_NUMPY_DEC: N <= 4, 64 games per wave)
+static sn_status dec_play(const DevState& s, const PlayArgs& c, size_t shmem, hipStream_t st) {
+    SN_DISPATCH_N(s.N, {
+        if constexpr (NN <= kSplitMaxPlayers) {
+            HIP_TRY(hipFuncSetAttribute((const void*)k_play<NN, RNG_NUMPY_DEC>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
+            hipLaunchKernelGGL((k_play<NN, RNG_NUMPY_DEC>), dim3(grid_for(s.B)), dim3(kBlock), shmem, st, s, c);
+        }
+    });
+    HIP_TRY(hipGetLastError());
+    return SN_OK;
+}
+
+// records of episodes [e0, e0 + ne) (global counter since the pipeline start) on stream st
+static sn_status dec_launch(sn_env* e, int64_t e0, int ne, int phi0, int tpar, hipStream_t st) {
+    const DevState& s = e->s;
+    const DecArgs d{(int)(e0 % kDecRecords), ne, phi0, tpar};
+    const dim3 grid((unsigned)((s.B + kDecBlock - 1) / kDecBlock));
+    SN_DISPATCH_N(s.N, {
+        if constexpr (NN <= kSplitMaxPlayers) hipLaunchKernelGGL((k_decode<NN>), grid, dim3(kDecBlock), 0, st, s, d);
+    });
+    HIP_TRY(hipGetLastError());
+    return SN_OK;
+}
+
+// Decode-ahead applies to in-kernel DrunkHamster rollouts with auto-reset of
+// a plain (non-tournament) handle of N <= 4 whose games are in lockstep
+// (e->phase known): every launch's random decisions are then the same
+// function of the stream for every game.
+static bool dec_ok(const sn_env* e, const PlayArgs& a) {
+    return e->pipe_dec && e->phase >= 0 && (a.flags & SN_AUTO_RESET) && !a.actions && !a.invalid && !e->s.lg_K &&
+           e->s.N <= kSplitMaxPlayers && e->pipe_gpw == 64 && e->s.drec;
+}
+
 static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     DevState& s = e->s;
     int wave;
     const int gpw = e->pipe_gpw;
-    const size_t shmem = pipe_lds(s, a, gpw, &wave);
-    a.wave_lds = wave;
+    const bool dec = dec_ok(e, a);
+    size_t shmem = pipe_lds(s, a, gpw, &wave);
     a.ring_lds = kPipeSlot;
+    if (dec) {  // the obs staging only (no deck, no ring window)
+        wave = (a.obs && a.obs_stride == 48 && (((uintptr_t)a.obs) & 15) == 0) ? 64 * obs_stage_pieces(s.N) * 16 : 16;
+        shmem = (size_t)wave * (kBlock / 64);
+        a.ring_lds = 0;
+    }
+    a.wave_lds = wave;
     a.vec_out = ((((uintptr_t)a.rewards) & 15) == 0) && ((((uintptr_t)a.actions_out) & 3) == 0);
     const dim3 pg((unsigned)((s.B + kBlock / 64 - 1) / (kBlock / 64)));
     const int64_t B = s.B, N = s.N;
@@ -1876,21 +2137,31 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     // for K <= 5 (3 623 words), and mt0 the five word-0 crossings that span.
     const int K = e->twist_every;
     const bool round_tw = e->twist_round;
-    if (e->pvalid && e->pK != K) {  // restart with the other group size
+    if (e->pvalid && (e->pK != K || (e->pdec != 0) != dec)) {  // restart with the other group size / form
         const sn_status r = sn_pipe_sync(e, st);
         if (r != SN_OK) return r;
     }
-    const int lead = e->pipe_lead * K;
+    // Decode-ahead: the twists lead the DECODER (pabsc[kDecSlot]) by 300 (K + 2) words -- the
+    // K + 1 episodes (~195 words each at N = 4) a decode launch may need -- and the play
+    // launches read no ring at all.  Otherwise they lead the play consumer by 600 K words.
+    const int lead = dec ? e->pipe_lead * (K + 2) / 2 : e->pipe_lead * K;
     constexpr uint32_t kSlotMask = (uint32_t)kPipeSlots - 1u;
     if (!e->pvalid) {  // start the pipeline from mt_pos: twist the lead ahead, synchronously
-        const AheadArgs aa{(int)kSlotMask, 0, 1, lead, e->perr_host_dev};
+        const AheadArgs aa{dec ? kDecSlot : (int)kSlotMask, 0, 1, lead, e->perr_host_dev, dec ? (int)kSlotMask : -1};
         e->tw_out = 1, e->pl_cout = (int)kSlotMask, e->pphase = 0;
         if (round_tw) hipLaunchKernelGGL((k_mt_ahead<true, true>), pg, dim3(kBlock), 0, st, s, aa);
         else hipLaunchKernelGGL((k_mt_ahead<true, false>), pg, dim3(kBlock), 0, st, s, aa);
         HIP_TRY(hipGetLastError());
+        if (dec) {  // the records of the first group's launches (episodes 0 .. K), from the current step on
+            e->dec_e = 0;
+            const sn_status r = dec_launch(e, 0, K + 1, e->phase, 1, st);
+            if (r != SN_OK) return r;
+            e->dec_next = K + 1;
+        }
         HIP_TRY(hipEventRecord(e->ev_prep, st));
         e->pvalid = 1;
         e->pK = K;
+        e->pdec = dec ? 1 : 0;
     } else {
         // order behind the last pipelined k_play (recorded on the stream of
         // that call): always, also on the same stream -- a stream handle's
@@ -1902,6 +2173,7 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
     // launches keep the pair tail < 1e-26 up to K = 8 agents at N <= 4
     // (tools/pipe_tail.py), beyond that 5-step launches
     const int chunk = min(e->chunk_steps, (s.lg_K > 8) ? 5 : pipe_max_chunk(s.N));
+    int phase = dec ? e->phase : 0;  // decode-ahead: the games' step within their episode
     const unsigned nblk = (gpw == 32) ? (unsigned)((s.B + 32 * (kBlock / 64) - 1) / (32 * (kBlock / 64)))
                                       : (unsigned)grid_for(s.B);
     for (int t0 = 0; t0 < a.steps; t0 += chunk) {
@@ -1914,17 +2186,27 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         if (a.obs) c.obs = a.obs + (int64_t)t0 * B * N * a.obs_stride;
         const uint64_t p = e->pphase;
         c.pipe_cin = (int)((p + kSlotMask) & kSlotMask), c.pipe_cout = (int)(p & kSlotMask);
+        if (dec) {  // the launch's records: its episode's and (crossing a deal) the next one's
+            c.n0 = phase;
+            c.drec0 = (int)(e->dec_e % kDecRecords), c.drec1 = (int)((e->dec_e + 1) % kDecRecords);
+        }
         const uint64_t G = p / (uint64_t)K;
         const bool first = (p % (uint64_t)K) == 0u;  // twist G beside this launch
         c.pipe_t = (int)((G + 1u) & 1u);              // twist G-1's end (INIT's for group 0)
         if (first && G >= 1u) HIP_TRY(hipStreamWaitEvent(st, e->evt[(G + 1u) & 1u], 0));  // twist G-1
         if (first && !e->pipe_serial) HIP_TRY(hipEventRecord(e->ev_main, st));  // launch p-1's consumption is final
-        if (e->tn < e->tcap) e->tev_tw[e->tn] = first ? 1 : 0;
-        hipEvent_t* tv = (e->tn < e->tcap) ? e->tev + 4 * e->tn++ : nullptr;
+        const int ti = (e->tn < e->tcap) ? e->tn++ : -1;  // SN_OPT_TIMING: this launch's events
+        hipEvent_t* tv = (ti >= 0) ? e->tev + kTimingEvents * ti : nullptr;
+        if (tv) e->tev_tw[ti] = first ? 1 : 0;
         if (tv) HIP_TRY(hipEventRecord(tv[0], st));
         {
-            const sn_status r = pipe_play(s, c, gpw, nblk, shmem, st);
+            const sn_status r = dec ? dec_play(s, c, shmem, st) : pipe_play(s, c, gpw, nblk, shmem, st);
             if (r != SN_OK) return r;
+        }
+        const int64_t e_start = e->dec_e;  // the episode this launch started in
+        if (dec) {
+            phase += c.steps;
+            if (phase >= kHand) phase -= kHand, e->dec_e++;
         }
         if (tv) HIP_TRY(hipEventRecord(tv[1], st));
         if (first) {
@@ -1933,12 +2215,29 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
             HIP_TRY(hipStreamWaitEvent(e->side, e->ev_main, 0));
             if (tv) HIP_TRY(hipEventRecord(tv[2], e->side));
             // SN_OPT_TWIST_SKIP (tests only): the overrun detector under the default schedule
-            const AheadArgs aa{c.pipe_cin, c.pipe_t, (int)(G & 1u), (e->twist_skip && G >= 1u) ? 0 : lead,
-                               e->perr_host_dev};
+            const AheadArgs aa{dec ? kDecSlot : c.pipe_cin, c.pipe_t, (int)(G & 1u),
+                               (e->twist_skip && G >= 1u) ? 0 : lead, e->perr_host_dev, -1};
             if (round_tw) hipLaunchKernelGGL((k_mt_ahead<false, true>), pg, dim3(kBlock), 0, e->side, s, aa);
             else hipLaunchKernelGGL((k_mt_ahead<false, false>), pg, dim3(kBlock), 0, e->side, s, aa);
             HIP_TRY(hipGetLastError());
             if (tv) HIP_TRY(hipEventRecord(tv[3], e->side));
+            if (dec) {
+                // the records group G+1 may touch: its launches start at most K episodes past this
+                // launch's and touch at most one more each -- episodes < e_start + 2K + 1 (the ring
+                // of kDecRecords >= 2K + 2 slots never overwrites one this group still reads: this
+                // decode runs after launch p-1, and group G reads episodes <= e_start + K)
+                const int64_t target = e_start + 2 * K + 1;
+                if (target > e->dec_next) {
+                    if (tv) HIP_TRY(hipEventRecord(tv[4], e->side));
+                    const sn_status r = dec_launch(e, e->dec_next, (int)(target - e->dec_next), 0, (int)(G & 1u), e->side);
+                    if (r != SN_OK) return r;
+                    e->dec_next = target;
+                    if (tv) {
+                        HIP_TRY(hipEventRecord(tv[5], e->side));
+                        e->tev_tw[ti] |= 2;
+                    }
+                }
+            }
             HIP_TRY(hipEventRecord(e->evt[G & 1u], e->side));
             HIP_TRY(hipEventRecord(e->ev_prep, e->side));
             e->tw_out = (int)(G & 1u);
@@ -2318,23 +2617,33 @@ sn_status sn_reset1(sn_env* e, const uint32_t* key_host, int32_t pos, uint32_t* 
 }
 
 sn_status sn_kernel_times(sn_env* e, float* play_ms, float* ahead_ms, int32_t* n) {
+    return sn_kernel_times_dec(e, play_ms, ahead_ms, nullptr, n);
+}
+
+sn_status sn_kernel_times_dec(sn_env* e, float* play_ms, float* ahead_ms, float* decode_ms, int32_t* n) {
     if (!e || !play_ms || !ahead_ms || !n) return fail(SN_EINVAL, "NULL argument");
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipDeviceSynchronize());
-    double sp = 0.0, sa = 0.0;
-    int na = 0;
+    double sp = 0.0, sa = 0.0, sd = 0.0;
+    int na = 0, nd = 0;
     for (int i = 0; i < e->tn; i++) {
-        float a = 0.f, b = 0.f;
-        HIP_TRY(hipEventElapsedTime(&a, e->tev[4 * i], e->tev[4 * i + 1]));
+        const hipEvent_t* tv = e->tev + kTimingEvents * i;
+        float a = 0.f, b = 0.f, c = 0.f;
+        HIP_TRY(hipEventElapsedTime(&a, tv[0], tv[1]));
         sp += a;
-        if (e->tev_tw[i]) {  // a twist ran beside this launch (every launch unless SN_OPT_TWIST_EVERY > 1)
-            HIP_TRY(hipEventElapsedTime(&b, e->tev[4 * i + 2], e->tev[4 * i + 3]));
+        if (e->tev_tw[i] & 1) {  // a twist ran beside this launch (the first of its group)
+            HIP_TRY(hipEventElapsedTime(&b, tv[2], tv[3]));
             sa += b, na++;
+        }
+        if (e->tev_tw[i] & 2) {  // and a decode-ahead launch after it
+            HIP_TRY(hipEventElapsedTime(&c, tv[4], tv[5]));
+            sd += c, nd++;
         }
     }
     *n = e->tn;
     *play_ms = e->tn ? (float)(sp / e->tn) : 0.f;
     *ahead_ms = na ? (float)(sa / na) : 0.f;
+    if (decode_ms) *decode_ms = nd ? (float)(sd / nd) : 0.f;
     return SN_OK;
 }
 
@@ -2387,6 +2696,23 @@ sn_status sn_pipe_errors(sn_env* e, uint32_t* count) {
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(count, e->s.perr, sizeof(uint32_t), hipMemcpyDeviceToHost));
     if (e->perr_host && *count) __atomic_store_n(e->perr_host, *count, __ATOMIC_RELAXED);
+    return SN_OK;
+}
+
+sn_status sn_debug_pipe_words(sn_env* e, int what, int slot, uint32_t* out) {
+    if (!e || !out) return fail(SN_EINVAL, "NULL argument");
+    if (!e->s.pabsc) return fail(SN_EUNSUPPORTED, "no pipeline (numpy-compat handles only)");
+    const int64_t B = e->s.B;
+    const void* src = nullptr;
+    size_t bytes = 0;
+    if (what == 0 && slot >= 0 && slot <= kPipeSlots) src = e->s.pabsc + (int64_t)slot * B, bytes = 4 * B;
+    else if (what == 1 && slot >= 0 && slot < 2) src = e->s.ptend + (int64_t)slot * B, bytes = 4 * B;
+    else if (what == 2 && slot >= 0 && slot < kDecRecords && e->s.drec)
+        src = e->s.drec + (int64_t)slot * kDecQuads * B, bytes = sizeof(u32x4) * kDecQuads * B;
+    else return fail(SN_EINVAL, "what / slot out of range");
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, src, bytes, hipMemcpyDeviceToHost));
     return SN_OK;
 }
 

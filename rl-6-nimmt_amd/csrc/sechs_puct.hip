@@ -872,6 +872,39 @@ constexpr int kRollSeats = 32;  // seats per wave's group (32 / L... 64 / L / 2 
 constexpr int kRollWaveLds = kRollSeats * kSeatRowLds * 2 + kRollSeats * kBaseLds * 2 + kRollSeats * kHand * 4 +
                              8 * kRoWords * 4;  // rows (aliased by logits) + base + cards + states: 15 104 B
 
+// k_puct_rollouts phase profiler (diagnostics, -DSECHS_PHASE_PROF builds only,
+// sn_debug_puct_phases): shader-clock cycles per wave in the state copy-in,
+// the seat rows (phase 1), the per-seat layer-1 MFMA (phase 2), the
+// candidate tiles (phase 3) and the step; [7] counts waves
+enum { RP_COPY = 0, RP_ROWS, RP_BASE, RP_TILES, RP_STEP, RP_N };
+#ifdef SECHS_PHASE_PROF
+__device__ unsigned long long g_puct_phase[8];
+struct RollProf {
+    uint64_t t, acc[RP_N];
+    __device__ __forceinline__ void start() {
+        t = __builtin_readcyclecounter();
+        for (int k = 0; k < RP_N; k++) acc[k] = 0ull;
+    }
+    __device__ __forceinline__ void mark(int k) {
+        const uint64_t n = __builtin_readcyclecounter();
+        acc[k] += n - t;
+        t = n;
+    }
+    __device__ __forceinline__ void flush(int lane) {
+        if (lane == 0) {
+            for (int k = 0; k < RP_N; k++) atomicAdd(&g_puct_phase[k], (unsigned long long)acc[k]);
+            atomicAdd(&g_puct_phase[7], 1ull);
+        }
+    }
+};
+#else
+struct RollProf {
+    __device__ __forceinline__ void start() {}
+    __device__ __forceinline__ void mark(int) {}
+    __device__ __forceinline__ void flush(int) {}
+};
+#endif
+
 // sn_puct_mlp_seats' arithmetic.
 template <int N, int L>
 __global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a, int r0, int nr, int32_t* ro_base,
@@ -906,6 +939,8 @@ __global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a
     const int64_t groups = (a.D + DG - 1) / DG;
     auto fence = [] { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); };
     const int sl = lane & (kRollSeats - 1), p0 = lane >> 5;  // phase 1: seat sl, parts p0 and p0 + 2
+    RollProf pf;
+    pf.start();
     for (int64_t grp = (int64_t)blockIdx.x * kWaves + wave; grp < groups; grp += (int64_t)gridDim.x * kWaves) {
         const int64_t d0 = grp * DG;
         const int nd = (int)min<int64_t>(DG, a.D - d0);
@@ -919,6 +954,7 @@ __global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a
             }
             ar.ro = sRo - d0 * kRoWords;
             fence();
+            pf.mark(RP_COPY);
             for (int t = 0; t < a.n; t++) {
                 const int m = a.n - t;
                 // phase 1: two lanes per seat (rows past the group's seats repeat its last)
@@ -929,6 +965,7 @@ __global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a
                     seat_row_part(in, m, part, sRow + sl * kSeatRowLds, sCard + sl * kHand, sLut);
                 }
                 fence();
+                pf.mark(RP_ROWS);
                 // phase 2: base[seat][j] = sum_k W1s[j][k] rows[seat][k] (one 32-seat tile)
                 {
                     // the A fragments (W1s rows 32 mt + col) from L1 / L2 per step: held across phase 3
@@ -960,6 +997,7 @@ __global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a
                         }
                 }
                 fence();
+                pf.mark(RP_BASE);
                 // phase 3: the group's candidate rows, 64 per tile, logits to LDS (over the dead rows)
                 const uint32_t rows = (uint32_t)nseat * (uint32_t)m;
                 const uint32_t tiles = (rows + 32u * TNT - 1u) / (32u * TNT);
@@ -983,15 +1021,18 @@ __global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a
                         if (half == 0 && rw[nt] < rows) sLogit[rw[nt]] = out[nt];
                 }
                 fence();
+                pf.mark(RP_TILES);
                 // the step: L lanes per decision (step_seat, as k_puct_step_seats); lanes past the
                 // group's DG decisions (the upper half of the wave) follow along and write nothing
                 step_seat<N, L>(
                     s, ar, [&](int64_t dd, int q, int k) { return sLogit[((dd - d0) * N + q) * m + k]; }, t, m,
                     d0 * L + lane, d0 + nd, d0);
                 fence();
+                pf.mark(RP_STEP);
             }
         }
     }
+    pf.flush(lane);
 }
 
 // _choose_action_from_outcomes (mcts.py:156-165, temperature None): best mean
@@ -1284,6 +1325,21 @@ sn_status sn_puct_rollouts(sn_env* e, const sn_puct* q, int r0, int nr, void* ro
 #undef SN_ROLLOUTS
     HIP_TRY(hipGetLastError());
     return SN_OK;
+}
+
+sn_status sn_debug_puct_phases(uint64_t* out, int n) {
+    if (!out || n < 1) return set_error(SN_EINVAL, "NULL argument");
+#ifdef SECHS_PHASE_PROF
+    unsigned long long h[8];
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_puct_phase), sizeof(h)));
+    for (int k = 0; k < n; k++) out[k] = (k < 8) ? (uint64_t)h[k] : 0ull;
+    const unsigned long long z[8] = {};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_puct_phase), z, sizeof(z)));
+    return SN_OK;
+#else
+    return set_error(SN_EUNSUPPORTED, "phase counters: build libsechs_prof.so (-DSECHS_PHASE_PROF)");
+#endif
 }
 
 sn_status sn_puct_choose(sn_env* e, const sn_puct* q, int32_t* actions, int32_t* best_index, void* stream) {

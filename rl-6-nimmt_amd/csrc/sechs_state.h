@@ -49,6 +49,8 @@ struct DevState {
     uint32_t* ptend; // [kPipeSlots][B] end of the twisted words after a prep launch (the same)
     uint32_t* ptp;   // [B] twist pointer (MtGen's pos field), owned by k_mt_ahead
     uint32_t* perr;  // [1] play lanes that ran past the twisted words (must stay 0)
+    u32x4* drec;     // [kDecRecords][kDecQuads][B] decode-ahead records (k_decode -> k_play<RNG_NUMPY_DEC>), one
+                     // per episode: start position, per-step stream offsets, the draws, the dealt hands / rows
     // batched tournament (sn_league_config): per game the current game's
     // player count k and seat agents, k | agent(seat p) << (4 + 4p)
     uint32_t* lgs;   // [B]
@@ -58,8 +60,12 @@ struct DevState {
     int32_t* lpf;    // [B] 1 (| 2: quirk Q6): lpc holds this step's non-external cards
 };
 
-constexpr int kMt0Levels = 5;    // word-0 crossings kept in mt0 (a K = 5 lead + a round spans up to five)
+constexpr int kMt0Levels = 8;    // word-0 crossings kept in mt0 (the decode-ahead span: up to seven rounds)
 constexpr int kPipeSlots = 8;    // pabsc buffers (by play launch index mod 8; ptend uses 2, by twist parity)
+constexpr int kDecSlot = kPipeSlots;  // pabsc slot kPipeSlots: the decoder's stream position (decode-ahead mode)
+constexpr int kDecRecords = 16;  // decode-ahead record ring (episodes; >= 2K + 2 for K <= 5)
+constexpr int kDecQuads = 6;     // 16-B pieces per record (24 dwords, the layout at DecSrc)
+constexpr int kTimingEvents = 6; // SN_OPT_TIMING events per launch: play, twist, decode (start, end)
 constexpr int kPipeRing = 4096;  // ring bytes per game (>= the lead 600 K + a whole round's overshoot: 3 623 at K = 5)
 
 // pring layout: 64-byte chunks interleaved over games -- stream positions
@@ -306,6 +312,34 @@ struct RingPipe {
         }
         buf.clear();
     }
+    // the same from an explicit position (k_decode: the decoder's own position, the twist's end)
+    __device__ __forceinline__ void load_at(const DevState& s, int64_t gg, ByteBuf& buf, uint8_t* lds_slot, uint32_t c,
+                                            uint32_t tend) {
+        g = gg, B = s.B;
+        c0 = c;
+        const int32_t av = (int32_t)(tend - c0);
+        if (av < 0) atomicAdd(s.perr, 1u);
+        avail = (av < 0) ? 0u : (uint32_t)av;
+        win = min(avail, (uint32_t)kPipeWin);
+        off = c0 & 15u;
+        slot = lds_slot;
+        ring = (const uint8_t*)s.pring;
+        err = s.perr;
+        take = 0u;
+        const uint32_t q0 = (c0 & (uint32_t)(kPipeRing - 1)) >> 4;
+        const uint32_t nch = (off + win + 15u) >> 4;
+        u32x4 v[(kPipeWin + 30) / 16];  // every load in flight before the first LDS write
+#pragma unroll
+        for (uint32_t i = 0; i < (uint32_t)((kPipeWin + 30) / 16); i++)
+            if (i < nch) v[i] = s.pring[ring16(q0 + i, g, B)];
+#pragma unroll
+        for (uint32_t i = 0; i < (uint32_t)((kPipeWin + 30) / 16); i++)
+            if (i < nch) {
+                *(uint64_t*)(lds_slot + 16u * i) = (uint64_t)v[i].x | ((uint64_t)v[i].y << 32);
+                *(uint64_t*)(lds_slot + 16u * i + 8u) = (uint64_t)v[i].z | ((uint64_t)v[i].w << 32);
+            }
+        buf.clear();
+    }
     __device__ __forceinline__ uint32_t consumed(const ByteBuf& buf) const { return c0 + take - buf.cnt; }
     // forced = the buffer is empty and a draw needs a word now
     __device__ __forceinline__ bool gen(ByteBuf& buf, bool forced) {
@@ -322,6 +356,73 @@ struct RingPipe {
         const PipeSlow r = pipe_slow(ring, B, g, c0 + take, left, err);
         buf.append(r.bytes, r.k);
         take += r.k;
+        return true;
+    }
+    __device__ __forceinline__ void topup(ByteBuf& buf) {
+        if (buf.cnt <= 24u) gen(buf, false);
+    }
+    __device__ __forceinline__ void force(ByteBuf& buf) { gen(buf, true); }
+};
+
+// The pipelined ring read straight from HBM (k_decode, the decode-ahead
+// producer): the next 8 bytes at any stream position from two 16-B units
+// held in registers (the one holding the position and the next, loaded one
+// unit ahead), the same words RingPipe hands out.  A top-up never reads past
+// the twisted end; a draw that needs a word past it counts an overrun (perr,
+// sticky) and takes zero bytes, as pipe_slow.
+struct RingDirect {
+    static constexpr int kAhead = 4;  // 16-B units in flight past the one being read (~64 words of draws)
+    const u32x4* ring;
+    uint32_t* err;
+    int64_t B, g;
+    uint32_t pos;  // stream position of the next byte not yet appended
+    uint32_t end;  // twisted end (ptend)
+    uint32_t unit;  // pos >> 4 (the unit `cur` holds)
+    u32x4 cur, nx[kAhead];  // units unit, unit + 1 .. unit + kAhead (a register queue: static indices only)
+
+    __device__ __forceinline__ void load(const DevState& s, int64_t gg, uint32_t c, uint32_t tend, ByteBuf& buf) {
+        ring = s.pring, err = s.perr, B = s.B, g = gg;
+        pos = c, end = tend, unit = c >> 4;
+        cur = ring[ring16(unit, g, B)];
+#pragma unroll
+        for (int k = 0; k < kAhead; k++) nx[k] = ring[ring16(unit + 1u + (uint32_t)k, g, B)];
+        buf.clear();
+    }
+    __device__ __forceinline__ uint32_t consumed(const ByteBuf& buf) const { return pos - buf.cnt; }
+    __device__ __forceinline__ uint64_t peek8() const {
+        const uint32_t off = pos & 15u, sh = 8u * (off & 7u);
+        const uint64_t q0 = (uint64_t)cur.x | ((uint64_t)cur.y << 32), q1 = (uint64_t)cur.z | ((uint64_t)cur.w << 32);
+        const uint64_t q2 = (uint64_t)nx[0].x | ((uint64_t)nx[0].y << 32);
+        const uint64_t lo = (off >= 8u) ? q1 : q0, hi = (off >= 8u) ? q2 : q1;
+        return sh ? ((lo >> sh) | (hi << (64u - sh))) : lo;
+    }
+    __device__ __forceinline__ void advance(uint32_t k) {
+        pos += k;
+        const uint32_t u = pos >> 4;  // (positions wrap at 2^32: a start-up consumer sits just below 0)
+        if (u != unit) {              // at most one unit per call (k <= 8)
+            unit = u;
+            cur = nx[0];
+#pragma unroll
+            for (int q = 0; q + 1 < kAhead; q++) nx[q] = nx[q + 1];
+            nx[kAhead - 1] = ring[ring16(unit + (uint32_t)kAhead, g, B)];
+        }
+    }
+    // forced = the buffer is empty and a draw needs a word now
+    __device__ __forceinline__ bool gen(ByteBuf& buf, bool forced) {
+        const uint32_t left = ((int32_t)(end - pos) > 0) ? end - pos : 0u;
+        if (left >= 8u) {
+            buf.append(peek8(), 8u);
+            advance(8u);
+            return true;
+        }
+        if (left == 0u) {
+            if (!forced) return false;  // prefetch stops at the twisted end
+            atomicAdd(err, 1u);         // an overrun: the stream is lost, draw zeros
+            buf.append(0ull, 8u);
+            return true;
+        }
+        buf.append(peek8(), left);
+        advance(left);
         return true;
     }
     __device__ __forceinline__ void topup(ByteBuf& buf) {
@@ -856,6 +957,10 @@ struct sn_env {
     int pK;           // SN_OPT_TWIST_EVERY of the running pipeline
     hipEvent_t evt[2];  // after twist G, slot G mod 2
     int twist_skip;   // SN_OPT_TWIST_SKIP (tests only): steady twists after the first group twist nothing
+    int pipe_dec;     // SN_OPT_PIPE_DEC: decode-ahead (k_decode + k_play<RNG_NUMPY_DEC>) where it applies
+    int pdec;         // the running pipeline decodes ahead
+    int64_t dec_e;    // decode-ahead: episodes the play launches finished since the pipeline start
+    int64_t dec_next; // decode-ahead: the next episode k_decode will decode
     sechs::DevState s;
     // pipelined twist-ahead (sechs_env.hip launch_pipe): a k_mt_ahead for the
     // next play launch may be in flight on `side` (ev_prep) after a rollout
@@ -868,9 +973,9 @@ struct sn_env {
     uint32_t* hbuf;      // one-game fast path (sn_step1 / sn_reset1): pinned, device-mapped exchange words
     uint32_t* hbuf_dev;
     // SN_OPT_TIMING: per-launch event pairs (k_play start/end on the launch
-    // stream, k_mt_ahead start/end on `side`), tcap pairs, tn recorded
+    // stream, k_mt_ahead and k_decode start/end on `side`), tcap launches, tn recorded
     hipEvent_t* tev;
-    int* tev_tw;  // per recorded launch: 1 if a twist ran beside it (its pair of side events is valid)
+    int* tev_tw;  // per recorded launch: bit 0 a twist ran beside it, bit 1 a decode after that (their events valid)
     int tcap, tn;
 };
 

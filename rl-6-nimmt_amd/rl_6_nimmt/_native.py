@@ -25,6 +25,7 @@ SN_OPT_PLAY_SPLIT = 7
 SN_OPT_TWIST_ROUND = 9
 SN_OPT_TWIST_EVERY = 10
 SN_OPT_TWIST_SKIP = 12  # test knob: the default schedule runs its ring dry
+SN_OPT_PIPE_DEC = 13
 SN_AGENT_RANDOM, SN_AGENT_MCS, SN_AGENT_EXTERNAL = 0, 1, 2
 
 class SnPuct(ctypes.Structure):
@@ -78,7 +79,10 @@ SIGNATURES = {
     "sn_set_option": ([_P, _I, _I], _I),
     "sn_pipe_errors": ([_P, _P], _I),
     "sn_kernel_times": ([_P, _P, _P, _P], _I),
+    "sn_kernel_times_dec": ([_P, _P, _P, _P, _P], _I),
     "sn_debug_phases": ([_P, _I], _I),
+    "sn_debug_puct_phases": ([_P, _I], _I),
+    "sn_debug_pipe_words": ([_P, _I, _I, _P], _I),
     "sn_debug_failures": ([_P, _P, _I], _I),
     "sn_step1": ([_P, _P, _P, _I], _I),
     "sn_reset1": ([_P, _P, ctypes.c_int32, _P, _P, _P, _I], _I),

@@ -186,10 +186,11 @@ class VecSechsNimmtEnv:
 
     # ------------------------------------------------------------ numpy RNG bridge
     def set_option(self, ring_words=None, chunk_steps=None, pipeline=None, pipe_gpw=None, pipe_lead=None,
-                   play_split=None, twist_round=None, twist_every=None, twist_skip=None):
+                   play_split=None, twist_round=None, twist_every=None, twist_skip=None, pipe_dec=None):
         """rollout tuning (include/sechs.h SN_OPT_*; all numpy-compat only except play_split,
         the role-split kernel of philox handles; twist_round: whole-round MT twists in
-        k_mt_ahead; twist_every: one twist-ahead launch per K = 1 .. 5 play launches); results never
+        k_mt_ahead; twist_every: one twist-ahead launch per K = 1 .. 5 play launches; pipe_dec:
+        decode-ahead, k_decode + k_play from the records); results never
         depend on it (except the test knobs pipe_lead < 600 and twist_skip = 1, which make
         overruns -- PipeOverrunError -- likely / certain)"""
         if pipe_lead is not None:
@@ -202,6 +203,8 @@ class VecSechsNimmtEnv:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_TWIST_EVERY, int(twist_every)), "sn_set_option")
         if twist_round is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_TWIST_ROUND, int(twist_round)), "sn_set_option")
+        if pipe_dec is not None:
+            nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_PIPE_DEC, int(pipe_dec)), "sn_set_option")
         if twist_skip is not None:
             nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_TWIST_SKIP, int(twist_skip)), "sn_set_option")
         if pipeline is not None:
@@ -216,11 +219,13 @@ class VecSechsNimmtEnv:
         k_mt_ahead launches, each on its own stream (0 = off)"""
         nat.check(nat.lib().sn_set_option(self._h, nat.SN_OPT_TIMING, int(launches)), "sn_set_option")
 
-    def kernel_times(self):
-        """(mean k_play ms, mean k_mt_ahead ms, launches recorded) [sync]"""
-        a, b, n = ctypes.c_float(), ctypes.c_float(), ctypes.c_int32()
-        nat.check(nat.lib().sn_kernel_times(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)), "sn_kernel_times")
-        return a.value, b.value, n.value
+    def kernel_times(self, with_decode=False):
+        """(mean k_play ms, mean k_mt_ahead ms, launches recorded) [sync];
+        with_decode: (k_play, k_mt_ahead, k_decode ms, launches)"""
+        a, b, c, n = ctypes.c_float(), ctypes.c_float(), ctypes.c_float(), ctypes.c_int32()
+        nat.check(nat.lib().sn_kernel_times_dec(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c),
+                                                ctypes.byref(n)), "sn_kernel_times_dec")
+        return (a.value, b.value, c.value, n.value) if with_decode else (a.value, b.value, n.value)
 
     def pipe_errors(self):
         """draws of pipelined rollouts that ran past the twisted words (must be 0) [sync]"""

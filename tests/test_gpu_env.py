@@ -599,6 +599,47 @@ def test_pipelined_launch_plans_match_oracle(plan):
     assert env.pipe_errors() == 0
 
 
+@pytest.mark.parametrize("N,C,summ", [(4, 104, True), (2, 104, False), (3, 40, True), (1, 104, True)])
+def test_decode_ahead_equals_ring_play(N, C, summ):
+    """SN_OPT_PIPE_DEC (round 6, the default where it applies): k_decode
+    walks the ring a group ahead and k_play<RNG_NUMPY_DEC> plays from its
+    records -- the same outputs as k_play drawing from the ring itself
+    (pipe_dec=0), launch plans that start mid-episode and cross deals
+    (25 / 1 / 7 / 3 / 30 / 10 steps: records of two episodes per launch),
+    the pipeline restarted after a mid-rollout MT export (phi0 > 0 at the
+    new start), K = 1 / 4 groups; then the same exported numpy states, the
+    same results, and the oracle agrees on the first rollouts."""
+    B, seed = 1500, 5
+    outs = {}
+    for dec in (1, 0):
+        for K in (4, 1):
+            env = venv(B, N, num_cards=C, seed=seed, rng="numpy", include_summaries=summ)
+            env.set_option(pipe_dec=dec, twist_every=K)
+            env.reset()
+            got = []
+            for i, T in enumerate((25, 1, 7, 3, 30, 10)):
+                o = env.rollout(T, want_actions=True, want_obs=True, check=True)
+                got.append({k: v.cpu().numpy() for k, v in o.items()})
+                if i == 2:  # a sync in the middle: the pipeline restarts at step 3 of an episode
+                    got.append({"mt": np.append(*env.get_mt_state(B // 2))})
+            s_, e_ = env.results()
+            got.append({"sums": s_.cpu().numpy(), "eps": e_.cpu().numpy(), "hands": env.hands().cpu().numpy()})
+            got.append({f"mt{g}": np.append(*env.get_mt_state(g)) for g in (0, 777, B - 1)})
+            assert env.pipe_errors() == 0
+            outs[(dec, K)] = got
+            env.close()
+    for key in ((1, 4), (1, 1), (0, 1)):
+        for a, b in zip(outs[key], outs[(0, 4)]):
+            assert a.keys() == b.keys()
+            for k in a:
+                assert np.array_equal(a[k], b[k]), (key, k)
+    ref = O.VecOracle(B, N, rng_mode=O.RNG_NUMPY_MT, seed=seed, num_cards=C)
+    ref.reset()
+    rr, rd, ra, ro = ref.rollout(25, include_summaries=summ, want_obs=True)
+    assert np.array_equal(outs[(1, 4)][0]["rewards"], rr) and np.array_equal(outs[(1, 4)][0]["actions"], ra)
+    assert np.array_equal(outs[(1, 4)][0]["obs"][..., : O.obs_len(summ)], ro)
+
+
 def test_pipelined_full_size_across_streams():
     """65 536 games, 12 back-to-back episodes of the pipeline with the
     caller's stream switching between rollouts (the library orders a new

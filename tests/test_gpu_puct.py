@@ -824,3 +824,65 @@ def test_puct_search_statistics_match_reference_in_law():
         report[name] = (float(ours[name].mean()), float(ref[name].mean()), float(se))
         assert abs(diff.mean()) <= 4 * se, (name, report[name])
     print("F14 (ours, reference, paired s.e.):", report)
+
+
+def test_puct_search_at_configured_budget_matches_reference_in_law():
+    """VERDICT r05 #5, golden F14b (tools/gen_puct_stats.py with
+    SECHS_F14_MC_MAX=100): G seeded reference games of GameSession(PUCTAgent
+    (mc_max=100 -- the reference's default budget, mcts.py:25 -- with the F8
+    weights), DrunkHamster x 3), seat 0's decisions at n = 10, 6 and 3 (the
+    min/max/median normalisation and the unvisited-median fill of
+    mcts.py:295-315 drive these searches; n = 3 runs 60 playouts).  The
+    batched engine replays the same deals and must agree in law, game-paired,
+    within 4 standard errors of the paired difference: seat 0's final
+    penalty, and at each n the visit-weighted mean hand rank, the largest
+    visit share and the chosen card's rank."""
+    d = load("puct_search_mc100.json")
+    games = d["games"]
+    G = len(games)
+    assert d["mc_max"] == 100
+    z = np.load(os.path.join(GOLDEN, "puct_policy.npz"))
+    weights = {k: torch.from_numpy(z[k]) for k in z.files if "net" in k}
+    env, eng = _engine(B=G, N=4, mask=1, dtype=torch.bfloat16, mc_max=d["mc_max"], mc_per_card=d["mc_per_card"],
+                       seed=2025, weights=weights)
+    board = np.full((G, 4, 6), -1, dtype=np.int8)
+    hands = np.full((G, 4, 10), -1, dtype=np.int8)
+    for g, r in enumerate(games):
+        for i, row in enumerate(r["board0"]):
+            board[g, i, : len(row)] = row
+        hands[g] = np.array(r["hands0"], dtype=np.int8)
+    env.reset_to(torch.from_numpy(board), torch.from_numpy(hands))
+    total = torch.zeros((G, 4), dtype=torch.int32, device=env.device)
+    torch.manual_seed(8)
+    ours_dec = {}
+    for t in range(10):
+        n = 10 - t
+        acts = eng.decide(n)
+        if str(n) in games[0]["dec"]:
+            ours_dec[n] = (eng.stats[:G, 10:10 + n].cpu().numpy().astype(np.float64),
+                           eng.best_index[:G].cpu().numpy().astype(np.float64))
+        acts = torch.where(torch.tensor([True, False, False, False], device=env.device)[None, :], acts,
+                           eng._random_moves())
+        rew, done, inv = env.step(acts)
+        assert (inv.cpu() == -1).all()
+        total += rew
+    assert bool(done.all())
+    report = {}
+
+    def check(name, ours, ref):
+        diff = ours - ref
+        se = diff.std(ddof=1) / np.sqrt(len(diff))
+        report[name] = (round(float(ours.mean()), 4), round(float(ref.mean()), 4), round(float(se), 4))
+        assert abs(diff.mean()) <= 4 * se, (name, report[name])
+
+    check("penalty", -total[:, 0].cpu().numpy().astype(np.float64),
+          np.array([-r["results"][0] for r in games], dtype=np.float64))
+    for n, (visits, best) in ours_dec.items():
+        rv = np.array([r["dec"][str(n)]["visits"] for r in games], dtype=np.float64)
+        assert np.array_equal(visits.sum(axis=1), rv.sum(axis=1))  # n_mc playouts per decision, all backed up
+        k = np.arange(n, dtype=np.float64)
+        check(f"visit_rank@{n}", (visits * k).sum(axis=1) / visits.sum(axis=1), (rv * k).sum(axis=1) / rv.sum(axis=1))
+        check(f"max_share@{n}", visits.max(axis=1) / visits.sum(axis=1), rv.max(axis=1) / rv.sum(axis=1))
+        check(f"chosen_rank@{n}", best,
+              np.array([r["dec"][str(n)]["legal"].index(r["dec"][str(n)]["chosen"]) for r in games], dtype=np.float64))
+    print("F14b (ours, reference, paired s.e.):", report)

@@ -12,8 +12,10 @@ def main():
     r = last_json(path)
     if kind == "head":
         roof = r["roofline"]
+        conc = roof["concurrent"] or {}
         print(tags, round(r["value"] / 1e9, 3), "G ms", round(r["ms_per_step"], 4), "k_play",
-              round(roof["kernel_ms"] * 1e3, 1), "ahead", round(roof["concurrent"]["kernel_ms"] * 1e3, 1))
+              round(roof["kernel_ms"] * 1e3, 1), "ahead", round((conc.get("kernel_ms") or 0) * 1e3, 1),
+              "decode", round((conc.get("decode_kernel_ms") or 0) * 1e3, 1))
     elif kind == "puct":
         x = r["extra_config4_puct"]
         print(tags, round(x["value"] / 1e6, 1), "M playout env-steps/s wall", round(x["wall_s"], 3), x["mlp"])
