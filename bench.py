@@ -58,7 +58,7 @@ ALGO_BYTES_PER_STEP = (33 * N_PLAYERS + 57) + 47 * N_PLAYERS  # 377 B at N = 4
 # live timing.
 LIB_TWIST_EVERY = 4  # the library's SN_OPT_TWIST_EVERY default (include/sechs.h)
 SQ_CONFIG4_ROLLOUTS = "profiles/r05_sq_config4_rollouts.json"  # SQ pass of k_puct_rollouts (eager launches)
-PMC_TRAFFIC = {"numpy": os.path.join(ROOT, "profiles", "r05_pmc_traffic_numpy.json"),  # tools/r05_final.sh
+PMC_TRAFFIC = {"numpy": os.path.join(ROOT, "profiles", "r06_base_pmc_traffic_numpy.json"),  # tools/r06_base.sh
                "philox": os.path.join(ROOT, "profiles", "r04_pmc_traffic_philox.json")}
 
 
@@ -816,11 +816,20 @@ def bench_acer(games, episodes=3):
 
 
 def pmc_traffic(rng, games):
+    """per-dispatch HBM bytes of the headline kernels from the committed
+    rocprofv3 PMC passes (tools/pmc_traffic.py), and -- numpy mode -- the
+    step traffic recomputed from the same file: each kernel's bytes per
+    dispatch x its MEASURED dispatches per play launch in that run (the
+    start-up twist k_mt_ahead<true, ..> excluded: once per pipeline start)"""
     path = PMC_TRAFFIC[rng]
     if games != 65536 or not os.path.exists(path):
         return None, None
     rec = json.load(open(path))
     per_kernel = {k: v["traffic_bytes_per_dispatch"] for k, v in rec["kernels"].items()}
+    per_kernel["_ratio"] = {k: v.get("dispatches_per_play_launch") for k, v in rec["kernels"].items()}
+    per_kernel["_step"] = sum(v["traffic_bytes_per_dispatch"] * v["dispatches_per_play_launch"]
+                              for k, v in rec["kernels"].items()
+                              if "dispatches_per_play_launch" in v and "k_mt_ahead<true" not in k) or None
     return per_kernel, os.path.relpath(path, ROOT)
 
 
@@ -906,6 +915,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": wall / args.steps * 1e3,
+        "timed_region_s": wall,
         "host_enqueue_ms_per_step": ENQUEUE_S / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
@@ -948,12 +958,14 @@ def main():
                                              "episode records -- draws, deals, stream offsets -- for k_play<4, "
                                              "RNG_NUMPY_DEC>; SN_OPT_PIPE_DEC)",
                             "decode_kernel_ms": kt.get("k_decode"),
-                            "traffic": per_kernel.get("k_mt_ahead") if per_kernel else None,
-                            "traffic_unit": "HBM bytes per twist dispatch (PMC)"}
+                            "traffic": per_kernel.get("k_mt_ahead<false") if per_kernel else None,
+                            "traffic_unit": "HBM bytes per steady twist dispatch (PMC)",
+                            "twist_dispatches_per_play_launch": (per_kernel["_ratio"].get("k_mt_ahead<false")
+                                                                 if per_kernel else None)}
                            if args.rng == "numpy" else None),
-            # one twist dispatch per K play launches (SN_OPT_TWIST_EVERY): its traffic per launch is 1/K
-            "step_traffic": ((per_kernel.get("k_play<4", 0.0) + per_kernel.get("k_mt_ahead", 0.0) / twist_k)
-                             if per_kernel else None),
+            # sum over the step's kernels of PMC bytes per dispatch x measured dispatches per play launch
+            # (the traffic file's own counts: recomputable by hand from it)
+            "step_traffic": per_kernel.get("_step") if per_kernel else None,
             "twist_every": twist_k if args.rng == "numpy" else None,
         },
         "episodes_checksum": {"episodes": int(eps.sum().item()) * world, "mean_score_per_seat": (tot / (eps.sum().item() * world)).tolist()},

@@ -174,14 +174,14 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          launch.
      SN_OPT_PIPE_FUSED   removed (round 6): the twist folded into k_play_quad,
                          measured slower; SN_EUNSUPPORTED.
-     SN_OPT_PIPE_DEC     1: pipelined numpy-compat DrunkHamster rollouts
+     SN_OPT_PIPE_DEC     1 (default): pipelined numpy-compat DrunkHamster rollouts
                          with auto-reset of a plain handle of N <= 4 whose games
                          are in lockstep (after sn_reset) decode ahead: on the
                          side stream, after each group's twist, k_decode walks
                          every game's ring and writes one record per episode
                          (its draws, the next deal's sorted hands and rows, the
                          stream offsets), and k_play plays from the records
-                         with no RNG work; 0 (default): k_play draws from the ring.
+                         with no RNG work; 0: k_play draws from the ring itself.
                          Same words, same outputs, same exported numpy states.
      SN_OPT_TWIST_SKIP   TEST KNOB: 1 = every steady twist after the first
                          group's twists nothing, so the default schedule

@@ -1029,19 +1029,22 @@ __global__ __launch_bounds__(kBlock) void k_play(DevState s, PlayArgs a) {
 // same stream (ptend[tpar]) leads the decoder position by the lead.
 struct DecArgs {
     int e0, ne, phi0, tpar;
+    int cin, cout;  // pabsc slots of the decoder position read / written
 };
 
 // One lane per game.  Per episode the lane copies a RingPipe window of its
 // ring (kPipeWin bytes from the decoder position, all loads in flight at
 // once) to LDS and reads the words from there -- the draws through the byte
 // buffer, the shuffle targets straight from the window by position -- as
-// the play kernel's own RingPipe path does; the deck then overlays the dead
-// window.  (Reading the ring from HBM unit by unit was twice as slow: the
-// loop's loads waited one by one.)  Per lane: window (kPipeSlot) + swap
-// targets (104) at an odd 8-B stride.
-constexpr int kDecBlock = 128;
-constexpr int kDecLane = 376;  // >= kPipeSlot + 104, 47 x 8 B
-static_assert(kDecLane >= kPipeSlot + 104 && kDecLane % 8 == 0 && (kDecLane / 8) % 2 == 1, "decoder LDS lane");
+// the play kernel's own RingPipe path does.  (Reading the ring from HBM unit
+// by unit was twice as slow: the loop's loads waited one by one.)  Per lane
+// kPipeSlot bytes (an odd 8-B stride): the window; the swap targets overlay
+// its first 104 bytes (target k lands on window byte k while the reads are
+// past stream offset 36 + k: every earlier draw took >= 1 word), and the
+// deck its bytes 112..219 once the targets are drawn.
+constexpr int kDecBlock = 64;  // one wave per workgroup: packs beside the play blocks
+constexpr int kDecLane = kPipeSlot;
+static_assert(kDecLane % 8 == 0 && (kDecLane / 8) % 2 == 1 && kDecLane >= 112 + 108, "decoder LDS lane");
 
 template <int N>
 __global__ __launch_bounds__(kDecBlock) void k_decode(DevState s, DecArgs d) {
@@ -1050,9 +1053,10 @@ __global__ __launch_bounds__(kDecBlock) void k_decode(DevState s, DecArgs d) {
     const int64_t g = (int64_t)blockIdx.x * kDecBlock + threadIdx.x;
     if (g >= s.B) return;
     const int64_t B = s.B;
-    uint8_t* win = lds + threadIdx.x * kDecLane;  // the ring window; the deck once the targets are drawn
-    uint8_t* jslot = win + kPipeSlot;
-    uint32_t pos = s.pabsc[(int64_t)kDecSlot * B + g];
+    uint8_t* win = lds + threadIdx.x * kDecLane;  // the ring window
+    uint8_t* jslot = win;                         // the swap targets, over the window's consumed head
+    uint8_t* deck = win + 112;                    // the deck, once the window is dead
+    uint32_t pos = s.pabsc[(int64_t)d.cin * B + g];
     const uint32_t tend = s.ptend[(int64_t)d.tpar * B + g];
     PhaseProf pq;
     pq.start();
@@ -1080,15 +1084,15 @@ __global__ __launch_bounds__(kDecBlock) void k_decode(DevState s, DecArgs d) {
         }
         pq.mark(PR_DRAWS);
         // step 9 plays each seat's last card (no draw), then the auto-reset deal
-        shuffle_targets(rng, buf, jslot, s.C);  // the window's own form (by position, no byte buffer)
+        shuffle_targets(rng, buf, jslot, s.C, kDecLane - 1);  // the window's own form (by position), dummy past it
         pos = rng.consumed(buf);
         pq.mark(PR_TARGETS);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the window reads before the deck's writes
-        for (int k = 0; k < s.C; k += 4) *(uint32_t*)(win + k) = (uint32_t)k * 0x01010101u + 0x03020100u;
-        shuffle_apply(win, jslot, s.C);
+        for (int k = 0; k < s.C; k += 4) *(uint32_t*)(deck + k) = (uint32_t)k * 0x01010101u + 0x03020100u;
+        shuffle_apply(deck, jslot, s.C);
         pq.mark(PR_APPLY);
         Game<N> G;
-        deal_from_deck<N>(win, s.C, G);
+        deal_from_deck<N>(deck, s.C, G);
         pq.mark(PR_HANDS);
         {
             const uint32_t o = pos - start;
@@ -1115,7 +1119,7 @@ __global__ __launch_bounds__(kDecBlock) void k_decode(DevState s, DecArgs d) {
         pq.mark(PR_STORE);
     }
     pq.flush(lane, 1);
-    s.pabsc[(int64_t)kDecSlot * B + g] = pos;
+    s.pabsc[(int64_t)d.cout * B + g] = pos;
 }
 
 // ---- one-game fast path (the scalar drop-in SechsNimmtEnv, B == 1) -------
@@ -1692,7 +1696,7 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
         const char* ps = getenv("SECHS_PIPE_SERIAL");
         e->pipe_serial = (ps && ps[0] == '1') ? 1 : 0;
     }
-    e->pipe_dec = 0;  // decode-ahead: measured slower so far, opt-in
+    e->pipe_dec = 1;  // decode-ahead where it applies: 0.0776 -> 0.069 ms per step same box
     {
         const char* pd = getenv("SECHS_PIPE_DEC");  // default override (A/B runs of whole legs)
         if (pd && (pd[0] == '0' || pd[0] == '1')) e->pipe_dec = pd[0] - '0';
@@ -1704,7 +1708,7 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
             void** p;
             size_t bytes;
         } pal[] = {{(void**)&s.pring, (size_t)kPipeRing * B},
-                   {(void**)&s.pabsc, sizeof(uint32_t) * (kPipeSlots + 1) * B},  // + the decoder's slot
+                   {(void**)&s.pabsc, sizeof(uint32_t) * (kPipeSlots + 2) * B},  // + the decoder's two slots
                    {(void**)&s.ptend, sizeof(uint32_t) * kPipeSlots * B}, {(void**)&s.ptp, sizeof(uint32_t) * B},
                    {(void**)&s.perr, sizeof(uint32_t)},
                    {(void**)&s.drec, N <= kSplitMaxPlayers ? sizeof(u32x4) * kDecRecords * kDecQuads * B : 16}};
@@ -1721,6 +1725,8 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
         const char* sf = getenv("SECHS_EV_SYSFENCE");
         const unsigned evf = hipEventDisableTiming | ((sf && sf[0] == '1') ? 0u : (unsigned)hipEventDisableSystemFence);
         if (hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&e->side2, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&e->ev_prep2, evf) != hipSuccess ||
             hipEventCreateWithFlags(&e->ev_prep, evf) != hipSuccess ||
             hipEventCreateWithFlags(&e->ev_main, evf) != hipSuccess ||
             hipEventCreateWithFlags(&e->ev_play, evf) != hipSuccess) {
@@ -1728,7 +1734,8 @@ sn_status sn_create(sn_env** out, int device, int64_t num_games, int num_players
             return fail(SN_EHIP, "stream/event creation failed");
         }
         for (int k = 0; k < 2; k++)
-            if (hipEventCreateWithFlags(&e->evt[k], evf) != hipSuccess) {
+            if (hipEventCreateWithFlags(&e->evt[k], evf) != hipSuccess ||
+                hipEventCreateWithFlags(&e->evd[k], evf) != hipSuccess) {
                 sn_destroy(e);
                 return fail(SN_EHIP, "stream/event creation failed");
             }
@@ -1767,8 +1774,12 @@ sn_status sn_destroy(sn_env* e) {
     if (e->ev_prep) (void)hipEventDestroy(e->ev_prep);
     if (e->ev_main) (void)hipEventDestroy(e->ev_main);
     if (e->ev_play) (void)hipEventDestroy(e->ev_play);
-    for (int k = 0; k < 2; k++)
+    for (int k = 0; k < 2; k++) {
         if (e->evt[k]) (void)hipEventDestroy(e->evt[k]);
+        if (e->evd[k]) (void)hipEventDestroy(e->evd[k]);
+    }
+    if (e->ev_prep2) (void)hipEventDestroy(e->ev_prep2);
+    if (e->side2) (void)hipStreamDestroy(e->side2);
     if (e->perr_host) (void)hipHostFree(e->perr_host);
     if (e->hbuf) (void)hipHostFree(e->hbuf);
     if (e->side) (void)hipStreamDestroy(e->side);
@@ -2017,6 +2028,8 @@ sn_status sn_pipe_sync(sn_env* e, hipStream_t st) {
     HIP_TRY(hipStreamWaitEvent(st, e->ev_play, 0));
     HIP_TRY(hipEventRecord(e->ev_prep, e->side));
     HIP_TRY(hipStreamWaitEvent(st, e->ev_prep, 0));
+    HIP_TRY(hipEventRecord(e->ev_prep2, e->side2));  // the decodes (their ring reads) are done too
+    HIP_TRY(hipStreamWaitEvent(st, e->ev_prep2, 0));
     // the last play launch wrote pabsc[pl_cout]; the last twist ptend[tw_out]
     hipLaunchKernelGGL(k_pipe_code, dim3((unsigned)((e->s.B + kBlock / 64 - 1) / (kBlock / 64))), dim3(kBlock), 0, st,
                        e->s, e->pl_cout, e->tw_out);
@@ -2088,9 +2101,9 @@ static sn_status dec_play(const DevState& s, const PlayArgs& c, size_t shmem, hi
 }
 
 // records of episodes [e0, e0 + ne) (global counter since the pipeline start) on stream st
-static sn_status dec_launch(sn_env* e, int64_t e0, int ne, int phi0, int tpar, hipStream_t st) {
+static sn_status dec_launch(sn_env* e, int64_t e0, int ne, int phi0, int tpar, int cin, int cout, hipStream_t st) {
     const DevState& s = e->s;
-    const DecArgs d{(int)(e0 % kDecRecords), ne, phi0, tpar};
+    const DecArgs d{(int)(e0 % kDecRecords), ne, phi0, tpar, cin, cout};
     const dim3 grid((unsigned)((s.B + kDecBlock - 1) / kDecBlock));
     SN_DISPATCH_N(s.N, {
         if constexpr (NN <= kSplitMaxPlayers) hipLaunchKernelGGL((k_decode<NN>), grid, dim3(kDecBlock), 0, st, s, d);
@@ -2141,12 +2154,16 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         const sn_status r = sn_pipe_sync(e, st);
         if (r != SN_OK) return r;
     }
-    // Decode-ahead: the twists lead the DECODER (pabsc[kDecSlot]) by 300 (K + 2) words -- the
-    // K + 1 episodes (~195 words each at N = 4) a decode launch may need -- and the play
-    // launches read no ring at all.  Otherwise they lead the play consumer by 600 K words.
-    const int lead = dec ? e->pipe_lead * (K + 2) / 2 : e->pipe_lead * K;
+    // Decode-ahead: twist G runs on `side` CONCURRENTLY with decode G on `side2`, so it leads
+    // the decoder position after decode G-1 (slot kDecSlot + ((G - 1) & 1)) by the words of
+    // the 2K + 1 episodes decode G+1 may need: 600 (K + 1) words (~200 per episode at N <= 4;
+    // the ring holds the lead + a round up to 3 472), and the play launches read no ring at
+    // all.  Otherwise the twists lead the play consumer by 600 K words.
+    const int lead = dec ? min(e->pipe_lead * (K + 1), kPipeRing - kMtN) : e->pipe_lead * K;
     constexpr uint32_t kSlotMask = (uint32_t)kPipeSlots - 1u;
     if (!e->pvalid) {  // start the pipeline from mt_pos: twist the lead ahead, synchronously
+        // decode-ahead: the start position to the decoder's input slot of the first decode and
+        // the play slot (a sync before any play launch exports it)
         const AheadArgs aa{dec ? kDecSlot : (int)kSlotMask, 0, 1, lead, e->perr_host_dev, dec ? (int)kSlotMask : -1};
         e->tw_out = 1, e->pl_cout = (int)kSlotMask, e->pphase = 0;
         if (round_tw) hipLaunchKernelGGL((k_mt_ahead<true, true>), pg, dim3(kBlock), 0, st, s, aa);
@@ -2154,7 +2171,7 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         HIP_TRY(hipGetLastError());
         if (dec) {  // the records of the first group's launches (episodes 0 .. K), from the current step on
             e->dec_e = 0;
-            const sn_status r = dec_launch(e, 0, K + 1, e->phase, 1, st);
+            const sn_status r = dec_launch(e, 0, K + 1, e->phase, 1, kDecSlot, kDecSlot + 1, st);  // "decode -1"
             if (r != SN_OK) return r;
             e->dec_next = K + 1;
         }
@@ -2193,7 +2210,8 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
         const uint64_t G = p / (uint64_t)K;
         const bool first = (p % (uint64_t)K) == 0u;  // twist G beside this launch
         c.pipe_t = (int)((G + 1u) & 1u);              // twist G-1's end (INIT's for group 0)
-        if (first && G >= 1u) HIP_TRY(hipStreamWaitEvent(st, e->evt[(G + 1u) & 1u], 0));  // twist G-1
+        // twist G-1 (decode-ahead: decode G-1, which waited for twist G-1 itself)
+        if (first && G >= 1u) HIP_TRY(hipStreamWaitEvent(st, (dec ? e->evd : e->evt)[(G + 1u) & 1u], 0));
         if (first && !e->pipe_serial) HIP_TRY(hipEventRecord(e->ev_main, st));  // launch p-1's consumption is final
         const int ti = (e->tn < e->tcap) ? e->tn++ : -1;  // SN_OPT_TIMING: this launch's events
         hipEvent_t* tv = (ti >= 0) ? e->tev + kTimingEvents * ti : nullptr;
@@ -2215,28 +2233,37 @@ static sn_status launch_pipe(sn_env* e, PlayArgs a, hipStream_t st) {
             HIP_TRY(hipStreamWaitEvent(e->side, e->ev_main, 0));
             if (tv) HIP_TRY(hipEventRecord(tv[2], e->side));
             // SN_OPT_TWIST_SKIP (tests only): the overrun detector under the default schedule
-            const AheadArgs aa{dec ? kDecSlot : c.pipe_cin, c.pipe_t, (int)(G & 1u),
+            const AheadArgs aa{dec ? kDecSlot + (int)((G + 1u) & 1u) : c.pipe_cin, c.pipe_t, (int)(G & 1u),
                                (e->twist_skip && G >= 1u) ? 0 : lead, e->perr_host_dev, -1};
             if (round_tw) hipLaunchKernelGGL((k_mt_ahead<false, true>), pg, dim3(kBlock), 0, e->side, s, aa);
             else hipLaunchKernelGGL((k_mt_ahead<false, false>), pg, dim3(kBlock), 0, e->side, s, aa);
             HIP_TRY(hipGetLastError());
             if (tv) HIP_TRY(hipEventRecord(tv[3], e->side));
             if (dec) {
-                // the records group G+1 may touch: its launches start at most K episodes past this
-                // launch's and touch at most one more each -- episodes < e_start + 2K + 1 (the ring
-                // of kDecRecords >= 2K + 2 slots never overwrites one this group still reads: this
-                // decode runs after launch p-1, and group G reads episodes <= e_start + K)
+                // decode G on side2, concurrent with twist G: the records group G+1 may touch --
+                // its launches start at most K episodes past this launch's and touch at most one
+                // more each: episodes < e_start + 2K + 1 (the ring of kDecRecords >= 2K + 2
+                // slots never overwrites one a running launch reads: the oldest, launch p-K,
+                // reads episodes >= e_start - K, 3K + 1 <= kDecRecords).  It reads the words twist
+                // G-1 twisted (ptend slot (G-1) & 1) and waits for that twist only (which waited
+                // for launch p-K-1), and its position goes to slot kDecSlot + (G & 1), which
+                // twist G+1 reads.
                 const int64_t target = e_start + 2 * K + 1;
-                if (target > e->dec_next) {
-                    if (tv) HIP_TRY(hipEventRecord(tv[4], e->side));
-                    const sn_status r = dec_launch(e, e->dec_next, (int)(target - e->dec_next), 0, (int)(G & 1u), e->side);
-                    if (r != SN_OK) return r;
-                    e->dec_next = target;
-                    if (tv) {
-                        HIP_TRY(hipEventRecord(tv[5], e->side));
-                        e->tev_tw[ti] |= 2;
-                    }
+                // (group 0: the start-up twist and decode ran on the play stream, before ev_main)
+                if (e->pipe_serial || G == 0u) HIP_TRY(hipStreamWaitEvent(e->side2, e->ev_main, 0));
+                if (G >= 1u) HIP_TRY(hipStreamWaitEvent(e->side2, e->evt[(G + 1u) & 1u], 0));
+                if (tv) HIP_TRY(hipEventRecord(tv[4], e->side2));
+                const int ne = target > e->dec_next ? (int)(target - e->dec_next) : 0;
+                // ne == 0 (short launches): still a launch, so the position moves to slot G & 1
+                const sn_status r = dec_launch(e, e->dec_next, ne, 0, (int)((G + 1u) & 1u),
+                                               kDecSlot + (int)((G + 1u) & 1u), kDecSlot + (int)(G & 1u), e->side2);
+                if (r != SN_OK) return r;
+                e->dec_next = max(e->dec_next, target);
+                if (tv) {
+                    HIP_TRY(hipEventRecord(tv[5], e->side2));
+                    e->tev_tw[ti] |= 2;
                 }
+                HIP_TRY(hipEventRecord(e->evd[G & 1u], e->side2));
             }
             HIP_TRY(hipEventRecord(e->evt[G & 1u], e->side));
             HIP_TRY(hipEventRecord(e->ev_prep, e->side));

@@ -62,7 +62,7 @@ struct DevState {
 
 constexpr int kMt0Levels = 8;    // word-0 crossings kept in mt0 (the decode-ahead span: up to seven rounds)
 constexpr int kPipeSlots = 8;    // pabsc buffers (by play launch index mod 8; ptend uses 2, by twist parity)
-constexpr int kDecSlot = kPipeSlots;  // pabsc slot kPipeSlots: the decoder's stream position (decode-ahead mode)
+constexpr int kDecSlot = kPipeSlots;  // pabsc slots kDecSlot + (G & 1): the decoder's position after decode G
 constexpr int kDecRecords = 16;  // decode-ahead record ring (episodes; >= 2K + 2 for K <= 5)
 constexpr int kDecQuads = 6;     // 16-B pieces per record (24 dwords, the layout at DecSrc)
 constexpr int kTimingEvents = 6; // SN_OPT_TIMING events per launch: play, twist, decode (start, end)
@@ -443,7 +443,10 @@ __device__ __forceinline__ uint64_t pipe_peek8(const RingPipe& r, uint32_t t) {
     return sh ? ((lo >> sh) | (hi << (64u - sh))) : lo;
 }
 
-__device__ __forceinline__ void shuffle_targets(RingPipe& rng, ByteBuf& buf, uint8_t* jslot, int C) {
+// dummy: the byte a rejected word's store goes to (jslot[103] by default; k_decode, whose targets overlay
+// the window's consumed head, passes a byte past the window's live bytes)
+__device__ __forceinline__ void shuffle_targets(RingPipe& rng, ByteBuf& buf, uint8_t* jslot, int C,
+                                                uint32_t dummy = 103u) {
     uint32_t t = rng.take - buf.cnt;  // next unconsumed byte (buffered bytes are re-read from the window)
     buf.clear();
     uint32_t i = (uint32_t)C - 1u;
@@ -467,7 +470,7 @@ __device__ __forceinline__ void shuffle_targets(RingPipe& rng, ByteBuf& buf, uin
             const uint32_t m = 0xFFFFFFFFu >> __builtin_clz(ii | 1u);
             const uint32_t x = (uint32_t)(w >> (8u * q)) & m;
             const bool acc = act && (x <= ii);
-            jslot[acc ? (uint32_t)C - 1u - ii : 103u] = (uint8_t)x;
+            jslot[acc ? (uint32_t)C - 1u - ii : dummy] = (uint8_t)x;
             ii -= acc ? 1u : 0u;
             used = act ? q + 1u : used;
         }
@@ -967,6 +970,8 @@ struct sn_env {
     int pvalid;         // ring + ptend/pabsc/ptp are the live RNG state (mt_pos is stale)
     uint64_t pcount;    // pipelined play launches so far
     hipStream_t side;
+    hipStream_t side2;                      // decode-ahead: k_decode, concurrent with the twists on `side`
+    hipEvent_t evd[2], ev_prep2;            // after decode G (slot G mod 2); behind side2 (sn_pipe_sync)
     hipEvent_t ev_prep, ev_main, ev_play;  // ev_play: after the last pipelined k_play (recorded on that call's stream)
     uint32_t* perr_host;                    // pinned, device-mapped mirror of s.perr (PlayArgs::perr_mirror)
     uint32_t* perr_host_dev;

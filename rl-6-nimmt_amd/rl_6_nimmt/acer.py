@@ -74,21 +74,22 @@ def make_actor_critic(hidden_sizes=(100, 100), activation=None):
 def distinct_picks(S, rows, k, gen, dev):
     """[rows, k] indices into range(S), each row k DISTINCT uniform picks
     (random.sample per row, as the reference draws its off-policy batch):
-    rows with a repeated index are redrawn whole, which leaves every row
-    uniform over the ordered k-tuples of distinct indices"""
+    pick j is uniform over the S - j values not picked yet -- x uniform in
+    [0, S - j), then stepped past the row's earlier picks in ascending order
+    (x + 1 for each one <= x) -- so every ordered k-tuple of distinct values
+    is equally likely.  A fixed amount of device work, no host sync (the
+    round-5 rejection loop read a duplicate count back every round)."""
     if k > S:
         raise ValueError(f"sample of {k} distinct sequences from {S}")
-    if S <= 4 * k:  # few candidates: a permutation per row
-        return torch.rand((rows, S), generator=gen, device=dev).argsort(dim=1)[:, :k]
-    pick = torch.randint(0, S, (rows, k), generator=gen, device=dev)
-    for _ in range(64):
-        srt = pick.sort(dim=1).values
-        dup = (srt[:, 1:] == srt[:, :-1]).any(dim=1)
-        n = int(dup.sum())
-        if n == 0:
-            return pick
-        pick[dup] = torch.randint(0, S, (n, k), generator=gen, device=dev)
-    raise RuntimeError("distinct_picks: no distinct draw after 64 rounds")
+    cols, taken = [], None  # taken: the row's picks so far, ascending
+    for j in range(k):
+        x = torch.randint(0, S - j, (rows, 1), generator=gen, device=dev)
+        if taken is not None:
+            for m in range(j):  # ascending: each earlier pick at or below x shifts it up by one
+                x = x + (x >= taken[:, m:m + 1]).to(x.dtype)
+        cols.append(x)
+        taken = x if taken is None else torch.cat((taken, x), dim=1).sort(dim=1).values
+    return torch.cat(cols, dim=1)
 
 
 class BatchedACER(BatchedPUCT):
@@ -333,8 +334,12 @@ class BatchedACER(BatchedPUCT):
         seqs = self.stored_sequences(upto_chunk)
         S, dev = len(seqs), self.env.device
         pick = torch.rand((self.D, S), generator=self._gen, device=dev).argsort(dim=1)[:, : self.minibatch]
-        tab = torch.tensor(seqs, dtype=torch.long, device=dev)  # [S, 2]
-        return tab[pick, 0], tab[pick, 1]
+        # [S, 2] built on the device: a host tensor copied per call would wait for the stream
+        sl = torch.tensor([q for q, _ in seqs], dtype=torch.long).pin_memory().to(dev, non_blocking=True) \
+            if dev.type == "cuda" else torch.tensor([q for q, _ in seqs], dtype=torch.long)
+        ch = torch.tensor([c for _, c in seqs], dtype=torch.long).pin_memory().to(dev, non_blocking=True) \
+            if dev.type == "cuda" else torch.tensor([c for _, c in seqs], dtype=torch.long)
+        return sl[pick], ch[pick]
 
     # ------------------------------------------------------------ tournament mode (decision lists)
     def league_batches(self, chunk):
@@ -350,11 +355,13 @@ class BatchedACER(BatchedPUCT):
         on = (torch.full((Dn, 1), s_new, dtype=torch.long, device=dev),
               torch.full((Dn, 1), chunk, dtype=torch.long, device=dev),
               torch.arange(Dn, device=dev)[:, None])
+        # built on the device (a host tensor copied per call would wait for the stream)
         tab = []
         for sl, c in self.stored_sequences(chunk):
             nd = self.rep_nd[sl]
-            tab.append(torch.stack((torch.full((nd,), sl), torch.full((nd,), c), torch.arange(nd)), dim=1))
-        tab = torch.cat(tab, dim=0).to(dev)
+            tab.append(torch.stack((torch.full((nd,), sl, device=dev), torch.full((nd,), c, device=dev),
+                                    torch.arange(nd, device=dev)), dim=1))
+        tab = torch.cat(tab, dim=0)
         pick = distinct_picks(tab.shape[0], Dn, self.minibatch, self._gen, dev)
         off = (tab[pick, 0], tab[pick, 1], tab[pick, 2])
         return on, off

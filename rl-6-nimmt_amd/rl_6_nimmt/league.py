@@ -494,10 +494,13 @@ class BatchedTournament:
                 nat.check(L.sn_league_step(env._h, nat.ptr(acts), nat.ptr(per_step[t]), None,
                                            nat.ptr(rec) if t == T_STEPS - 1 else None, nat.ptr(invalid[t]),
                                            nat.ptr(status), st), "sn_league_step")
-            if self.engines:  # external seats played: an illegal card fails the round at its step (sechs.h)
-                bad = int((invalid[t] >= 0).sum())
-                if bad:
-                    raise RuntimeError(f"sn_league_step: {bad} illegal moves of the net agents' engines at step {t}")
+        if self.engines:  # external seats played: an illegal card fails the round (sechs.h) -- checked once
+            # per round, not per step: a host read-back per step kept the host from enqueueing the next
+            # step's searches while the GPU ran this one
+            bad = (invalid >= 0).sum(dim=1).cpu()
+            if int(bad.sum()):
+                t = int(torch.nonzero(bad).flatten()[0])
+                raise RuntimeError(f"sn_league_step: {int(bad[t])} illegal moves of the net agents' engines at step {t}")
         q6 = int(status.sum())
         if q6:
             self.q6_slot_rounds += q6
