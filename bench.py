@@ -58,7 +58,8 @@ ALGO_BYTES_PER_STEP = (33 * N_PLAYERS + 57) + 47 * N_PLAYERS  # 377 B at N = 4
 # live timing.
 LIB_TWIST_EVERY = 4  # the library's SN_OPT_TWIST_EVERY default (include/sechs.h)
 SQ_CONFIG4_ROLLOUTS = "profiles/r05_sq_config4_rollouts.json"  # SQ pass of k_puct_rollouts (eager launches)
-PMC_TRAFFIC = {"numpy": os.path.join(ROOT, "profiles", "r06_base_pmc_traffic_numpy.json"),  # tools/r06_base.sh
+PMC_TRAFFIC = {"numpy": os.path.join(ROOT, "profiles", "r06_dec_pmc_traffic_numpy.json"),  # tools/r06_final.sh
+               "numpy_ring": os.path.join(ROOT, "profiles", "r06_base_pmc_traffic_numpy.json"),  # --pipe-dec 0
                "philox": os.path.join(ROOT, "profiles", "r04_pmc_traffic_philox.json")}
 
 
@@ -902,7 +903,9 @@ def main():
     play_mode = ("RNG_PHILOX" if args.rng != "numpy" else
                  "RNG_NUMPY_DEC" if (kt.get("k_decode") or 0.0) > 0.0 else "RNG_NUMPY_PIPE")
     achieved = launch_steps * ALGO_BYTES_PER_STEP / (play_ms * 1e-3) / 1e9
-    per_kernel, traffic_src = pmc_traffic(args.rng, B) if not args.no_obs else (None, None)
+    dec = play_mode == "RNG_NUMPY_DEC"
+    per_kernel, traffic_src = (pmc_traffic(args.rng if dec or args.rng != "numpy" else "numpy_ring", B)
+                               if not args.no_obs else (None, None))
     traffic = per_kernel.get("k_play<4") if per_kernel else None
     # bytes the counters saw per launch / its duration: below `frac` when the
     # game state stays in VGPRs within a launch (SURVEY §8(d) counts it twice)
@@ -954,10 +957,13 @@ def main():
             "concurrent": ({"kernel": "k_mt_ahead<false, true> (side stream: one dispatch per twist_every play "
                                       "launches, whole MT19937 rounds ahead of the consumer)",
                             "kernel_ms": kt.get("k_mt_ahead"),
-                            "decode_kernel": "k_decode<4> (side stream, after the group's twist: the next group's "
-                                             "episode records -- draws, deals, stream offsets -- for k_play<4, "
-                                             "RNG_NUMPY_DEC>; SN_OPT_PIPE_DEC)",
+                            "decode_kernel": "k_decode<4> (second side stream, concurrent with the group's twist: "
+                                             "the next group's episode records -- draws, deals, stream offsets -- "
+                                             "for k_play<4, RNG_NUMPY_DEC>; SN_OPT_PIPE_DEC)",
                             "decode_kernel_ms": kt.get("k_decode"),
+                            "decode_traffic": per_kernel.get("k_decode") if per_kernel else None,
+                            "decode_dispatches_per_play_launch": (per_kernel["_ratio"].get("k_decode")
+                                                                  if per_kernel else None),
                             "traffic": per_kernel.get("k_mt_ahead<false") if per_kernel else None,
                             "traffic_unit": "HBM bytes per steady twist dispatch (PMC)",
                             "twist_dispatches_per_play_launch": (per_kernel["_ratio"].get("k_mt_ahead<false")

@@ -19,6 +19,7 @@
 #include <hip/hip_bf16.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "sechs_state.h"
 
@@ -998,28 +999,33 @@ __global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a
                 }
                 fence();
                 pf.mark(RP_BASE);
-                // phase 3: the group's candidate rows, 64 per tile, logits to LDS (over the dead rows)
+                // phase 3: the group's candidate rows, 64 per tile, logits to LDS (over the dead rows);
+                // a last tile of <= 32 rows as one 32-row half (odd n_cur: half the MFMAs and B fragments)
                 const uint32_t rows = (uint32_t)nseat * (uint32_t)m;
-                const uint32_t tiles = (rows + 32u * TNT - 1u) / (32u * TNT);
-                for (uint32_t tile = 0; tile < tiles; tile++) {
-                    uint32_t rw[TNT];
-                    float x[TNT];
-                    const uint16_t* brow[TNT];
+                auto run_tile = [&](auto tnt, uint32_t base) {
+                    constexpr int T = decltype(tnt)::value;
+                    uint32_t rw[T];
+                    float x[T];
+                    const uint16_t* brow[T];
 #pragma unroll
-                    for (int nt = 0; nt < TNT; nt++) {
-                        rw[nt] = tile * 32u * TNT + 32u * nt + (uint32_t)col;
+                    for (int nt = 0; nt < T; nt++) {
+                        rw[nt] = base + 32u * nt + (uint32_t)col;
                         const uint32_t rc = rw[nt] < rows ? rw[nt] : rows - 1u;
                         const uint32_t q = rc / (uint32_t)m;
                         x[nt] = sCard[q * kHand + (rc - q * (uint32_t)m)];
                         brow[nt] = sBase + q * kBaseLds;
                     }
-                    float out[TNT];
-                    mlp_tile<TNT>(brow, x, sW, sC, sH2, col, half, out);
-                    if (tile == 0) fence();  // every lane's phase-2 row reads are done before logits land on them
+                    float out[T];
+                    mlp_tile<T>(brow, x, sW, sC, sH2, col, half, out);
+                    if (base == 0u) fence();  // every lane's phase-2 row reads are done before logits land on them
 #pragma unroll
-                    for (int nt = 0; nt < TNT; nt++)
+                    for (int nt = 0; nt < T; nt++)
                         if (half == 0 && rw[nt] < rows) sLogit[rw[nt]] = out[nt];
-                }
+                };
+                const uint32_t full = rows / (32u * TNT), rest = rows - full * 32u * TNT;
+                for (uint32_t tile = 0; tile < full; tile++) run_tile(std::integral_constant<int, TNT>{}, tile * 32u * TNT);
+                if (rest > 32u) run_tile(std::integral_constant<int, TNT>{}, full * 32u * TNT);
+                else if (rest) run_tile(std::integral_constant<int, 1>{}, full * 32u * TNT);
                 fence();
                 pf.mark(RP_TILES);
                 // the step: L lanes per decision (step_seat, as k_puct_step_seats); lanes past the
