@@ -176,9 +176,11 @@ sn_status sn_philox_counter(sn_env* env, int64_t game, uint64_t* counter_host);
                          measured slower; SN_EUNSUPPORTED.
      SN_OPT_PIPE_DEC     1 (default): pipelined numpy-compat DrunkHamster rollouts
                          with auto-reset of a plain handle of N <= 4 whose games
-                         are in lockstep (after sn_reset) decode ahead: on the
-                         side stream, after each group's twist, k_decode walks
-                         every game's ring and writes one record per episode
+                         are in lockstep (after sn_reset) decode ahead: on a
+                         second side stream, concurrent with each group's
+                         twist (reading the words the twist before produced),
+                         k_decode walks every game's ring a group ahead of the
+                         play launches and writes one record per episode
                          (its draws, the next deal's sorted hands and rows, the
                          stream offsets), and k_play plays from the records
                          with no RNG work; 0: k_play draws from the ring itself.

@@ -395,13 +395,59 @@ __device__ double hist_median(const int32_t* hist, int32_t total) {
     return 0.5 * ((double)v0 + (double)v1);
 }
 
+// hist_median over the L lanes of a decision (step_seat's lanes lead .. lead + L - 1,
+// every one calling it): lane q scans bins [kChunk q, kChunk (q + 1)) -- its count,
+// an exclusive prefix over the lanes by shuffles, then the lane holding rank k0
+// (k1) finds its bin -- a quarter (L = 4) of the serial scan's loads and VALU on
+// every lane.  Same value as hist_median.
+template <int L>
+__device__ __forceinline__ double hist_median_lanes(const int32_t* hist, int32_t total, int q, int lead) {
+    constexpr int kChunk = ((kHistBins + 4 * L - 1) / (4 * L)) * 4;  // bins per lane, 4-aligned (L = 4: 44)
+    const int32_t k0 = (total - 1) / 2, k1 = total / 2;
+    int32_t mine = 0;
+    const int4* h4 = reinterpret_cast<const int4*>(hist + kChunk * q);
+#pragma unroll 2
+    for (int c = 0; c < kChunk / 4; c++) {  // kHistBins % 4 == 0: whole int4 pieces
+        const int4 w = (kChunk * q + 4 * c < kHistBins) ? h4[c] : make_int4(0, 0, 0, 0);
+        mine += w.x + w.y + w.z + w.w;
+    }
+    int32_t pre = 0;  // outcomes in the lanes before this one
+#pragma unroll
+    for (int r = 0; r < L - 1; r++) {
+        const int32_t c = __shfl(mine, lead + r);
+        pre += (r < q) ? c : 0;
+    }
+    int32_t acc = pre, v0 = INT32_MIN, v1 = INT32_MIN;
+    if (pre <= k1 && pre + mine > k0) {  // this lane holds rank k0 or k1: its bins again (L1)
+#pragma unroll 2
+        for (int c = 0; c < kChunk / 4; c++) {
+            const int4 w = (kChunk * q + 4 * c < kHistBins) ? h4[c] : make_int4(0, 0, 0, 0);
+            const int32_t cs[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int32_t b = kChunk * q + 4 * c + j - 171;
+                if (acc <= k0 && acc + cs[j] > k0) v0 = b;
+                if (acc <= k1 && acc + cs[j] > k1) v1 = b;
+                acc += cs[j];
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < L; r++) {  // the owners' bins to every lane of the decision
+        v0 = max(v0, __shfl(v0, lead + r));
+        v1 = max(v1, __shfl(v1, lead + r));
+    }
+    return 0.5 * ((double)v0 + (double)v1);
+}
+
 // PUCTAgent._compute_pucts + argmax (mcts.py:282-315) with numpy's float
 // types: c_puct * probs is float32 (a Python float times a float32 array);
 // (n_total + 1e-9) ** 0.5 is a numpy float64 scalar, which promotes the
 // product to float64 (numpy >= 2 promotion, the version the golden vectors
 // were recorded with); q and the division by (1 + n) are float64
-__device__ int puct_choose(const int32_t* st, const int32_t* hist, const float* probs, int n, double c_puct,
-                           double* pucts_out) {
+// med_all: np.median of all outcomes (read only when st[20] >= 10)
+__device__ __forceinline__ int puct_choose_med(const int32_t* st, double med_all, const float* probs, int n,
+                                               double c_puct, double* pucts_out) {
     const int32_t total = st[20];
     int32_t n_total = 0;
     for (int k = 0; k < n; k++) n_total += st[10 + k];
@@ -409,7 +455,7 @@ __device__ int puct_choose(const int32_t* st, const int32_t* hist, const float* 
     if (total < 10) {
         mx = 0.0, mn = -10.0, med = -5.0;  // _normalize_q fallback (quirk Q8)
     } else {
-        mx = (double)st[22], mn = (double)st[21], med = hist_median(hist, total);
+        mx = (double)st[22], mn = (double)st[21], med = med_all;
     }
     const double sq = sqrt((double)n_total + 1e-9);
     double best = -__builtin_inf();
@@ -425,6 +471,68 @@ __device__ int puct_choose(const int32_t* st, const int32_t* hist, const float* 
         if (v > best) best = v, choice = k;  // strict '>': NaN never wins, index 0 stays
     }
     return choice;
+}
+
+// puct_choose_med over the L lanes of a decision (lane q scores moves k = q, q + L, ..;
+// every lane of the decision calls it, lead = its first lane): the same f64 arithmetic
+// per move, the counts' sum and the first strict maximum (ties to the lower index, NaN
+// never wins, move 0 when nothing does) combined by shuffles.  Same choice.
+template <int L>
+__device__ __forceinline__ int puct_choose_lanes(const int32_t* st, double med_all, const float* probs, int n,
+                                                 double c_puct, int q, int lead) {
+    constexpr int KL = (kHand + L - 1) / L;
+    int32_t cnt[KL], sum[KL];
+    float pr[KL];
+    int32_t n_total = 0;
+#pragma unroll
+    for (int j = 0; j < KL; j++) {
+        const int k = q + L * j;
+        const bool on = k < n;
+        cnt[j] = on ? st[10 + k] : 0;
+        sum[j] = on ? st[k] : 0;
+        pr[j] = on ? probs[k] : 0.f;
+        n_total += cnt[j];
+    }
+#pragma unroll
+    for (int r = 1; r < L; r <<= 1) n_total += __shfl_xor(n_total, r);  // lanes lead .. lead + L - 1 (aligned)
+    const int32_t total = st[20];
+    double mx, mn, med;
+    if (total < 10) {
+        mx = 0.0, mn = -10.0, med = -5.0;  // _normalize_q fallback (quirk Q8)
+    } else {
+        mx = (double)st[22], mn = (double)st[21], med = med_all;
+    }
+    const double sq = sqrt((double)n_total + 1e-9);
+    double best = -__builtin_inf();
+    int choice = 0;
+#pragma unroll
+    for (int j = 0; j < KL; j++) {
+        const int k = q + L * j;
+        if (k < n) {
+            double qv = cnt[j] ? (double)sum[j] / (double)cnt[j] : med;
+            qv = (qv - mn) / (mx - mn);
+            qv = (qv < 0.0) ? 0.0 : (qv > 1.0) ? 1.0 : qv;
+            const double t = (double)((float)c_puct * pr[j]) * sq;
+            const double v = qv + t / (1.0 + (double)cnt[j]);
+            if (v > best) best = v, choice = k;
+        }
+    }
+#pragma unroll
+    for (int r = 1; r < L; r <<= 1) {
+        const double ob = __shfl_xor(best, r);
+        const int oc = __shfl_xor(choice, r);
+        const bool take = ob > best || (ob == best && oc < choice);
+        best = take ? ob : best;
+        choice = take ? oc : choice;
+    }
+    (void)lead;
+    return choice;
+}
+
+__device__ int puct_choose(const int32_t* st, const int32_t* hist, const float* probs, int n, double c_puct,
+                           double* pucts_out) {
+    const int32_t total = st[20];
+    return puct_choose_med(st, total >= 10 ? hist_median(hist, total) : 0.0, probs, n, c_puct, pucts_out);
 }
 
 // Categorical(probs).sample() with u from Philox: the first k whose
@@ -580,14 +688,22 @@ __device__ __forceinline__ void step_seat(const DevState& s, const PuctArgs& a, 
     }
     uint32_t card = 0xFFu;
     int idx = 0;
+    const int lead_lane = (int)(threadIdx.x & 63) & ~(L - 1);
+    int root_idx = 0;
+    if (t == 0 && (a.flags & 1)) {  // the root PUCT choice: every lane of the decision scores a part
+        const int32_t total = a.stats[dd * kStatWords + 20];
+        double med = __builtin_nan("");
+        if (total >= 10) med = hist_median_lanes<L>(a.hist + dd * kHistBins, total, q, lead_lane);
+        root_idx = puct_choose_lanes<L>(a.stats + dd * kStatWords, med, a.root_probs + dd * kHand, n_cur, a.c_puct, q,
+                                        lead_lane);
+    }
     if (seat) {
         float lg[kHand];
 #pragma unroll
         for (int k = 0; k < kHand; k++) lg[k] = (k < n_cur) ? logit(dd, q, k) : 0.f;
         Hand h = ro_hand(ro, q);
         if (t == 0 && q == 0 && (a.flags & 1)) {
-            idx = puct_choose(a.stats + dd * kStatWords, a.hist + dd * kHistBins, a.root_probs + dd * kHand, n_cur,
-                              a.c_puct, nullptr);
+            idx = root_idx;
         } else {
             const uint64_t gid = s.game_offset + (uint64_t)g;
             const uint64_t stream =
@@ -876,8 +992,9 @@ constexpr int kRollWaveLds = kRollSeats * kSeatRowLds * 2 + kRollSeats * kBaseLd
 // k_puct_rollouts phase profiler (diagnostics, -DSECHS_PHASE_PROF builds only,
 // sn_debug_puct_phases): shader-clock cycles per wave in the state copy-in,
 // the seat rows (phase 1), the per-seat layer-1 MFMA (phase 2), the
-// candidate tiles (phase 3) and the step; [7] counts waves
-enum { RP_COPY = 0, RP_ROWS, RP_BASE, RP_TILES, RP_STEP, RP_N };
+// candidate tiles (phase 3), the step (t > 0) and the first step (t = 0: the
+// PUCT root choice); [7] counts waves
+enum { RP_COPY = 0, RP_ROWS, RP_BASE, RP_TILES, RP_STEP, RP_STEP0, RP_N };  // RP_STEP0: the t = 0 step (PUCT choice)
 #ifdef SECHS_PHASE_PROF
 __device__ unsigned long long g_puct_phase[8];
 struct RollProf {
@@ -1034,7 +1151,7 @@ __global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a
                     s, ar, [&](int64_t dd, int q, int k) { return sLogit[((dd - d0) * N + q) * m + k]; }, t, m,
                     d0 * L + lane, d0 + nd, d0);
                 fence();
-                pf.mark(RP_STEP);
+                pf.mark(t == 0 ? RP_STEP0 : RP_STEP);
             }
         }
     }

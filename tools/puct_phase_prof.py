@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.join(ROOT, "rl-6-nimmt_amd"))
 
 import torch  # noqa: E402
 
-NAMES = ["copy_in", "seat_rows", "layer1_base", "tiles", "step"]
+NAMES = ["copy_in", "seat_rows", "layer1_base", "tiles", "step", "step_t0"]
 
 
 def main():
