@@ -658,10 +658,18 @@ __global__ void k_puct_step(DevState s, PuctArgs a, const void* logits, int ls, 
 // times the lanes of k_puct_step (D = 8192 x 4 decisions: 2 waves per SIMD
 // instead of half a wave), the per-decision latency chain split over them.
 // lane i of the step (seat i & (L - 1) of decision i / L); logit(dd, q, k):
-// candidate k's logit of seat q of decision dd
-template <int N, int L, class Logit>
+// candidate k's logit of seat q of decision dd; info(dd, g, p, kp): its game, seat and the
+// game's players (dec_info from the decision list / tournament seats, or a cached copy)
+struct DecInfo {
+    __device__ __forceinline__ void operator()(const PuctArgs& a, int64_t dd, int64_t& g, int& p, int& kp) const {
+        dec_to_gp(a, dd, g, p);
+        kp = players_of(a, g);
+    }
+};
+
+template <int N, int L, class Logit, class Info = DecInfo>
 __device__ __forceinline__ void step_seat(const DevState& s, const PuctArgs& a, Logit logit, int t, int n_cur,
-                                          int64_t i, int64_t d_hi = -1, int64_t d_dead = -1) {
+                                          int64_t i, int64_t d_hi = -1, int64_t d_dead = -1, Info info = Info{}) {
     const int64_t d = i / L;
     const int q = (int)(i & (L - 1));
     // lanes past the last decision (or past d_hi, with d_dead a decision they may read) follow along
@@ -669,21 +677,21 @@ __device__ __forceinline__ void step_seat(const DevState& s, const PuctArgs& a, 
     const bool live = d < a.D && (d_hi < 0 || d < d_hi);
     const int64_t dd = live ? d : (d_dead >= 0 ? d_dead : a.D - 1);
     int64_t g;
-    int p;
-    dec_to_gp(a, dd, g, p);
+    int p, kp;
+    info(a, dd, g, p, kp);
     int32_t* ro = a.ro + dd * kRoWords;
-    const int kp = players_of(a, g);
     const bool seat = q < N && q < kp;
     // the resolving lane's words, loaded with the seat's (no second round trip after the shuffles;
     // nothing below writes them before the resolve)
     Board b{};
-    int32_t r40 = 0, r41 = 0, s20 = 0, s21 = 0, s22 = 0;
+    int32_t r40 = 0, r41 = 0, s20 = 0, s21 = 0, s22 = 0, sf = 0, cf = 0;
     if (q == 0) {
         b = ro_board(ro);
         r40 = ro[40], r41 = ro[41];
         if (n_cur == 1) {
             const int32_t* st = a.stats + dd * kStatWords;
             s20 = st[20], s21 = st[21], s22 = st[22];
+            if (t > 0) sf = st[r41], cf = st[10 + r41];  // the backed-up move's words (first = r41 past t = 0)
         }
     }
     uint32_t card = 0xFFu;
@@ -731,8 +739,13 @@ __device__ __forceinline__ void step_seat(const DevState& s, const PuctArgs& a, 
     const int32_t outcome = r40 - (int32_t)pen[0];
     if (n_cur == 1) {
         int32_t* st = a.stats + dd * kStatWords;
-        st[first] += outcome;
-        st[10 + first] += 1;
+        if (t > 0) {
+            st[first] = sf + outcome;
+            st[10 + first] = cf + 1;
+        } else {
+            st[first] += outcome;
+            st[10 + first] += 1;
+        }
         const int32_t total = s20 + 1;
         st[20] = total;
         st[21] = (total == 1) ? outcome : min(s21, outcome);
@@ -785,6 +798,18 @@ struct SeatIn {
     int kp;               // players of the seat's game
     bool live;            // a seated player (q < kp)
 };
+
+// the same for seat q of decision d whose game seats kp players (known)
+__device__ __forceinline__ SeatIn seat_load_kp(const PuctArgs& a, int64_t d, int q, int kp, int part) {
+    const int32_t* ro = a.ro + d * kRoWords;
+    SeatIn in;
+    in.kp = kp;
+    in.live = q < kp;
+    const int qq = in.live ? q : 0;
+    in.h0 = (uint32_t)ro[8 + 3 * qq], in.h1 = (uint32_t)ro[9 + 3 * qq], in.h2 = (uint32_t)ro[10 + 3 * qq];
+    in.lo = (uint32_t)ro[part], in.hi = (uint32_t)ro[4 + part];
+    return in;
+}
 
 __device__ __forceinline__ SeatIn seat_load(const PuctArgs& a, int N, int64_t i, int part) {
     const int64_t d = i / N;
@@ -987,7 +1012,8 @@ __global__ __launch_bounds__(256, 2) void k_puct_mlp_seats(PuctArgs a, int N, in
 // wave's copy in LDS is the one the steps read and write.
 constexpr int kRollSeats = 32;  // seats per wave's group (32 / L... 64 / L / 2 decisions)
 constexpr int kRollWaveLds = kRollSeats * kSeatRowLds * 2 + kRollSeats * kBaseLds * 2 + kRollSeats * kHand * 4 +
-                             8 * kRoWords * 4;  // rows (aliased by logits) + base + cards + states: 15 104 B
+                             8 * kRoWords * 4 + 8 * 2 * 4;  // rows (aliased by logits) + base + cards + states +
+                                                            // the decisions' game / seat / players: 15 168 B
 
 // k_puct_rollouts phase profiler (diagnostics, -DSECHS_PHASE_PROF builds only,
 // sn_debug_puct_phases): shader-clock cycles per wave in the state copy-in,
@@ -1054,6 +1080,7 @@ __global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a
     float* sLogit = (float*)sWave[wave];
     float* sCard = (float*)(sBase + kRollSeats * kBaseLds);  // [32][10]
     int32_t* sRo = (int32_t*)(sCard + kRollSeats * kHand);   // [DG][48]
+    int32_t* sInf = sRo + 8 * kRoWords;                       // [DG][2]: game, seat | players << 8
     const int64_t groups = (a.D + DG - 1) / DG;
     auto fence = [] { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); };
     const int sl = lane & (kRollSeats - 1), p0 = lane >> 5;  // phase 1: seat sl, parts p0 and p0 + 2
@@ -1063,6 +1090,21 @@ __global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a
         const int64_t d0 = grp * DG;
         const int nd = (int)min<int64_t>(DG, a.D - d0);
         const int nseat = nd * N;
+        // the decisions' game, seat and players (a tournament's decision list and seat words: global loads
+        // once per group instead of per step and lane)
+        if (lane < DG) {
+            int64_t g;
+            int p, kp;
+            DecInfo{}(a, d0 + min(lane, nd - 1), g, p, kp);
+            sInf[2 * lane] = (int32_t)g, sInf[2 * lane + 1] = p | (kp << 8);
+        }
+        fence();
+        auto info = [&](const PuctArgs&, int64_t dd, int64_t& g, int& p, int& kp) {
+            const int j = (int)(dd - d0);
+            g = sInf[2 * j];
+            const int w = sInf[2 * j + 1];
+            p = w & 255, kp = w >> 8;
+        };
         for (int r = r0; r < r0 + nr; r++) {
             PuctArgs ar = a;
             ar.rollout = (uint32_t)r;
@@ -1079,7 +1121,8 @@ __global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a
 #pragma unroll
                 for (int pp = 0; pp < 2; pp++) {
                     const int part = p0 + 2 * pp;
-                    const SeatIn in = seat_load(ar, N, d0 * N + min(sl, nseat - 1), part);
+                    const int si = min(sl, nseat - 1), dj = si / N;
+                    const SeatIn in = seat_load_kp(ar, d0 + dj, si - dj * N, sInf[2 * dj + 1] >> 8, part);
                     seat_row_part(in, m, part, sRow + sl * kSeatRowLds, sCard + sl * kHand, sLut);
                 }
                 fence();
@@ -1149,7 +1192,7 @@ __global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a
                 // group's DG decisions (the upper half of the wave) follow along and write nothing
                 step_seat<N, L>(
                     s, ar, [&](int64_t dd, int q, int k) { return sLogit[((dd - d0) * N + q) * m + k]; }, t, m,
-                    d0 * L + lane, d0 + nd, d0);
+                    d0 * L + lane, d0 + nd, d0, info);
                 fence();
                 pf.mark(t == 0 ? RP_STEP0 : RP_STEP);
             }
