@@ -57,7 +57,7 @@ ALGO_BYTES_PER_STEP = (33 * N_PLAYERS + 57) + 47 * N_PLAYERS  # 377 B at N = 4
 # run, so the committed summary of the current kernels is reported beside the
 # live timing.
 LIB_TWIST_EVERY = 4  # the library's SN_OPT_TWIST_EVERY default (include/sechs.h)
-SQ_CONFIG4_ROLLOUTS = "profiles/r05_sq_config4_rollouts.json"  # SQ pass of k_puct_rollouts (eager launches)
+SQ_CONFIG4_ROLLOUTS = "profiles/r06_sq_config4_rollouts.json"  # SQ pass of k_puct_rollouts (eager launches)
 PMC_TRAFFIC = {"numpy": os.path.join(ROOT, "profiles", "r06_dec_pmc_traffic_numpy.json"),  # tools/r06_final.sh
                "numpy_ring": os.path.join(ROOT, "profiles", "r06_base_pmc_traffic_numpy.json"),  # --pipe-dec 0
                "philox": os.path.join(ROOT, "profiles", "r04_pmc_traffic_philox.json")}
@@ -311,6 +311,7 @@ def host_cpu_info():
 # instruction per 2 cycles each (MI355X_MICROARCH.md "Wave scheduling"), at
 # the 2.4 GHz peak engine clock
 VALU_PEAK_GINSTR = 256 * 4 * 2.4 / 2  # 1228.8 G wave-instructions/s
+CLOCK_HZ = 2.4e9  # the peak engine clock
 SQ_EXTRAS = os.path.join(ROOT, "profiles", "r04_sq_extras.json")
 
 
@@ -413,9 +414,15 @@ def bench_puct(games, mc_max=100, mc_per_card=10):
         else:
             src = "profiles/r04_sq_config4_kernels.json"
             c = json.load(open(os.path.join(ROOT, src)))["k_puct_mlp_seats"]
-        sq4 = {"mfma_busy_cycles_per_launch": c["SQ_VALU_MFMA_BUSY_CYCLES"] / c["dispatches_per_pass"],
+        busy = c["SQ_VALU_MFMA_BUSY_CYCLES"] / c["dispatches_per_pass"]
+        sq4 = {"mfma_busy_cycles_per_launch": busy,
                "valu_per_wave": c["SQ_INSTS_VALU_per_wave"], "mfma_per_wave": c["SQ_INSTS_MFMA"] / c["SQ_WAVES"],
                "valu_per_mfma": c["SQ_INSTS_VALU"] / c["SQ_INSTS_MFMA"], "source": src}
+        if c.get("kernel_avg_ns"):
+            # MFMA-busy SIMD-cycles over the launch's SIMD-cycles (256 CUs x 4 SIMDs) at the 2.4 GHz peak clock
+            # (a lower clock would give a higher fraction)
+            sq4["mfma_busy_frac"] = busy / (1024 * c["kernel_avg_ns"] * 1e-9 * CLOCK_HZ)
+            sq4["kernel_avg_ns"] = c["kernel_avg_ns"]
     except (OSError, KeyError, ValueError, ZeroDivisionError):
         pass
     if fused:

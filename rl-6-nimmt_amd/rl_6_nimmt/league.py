@@ -380,8 +380,9 @@ class BatchedTournament:
         if kind == KIND_PUCT:
             return BatchedPUCT(env, agent.actor, mc_per_card=agent.mc_per_card, mc_max=agent.mc_max,
                                c_puct=getattr(agent, "c_puct", 2.0), seed=seed, puct_root=agent._puct_root,
-                               net_dtype=self.net_dtype, mcs_num_cards=agent.num_cards, max_decisions=B,
-                               fused_rollouts=False)  # a launch per step: measured faster here
+                               net_dtype=self.net_dtype, mcs_num_cards=agent.num_cards, max_decisions=B)
+            # whole rollouts per kernel (sn_puct_rollouts) since round 6: 0.783 vs 0.822-0.827 s per run.py
+            # league round against a launch per step (gpurun_out/r06_mixed3)
         if kind == KIND_CUSTOMED:
             return BatchedPUCTCustomed(env, agent.actor, net_dtype=self.net_dtype, seed=seed, max_decisions=B)
         if kind == KIND_REINFORCE:

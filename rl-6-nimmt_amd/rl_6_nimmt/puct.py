@@ -184,9 +184,9 @@ class BatchedPUCT:
         # then running on its slice); 0: one sn_puct_deal per rollout (A/B, tests)
         self.deal_batch = int(os.environ.get("SECHS_PUCT_DEAL_BATCH", "16"))
         # whole rollouts in one kernel per deal batch (sn_puct_rollouts: a wave per group of 8
-        # decisions, logits in LDS; 0.96 vs 0.87 G playout env-steps/s on config 4) or a launch
-        # per step (fused_rollouts=False: the tournament's engines, where the whole-rollout kernel
-        # measured slower); SECHS_PUCT_ROLLOUTS=0 / 1 overrides (A/B runs, tests)
+        # decisions, logits in LDS; round 6: 1.10 G playout env-steps/s on config 4, and the
+        # tournament's engines too) or a launch per step (fused_rollouts=False);
+        # SECHS_PUCT_ROLLOUTS=0 / 1 overrides (A/B runs, tests)
         env_ro = os.environ.get("SECHS_PUCT_ROLLOUTS")
         self.fused_rollouts = (env_ro != "0") if env_ro is not None else (True if fused_rollouts is None
                                                                             else bool(fused_rollouts))
