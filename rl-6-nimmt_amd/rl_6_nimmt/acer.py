@@ -280,7 +280,6 @@ class BatchedACER(BatchedPUCT):
         else:
             d = decs[:, :, None].expand(D, K, L)
         s = slots[:, :, None].expand(D, K, L)
-        rows = self.rep_rows[s, t, d]  # [D, K, L, 10, 48]
         act = self.rep_act[s, t, d].to(dev)
         logp_then = self.rep_logp[s, t, d].to(dev)
         rew = self.rep_rew[s, t, d].to(dev)
@@ -288,9 +287,17 @@ class BatchedACER(BatchedPUCT):
         n = (T_STEPS - t).to(dev)
         valid = valid.to(dev)
         legal = torch.arange(10, device=dev) < n[..., None]
-        logit, q = train_forward(self.actor, rows.to(dev).reshape(-1, ROW))
-        logit = logit.reshape(D, K, L, 10).masked_fill(~legal, float("-inf"))
-        q = q.reshape(D, K, L, 10).masked_fill(~legal, 0.0)
+        # the net runs on the legal candidates' rows only (a step with n cards has n of the 10
+        # slots: 55 % of them over an episode); the padded slots' logits are -inf and their
+        # q 0 -- what masking the padded rows' outputs gave -- so they carry no gradient either
+        lg_idx = legal.reshape(-1).nonzero()[:, 0]  # one host sync per loss call (sizes the batch)
+        r_idx = lg_idx // 10
+        rows = self.rep_rows[s.reshape(-1)[r_idx], t.reshape(-1)[r_idx], d.reshape(-1)[r_idx], lg_idx % 10]
+        lg_sel, q_sel = train_forward(self.actor, rows.to(dev))
+        logit = torch.full((D * K * L * 10,), float("-inf"), dtype=lg_sel.dtype, device=dev)
+        logit = logit.index_copy(0, lg_idx.to(dev), lg_sel.reshape(-1)).reshape(D, K, L, 10)
+        q = torch.zeros((D * K * L * 10,), dtype=q_sel.dtype, device=dev)
+        q = q.index_copy(0, lg_idx.to(dev), q_sel.reshape(-1)).reshape(D, K, L, 10)
         logp = torch.log_softmax(logit, dim=-1).masked_fill(~legal, self.log_epsilon)
         a = act[..., None]
         q_a = q.gather(-1, a)[..., 0]
