@@ -1053,11 +1053,12 @@ struct RollProf {
 template <int N, int L>
 __global__ __launch_bounds__(512, 1) void k_puct_rollouts(DevState s, PuctArgs a, int r0, int nr, int32_t* ro_base,
                                                          const uint16_t* w1s, const float* w1c, const uint16_t* w2,
-                                                         const float* head) {
+                                                         const float* head, int DG) {
     constexpr int TNT = 2;
     constexpr int kWaves = 512 / 64;  // two per SIMD
-    constexpr int DG = kRollSeats / L;  // decisions per group
-    static_assert(DG <= 8 && DG * N <= kRollSeats, "a group's seats and states fit");
+    // DG: decisions per group (<= kRollSeats / L; the host picks the fewest that keep the
+    // rounds of groups over the grid's waves at their minimum)
+    static_assert(kRollSeats / L <= 8 && (kRollSeats / L) * N <= kRollSeats, "a group's seats and states fit");
     constexpr int kWld = kMlpLdsK, kWk = kMlpK;
     __shared__ __attribute__((aligned(16))) uint16_t sW[kMlpM * kWld];  // W2 [128][120], shared
     __shared__ __attribute__((aligned(16))) float sC[kMlpK];
@@ -1475,11 +1476,19 @@ sn_status sn_puct_rollouts(sn_env* e, const sn_puct* q, int r0, int nr, void* ro
     if (e->s.N < 3 || e->s.N > 8) return set_error(SN_EUNSUPPORTED, "sn_puct_rollouts: 3 <= N <= 8");
     hipStream_t s = (hipStream_t)stream;
     const int Lw = e->s.N <= 2 ? 2 : e->s.N <= 4 ? 4 : 8;
-    const int64_t groups = (a.D + kRollSeats / Lw - 1) / (kRollSeats / Lw);
-    const dim3 grid((unsigned)std::min<int64_t>((groups + 7) / 8, (int64_t)e->cus));  // one 8-wave workgroup per CU
+    // decisions per wave's group: a wave carries its groups one after the other, so the launch
+    // takes ceil(groups / waves) group-times; with the fewest rounds fixed, the smallest group
+    // that keeps them (fewer seat rows and candidate tiles per group-step: a tournament's
+    // decision count is rarely a multiple of 8 x the grid's waves)
+    const int dg_max = kRollSeats / Lw;
+    const int64_t slots = 8ll * e->cus;  // one 8-wave workgroup per CU
+    const int64_t rounds = std::max<int64_t>(1, (a.D + dg_max * slots - 1) / (dg_max * slots));
+    const int dg = (int)std::min<int64_t>(dg_max, std::max<int64_t>(1, (a.D + rounds * slots - 1) / (rounds * slots)));
+    const int64_t groups = (a.D + dg - 1) / dg;
+    const dim3 grid((unsigned)std::min<int64_t>((groups + 7) / 8, (int64_t)e->cus));
 #define SN_ROLLOUTS(NN_, L_)                                                                                  \
     hipLaunchKernelGGL((k_puct_rollouts<NN_, L_>), grid, dim3(512), 0, s, e->s, a, r0, nr, (int32_t*)ro_base, \
-                       (const uint16_t*)w1s, w1c, (const uint16_t*)w2, head)
+                       (const uint16_t*)w1s, w1c, (const uint16_t*)w2, head, dg)
     switch (e->s.N) {
         case 3: SN_ROLLOUTS(3, 4); break;
         case 4: SN_ROLLOUTS(4, 4); break;

@@ -422,12 +422,29 @@ class BatchedPUCT:
         reference's per-episode loss (mcts.py:244-255)."""
         dev = self.actor_device()
         loss = torch.zeros((), device=dev)
-        for rows, n, best in self.decisions:
-            e = best.shape[0] if d1 is None else d1
-            (logits,) = train_forward(self.actor, rows[d0 * n: e * n].to(dev))
+        for (logits,), n, best in decision_forwards(self.actor, self.decisions, d0, d1, dev):
             logp = torch.log_softmax(logits.reshape(-1, n), dim=1)
-            loss = loss - logp.gather(1, best[d0:e].to(dev).long()[:, None]).sum()
+            loss = loss - logp.gather(1, best[:, None]).sum()
         return loss
+
+
+def decision_forwards(actor, decisions, d0, d1, dev):
+    """the training forward of every recorded decision batch's root rows in ONE
+    pass (the batches' rows concatenated: one GEMM chain forward and backward
+    instead of one per hand size), split back per batch: yields (the net's
+    outputs, n, chosen indices) of deciders [d0, d1) per decision batch"""
+    parts, segs = [], []
+    for rows, n, best in decisions:
+        e = best.shape[0] if d1 is None else d1
+        parts.append(rows[d0 * n: e * n])
+        segs.append((n, (e - d0) * n, best[d0:e].to(dev).long()))
+    if not parts:
+        return
+    outs = train_forward(actor, torch.cat(parts).to(dev))
+    off = 0
+    for n, m, best in segs:
+        yield [o[off: off + m] for o in outs], n, best
+        off += m
 
 
 def make_actor_value(hidden_sizes=(100, 100), activation=None):
@@ -514,11 +531,9 @@ class BatchedPUCTCustomed(BatchedPUCT):
         target = self._decider_rewards(per_step)[:-1].sum(dim=0).float().to(dev)  # [D]
         target = target[d0:d1]
         logps, values = [], []
-        for rows, n, best in self.decisions:
-            e = best.shape[0] if d1 is None else d1
-            (out,) = train_forward(self.actor, rows[d0 * n: e * n].to(dev))
+        for (out,), n, best in decision_forwards(self.actor, self.decisions, d0, d1, dev):
             out = out.reshape(-1, n, 2)
-            best = best[d0:e].to(dev).long()[:, None]
+            best = best[:, None]
             logp = torch.log_softmax(out[:, :, 0], dim=1)
             logps.append(logp.gather(1, best)[:, 0])
             values.append(out[:, :, 1].gather(1, best)[:, 0])

@@ -21,8 +21,7 @@ import numpy as np
 import torch
 
 from . import _native as nat
-from .splitk import train_forward
-from .puct import ROW, BatchedPUCT, ctypes_ref, make_actor
+from .puct import ROW, BatchedPUCT, ctypes_ref, decision_forwards, make_actor
 
 
 class BatchedReinforce(BatchedPUCT):
@@ -95,11 +94,9 @@ class BatchedReinforce(BatchedPUCT):
         per_step = self.episode_rewards if per_step is None else per_step
         dev = self.actor_device()
         logps, ents = [], []
-        for rows, n, idx in self.decisions:
-            e = idx.shape[0] if d1 is None else d1
-            (logits,) = train_forward(self.actor, rows[d0 * n: e * n].to(dev))
+        for (logits,), n, idx in decision_forwards(self.actor, self.decisions, d0, d1, dev):
             logp = torch.log_softmax(logits.reshape(-1, n), dim=1)
-            logps.append(logp.gather(1, idx[d0:e].to(dev).long()[:, None])[:, 0])
+            logps.append(logp.gather(1, idx[:, None])[:, 0])
             ents.append(-(logp.exp() * logp).sum(dim=1))
         logps, ents = torch.stack(logps, dim=1), torch.stack(ents, dim=1)  # [D, T]
         T = logps.shape[1]
