@@ -79,6 +79,9 @@ def parse():
                     help="SN_OPT_PLAY_SPLIT (default: the library's)")
     ap.add_argument("--twist-round", type=int, default=None, choices=[0, 1],
                     help="SN_OPT_TWIST_ROUND: whole-round MT19937 twists in k_mt_ahead (default: the library's, 1)")
+    ap.add_argument("--launches-per-call", type=int, default=1,
+                    help="bench steps (launches of 10 env-steps) per sn_rollout call in the timed loop: each writes "
+                         "its own slice of a [10 x n]-step output (A/B of the host's per-call cost)")
     ap.add_argument("--pipe-dec", type=int, default=None, choices=[0, 1],
                     help="SN_OPT_PIPE_DEC: decode-ahead records (k_decode) for k_play (default: the library's, 1)")
     ap.add_argument("--twist-every", type=int, default=None, choices=[1, 2, 3, 4, 5],
@@ -175,20 +178,26 @@ def barrier(world):
 ENQUEUE_S = None
 
 
-def time_rollouts(env, out, steps, warmup, world):
+def time_rollouts(env, out, steps, warmup, world, per_call=1):
     """Warm up, then time exactly `steps` launches between barrier+sync on
     both sides (nothing else enqueued in between: per-launch timing events
     on the stream cost the pipelined step ~30 %).  Returns (wall seconds,
     mean per-launch ms from HIP events around each launch in a second pass of
     the same `steps` launches, per-kernel times)."""
+    one = {k: v[:STEPS_PER_LAUNCH] for k, v in out.items()}  # one launch's outputs
     for _ in range(warmup):
-        env.rollout(STEPS_PER_LAUNCH, out=out)
+        env.rollout(STEPS_PER_LAUNCH, out=one)
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(steps):
-        env.rollout(STEPS_PER_LAUNCH, out=out)
+    if per_call == 1:
+        for i in range(steps):
+            env.rollout(STEPS_PER_LAUNCH, out=one)
+    else:  # n launches per call, each into its own slice of the [10 n]-step output
+        for i in range(0, steps, per_call):
+            n = min(per_call, steps - i) * STEPS_PER_LAUNCH
+            env.rollout(n, out={k: v[:n] for k, v in out.items()})
     global ENQUEUE_S
     ENQUEUE_S = time.perf_counter() - t0  # host time to enqueue the timed launches (host-bound if ~ the wall)
     torch.cuda.synchronize()
@@ -201,7 +210,7 @@ def time_rollouts(env, out, steps, warmup, world):
         env.time_kernels(steps)
     for i in range(steps):
         ev[i][0].record()
-        env.rollout(STEPS_PER_LAUNCH, out=out)
+        env.rollout(STEPS_PER_LAUNCH, out=one)
         ev[i][1].record()
     torch.cuda.synchronize()
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
@@ -212,8 +221,8 @@ def time_rollouts(env, out, steps, warmup, world):
     return t1 - t0, kern_ms, {"k_play": play_ms, "k_mt_ahead": ahead_ms, "k_decode": dec_ms, "launches": n}
 
 
-def make_out(env, games, with_obs):
-    T, B, N = STEPS_PER_LAUNCH, games, N_PLAYERS
+def make_out(env, games, with_obs, launches=1):
+    T, B, N = STEPS_PER_LAUNCH * launches, games, N_PLAYERS
     dev = env.device
     out = {
         "rewards": torch.empty((T, B, N), dtype=torch.int32, device=dev),
@@ -877,8 +886,8 @@ def main():
         env.set_option(pipe_gpw=args.pipe_gpw, play_split=args.play_split, twist_round=args.twist_round,
                        twist_every=args.twist_every, pipe_dec=args.pipe_dec)
     env.reset()
-    out = make_out(env, B, not args.no_obs)
-    wall, kern_ms, kt = time_rollouts(env, out, args.steps, args.warmup, world)
+    out = make_out(env, B, not args.no_obs, args.launches_per_call)
+    wall, kern_ms, kt = time_rollouts(env, out, args.steps, args.warmup, world, args.launches_per_call)
 
     # pipelined draws must never have run past the twisted words (checked
     # after the timed region; a nonzero count would void the parity claim)
@@ -941,6 +950,7 @@ def main():
             "rng": args.rng,
             "obs": not args.no_obs,
             "parallelism": f"dp{world} (independent game shards, no data-path collective)",
+            "launches_per_call": args.launches_per_call,
         },
         "roofline": {
             "bound": "hbm",
