@@ -79,7 +79,7 @@ def parse():
                     help="SN_OPT_PLAY_SPLIT (default: the library's)")
     ap.add_argument("--twist-round", type=int, default=None, choices=[0, 1],
                     help="SN_OPT_TWIST_ROUND: whole-round MT19937 twists in k_mt_ahead (default: the library's, 1)")
-    ap.add_argument("--launches-per-call", type=int, default=1,
+    ap.add_argument("--launches-per-call", type=int, default=4,
                     help="bench steps (launches of 10 env-steps) per sn_rollout call in the timed loop: each writes "
                          "its own slice of a [10 x n]-step output (A/B of the host's per-call cost)")
     ap.add_argument("--pipe-dec", type=int, default=None, choices=[0, 1],
