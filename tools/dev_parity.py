@@ -45,7 +45,7 @@ def main():
                         print(f"  chunk {chunk} {nm}: {len(bad)} mismatches, first at {bad[0].tolist()} got "
                               f"{got[tuple(bad[0])]} ref {want[tuple(bad[0])]}", flush=True)
             perr = env.pipe_errors() if rng == "numpy" else 0
-            print(f"parity split={split} quad={quad} {rng} obs={want_obs} B={B} T={T}: {'OK' if ok and perr == 0 else 'FAIL'} perr={perr}",
+            print(f"parity split={split} {rng} obs={want_obs} B={B} T={T}: {'OK' if ok and perr == 0 else 'FAIL'} perr={perr}",
                   flush=True)
             if not ok or perr:
                 sys.exit(1)
