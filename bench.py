@@ -204,18 +204,21 @@ def time_rollouts(env, out, steps, warmup, world, per_call=1):
     barrier(world)
     t1 = time.perf_counter()
     # second pass: HIP events around each launch on the launch stream, and
-    # (numpy mode) inside the library around each kernel on its own stream
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    # (numpy mode) inside the library around each kernel on its own stream --
+    # over at least KERNEL_PASS_MIN launches (a 20-launch pass is dominated by
+    # its first groups: k_play 70-75 vs 57-59 us steady, gpurun_out/r06_drv1)
+    n2 = max(steps, KERNEL_PASS_MIN)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n2)]
     if env.rng == "numpy":
-        env.time_kernels(steps)
-    for i in range(steps):
+        env.time_kernels(n2)
+    for i in range(n2):
         ev[i][0].record()
         env.rollout(STEPS_PER_LAUNCH, out=one)
         ev[i][1].record()
     torch.cuda.synchronize()
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if env.rng != "numpy":
-        return t1 - t0, kern_ms, {"k_play": kern_ms, "launches": steps}
+        return t1 - t0, kern_ms, {"k_play": kern_ms, "launches": n2}
     play_ms, ahead_ms, dec_ms, n = env.kernel_times(with_decode=True)
     env.time_kernels(0)
     return t1 - t0, kern_ms, {"k_play": play_ms, "k_mt_ahead": ahead_ms, "k_decode": dec_ms, "launches": n}
@@ -321,6 +324,7 @@ def host_cpu_info():
 # the 2.4 GHz peak engine clock
 VALU_PEAK_GINSTR = 256 * 4 * 2.4 / 2  # 1228.8 G wave-instructions/s
 CLOCK_HZ = 2.4e9  # the peak engine clock
+KERNEL_PASS_MIN = 100  # launches in the per-kernel timing pass (outside the timed region)
 SQ_EXTRAS = os.path.join(ROOT, "profiles", "r04_sq_extras.json")
 
 
