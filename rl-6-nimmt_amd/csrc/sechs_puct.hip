@@ -316,6 +316,13 @@ __device__ __forceinline__ void mlp_tile(const uint16_t* const (&brow)[NT], cons
     // one k-step: the B fragments (16 features of the two 32-row halves), then 4 x 2 MFMAs
     auto kstep = [&](int ks, bool first) {
         const int k0 = 16 * ks + 8 * half;  // this lane's 8 features of the k-step
+        // the k-step's four W2 A fragments issued first, their LDS latency under the B fragments'
+        // VALU (the scheduler would otherwise sink each load to just before its MFMA pair)
+        bf16x8_t af[4];
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++)
+            af[mt] = __builtin_bit_cast(bf16x8_t, *(const uint4*)&sW[(32 * mt + col) * kMlpLdsK + k0]);
+        __builtin_amdgcn_sched_barrier(0);
         const float4 wa = *(const float4*)&sC[k0], wb = *(const float4*)&sC[k0 + 4];
         const float w[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
         bf16x8_t bfr[NT];
@@ -334,11 +341,10 @@ __device__ __forceinline__ void mlp_tile(const uint16_t* const (&brow)[NT], cons
         }
 #pragma unroll
         for (int mt = 0; mt < 4; mt++) {
-            const bf16x8_t a = __builtin_bit_cast(bf16x8_t, *(const uint4*)&sW[(32 * mt + col) * kMlpLdsK + k0]);
             const f32x16_t zero = {};
 #pragma unroll
             for (int nt = 0; nt < NT; nt++)
-                acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr[nt], first ? zero : acc[mt][nt], 0, 0, 0);
+                acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mt], bfr[nt], first ? zero : acc[mt][nt], 0, 0, 0);
         }
     };
     kstep(0, true);  // the accumulators start from the first k-step's products (no zeroing pass)
