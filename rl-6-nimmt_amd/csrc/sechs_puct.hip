@@ -352,23 +352,31 @@ __device__ __forceinline__ void mlp_tile(const uint16_t* const (&brow)[NT], cons
     for (int ks = 1; ks < kMlpK / 16; ks++) kstep(ks, false);
     // epilogue: ReLU, bf16 rounding, head dot over this lane's outputs o
     // (C layout: o = 32 mt + 8 g + 4 half + i, i = 0..3), then the other half's
+    // (the head pairs of an output tile read once for both row halves, the four issued together;
+    // each half's sum in the same mt, g order as before)
+    float sum[NT];
 #pragma unroll
-    for (int nt = 0; nt < NT; nt++) {
-        float sum = 0.f;
+    for (int nt = 0; nt < NT; nt++) sum[nt] = 0.f;
 #pragma unroll
-        for (int mt = 0; mt < 4; mt++)
+    for (int mt = 0; mt < 4; mt++) {
+        uint2 hw[4];
 #pragma unroll
-            for (int g = 0; g < 4; g++) {
-                const uint2 hw = *(const uint2*)&sH2[(32 * mt + 8 * g + 4 * half) / 2];
+        for (int g = 0; g < 4; g++) hw[g] = *(const uint2*)&sH2[(32 * mt + 8 * g + 4 * half) / 2];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int g = 0; g < 4; g++)
+#pragma unroll
+            for (int nt = 0; nt < NT; nt++) {
                 const uint32_t p0 = relu_bf16x2(pack_bf16(acc[mt][nt][4 * g], acc[mt][nt][4 * g + 1]));
                 const uint32_t p1 = relu_bf16x2(pack_bf16(acc[mt][nt][4 * g + 2], acc[mt][nt][4 * g + 3]));
-                sum = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, p0),
-                                                      __builtin_bit_cast(bf16x2_t, hw.x), sum, false);
-                sum = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, p1),
-                                                      __builtin_bit_cast(bf16x2_t, hw.y), sum, false);
+                sum[nt] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, p0),
+                                                          __builtin_bit_cast(bf16x2_t, hw[g].x), sum[nt], false);
+                sum[nt] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, p1),
+                                                          __builtin_bit_cast(bf16x2_t, hw[g].y), sum[nt], false);
             }
-        out[nt] = sum + __shfl_xor(sum, 32);
     }
+#pragma unroll
+    for (int nt = 0; nt < NT; nt++) out[nt] = sum[nt] + __shfl_xor(sum[nt], 32);
 }
 
 // the head as bf16 pairs in LDS (its values are bf16 weights: exact)
