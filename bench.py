@@ -58,7 +58,7 @@ ALGO_BYTES_PER_STEP = (33 * N_PLAYERS + 57) + 47 * N_PLAYERS  # 377 B at N = 4
 # live timing.
 LIB_TWIST_EVERY = 4  # the library's SN_OPT_TWIST_EVERY default (include/sechs.h)
 SQ_CONFIG4_ROLLOUTS = "profiles/r06_sq_config4_rollouts.json"  # SQ pass of k_puct_rollouts (eager launches)
-PMC_TRAFFIC = {"numpy": os.path.join(ROOT, "profiles", "r06_final2_pmc_traffic_numpy.json"),  # tools/r06_final.sh
+PMC_TRAFFIC = {"numpy": os.path.join(ROOT, "profiles", "r06_final3_pmc_traffic_numpy.json"),  # tools/r06_final.sh
                "numpy_ring": os.path.join(ROOT, "profiles", "r06_base_pmc_traffic_numpy.json"),  # --pipe-dec 0
                "philox": os.path.join(ROOT, "profiles", "r04_pmc_traffic_philox.json")}
 
