@@ -425,8 +425,10 @@ sn_status sn_puct_deal(sn_env* env, const sn_puct* q, void* stream);
    and run its steps there -- the same states, dealt with nr x D lanes. */
 sn_status sn_puct_deal_batch(sn_env* env, const sn_puct* q, int r0, int nr, void* ro_out, void* stream);
 /* Rollouts r0 .. r0 + nr - 1 of every decision in one launch, from the
-   states sn_puct_deal_batch dealt into ro_base: per workgroup a group of
-   decisions runs every step (sn_puct_mlp_seats' rows, MFMA layer 1 + 2 and
+   states sn_puct_deal_batch dealt into ro_base: one wave per group of up to
+   32 / L decisions (L = N rounded up to 4 or 8; the library picks the
+   smallest group that keeps the launch's rounds over its waves at their
+   minimum) runs every step (sn_puct_mlp_seats' rows, MFMA layer 1 + 2 and
    head into logits in LDS, then sn_puct_step's seat-lane step) of each
    rollout in order -- the same values as the launch-per-step loop (3 <= N
    <= 8; weights as sn_puct_mlp_seats). */
