@@ -867,33 +867,46 @@ __device__ __forceinline__ void seat_row_part(const SeatIn& in, int n_cur, int p
     h.lo = in.h0 | ((uint64_t)in.h1 << 32);
     h.hi = in.h2;
     auto card_bits = [&](uint32_t c) { return lut[kLutCard + (c == 0xFFu ? 0u : min(c, 103u) + 1u)]; };  // 0xFF: -1
+    // every table lookup first, then the row writes: the LDS reads in flight together (written
+    // interleaved, each write waited for its own read)
+    uint16_t hb[3], rc[kThreshold];
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const int k = part + 4 * j;
+        hb[j] = (k < kHand) ? card_bits(hand_get(h, (uint32_t)(k < kHand ? k : 0))) : (uint16_t)0;
+    }
+    const uint32_t lo = in.lo, hi = in.hi;
+    const uint32_t len = len_of(hi);
+    const uint16_t lenb = lut[kLutLen + min(len, 7u)];
+    const uint16_t endb = card_bits(end_of(hi));
+    const uint16_t headb = lut[kLutHeads + min(heads_in(hi), 63u)];  // <= 35 in a game
+#pragma unroll
+    for (int c = 0; c < kThreshold; c++) {
+        const uint32_t v = (c < 5 && (uint32_t)c < len) ? card_at(lo, hi, c < 5 ? c : 0) : 0xFFu;
+        rc[c] = card_bits(v);
+    }
+    const uint16_t kpb = lut[kLutN + min(kp, 15)];
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int j = 0; j < 3; j++) {
         const int k = part + 4 * j;
         if (k < kHand) {
-            const uint32_t c = hand_get(h, (uint32_t)k);
-            const uint16_t b = card_bits(c);
-            row[1 + k] = live ? b : (uint16_t)0;
-            cd[k] = (live && k < n_cur) ? __uint_as_float((uint32_t)b << 16) : 0.f;
+            row[1 + k] = live ? hb[j] : (uint16_t)0;
+            cd[k] = (live && k < n_cur) ? __uint_as_float((uint32_t)hb[j] << 16) : 0.f;
         }
     }
-    const uint32_t lo = in.lo, hi = in.hi;
-    const uint32_t len = len_of(hi);
-    row[12 + part] = live ? lut[kLutLen + min(len, 7u)] : (uint16_t)0;
-    row[16 + part] = live ? card_bits(end_of(hi)) : (uint16_t)0;
-    row[20 + part] = live ? lut[kLutHeads + min(heads_in(hi), 63u)] : (uint16_t)0;  // <= 35 in a game
+    row[12 + part] = live ? lenb : (uint16_t)0;
+    row[16 + part] = live ? endb : (uint16_t)0;
+    row[20 + part] = live ? headb : (uint16_t)0;
 #pragma unroll
-    for (int c = 0; c < kThreshold; c++) {
-        const uint32_t v = (c < 5 && (uint32_t)c < len) ? card_at(lo, hi, c < 5 ? c : 0) : 0xFFu;
-        row[24 + part * kThreshold + c] = live ? card_bits(v) : (uint16_t)0;
-    }
+    for (int c = 0; c < kThreshold; c++) row[24 + part * kThreshold + c] = live ? rc[c] : (uint16_t)0;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
         const int f = kRowLen + 1 + part + 4 * j;
         if (f < kSeatRowK) row[f] = 0;
     }
     if (part == 0) row[0] = 0;
-    if (part == 1) row[11] = live ? lut[kLutN + min(kp, 15)] : (uint16_t)0;
+    if (part == 1) row[11] = live ? kpb : (uint16_t)0;
     if (part == 2) row[kRowLen] = bf16_bits(1.f);
 }
 
